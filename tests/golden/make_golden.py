@@ -1,0 +1,267 @@
+"""Generate the golden fixtures in tests/golden/*.npz from the REFERENCE.
+
+Run in the build container only (needs /root/reference):
+    python tests/golden/make_golden.py
+Each fixture holds inputs, the reference's outputs and (tiny) weights, so the
+oracle and the HIP path can be checked against the reference without the
+reference being present (the GPU box has no /root/reference).
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import ref_harness  # noqa: E402
+
+R = ref_harness.load()
+
+
+def f32(t):
+    return t.detach().to(torch.float32).cpu().numpy()
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **arrays)
+    print("wrote", path, sum(a.nbytes for a in arrays.values()) // 1024, "KiB raw")
+
+
+def sd_arrays(module, prefix="w:"):
+    """Weights are bf16-representable (randomize rounds them), stored as raw bf16 bits."""
+    out = {}
+    for k, v in module.state_dict().items():
+        b = v.detach().to(torch.bfloat16)
+        assert torch.equal(b.float(), v.detach().float()), k
+        out[prefix + k] = b.view(torch.int16).numpy()
+    return out
+
+
+def randomize(module, seed, std=0.05):
+    """Random weights everywhere (the reference zero-inits adaLN / final layers)."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for name, p in module.named_parameters():
+            if name.endswith("norm.weight") or name.endswith("gamma"):
+                p.copy_(1.0 + 0.1 * torch.randn(p.shape, generator=g))
+            else:
+                p.copy_(std * torch.randn(p.shape, generator=g))
+            p.copy_(p.to(torch.bfloat16).float())
+
+
+# ---------------------------------------------------------------- G1 scheduler
+def g1_scheduler():
+    Sch = R["dpm"].DPMSolverMultistepScheduler
+    out = {}
+    for S in (1, 2, 5, 10, 20):
+        s = Sch(num_train_timesteps=1000, beta_schedule="cosine", prediction_type="v_prediction")
+        s.set_timesteps(S)
+        out[f"timesteps_{S}"] = s.timesteps.numpy()
+        out[f"sigmas_{S}"] = s.sigmas.numpy()
+        out[f"t_bf16_{S}"] = f32(s.timesteps.to(torch.bfloat16))
+        # a stepping trace on random model outputs, in fp32 and bf16
+        for dt, tag in ((torch.float32, "f32"), (torch.bfloat16, "bf16")):
+            g = torch.Generator().manual_seed(100 + S)
+            x = torch.randn(3, 64, generator=g).to(dt)
+            vs = torch.randn(S, 3, 64, generator=g).to(dt)
+            s.set_timesteps(S)
+            xs = []
+            cur = x
+            for i, t in enumerate(s.timesteps):
+                cur = s.step(vs[i], t, cur).prev_sample
+                xs.append(cur)
+            out[f"x_{tag}_{S}"] = f32(x)
+            out[f"v_{tag}_{S}"] = f32(vs)
+            out[f"trace_{tag}_{S}"] = f32(torch.stack(xs))
+    save("g1_scheduler.npz", **out)
+
+
+# ------------------------------------------------------------ G2/G3 diffusion head
+def head_module(H):
+    cfg = R["cfg"].VibeVoiceDiffusionHeadConfig(hidden_size=H, head_layers=4, head_ffn_ratio=3.0,
+                                                rms_norm_eps=1e-5, latent_size=64)
+    m = R["head"].VibeVoiceDiffusionHead(cfg)
+    randomize(m, seed=H)
+    return m.eval()
+
+
+class _FakeInf:
+    """Just enough of VibeVoiceForConditionalGenerationInference for the
+    reference's own sample_speech_tokens (modeling_vibevoice_inference.py:712-725)."""
+
+    def __init__(self, head, steps):
+        self.model = type("M", (), {})()
+        self.model.prediction_head = head
+        self.model.noise_scheduler = R["dpm"].DPMSolverMultistepScheduler(
+            num_train_timesteps=1000, beta_schedule="cosine", prediction_type="v_prediction")
+        self.ddpm_inference_steps = steps
+        self.config = type("C", (), {"acoustic_vae_dim": 64})()
+
+
+def g2_g3_head():
+    out = {}
+    H = 128
+    head = head_module(H)
+    out.update(sd_arrays(head))
+    g = torch.Generator().manual_seed(7)
+    for dt, tag in ((torch.float32, "f32"), (torch.bfloat16, "bf16")):
+        m = head.to(dt)
+        noisy = torch.randn(4, 64, generator=g).to(dt)
+        t = torch.tensor([999., 999., 500., 500.]).to(dt)
+        cond = torch.randn(4, H, generator=g).to(dt)
+        with torch.no_grad():
+            y = m(noisy, t, condition=cond)
+        out[f"fwd_noisy_{tag}"], out[f"fwd_t_{tag}"] = f32(noisy), f32(t)
+        out[f"fwd_cond_{tag}"], out[f"fwd_out_{tag}"] = f32(cond), f32(y)
+        for S in (5, 10):
+            n = 2
+            pos = torch.randn(n, H, generator=g).to(dt)
+            neg = torch.randn(n, H, generator=g).to(dt)
+            fake = _FakeInf(m, S)
+            torch.manual_seed(1234 + S)
+            with torch.no_grad():
+                lat = R["mvi"].VibeVoiceForConditionalGenerationInference.sample_speech_tokens(
+                    fake, pos, neg, cfg_scale=1.3)
+            torch.manual_seed(1234 + S)
+            noise = torch.randn(2 * n, 64)        # the draw made inside (:716)
+            out[f"sst_pos_{tag}_{S}"], out[f"sst_neg_{tag}_{S}"] = f32(pos), f32(neg)
+            out[f"sst_noise_{S}_{tag}"] = noise.numpy()
+            out[f"sst_out_{tag}_{S}"] = f32(lat)
+    save("g2_head.npz", **out)
+
+
+# ------------------------------------------------------------------ G4/G5 codec
+def codec_cfgs():
+    return {
+        "small": dict(encoder_n_filters=8, decoder_n_filters=8, encoder_ratios=[2, 2],
+                      encoder_depths="1-1-2", vae_dim=16),
+        "hop3200": dict(encoder_n_filters=2, decoder_n_filters=2, encoder_ratios=[8, 5, 5, 4, 2, 2],
+                        encoder_depths="1-1-1-1-1-1-1", vae_dim=16),
+    }
+
+
+def g4_g5_codec():
+    out = {}
+    C = R["cfg"]
+    for name, kw in codec_cfgs().items():
+        acfg = C.VibeVoiceAcousticTokenizerConfig(**kw)
+        m = R["tok"].VibeVoiceAcousticTokenizerModel(acfg).eval()
+        randomize(m, seed=len(name), std=0.2)
+        out.update({f"{name}/{k}": v for k, v in sd_arrays(m).items()})
+        hop = int(np.prod(kw["encoder_ratios"]))
+        g = torch.Generator().manual_seed(11)
+        for dt, tag in ((torch.float32, "f32"), (torch.bfloat16, "bf16")):
+            mm = m.to(dt)
+            # streaming decode: 2 samples, 5 steps, sample 1 skips step 2, set_to_zero(0) after step 3
+            B, steps = 2, 5
+            z = torch.randn(steps, B, kw["vae_dim"], 1, generator=g).to(dt)
+            cache = R["tok"].VibeVoiceTokenizerStreamingCache()
+            outs = []
+            sched = [[0, 1], [0, 1], [0], [0, 1], [0, 1]]
+            for s in range(steps):
+                idx = torch.tensor(sched[s])
+                with torch.no_grad():
+                    a = mm.decode(z[s, idx], cache=cache, sample_indices=idx, use_cache=True)
+                full = torch.zeros(B, 1, hop, dtype=dt)
+                full[idx] = a
+                outs.append(full)
+                if s == 2:
+                    cache.set_to_zero(torch.tensor([0]))
+            out[f"{name}/dec_z_{tag}"] = f32(z)
+            out[f"{name}/dec_audio_{tag}"] = f32(torch.stack(outs))
+            # non-streaming decode of 4 frames == streaming (KAT-3)
+            zz = torch.randn(1, kw["vae_dim"], 4, generator=g).to(dt)
+            with torch.no_grad():
+                out[f"{name}/dec_ns_audio_{tag}"] = f32(mm.decode(zz))
+            out[f"{name}/dec_ns_z_{tag}"] = f32(zz)
+            # streaming encode of 3 frames of audio, 2 samples
+            aud = (0.3 * torch.randn(3, B, 1, hop, generator=g)).to(dt)
+            cache = R["tok"].VibeVoiceTokenizerStreamingCache()
+            lats = []
+            for s in range(3):
+                idx = torch.arange(B)
+                with torch.no_grad():
+                    lats.append(mm.encode(aud[s], cache=cache, sample_indices=idx, use_cache=True).mean)
+            out[f"{name}/enc_audio_{tag}"] = f32(aud)
+            out[f"{name}/enc_mean_{tag}"] = f32(torch.stack(lats))
+            # non-streaming encode of a length that is NOT a multiple of hop (voice prompt path)
+            L = 2 * hop + hop // 2 + 3
+            a2 = (0.3 * torch.randn(2, 1, L, generator=g)).to(dt)
+            with torch.no_grad():
+                out[f"{name}/enc_ns_mean_{tag}"] = f32(mm.encode(a2).mean)
+            out[f"{name}/enc_ns_audio_{tag}"] = f32(a2)
+    save("g4_codec.npz", **out)
+
+
+# -------------------------------------------------------------- G6 connectors
+def g6_connector():
+    out = {}
+    SC = R["mv"].SpeechConnector
+    for din in (64, 128):
+        m = SC(din, 256).eval()
+        randomize(m, seed=din)
+        out.update({f"{din}/{k}": v for k, v in sd_arrays(m).items()})
+        g = torch.Generator().manual_seed(din)
+        for dt, tag in ((torch.float32, "f32"), (torch.bfloat16, "bf16")):
+            x = torch.randn(3, 1, din, generator=g).to(dt)
+            with torch.no_grad():
+                y = m.to(dt)(x)
+            out[f"{din}/x_{tag}"], out[f"{din}/y_{tag}"] = f32(x), f32(y)
+    save("g6_connector.npz", **out)
+
+
+# ------------------------------------------------------------------ G7 Qwen2
+def lm_cfg():
+    from transformers import Qwen2Config
+    return Qwen2Config(hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=2,
+                       num_key_value_heads=1, head_dim=128, rms_norm_eps=1e-6, rope_theta=1e6,
+                       vocab_size=64, max_position_embeddings=4096, tie_word_embeddings=False,
+                       attn_implementation="eager")
+
+
+def g7_qwen2():
+    from transformers import AutoModel
+    from transformers.cache_utils import DynamicCache
+    cfg = lm_cfg()
+    out = {}
+    torch.manual_seed(3)
+    m = AutoModel.from_config(cfg).eval()
+    randomize(m, seed=3, std=0.05)
+    out.update(sd_arrays(m))
+    g = torch.Generator().manual_seed(5)
+    for dt, tag in ((torch.float32, "f32"), (torch.bfloat16, "bf16")):
+        mm = m.to(dt)
+        B, L = 2, 7
+        pad = [0, 3]                      # sample 1 is left-padded by 3 (vibevoice_processor.py:351-353)
+        mask = torch.ones(B, L, dtype=torch.long)
+        mask[1, :pad[1]] = 0
+        emb = torch.randn(B, L, 256, generator=g).to(dt)
+        cache = DynamicCache()
+        pos = (mask.cumsum(-1) - 1).masked_fill(mask == 0, 1)   # HF 4.51.3 prepare_inputs_for_generation
+        with torch.no_grad():
+            o = mm(inputs_embeds=emb, attention_mask=mask, position_ids=pos, past_key_values=cache,
+                   use_cache=True)
+        hs = [o.last_hidden_state[:, -1]]
+        steps = torch.randn(3, B, 1, 256, generator=g).to(dt)
+        for s in range(3):
+            mask = torch.cat([mask, torch.ones(B, 1, dtype=torch.long)], dim=1)
+            p = (mask.cumsum(-1) - 1)[:, -1:]
+            with torch.no_grad():
+                o = mm(inputs_embeds=steps[s], attention_mask=mask, position_ids=p, past_key_values=cache,
+                       use_cache=True)
+            hs.append(o.last_hidden_state[:, -1])
+        out[f"emb_{tag}"], out[f"steps_{tag}"] = f32(emb), f32(steps)
+        out[f"mask0"] = mask[:, :L].numpy()
+        out[f"hidden_{tag}"] = f32(torch.stack(hs))
+    save("g7_qwen2.npz", **out)
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(8)
+    g1_scheduler()
+    g2_g3_head()
+    g4_g5_codec()
+    g6_connector()
+    g7_qwen2()

@@ -1,0 +1,158 @@
+"""The CPU oracle (oracle/) against the reference's golden vectors.
+
+Fixtures come from tests/golden/make_golden.py, which runs the reference's
+own modules.  fp32 comparisons are tight; bf16 ones allow for the oracle's
+different (but same-rounding-point) op grouping.
+"""
+import pytest
+import torch
+
+from golden_io import DT, load, t, weights
+from oracle import codec, head, lm, scheduler
+
+
+def close(a, b, rtol, atol):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    scale = max(1.0, b.abs().max().item())
+    assert torch.allclose(a, b, rtol=rtol, atol=atol * scale), f"max abs err {err} (scale {scale})"
+
+
+TOL = {"f32": (1e-5, 1e-5), "bf16": (2e-2, 2e-2)}
+
+
+@pytest.mark.parametrize("S", [1, 2, 5, 10, 20])
+def test_scheduler_tables(S):
+    z = load("g1_scheduler.npz")
+    s = scheduler.DPMSolverPP()
+    s.set_timesteps(S)
+    assert (s.timesteps.numpy() == z[f"timesteps_{S}"]).all()
+    assert (s.sigmas.numpy() == z[f"sigmas_{S}"]).all()
+    assert (s.timesteps.to(torch.bfloat16).float().numpy() == z[f"t_bf16_{S}"]).all()
+
+
+@pytest.mark.parametrize("S", [1, 2, 5, 10, 20])
+@pytest.mark.parametrize("tag", ["f32", "bf16"])
+def test_scheduler_step_trace_bitexact(S, tag):
+    """x0 in the sample dtype, fp32 update, cast back: bit-exact vs the reference."""
+    z = load("g1_scheduler.npz")
+    s = scheduler.DPMSolverPP()
+    s.set_timesteps(S)
+    x = t(z, f"x_{tag}_{S}", DT[tag])
+    vs = t(z, f"v_{tag}_{S}", DT[tag])
+    ref = t(z, f"trace_{tag}_{S}")
+    for i in range(S):
+        x = s.step(vs[i], x)
+        assert torch.equal(x.float(), ref[i]), f"step {i}"
+
+
+@pytest.mark.parametrize("tag", ["f32", "bf16"])
+def test_head_forward(tag):
+    z = load("g2_head.npz")
+    sd = weights(z, dtype=DT[tag])
+    y = head.head_forward(sd, t(z, f"fwd_noisy_{tag}", DT[tag]), t(z, f"fwd_t_{tag}", DT[tag]),
+                          t(z, f"fwd_cond_{tag}", DT[tag]), n_layers=4)
+    close(y, t(z, f"fwd_out_{tag}"), *TOL[tag])
+
+
+@pytest.mark.parametrize("S", [5, 10])
+@pytest.mark.parametrize("tag", ["f32", "bf16"])
+def test_sample_speech_tokens(S, tag):
+    z = load("g2_head.npz")
+    sd = weights(z, dtype=DT[tag])
+    lat = head.sample_speech_tokens(sd, t(z, f"sst_pos_{tag}_{S}", DT[tag]), t(z, f"sst_neg_{tag}_{S}", DT[tag]),
+                                    t(z, f"sst_noise_{S}_{tag}").to(DT[tag]), S, 1.3, n_layers=4)
+    close(lat, t(z, f"sst_out_{tag}_{S}"), *TOL[tag])
+
+
+CODEC = {"small": dict(encoder_n_filters=8, decoder_n_filters=8, encoder_ratios=[2, 2],
+                       encoder_depths="1-1-2", vae_dim=16),
+         "hop3200": dict(encoder_n_filters=2, decoder_n_filters=2, encoder_ratios=[8, 5, 5, 4, 2, 2],
+                         encoder_depths="1-1-1-1-1-1-1", vae_dim=16)}
+
+
+@pytest.mark.parametrize("name", list(CODEC))
+@pytest.mark.parametrize("tag", ["f32", "bf16"])
+def test_codec_streaming_decode(name, tag):
+    z = load("g4_codec.npz")
+    sd = weights(z, prefix=f"{name}/w:", dtype=DT[tag])
+    dims = codec.codec_dims(CODEC[name], "decoder")
+    zs = t(z, f"{name}/dec_z_{tag}", DT[tag])
+    ref = t(z, f"{name}/dec_audio_{tag}")
+    st = codec.StreamState(2)
+    sched = [[0, 1], [0, 1], [0], [0, 1], [0, 1]]
+    for s in range(zs.shape[0]):
+        idx = torch.tensor(sched[s])
+        a = codec.decode(sd, dims, zs[s, idx], st, idx)
+        close(a, ref[s, idx], *TOL[tag])
+        if s == 2:
+            st.zero(torch.tensor([0]))
+
+
+@pytest.mark.parametrize("name", list(CODEC))
+@pytest.mark.parametrize("tag", ["f32", "bf16"])
+def test_codec_nonstreaming_decode(name, tag):
+    z = load("g4_codec.npz")
+    sd = weights(z, prefix=f"{name}/w:", dtype=DT[tag])
+    dims = codec.codec_dims(CODEC[name], "decoder")
+    a = codec.decode(sd, dims, t(z, f"{name}/dec_ns_z_{tag}", DT[tag]), None, None, streaming=False)
+    close(a, t(z, f"{name}/dec_ns_audio_{tag}"), *TOL[tag])
+    if tag == "f32":   # KAT-3: streaming frame-by-frame == one-shot non-streaming
+        st = codec.StreamState(1)
+        zz = t(z, f"{name}/dec_ns_z_{tag}")
+        parts = [codec.decode(sd, dims, zz[:, :, i:i + 1], st, torch.tensor([0])) for i in range(zz.shape[2])]
+        close(torch.cat(parts, dim=-1), a, 1e-5, 1e-5)
+
+
+@pytest.mark.parametrize("name", list(CODEC))
+@pytest.mark.parametrize("tag", ["f32", "bf16"])
+def test_codec_encode(name, tag):
+    z = load("g4_codec.npz")
+    sd = weights(z, prefix=f"{name}/w:", dtype=DT[tag])
+    dims = codec.codec_dims(CODEC[name], "encoder")
+    aud = t(z, f"{name}/enc_audio_{tag}", DT[tag])
+    ref = t(z, f"{name}/enc_mean_{tag}")
+    st = codec.StreamState(2)
+    for s in range(aud.shape[0]):
+        m = codec.encode(sd, dims, aud[s], st, torch.arange(2))
+        close(m, ref[s], *TOL[tag])
+    m = codec.encode(sd, dims, t(z, f"{name}/enc_ns_audio_{tag}", DT[tag]), None, None, streaming=False)
+    close(m, t(z, f"{name}/enc_ns_mean_{tag}"), *TOL[tag])
+
+
+@pytest.mark.parametrize("din", [64, 128])
+@pytest.mark.parametrize("tag", ["f32", "bf16"])
+def test_connector(din, tag):
+    z = load("g6_connector.npz")
+    sd = weights(z, prefix=f"{din}/w:", dtype=DT[tag])
+    x = t(z, f"{din}/x_{tag}", DT[tag])
+    y = torch.nn.functional.linear(x, sd["fc1.weight"], sd["fc1.bias"])
+    y = lm.rms(y, sd["norm.weight"], 1e-6)
+    y = torch.nn.functional.linear(y, sd["fc2.weight"], sd["fc2.bias"])
+    close(y, t(z, f"{din}/y_{tag}"), *TOL[tag])
+
+
+LMCFG = dict(hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=2,
+             num_key_value_heads=1, head_dim=128, rms_norm_eps=1e-6, rope_theta=1e6)
+
+
+@pytest.mark.parametrize("tag", ["f32", "bf16"])
+def test_qwen2_compacted_kv(tag):
+    """Left-padded prefill + 3 decode steps == compacted per-row caches with
+    positions = number of cached entries (cumsum(mask)-1)."""
+    z = load("g7_qwen2.npz")
+    sd = weights(z, dtype=DT[tag])
+    emb = t(z, f"emb_{tag}", DT[tag])
+    steps = t(z, f"steps_{tag}", DT[tag])
+    mask = z["mask0"]
+    ref = t(z, f"hidden_{tag}")
+    kvs = [lm.RowKV(2) for _ in range(2)]
+    last = []
+    for r in range(2):
+        keep = torch.from_numpy(mask[r]).bool()
+        h = lm.forward_rows(sd, LMCFG, emb[r:r + 1, keep], kvs[r:r + 1])
+        last.append(h[0, -1])
+    close(torch.stack(last), ref[0], *TOL[tag])
+    for s in range(steps.shape[0]):
+        h = lm.forward_rows(sd, LMCFG, steps[s], kvs)
+        close(h[:, -1], ref[s + 1], *TOL[tag])
