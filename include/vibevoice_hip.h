@@ -1,0 +1,127 @@
+/*
+ * vibevoice_hip.h — C ABI of libvibevoice_hip.so, the MI355X (gfx950) engine
+ * behind VibeVoice's next-token-diffusion generate loop.
+ *
+ * The reference has no FFI: its hot path sits behind the Hugging Face plugin
+ * surface (AutoModelForCausalLM.register + .generate(),
+ * vibevoice/modular/modeling_vibevoice_inference.py:327-710, :728).  The Python
+ * host in vibevoice_amd/ keeps that surface and calls these entry points for
+ * every piece of arithmetic of the loop body:
+ *
+ *   vv_lm_forward        <- self(...) positive pass :483-486 and negative pass
+ *                           :598-600 (Qwen2 decode, batched as one set of rows),
+ *                           and the prompt prefill :468-486 / :222-238
+ *   vv_diffusion_sample  <- sample_speech_tokens :712-725 (+ prediction_head,
+ *                           modular_vibevoice_diffusion_head.py:254-280, and
+ *                           DPMSolverMultistepScheduler.step, dpm_solver.py:935)
+ *   vv_codec_step        <- acoustic_tokenizer.decode :651-658, semantic_tokenizer
+ *                           .encode :673-679, acoustic/semantic connectors :682-687
+ *   vv_codec_reset       <- acoustic_cache/semantic_cache.set_to_zero :557-560
+ *   vv_acoustic_encode   <- _process_speech_inputs encode :150-164 (voice prompt)
+ *   vv_connector         <- SpeechConnector.forward (modeling_vibevoice.py:58-69)
+ *
+ * Conventions: all tensor arguments are caller-owned DEVICE pointers (bf16 =
+ * 2-byte bfloat16, int = int32) with explicit sizes; weights are borrowed (the
+ * caller keeps them alive).  Every call is asynchronous on the caller's stream.
+ * Return value 0 = ok; otherwise vv_last_error() (thread-local) describes it.
+ */
+#ifndef VIBEVOICE_HIP_H
+#define VIBEVOICE_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct vv_ctx vv_ctx;
+typedef void* vv_stream; /* hipStream_t */
+
+#define VV_MAX_STAGES 8
+
+typedef struct vv_config {
+  /* Qwen2 decoder (vibevoice/configs/qwen2.5_1.5b_64k.json decoder_config) */
+  int hidden, n_layers, n_heads, n_kv_heads, head_dim, intermediate;
+  float rms_eps, rope_theta;
+  /* diffusion head (diffusion_head_config) */
+  int head_layers, head_ffn, latent_dim;
+  float head_eps;
+  /* σ-VAE codec (acoustic_tokenizer_config / semantic_tokenizer_config) */
+  int n_stages;                    /* len(depths) */
+  int ratios[VV_MAX_STAGES];       /* decoder order: [8,5,5,4,2,2] */
+  int dec_depths[VV_MAX_STAGES];   /* [8,3,3,3,3,3,3] */
+  int enc_depths[VV_MAX_STAGES];   /* [3,3,3,3,3,3,8] */
+  int dec_n_filters, sem_n_filters, ac_enc_n_filters;
+  int semantic_dim;                /* 128 */
+  float codec_eps;
+  /* capacity */
+  int max_batch;                   /* samples (LM rows = 2 * max_batch) */
+  int max_ctx;                     /* KV positions per LM row */
+} vv_config;
+
+const char* vv_last_error(void);
+int vv_create(const vv_config* cfg, int device, vv_ctx** out);
+void vv_destroy(vv_ctx* ctx);
+
+/* Borrow a device weight under an engine name (see vibevoice_amd/weights.py
+ * for the name list and the packing applied to the reference's tensors). */
+int vv_bind_weight(vv_ctx* ctx, const char* name, const void* dev_ptr, const int64_t* shape, int ndim);
+/* Check every required weight is bound; allocate KV / codec state / workspaces. */
+int vv_finalize(vv_ctx* ctx);
+
+/* ids of the constrained vocabulary (speech_start, speech_end, diffusion, eos). */
+int vv_set_valid_ids(vv_ctx* ctx, int n, const int* host_ids);
+
+/* Diffusion schedule for `steps` steps.  coef: host float[steps * 8] =
+ * {alpha_s, sigma_s, c_x, c_d0, c_d1, inv_r0, order, 0} per step; tfreq: device
+ * bf16[steps, 256] sinusoidal timestep features. */
+int vv_set_schedule(vv_ctx* ctx, int steps, const float* coef, const void* tfreq, vv_stream st);
+
+/* Token rows through the Qwen2 decoder.  Token i has KV slot slot[i] and
+ * position pos[i]; its K/V are written at cache index pos[i] of that slot and
+ * it attends to cache entries [0, pos[i]].  max_pos_p1 = 1 + max(pos).
+ * For the nout rows listed in out_idx the final-norm hidden state is written to
+ * hidden_out[nout, H] and the valid-id logits to logits_out[nout, n_valid]. */
+int vv_lm_forward(vv_ctx* ctx, int ntok, const void* embeds, const int* slot, const int* pos, int max_pos_p1,
+                  int nout, const int* out_idx, void* hidden_out, float* logits_out, vv_stream st);
+
+/* embeds_out[i] = embed_tokens[ids[i]] */
+int vv_embed(vv_ctx* ctx, int n, const int* ids, void* embeds_out, vv_stream st);
+
+/* n samples: pos_h, neg_h [n, H] conditions; x_io [n, latent] holds the first n
+ * rows of the noise draw on entry and the denoised latent on return. */
+int vv_diffusion_sample(vv_ctx* ctx, int n, const void* pos_h, const void* neg_h, void* x_io, float cfg_scale,
+                        vv_stream st);
+
+/* One streaming codec step for n samples in codec slots slots[n]:
+ * latent [n, latent] -> audio_out [n, hop]; semantic features -> sem_out
+ * [n, semantic_dim] (may be NULL); acoustic_connector(latent) +
+ * semantic_connector(sem) -> row embed_rows[i] of embeds_out [*, H]. */
+int vv_codec_step(vv_ctx* ctx, int n, const int* slots, const void* latent, void* audio_out, void* sem_out,
+                  void* embeds_out, const int* embed_rows, vv_stream st);
+int vv_codec_reset(vv_ctx* ctx, int n, const int* slots, vv_stream st);
+
+/* Non-streaming acoustic encoder over nv voice prompts of L samples (zero
+ * padded): audio [nv, L] bf16 -> mean_out [nv, ceil(L/hop), latent] bf16. */
+int vv_acoustic_encode(vv_ctx* ctx, int nv, int L, const void* audio, void* mean_out, vv_stream st);
+
+/* z = mean + std[v]*noise; feat = (z + bias) * scale   (rows = nv * frames) */
+int vv_vae_features(vv_ctx* ctx, int nv, int frames, const void* mean, const void* stdv, const void* noise,
+                    void* feat_out, vv_stream st);
+
+/* which: 0 = acoustic connector (in = latent), 1 = semantic connector. */
+int vv_connector(vv_ctx* ctx, int which, int n, const void* x, void* out, vv_stream st);
+
+/* dst[idx[i]] = src[i] for bf16 rows of C elements (row strides in elements). */
+int vv_scatter_rows(vv_ctx* ctx, int n, int C, const void* src, int64_t lds, const int* idx, void* dst,
+                    int64_t ldd, vv_stream st);
+
+/* Low-level kernel entry points (used by the parity tests). */
+int vv_gemm_bf16(int M, int N, int K, const void* A, int64_t lda, const void* W, const void* bias, int epi,
+                 void* Y, int64_t ldy, const void* res, const void* gamma, vv_ctx* ws_ctx, vv_stream st);
+int vv_rmsnorm_bf16(int M, int C, const void* x, int64_t ldx, const void* w, float eps, void* y, int64_t ldy,
+                    vv_stream st);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,74 @@
+"""Streaming σ-VAE codec step on the GPU (vv_codec_step / vv_codec_reset) vs
+the CPU oracle at the real 1.5B codec shapes (acoustic decoder 64 -> 3200
+samples per frame, semantic encoder 3200 -> 128, both connectors).
+
+Covers: per-slot streaming state over several frames, a sample that skips a
+frame (its state must not move), set_to_zero on speech_end, and the
+acoustic+semantic connector sum written into the next-embedding rows.
+Tolerance (bf16 model, 60+ layers deep, different GEMM accumulation order
+than the reference / oracle): rel L2 < 3e-2 and cosine > 0.999.
+"""
+import pytest
+import torch
+
+from gpu_util import cos, rel_err
+from oracle import codec as ocodec
+from oracle import lm as olm
+from tiny import tiny_config
+from vibevoice_amd.engine import Engine
+from vibevoice_amd.weights import synthetic_state_dict
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def sub(sd, prefix):
+    return {k[len(prefix):]: v for k, v in sd.items() if k.startswith(prefix)}
+
+
+def connector(sd, p, x):
+    F = torch.nn.functional
+    y = F.linear(x, sd[p + "fc1.weight"], sd[p + "fc1.bias"])
+    y = olm.rms(y, sd[p + "norm.weight"], 1e-6)
+    return F.linear(y, sd[p + "fc2.weight"], sd[p + "fc2.bias"])
+
+
+def test_codec_stream_real_shapes():
+    cfg = tiny_config(ratios=(8, 5, 5, 4, 2, 2), depths="3-3-3-3-3-3-8", nf=32)
+    sd = synthetic_state_dict(cfg, seed=3, device="cpu", mode="test", with_acoustic_encoder=False)
+    eng = Engine(cfg, sd, dev, max_batch=3, max_ctx=64)
+    hop = cfg.hop
+    H = cfg.decoder_config.hidden_size
+    dd = ocodec.codec_dims(cfg.acoustic_tokenizer_config, "decoder")
+    ed = ocodec.codec_dims(cfg.semantic_tokenizer_config, "encoder")
+    sd_a, sd_s = sub(sd, "model.acoustic_tokenizer."), sub(sd, "model.semantic_tokenizer.")
+    st_a, st_s = ocodec.StreamState(3), ocodec.StreamState(3)
+    s_f, b_f = sd["model.speech_scaling_factor"], sd["model.speech_bias_factor"]
+    g = torch.Generator().manual_seed(5)
+    sched = [[0, 2], [0, 2], [2], [0, 1, 2]]
+    worst = []
+    for step, slots in enumerate(sched):
+        n = len(slots)
+        lat = torch.randn(n, 64, generator=g).bfloat16()
+        # --- GPU
+        d_slots = torch.tensor(slots, dtype=torch.int32, device=dev)
+        audio = torch.empty(n, hop, dtype=torch.bfloat16, device=dev)
+        sem = torch.empty(n, 128, dtype=torch.bfloat16, device=dev)
+        emb = torch.zeros(3, H, dtype=torch.bfloat16, device=dev)
+        eng.codec_step(d_slots, lat.to(dev), audio, sem, emb, d_slots)
+        # --- oracle (modeling_vibevoice_inference.py:651-687)
+        idx = torch.tensor(slots)
+        z = (lat / s_f - b_f).unsqueeze(-1)
+        a_ref = ocodec.decode(sd_a, dd, z, st_a, idx)
+        s_ref = ocodec.encode(sd_s, ed, a_ref, st_s, idx)[:, 0]
+        e_ref = connector(sd, "model.acoustic_connector.", lat) + connector(sd, "model.semantic_connector.", s_ref)
+        torch.cuda.synchronize()
+        for name, got, ref in (("audio", audio, a_ref[:, 0]), ("sem", sem, s_ref), ("emb", emb[idx.to(dev)], e_ref)):
+            e, c = rel_err(got, ref), cos(got, ref)
+            worst.append((step, name, e, c))
+            print(f"step {step} {name}: rel_err {e:.3e} cos {c:.6f}")
+            assert e < 3e-2 and c > 0.999, (step, name, e, c)
+        if step == 1:   # speech_end for slot 0 (set_to_zero, :556-560)
+            eng.codec_reset(torch.tensor([0], dtype=torch.int32, device=dev))
+            st_a.zero(torch.tensor([0]))
+            st_s.zero(torch.tensor([0]))

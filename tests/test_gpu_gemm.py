@@ -1,0 +1,80 @@
+"""GEMM / GEMV kernel family (csrc/gemm.hip) vs a plain PyTorch fp32 reference.
+
+Tolerance: the kernels accumulate in fp32 and round once to bf16, so the
+result must match fp32(A)·fp32(W)^T rounded to bf16 within 1 bf16 ulp-ish
+(rel L2 < 4e-3).
+"""
+import ctypes
+
+import pytest
+import torch
+
+from gpu_util import max_rel, rel_err
+from vibevoice_amd import _lib
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def P(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def run(M, N, K, epi, bias=True, res=False, gamma=False, ws_ctx=None):
+    g = torch.Generator(device=dev).manual_seed(M * 7 + N + K)
+    A = torch.randn(M, K, device=dev, generator=g).bfloat16()
+    W = (torch.randn(N, K, device=dev, generator=g) / K ** 0.5).bfloat16()
+    b = (0.1 * torch.randn(N, device=dev, generator=g)).bfloat16() if bias else None
+    outN = N // 2 if epi == "silu_mul" else N
+    Y = torch.empty(M, outN, device=dev, dtype=torch.float32 if epi == "f32" else torch.bfloat16)
+    R = torch.randn(M, outN, device=dev, generator=g).bfloat16() if res else None
+    G = torch.randn(outN, device=dev, generator=g).bfloat16() if gamma else None
+    rc = _lib.lib().vv_gemm_bf16(M, N, K, P(A), K, P(W), P(b), _lib.EPI[epi], P(Y), outN, P(R), P(G), ws_ctx,
+                                 ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    _lib.check(rc, "gemm")
+    torch.cuda.synchronize()
+    acc = A.float() @ W.float().t()
+    if b is not None:
+        acc = acc + b.float()
+    if epi == "store":
+        ref = acc.bfloat16()
+    elif epi == "f32":
+        ref = acc
+    elif epi == "gelu":
+        ref = torch.nn.functional.gelu(acc.bfloat16().float()).bfloat16()
+    elif epi == "silu_mul":
+        a = acc.view(M, N // 16, 2, 8)
+        gate, up = a[:, :, 0].reshape(M, N // 2), a[:, :, 1].reshape(M, N // 2)
+        ref = (torch.nn.functional.silu(gate.bfloat16().float()).bfloat16().float() * up.bfloat16().float()).bfloat16()
+    else:
+        y = acc.bfloat16().float()
+        if G is not None:
+            y = (y * G.float()).bfloat16().float()
+        ref = (R.float() + y).bfloat16()
+    return Y, ref
+
+
+@pytest.mark.parametrize("M", [1, 2, 5, 16, 17, 33, 64])
+@pytest.mark.parametrize("N,K", [(1536, 1536), (2048, 1536), (1536, 8960), (64, 1536), (1536, 64), (128, 448)])
+def test_gemv_store(M, N, K):
+    Y, ref = run(M, N, K, "store")
+    assert rel_err(Y, ref) < 4e-3 and max_rel(Y, ref) < 2e-2
+
+
+@pytest.mark.parametrize("M", [65, 200, 3200])
+@pytest.mark.parametrize("N,K", [(128, 32), (32, 128), (512, 128), (64, 256), (2048, 1536)])
+def test_tiled_store(M, N, K):
+    Y, ref = run(M, N, K, "store")
+    assert rel_err(Y, ref) < 4e-3
+
+
+@pytest.mark.parametrize("M", [2, 16, 300])
+@pytest.mark.parametrize("epi", ["gelu", "silu_mul", "f32", "res"])
+def test_epilogues(M, epi):
+    Y, ref = run(M, 1024, 512, epi, bias=epi != "silu_mul", res=epi == "res", gamma=epi == "res")
+    assert rel_err(Y, ref) < 5e-3
+
+
+def test_shape_rejected():
+    with pytest.raises(RuntimeError):
+        run(4, 100, 64, "store")

@@ -1,0 +1,100 @@
+"""Qwen2 decoder rows on the GPU (vv_lm_forward): compacted per-row KV cache,
+RoPE, GQA attention (single and split-K), SwiGLU, final norm, restricted lm_head.
+
+Pinned against the reference's Qwen2 golden (g7: left-padded prefill + 3 decode
+steps, bf16) and against the CPU oracle at the 1.5B layer shapes (12 q / 2 kv
+heads, H 1536, I 8960) with contexts beyond one attention split (256 keys).
+Tolerance: rel L2 < 2e-2, cosine > 0.999 (bf16 model).
+"""
+import pytest
+import torch
+
+from golden_io import load, t, weights
+from gpu_util import cos, rel_err
+from oracle import lm as olm
+from tiny import tiny_config
+from vibevoice_amd.engine import Engine
+from vibevoice_amd.weights import synthetic_state_dict
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+I32 = dict(dtype=torch.int32, device=dev)
+
+
+def make_engine(cfg, lm_sd=None, seed=0, max_batch=2, max_ctx=1024):
+    sd = synthetic_state_dict(cfg, seed=seed, device="cpu", mode="test", with_acoustic_encoder=False)
+    if lm_sd is not None:
+        for k, v in lm_sd.items():
+            sd["model.language_model." + k] = v
+        sd["lm_head.weight"] = sd["model.language_model.embed_tokens.weight"]
+    eng = Engine(cfg, sd, dev, max_batch=max_batch, max_ctx=max_ctx, valid_ids=[151643, 151652, 151653, 151654])
+    return eng, sd
+
+
+def test_lm_vs_reference_golden():
+    z = load("g7_qwen2.npz")
+    cfg = tiny_config(hidden=256, layers=2, heads=2, kv_heads=1, inter=512)
+    lm_sd = weights(z, dtype=torch.bfloat16)
+    lm_sd.pop("embed_tokens.weight")
+    eng, _ = make_engine(cfg, lm_sd)
+    emb = t(z, "emb_bf16", torch.bfloat16)
+    steps = t(z, "steps_bf16", torch.bfloat16)
+    mask = torch.from_numpy(z["mask0"]).bool()
+    ref = t(z, "hidden_bf16")
+    keep = [emb[r][mask[r]] for r in range(2)]
+    lens = [k.shape[0] for k in keep]
+    x = torch.cat(keep).to(dev)
+    slots = torch.cat([torch.full((n,), r) for r, n in enumerate(lens)]).to(**I32)
+    pos = torch.cat([torch.arange(n) for n in lens]).to(**I32)
+    out_idx = torch.tensor([lens[0] - 1, lens[0] + lens[1] - 1]).to(**I32)
+    h, _ = eng.lm_forward(x, slots, pos, out_idx)
+    torch.cuda.synchronize()
+    print("prefill", rel_err(h, ref[0]), cos(h, ref[0]))
+    assert rel_err(h, ref[0]) < 2e-2 and cos(h, ref[0]) > 0.999
+    L = torch.tensor(lens)
+    for s in range(3):
+        h, _ = eng.lm_forward(steps[s, :, 0].contiguous().to(dev), torch.arange(2).to(**I32), L.to(**I32),
+                              torch.arange(2).to(**I32))
+        L += 1
+        torch.cuda.synchronize()
+        print("step", s, rel_err(h, ref[s + 1]), cos(h, ref[s + 1]))
+        assert rel_err(h, ref[s + 1]) < 2e-2 and cos(h, ref[s + 1]) > 0.999
+
+
+def oracle_sd(sd):
+    return {k[len("model.language_model."):]: v for k, v in sd.items() if k.startswith("model.language_model.")}
+
+
+@pytest.mark.parametrize("ctx", [40, 600])
+def test_lm_real_shapes_vs_oracle(ctx):
+    cfg = tiny_config(hidden=1536, layers=2, heads=12, kv_heads=2, inter=8960)
+    eng, sd = make_engine(cfg, seed=1, max_batch=2, max_ctx=1024)
+    lcfg = dict(cfg.decoder_config)
+    osd = oracle_sd(sd)
+    g = torch.Generator().manual_seed(ctx)
+    lens = [ctx, ctx // 3 + 1]
+    xs = [torch.randn(n, 1536, generator=g).bfloat16() for n in lens]
+    kvs = [olm.RowKV(2) for _ in lens]
+    ref = torch.stack([olm.forward_rows(osd, lcfg, xs[r][None], kvs[r:r + 1])[0, -1] for r in range(2)])
+    x = torch.cat(xs).to(dev)
+    slots = torch.cat([torch.full((n,), r) for r, n in enumerate(lens)]).to(**I32)
+    pos = torch.cat([torch.arange(n) for n in lens]).to(**I32)
+    out_idx = torch.tensor([lens[0] - 1, sum(lens) - 1]).to(**I32)
+    h, logits = eng.lm_forward(x, slots, pos, out_idx)
+    torch.cuda.synchronize()
+    print("prefill", rel_err(h, ref), cos(h, ref))
+    assert rel_err(h, ref) < 2e-2 and cos(h, ref) > 0.999
+    # restricted lm_head: bf16(h . W[id]) for the 4 valid ids
+    W = sd["lm_head.weight"]
+    lref = (h.float().cpu() @ W[[151643, 151652, 151653, 151654]].float().t()).bfloat16().float()
+    assert torch.allclose(logits.cpu(), lref, rtol=1e-2, atol=1e-2 * lref.abs().max().item())
+    # decode steps: both rows, positions continue after their prompts
+    L = torch.tensor(lens)
+    for s in range(3):
+        step_x = torch.randn(2, 1536, generator=g).bfloat16()
+        ref = olm.forward_rows(osd, lcfg, step_x[:, None], kvs)[:, -1]
+        h, _ = eng.lm_forward(step_x.to(dev), torch.arange(2).to(**I32), L.to(**I32), torch.arange(2).to(**I32))
+        L += 1
+        torch.cuda.synchronize()
+        print("step", s, rel_err(h, ref), cos(h, ref))
+        assert rel_err(h, ref) < 2e-2 and cos(h, ref) > 0.999

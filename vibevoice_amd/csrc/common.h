@@ -1,0 +1,77 @@
+// Shared device helpers for the VibeVoice MI355X (gfx950) kernels.
+//
+// Storage type is bf16 (__bf16); arithmetic is fp32.  `rb()` rounds a float to
+// bf16 and back: the reference runs a bf16 model on the GPU
+// (demo/inference_from_file.py:265) where every torch op rounds its output to
+// bf16, so kernels call rb() exactly where a torch op boundary sits in the
+// reference and keep fp32 everywhere else.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define DEV __device__ __forceinline__
+
+DEV float bf(bf16 x) { return (float)x; }
+DEV bf16 tobf(float x) { return (bf16)x; }
+DEV float rb(float x) { return (float)(bf16)x; }
+
+DEV float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+// GELU, exact erf form (transformers ACT2FN["gelu"]; modular_vibevoice_tokenizer.py:589)
+DEV float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// Row addressing shared by every kernel that reads or writes "rows".
+// Logical row m belongs to group g = m / T (a sample), row t = m % T inside it.
+// The group's storage slot is idx[g] when idx != nullptr (streaming state is
+// kept per sample slot), else g.  Offsets are in elements.
+struct RowMap {
+  void* base;
+  long long sB;   // elements between slots
+  long long sT;   // elements between rows of one slot
+  int T;          // rows per group
+  int pad_;
+  const int* idx; // device int[groups] or nullptr
+};
+
+DEV long long rm_off(const RowMap& r, int m) {
+  int g = m / r.T;
+  int t = m - g * r.T;
+  long long s = r.idx ? (long long)r.idx[g] : (long long)g;
+  return s * r.sB + (long long)t * r.sT;
+}
+DEV const bf16* rm_bf(const RowMap& r, int m) { return (const bf16*)r.base + rm_off(r, m); }
+DEV bf16* rm_bfw(const RowMap& r, int m) { return (bf16*)r.base + rm_off(r, m); }
+
+// Epilogues (what a GEMM does with acc = sum_k A[m,k] W[n,k]):
+enum {
+  EPI_STORE = 0,     // y = bf16(acc + bias)
+  EPI_GELU = 1,      // y = bf16(gelu(bf16(acc + bias)))
+  EPI_SILU_MUL = 2,  // W rows packed [gate 8 | up 8] per 16: y = bf16(bf16(silu(bf16 g)) * bf16 u)
+  EPI_RES = 3,       // y = bf16(res + bf16(s * bf16(acc + bias)))  s: none / gamma[n] / gate[m,n]
+  EPI_F32 = 4,       // y(float) = acc + bias
+};
+
+struct EpiArgs {
+  int kind;
+  int pad_;
+  const bf16* bias;     // [N] or nullptr
+  RowMap out;           // bf16 (float for EPI_F32)
+  RowMap res;           // residual rows (EPI_RES), may alias out
+  const bf16* gamma;    // [N] per-column scale (EPI_RES) or nullptr
+  RowMap gate;          // per-(m,n) scale (EPI_RES) when gate.base != nullptr
+};

@@ -1,0 +1,905 @@
+// libvibevoice_hip.so — native engine for VibeVoice's generate loop on MI355X.
+//
+// Owns: borrowed weight pointers, the compacted LM KV cache, per-slot streaming
+// conv state of the acoustic decoder and semantic encoder, workspaces, and the
+// diffusion schedule.  Every entry point only enqueues kernels on the caller's
+// stream (no host sync, no allocation after vv_finalize except the grow-only
+// prefill / voice-prompt workspaces).  C ABI: include/vibevoice_hip.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/vibevoice_hip.h"
+#include "kernels.h"
+
+static thread_local std::string g_err;
+
+#define FAIL(msg)        \
+  do {                   \
+    g_err = (msg);       \
+    return -1;           \
+  } while (0)
+#define HIPCHK(x)                                                                 \
+  do {                                                                            \
+    hipError_t e_ = (x);                                                          \
+    if (e_ != hipSuccess) {                                                       \
+      g_err = std::string(#x) + ": " + hipGetErrorString(e_);                     \
+      return -1;                                                                  \
+    }                                                                             \
+  } while (0)
+#define KCHK(x)                                                                   \
+  do {                                                                            \
+    int r_ = (x);                                                                 \
+    if (r_) {                                                                     \
+      g_err = std::string("kernel launch rejected (") + std::to_string(r_) + "): " + #x; \
+      return -1;                                                                  \
+    }                                                                             \
+  } while (0)
+#define CHK(x)          \
+  do {                  \
+    if ((x) != 0) return -1; \
+  } while (0)
+
+namespace {
+
+struct Weight {
+  const void* p = nullptr;
+  std::vector<int64_t> shape;
+};
+
+// Per-slot conv input buffer: [ctx history rows | rows of this step (+ zero pad)] x C
+struct ConvBuf {
+  bf16* base = nullptr;
+  long long sB = 0;  // elements per slot
+  int ctx = 0, T = 0, C = 0, rows = 0;
+};
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t b) {
+    if (b <= bytes) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    if (hipMalloc(&p, b) != hipSuccess) {
+      g_err = "hipMalloc failed (" + std::to_string(b) + " bytes)";
+      return -1;
+    }
+    bytes = b;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
+// One causal conv stack of the σ-VAE codec (acoustic decoder, or an encoder),
+// laid out for `slots` sample slots and `T0` input rows per call.
+struct ConvNet {
+  bool decoder = true;
+  std::string wp;             // weight-name prefix: "dec", "sem", "aenc"
+  int nst = 0;
+  int depth[VV_MAX_STAGES] = {}, chans[VV_MAX_STAGES] = {}, rat[VV_MAX_STAGES] = {}, T[VV_MAX_STAGES] = {};
+  int in_ch = 0, out_ch = 0, T0 = 0, slots = 0, nmax = 0;
+  int Tin[VV_MAX_STAGES] = {};  // rows entering the strided conv before stage i (encoder)
+  ConvBuf stem, head;
+  std::vector<std::vector<ConvBuf>> mix;
+  ConvBuf tr[VV_MAX_STAGES];
+  DevBuf state;               // all ConvBufs
+  DevBuf work;                // X stages + A + F
+  bf16* X[VV_MAX_STAGES] = {};
+  bf16* A = nullptr;
+  bf16* F = nullptr;
+  std::vector<RollDesc> rolls;
+  DevBuf d_rolls;
+};
+
+}  // namespace
+
+struct vv_ctx {
+  vv_config cfg;
+  int device = 0;
+  std::unordered_map<std::string, Weight> w;
+  bool finalized = false;
+  // LM
+  int qkv_n = 0, lm_slots = 0;
+  DevBuf kv_k, kv_v;
+  KVLayout kv;
+  DevBuf lm_ws;  // h, a, qkv, q, att, act
+  size_t lm_ws_tokens = 0;
+  DevBuf attn_part;
+  DevBuf valid_ids;
+  int n_valid = 0;
+  // split-K
+  DevBuf splitk_ws, splitk_cnt;
+  // diffusion
+  int steps = 0;
+  std::vector<DpmCoef> coef;
+  DevBuf temb, tfreq_tmp;
+  DevBuf head_ws;
+  // codec
+  ConvNet dec, sem, aenc;
+  DevBuf codec_ws;  // connectors
+  DevBuf slot_scratch;
+};
+
+// ------------------------------------------------------------------ helpers
+static const bf16* W(vv_ctx* c, const std::string& n) {
+  auto it = c->w.find(n);
+  if (it == c->w.end()) return nullptr;
+  return (const bf16*)it->second.p;
+}
+
+static int need(vv_ctx* c, const std::string& n, const std::vector<int64_t>& shape) {
+  auto it = c->w.find(n);
+  if (it == c->w.end()) FAIL("missing weight: " + n);
+  if (!shape.empty() && it->second.shape != shape) {
+    std::string s = "shape mismatch for " + n + ": got [";
+    for (auto v : it->second.shape) s += std::to_string(v) + ",";
+    s += "] want [";
+    for (auto v : shape) s += std::to_string(v) + ",";
+    FAIL(s + "]");
+  }
+  return 0;
+}
+
+static GemmArgs gemm_args(vv_ctx* c, int M, int N, int K, RowMap a, const bf16* w, int epi, RowMap out,
+                          const bf16* bias = nullptr) {
+  GemmArgs g;
+  memset(&g, 0, sizeof(g));
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.ksplit = 1;
+  g.a = a;
+  g.w = w;
+  g.ldw = K;
+  g.epi.kind = epi;
+  g.epi.bias = bias;
+  g.epi.out = out;
+  g.ws = (float*)c->splitk_ws.p;
+  g.counters = (unsigned*)c->splitk_cnt.p;
+  return g;
+}
+
+static int gemm(vv_ctx* c, GemmArgs g, hipStream_t st) {
+  if (!g.w) FAIL("gemm: null weight");
+  KCHK(launch_gemm(g, st));
+  return 0;
+}
+
+static int rmsnorm(int M, int C, RowMap in, RowMap out, const bf16* w, float eps, hipStream_t st,
+                   const bf16* mod = nullptr, long long mod_ld = 0, int shift_off = 0, int scale_off = 0) {
+  NormArgs a;
+  memset(&a, 0, sizeof(a));
+  a.M = M;
+  a.C = C;
+  a.eps = eps;
+  a.in = in;
+  a.out = out;
+  a.w = w;
+  a.has_mod = mod != nullptr;
+  a.mod = mod;
+  a.mod_ld = mod_ld;
+  a.shift_off = shift_off;
+  a.scale_off = scale_off;
+  KCHK(launch_rmsnorm(a, st));
+  return 0;
+}
+
+// ------------------------------------------------------------------ codec layout
+static void convnet_shape(vv_ctx* c, ConvNet& n, bool decoder, const std::string& wp, int nf, int in_ch, int out_ch,
+                          int T0, int slots) {
+  const vv_config& k = c->cfg;
+  n.decoder = decoder;
+  n.wp = wp;
+  n.nst = k.n_stages;
+  n.in_ch = in_ch;
+  n.out_ch = out_ch;
+  n.T0 = T0;
+  n.slots = slots;
+  n.nmax = slots;
+  for (int i = 0; i < n.nst; ++i) {
+    if (decoder) {
+      n.depth[i] = k.dec_depths[i];
+      n.chans[i] = nf << (n.nst - 1 - i);
+      n.rat[i] = i == 0 ? 1 : k.ratios[i - 1];
+      n.T[i] = i == 0 ? T0 : n.T[i - 1] * n.rat[i];
+      n.Tin[i] = i == 0 ? T0 : n.T[i - 1];
+    } else {
+      n.depth[i] = k.enc_depths[i];
+      n.chans[i] = nf << i;
+      n.rat[i] = i == 0 ? 1 : k.ratios[n.nst - 1 - i];  // encoder ratios are reversed
+      n.Tin[i] = i == 0 ? T0 : n.T[i - 1];
+      n.T[i] = i == 0 ? T0 : (n.T[i - 1] + n.rat[i] - 1) / n.rat[i];
+    }
+  }
+}
+
+static int convnet_alloc(ConvNet& n, int kernel) {
+  // layout the per-slot buffers
+  std::vector<ConvBuf*> all;
+  size_t total = 0;
+  auto add = [&](ConvBuf& b, int ctx, int T, int rows_pad, int C) {
+    b.ctx = ctx;
+    b.T = T;
+    b.C = C;
+    b.rows = ctx + rows_pad;
+    b.sB = (long long)b.rows * C;
+    all.push_back(&b);
+    total += (size_t)b.sB * n.slots;
+  };
+  add(n.stem, kernel - 1, n.T0, n.T0, n.in_ch);
+  n.mix.assign(n.nst, {});
+  for (int i = 0; i < n.nst; ++i) {
+    if (i > 0) {
+      if (n.decoder) {
+        add(n.tr[i], 1, n.Tin[i], n.Tin[i], n.chans[i - 1]);
+      } else {
+        const int s = n.rat[i];
+        add(n.tr[i], s, n.Tin[i], n.T[i] * s, n.chans[i - 1]);
+      }
+    }
+    n.mix[i].resize(n.depth[i]);
+    for (int j = 0; j < n.depth[i]; ++j) add(n.mix[i][j], kernel - 1, n.T[i], n.T[i], n.chans[i]);
+  }
+  add(n.head, kernel - 1, n.T[n.nst - 1], n.T[n.nst - 1], n.chans[n.nst - 1]);
+  CHK(n.state.ensure(total * sizeof(bf16)));
+  HIPCHK(hipMemset(n.state.p, 0, total * sizeof(bf16)));
+  bf16* p = (bf16*)n.state.p;
+  n.rolls.clear();
+  for (ConvBuf* b : all) {
+    b->base = p;
+    p += (size_t)b->sB * n.slots;
+    RollDesc r;
+    r.base = b->base;
+    r.sB = b->sB;
+    r.ctx = b->ctx;
+    r.T = b->T;
+    r.C = b->C;
+    r.pad_ = 0;
+    n.rolls.push_back(r);
+  }
+  CHK(n.d_rolls.ensure(n.rolls.size() * sizeof(RollDesc)));
+  HIPCHK(hipMemcpy(n.d_rolls.p, n.rolls.data(), n.rolls.size() * sizeof(RollDesc), hipMemcpyHostToDevice));
+  // transient work: X per stage + A (normed rows) + F (ffn hidden)
+  size_t xw = 0, aw = 0, fw = 0;
+  for (int i = 0; i < n.nst; ++i) {
+    xw += (size_t)n.T[i] * n.chans[i];
+    aw = std::max(aw, (size_t)n.T[i] * n.chans[i]);
+    fw = std::max(fw, (size_t)n.T[i] * n.chans[i] * 4);
+  }
+  const size_t per = xw + aw + fw;
+  CHK(n.work.ensure(per * n.nmax * sizeof(bf16)));
+  bf16* q = (bf16*)n.work.p;
+  for (int i = 0; i < n.nst; ++i) {
+    n.X[i] = q;
+    q += (size_t)n.T[i] * n.chans[i] * n.nmax;
+  }
+  n.A = q;
+  q += aw * n.nmax;
+  n.F = q;
+  return 0;
+}
+
+static int convnet_check(vv_ctx* c, ConvNet& n) {
+  const std::string& p = n.wp;
+  const int k = 7;
+  if (n.decoder) {
+    CHK(need(c, p + ".stem_w", {n.chans[0], (int64_t)k * n.in_ch}));
+  } else {
+    CHK(need(c, p + ".stem_w", {n.chans[0], (int64_t)k}));
+  }
+  CHK(need(c, p + ".stem_b", {n.chans[0]}));
+  for (int i = 0; i < n.nst; ++i) {
+    const int C = n.chans[i];
+    if (i > 0) {
+      const std::string t = p + ".tr" + std::to_string(i);
+      const int Ci = n.chans[i - 1], r = n.rat[i];
+      if (n.decoder) {
+        CHK(need(c, t + "_w", {(int64_t)r * C, 2LL * Ci}));
+        CHK(need(c, t + "_b", {(int64_t)r * C}));
+      } else {
+        CHK(need(c, t + "_w", {C, 2LL * r * Ci}));
+        CHK(need(c, t + "_b", {C}));
+      }
+    }
+    for (int j = 0; j < n.depth[i]; ++j) {
+      const std::string b = p + ".s" + std::to_string(i) + ".b" + std::to_string(j);
+      CHK(need(c, b + ".dw_w", {C, k}));
+      CHK(need(c, b + ".dw_b", {C}));
+      CHK(need(c, b + ".gamma", {C}));
+      CHK(need(c, b + ".fc1_w", {4LL * C, C}));
+      CHK(need(c, b + ".fc1_b", {4LL * C}));
+      CHK(need(c, b + ".fc2_w", {C, 4LL * C}));
+      CHK(need(c, b + ".fc2_b", {C}));
+      CHK(need(c, b + ".ffn_gamma", {C}));
+    }
+  }
+  const int Cl = n.chans[n.nst - 1];
+  if (n.decoder) {
+    CHK(need(c, p + ".head_w", {k, Cl}));
+    CHK(need(c, p + ".head_b", {1}));
+  } else {
+    CHK(need(c, p + ".head_w", {n.out_ch, (int64_t)k * Cl}));
+    CHK(need(c, p + ".head_b", {n.out_ch}));
+  }
+  return 0;
+}
+
+// Rows of ConvBuf b, starting after its history, for the active samples (slot map).
+static RowMap buf_in_rows(const ConvBuf& b, int T, const int* slots) {
+  return rowmap(b.base + (long long)b.ctx * b.C, b.C, T, b.sB, slots);
+}
+
+// One block stack + transitions.  n active samples (slots[n]); input rows already
+// in `stem` (rows [ctx, ctx+T0)).  Decoder: writes audio to out (+ out2).
+// Encoder: writes [n, out_ch] features to out.
+static int convnet_run(vv_ctx* c, ConvNet& net, int n, const int* slots, RowMap out, RowMap out2, hipStream_t st) {
+  const std::string& p = net.wp;
+  const float eps = c->cfg.codec_eps;
+  const int k = 7;
+  // ---- stem
+  {
+    const int T = net.T[0], C = net.chans[0];
+    RowMap xo = rowmap(net.X[0], C, T, (long long)T * C);
+    if (net.decoder) {
+      RowMap a = rowmap(net.stem.base, net.stem.C, T, net.stem.sB, slots);
+      GemmArgs g = gemm_args(c, n * T, C, k * net.in_ch, a, W(c, p + ".stem_w"), EPI_STORE, xo, W(c, p + ".stem_b"));
+      CHK(gemm(c, g, st));
+    } else {
+      ConvIn1Args a;
+      a.M = n * T;
+      a.C = C;
+      a.K = k;
+      a.buf = rowmap(net.stem.base, 1, T, net.stem.sB, slots);
+      a.w = W(c, p + ".stem_w");
+      a.b = W(c, p + ".stem_b");
+      a.out = xo;
+      KCHK(launch_conv_cin1(a, st));
+    }
+  }
+  for (int i = 0; i < net.nst; ++i) {
+    const int T = net.T[i], C = net.chans[i];
+    RowMap X = rowmap(net.X[i], C, T, (long long)T * C);
+    if (i > 0) {
+      const ConvBuf& tb = net.tr[i];
+      const int Ci = net.chans[i - 1], r = net.rat[i];
+      const std::string t = p + ".tr" + std::to_string(i);
+      if (net.decoder) {
+        // 2-tap ConvTranspose: input row t = buffer rows [t, t+1] (1 history row)
+        RowMap a = rowmap(tb.base, Ci, net.Tin[i], tb.sB, slots);
+        RowMap o = rowmap(net.X[i], (long long)r * C, net.Tin[i], (long long)T * C);
+        GemmArgs g = gemm_args(c, n * net.Tin[i], r * C, 2 * Ci, a, W(c, t + "_w"), EPI_STORE, o, W(c, t + "_b"));
+        CHK(gemm(c, g, st));
+      } else {
+        // strided causal conv, k = 2r, ctx = r: output row t = buffer rows [t*r, t*r + 2r)
+        RowMap a = rowmap(tb.base, (long long)r * Ci, T, tb.sB, slots);
+        GemmArgs g = gemm_args(c, n * T, C, 2 * r * Ci, a, W(c, t + "_w"), EPI_STORE, X, W(c, t + "_b"));
+        CHK(gemm(c, g, st));
+      }
+    }
+    for (int j = 0; j < net.depth[i]; ++j) {
+      const std::string b = p + ".s" + std::to_string(i) + ".b" + std::to_string(j);
+      const ConvBuf& mb = net.mix[i][j];
+      // norm -> mixer buffer (this step's rows), depthwise conv + gamma + residual
+      CHK(rmsnorm(n * T, C, X, buf_in_rows(mb, T, slots), W(c, b + ".norm"), eps, st));
+      DwArgs d;
+      d.M = n * T;
+      d.C = C;
+      d.T = T;
+      d.K = k;
+      d.buf = rowmap(mb.base, C, T, mb.sB, slots);
+      d.x = X;
+      d.w = W(c, b + ".dw_w");
+      d.b = W(c, b + ".dw_b");
+      d.gamma = W(c, b + ".gamma");
+      KCHK(launch_dwconv(d, st));
+      // ffn
+      RowMap Am = rowmap(net.A, C);
+      RowMap Fm = rowmap(net.F, 4LL * C);
+      CHK(rmsnorm(n * T, C, X, Am, W(c, b + ".ffn_norm"), eps, st));
+      CHK(gemm(c, gemm_args(c, n * T, 4 * C, C, Am, W(c, b + ".fc1_w"), EPI_GELU, Fm, W(c, b + ".fc1_b")), st));
+      RowMap o = X;
+      const bool last = j == net.depth[i] - 1;
+      if (last) {
+        const ConvBuf& nb = (i + 1 < net.nst) ? net.tr[i + 1] : net.head;
+        o = buf_in_rows(nb, T, slots);
+      }
+      GemmArgs g = gemm_args(c, n * T, C, 4 * C, Fm, W(c, b + ".fc2_w"), EPI_RES, o, W(c, b + ".fc2_b"));
+      g.epi.res = X;
+      g.epi.gamma = W(c, b + ".ffn_gamma");
+      CHK(gemm(c, g, st));
+    }
+  }
+  // ---- head (disable_last_norm: no final norm, modular_vibevoice_tokenizer.py:908-911)
+  const int Tl = net.T[net.nst - 1], Cl = net.chans[net.nst - 1];
+  if (net.decoder) {
+    Conv1Args a;
+    a.M = n * Tl;
+    a.C = Cl;
+    a.K = k;
+    a.buf = rowmap(net.head.base, Cl, Tl, net.head.sB, slots);
+    a.w = W(c, p + ".head_w");
+    a.b = W(c, p + ".head_b");
+    a.out = out;
+    a.out2 = out2;
+    KCHK(launch_conv_cout1(a, st));
+  } else {
+    RowMap a = rowmap(net.head.base, Cl, Tl, net.head.sB, slots);
+    GemmArgs g = gemm_args(c, n * Tl, net.out_ch, k * Cl, a, W(c, p + ".head_w"), EPI_STORE, out, W(c, p + ".head_b"));
+    CHK(gemm(c, g, st));
+  }
+  return 0;
+}
+
+static int convnet_roll(ConvNet& net, int n, const int* slots, int mode, hipStream_t st) {
+  KCHK(launch_roll((const RollDesc*)net.d_rolls.p, (int)net.rolls.size(), slots, n, mode, st));
+  return 0;
+}
+
+// ------------------------------------------------------------------ C ABI
+extern "C" {
+
+const char* vv_last_error(void) { return g_err.c_str(); }
+
+int vv_create(const vv_config* cfg, int device, vv_ctx** out) {
+  if (!cfg || !out) FAIL("vv_create: null argument");
+  if (cfg->head_dim != 128) FAIL("head_dim must be 128");
+  if (cfg->n_stages < 1 || cfg->n_stages > VV_MAX_STAGES) FAIL("n_stages out of range");
+  if (cfg->n_heads % cfg->n_kv_heads || cfg->n_heads / cfg->n_kv_heads > 8) FAIL("unsupported GQA ratio");
+  if (cfg->max_batch < 1 || cfg->max_batch > 32) FAIL("max_batch must be in [1, 32]");
+  HIPCHK(hipSetDevice(device));
+  vv_ctx* c = new vv_ctx();
+  c->cfg = *cfg;
+  c->device = device;
+  *out = c;
+  return 0;
+}
+
+void vv_destroy(vv_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipDeviceSynchronize();
+  DevBuf* bufs[] = {&c->kv_k, &c->kv_v, &c->lm_ws, &c->attn_part, &c->valid_ids, &c->splitk_ws, &c->splitk_cnt,
+                    &c->temb, &c->tfreq_tmp, &c->head_ws, &c->codec_ws, &c->slot_scratch};
+  for (DevBuf* b : bufs) b->release();
+  ConvNet* nets[] = {&c->dec, &c->sem, &c->aenc};
+  for (ConvNet* n : nets) {
+    n->state.release();
+    n->work.release();
+    n->d_rolls.release();
+  }
+  delete c;
+}
+
+int vv_bind_weight(vv_ctx* c, const char* name, const void* p, const int64_t* shape, int ndim) {
+  if (!c || !name || !p) FAIL("vv_bind_weight: null argument");
+  Weight w;
+  w.p = p;
+  w.shape.assign(shape, shape + ndim);
+  c->w[name] = w;
+  return 0;
+}
+
+int vv_set_valid_ids(vv_ctx* c, int n, const int* ids) {
+  if (n < 1 || n > 4) FAIL("vv_set_valid_ids: 1..4 ids");
+  CHK(c->valid_ids.ensure(4 * sizeof(int)));
+  HIPCHK(hipMemcpy(c->valid_ids.p, ids, n * sizeof(int), hipMemcpyHostToDevice));
+  c->n_valid = n;
+  return 0;
+}
+
+int vv_finalize(vv_ctx* c) {
+  const vv_config& k = c->cfg;
+  HIPCHK(hipSetDevice(c->device));
+  const int H = k.hidden, d = k.head_dim;
+  c->qkv_n = (k.n_heads + 2 * k.n_kv_heads) * d;
+  // ---- LM weights
+  CHK(need(c, "lm.embed", {}));
+  CHK(need(c, "lm.lm_head", {}));
+  CHK(need(c, "lm.inv_freq", {d / 2}));
+  CHK(need(c, "lm.norm", {H}));
+  for (int l = 0; l < k.n_layers; ++l) {
+    const std::string p = "lm." + std::to_string(l);
+    CHK(need(c, p + ".in_norm", {H}));
+    CHK(need(c, p + ".qkv_w", {c->qkv_n, H}));
+    CHK(need(c, p + ".qkv_b", {c->qkv_n}));
+    CHK(need(c, p + ".o_w", {H, (int64_t)k.n_heads * d}));
+    CHK(need(c, p + ".post_norm", {H}));
+    CHK(need(c, p + ".gu_w", {2LL * k.intermediate, H}));
+    CHK(need(c, p + ".down_w", {H, k.intermediate}));
+  }
+  // ---- diffusion head
+  const int L = k.head_layers, F = k.head_ffn, D = k.latent_dim;
+  CHK(need(c, "head.noisy_w", {H, D}));
+  CHK(need(c, "head.cond_w", {H, H}));
+  CHK(need(c, "head.t0_w", {H, 256}));
+  CHK(need(c, "head.t2_w", {H, H}));
+  CHK(need(c, "head.ada_w", {(3LL * L + 2) * H, H}));
+  for (int l = 0; l < L; ++l) {
+    const std::string p = "head." + std::to_string(l);
+    CHK(need(c, p + ".norm", {H}));
+    CHK(need(c, p + ".gu_w", {2LL * F, H}));
+    CHK(need(c, p + ".down_w", {H, F}));
+  }
+  CHK(need(c, "head.final_w", {D, H}));
+  // ---- connectors + latent scaling
+  CHK(need(c, "conn.ac.fc1_w", {H, D}));
+  CHK(need(c, "conn.se.fc1_w", {H, k.semantic_dim}));
+  for (const char* q : {"conn.ac", "conn.se"}) {
+    const std::string s(q);
+    CHK(need(c, s + ".fc1_b", {H}));
+    CHK(need(c, s + ".norm", {H}));
+    CHK(need(c, s + ".fc2_w", {H, H}));
+    CHK(need(c, s + ".fc2_b", {H}));
+  }
+  CHK(need(c, "speech_scaling_factor", {}));
+  CHK(need(c, "speech_bias_factor", {}));
+  // ---- codec nets
+  const int hop = [&] {
+    int h = 1;
+    for (int i = 0; i + 1 < k.n_stages; ++i) h *= k.ratios[i];
+    return h;
+  }();
+  convnet_shape(c, c->dec, true, "dec", k.dec_n_filters, D, 1, 1, k.max_batch);
+  convnet_shape(c, c->sem, false, "sem", k.sem_n_filters, 1, k.semantic_dim, hop, k.max_batch);
+  CHK(convnet_check(c, c->dec));
+  CHK(convnet_check(c, c->sem));
+  const bool has_aenc = c->w.count("aenc.stem_w") > 0;
+  if (has_aenc) {
+    convnet_shape(c, c->aenc, false, "aenc", k.ac_enc_n_filters, 1, D, hop, 1);
+    CHK(convnet_check(c, c->aenc));
+  }
+  CHK(convnet_alloc(c->dec, 7));
+  CHK(convnet_alloc(c->sem, 7));
+  // ---- LM KV cache: [layer][slot][kv_head][ctx][d]
+  c->lm_slots = 2 * k.max_batch;
+  c->kv.d = d;
+  c->kv.max_ctx = k.max_ctx;
+  c->kv.s_head = (long long)k.max_ctx * d;
+  c->kv.s_slot = c->kv.s_head * k.n_kv_heads;
+  c->kv.s_layer = c->kv.s_slot * c->lm_slots;
+  const size_t kvb = (size_t)c->kv.s_layer * k.n_layers * sizeof(bf16);
+  CHK(c->kv_k.ensure(kvb));
+  CHK(c->kv_v.ensure(kvb));
+  c->kv.k = (bf16*)c->kv_k.p;
+  c->kv.v = (bf16*)c->kv_v.p;
+  // ---- split-K slabs + tickets
+  CHK(c->splitk_ws.ensure(64ull << 20));
+  CHK(c->splitk_cnt.ensure(65536 * sizeof(unsigned)));
+  HIPCHK(hipMemset(c->splitk_cnt.p, 0, 65536 * sizeof(unsigned)));
+  // ---- diffusion workspace (rows = 2 * max_batch)
+  {
+    const size_t R = 2 * (size_t)k.max_batch;
+    const size_t mod = (3 * (size_t)L + 2) * H;
+    const size_t elems = R * H * 6 + R * mod + R * F + R * D * 3 + (size_t)k.max_batch * D * 2;
+    CHK(c->head_ws.ensure(elems * sizeof(bf16)));
+  }
+  CHK(c->codec_ws.ensure((size_t)k.max_batch * (4 * H + 2 * 256) * sizeof(bf16) + 4096));
+  CHK(c->slot_scratch.ensure(4096));
+  HIPCHK(hipDeviceSynchronize());
+  c->finalized = true;
+  return 0;
+}
+
+int vv_set_schedule(vv_ctx* c, int steps, const float* coef, const void* tfreq, vv_stream vst) {
+  hipStream_t st = (hipStream_t)vst;
+  if (!c->finalized) FAIL("vv_set_schedule before vv_finalize");
+  if (steps < 1 || steps > 1000) FAIL("steps out of range");
+  const int H = c->cfg.hidden;
+  c->coef.resize(steps);
+  for (int s = 0; s < steps; ++s) {
+    const float* q = coef + 8 * s;
+    DpmCoef& e = c->coef[s];
+    e.alpha_s = q[0];
+    e.sigma_s = q[1];
+    e.c_x = q[2];
+    e.c_d0 = q[3];
+    e.c_d1 = q[4];
+    e.inv_r0 = q[5];
+    e.order = (int)q[6];
+    e.cfg = 0.f;
+  }
+  CHK(c->temb.ensure((size_t)steps * H * sizeof(bf16)));
+  CHK(c->tfreq_tmp.ensure((size_t)steps * H * sizeof(bf16)));
+  // t_emb = Linear2(SiLU(Linear0(t_freq)))  (TimestepEmbedder.forward, diffusion_head.py:90-93)
+  bf16* t1 = (bf16*)c->tfreq_tmp.p;
+  CHK(gemm(c, gemm_args(c, steps, H, 256, rowmap(tfreq, 256), W(c, "head.t0_w"), EPI_STORE, rowmap(t1, H)), st));
+  KCHK(launch_silu(steps * H, t1, t1, st));
+  CHK(gemm(c, gemm_args(c, steps, H, H, rowmap(t1, H), W(c, "head.t2_w"), EPI_STORE, rowmap(c->temb.p, H)), st));
+  c->steps = steps;
+  return 0;
+}
+
+int vv_embed(vv_ctx* c, int n, const int* ids, void* out, vv_stream vst) {
+  const int H = c->cfg.hidden;
+  KCHK(launch_gather_rows(n, H, W(c, "lm.embed"), H, ids, rowmap(out, H), (hipStream_t)vst));
+  return 0;
+}
+
+int vv_lm_forward(vv_ctx* c, int ntok, const void* embeds, const int* slot, const int* pos, int max_pos_p1, int nout,
+                  const int* out_idx, void* hidden_out, float* logits_out, vv_stream vst) {
+  hipStream_t st = (hipStream_t)vst;
+  if (!c->finalized) FAIL("vv_lm_forward before vv_finalize");
+  if (ntok <= 0) return 0;
+  if (max_pos_p1 > c->cfg.max_ctx) FAIL("position beyond max_ctx");
+  const vv_config& k = c->cfg;
+  const int H = k.hidden, d = k.head_dim, I = k.intermediate, nhd = k.n_heads * d;
+  // workspace
+  const size_t per = (size_t)H * 3 + c->qkv_n + nhd * 2 + I;
+  if ((size_t)ntok > c->lm_ws_tokens) {
+    CHK(c->lm_ws.ensure(per * ntok * sizeof(bf16) + 256));
+    c->lm_ws_tokens = ntok;
+  }
+  bf16* h = (bf16*)c->lm_ws.p;
+  bf16* a = h + (size_t)ntok * H;
+  bf16* qkv = a + (size_t)ntok * H;
+  bf16* q = qkv + (size_t)ntok * c->qkv_n;
+  bf16* att = q + (size_t)ntok * nhd;
+  bf16* act = att + (size_t)ntok * nhd;
+  bf16* fin = act + (size_t)ntok * I;
+  const int nsplit = attn_nsplit(max_pos_p1);
+  if (nsplit > 1) CHK(c->attn_part.ensure((size_t)ntok * k.n_heads * nsplit * (d + 2) * sizeof(float)));
+  HIPCHK(hipMemcpyAsync(h, embeds, (size_t)ntok * H * sizeof(bf16), hipMemcpyDeviceToDevice, st));
+  RowMap hm = rowmap(h, H), am = rowmap(a, H);
+  for (int l = 0; l < k.n_layers; ++l) {
+    const std::string p = "lm." + std::to_string(l);
+    CHK(rmsnorm(ntok, H, hm, am, W(c, p + ".in_norm"), k.rms_eps, st));
+    CHK(gemm(c, gemm_args(c, ntok, c->qkv_n, H, am, W(c, p + ".qkv_w"), EPI_STORE, rowmap(qkv, c->qkv_n),
+                          W(c, p + ".qkv_b")), st));
+    RopeArgs r;
+    r.R = ntok;
+    r.nh = k.n_heads;
+    r.nkv = k.n_kv_heads;
+    r.layer = l;
+    r.qkv = qkv;
+    r.ld_qkv = c->qkv_n;
+    r.q_out = q;
+    r.slots = slot;
+    r.pos = pos;
+    r.inv_freq = (const float*)c->w["lm.inv_freq"].p;
+    r.kv = c->kv;
+    KCHK(launch_rope_kv(r, st));
+    AttnArgs at;
+    at.nq = ntok;
+    at.nh = k.n_heads;
+    at.nkv = k.n_kv_heads;
+    at.layer = l;
+    at.nsplit = nsplit;
+    at.scale = 1.0f / sqrtf((float)d);
+    at.q = q;
+    at.out = att;
+    at.slots = slot;
+    at.pos = pos;
+    at.kv = c->kv;
+    at.part_o = (float*)c->attn_part.p;
+    at.part_ml = at.part_o ? at.part_o + (size_t)ntok * k.n_heads * nsplit * d : nullptr;
+    KCHK(launch_attn(at, st));
+    GemmArgs g = gemm_args(c, ntok, H, nhd, rowmap(att, nhd), W(c, p + ".o_w"), EPI_RES, hm);
+    g.epi.res = hm;
+    CHK(gemm(c, g, st));
+    CHK(rmsnorm(ntok, H, hm, am, W(c, p + ".post_norm"), k.rms_eps, st));
+    CHK(gemm(c, gemm_args(c, ntok, 2 * I, H, am, W(c, p + ".gu_w"), EPI_SILU_MUL, rowmap(act, I)), st));
+    g = gemm_args(c, ntok, H, I, rowmap(act, I), W(c, p + ".down_w"), EPI_RES, hm);
+    g.epi.res = hm;
+    CHK(gemm(c, g, st));
+  }
+  if (nout > 0) {
+    KCHK(launch_gather_rows(nout, H, h, H, out_idx, rowmap(fin, H), st));
+    CHK(rmsnorm(nout, H, rowmap(fin, H), rowmap(hidden_out, H), W(c, "lm.norm"), k.rms_eps, st));
+    if (logits_out && c->n_valid > 0)
+      KCHK(launch_lmhead_ids(nout, H, (const bf16*)hidden_out, H, W(c, "lm.lm_head"), (const int*)c->valid_ids.p,
+                             c->n_valid, logits_out, st));
+  }
+  return 0;
+}
+
+int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, void* x_io, float cfg_scale,
+                        vv_stream vst) {
+  hipStream_t st = (hipStream_t)vst;
+  if (!c->finalized || c->steps == 0) FAIL("vv_diffusion_sample: engine not finalized or no schedule");
+  if (n <= 0) return 0;
+  const vv_config& k = c->cfg;
+  if (n > k.max_batch) FAIL("vv_diffusion_sample: n > max_batch");
+  const int H = k.hidden, F = k.head_ffn, D = k.latent_dim, L = k.head_layers;
+  const int R = 2 * n;
+  const long long MODW = (3LL * L + 2) * H;
+  bf16* cat = (bf16*)c->head_ws.p;
+  bf16* condp = cat + (size_t)R * H;
+  bf16* sc = condp + (size_t)R * H;
+  bf16* xh = sc + (size_t)R * H;
+  bf16* a = xh + (size_t)R * H;
+  bf16* mod = a + (size_t)R * H;
+  bf16* act = mod + (size_t)R * MODW;
+  bf16* v = act + (size_t)R * F;
+  bf16* m1 = v + (size_t)R * D;
+  HIPCHK(hipMemcpyAsync(cat, pos_h, (size_t)n * H * sizeof(bf16), hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipMemcpyAsync(cat + (size_t)n * H, neg_h, (size_t)n * H * sizeof(bf16), hipMemcpyDeviceToDevice, st));
+  // cond_proj is step-invariant: computed once per token (bit-identical to per step)
+  CHK(gemm(c, gemm_args(c, R, H, H, rowmap(cat, H), W(c, "head.cond_w"), EPI_STORE, rowmap(condp, H)), st));
+  RowMap xh_m = rowmap(xh, H), a_m = rowmap(a, H);
+  for (int s = 0; s < c->steps; ++s) {
+    // x = noisy_images_proj(cat[x, x])  -- both halves read the same n latent rows
+    CHK(gemm(c, gemm_args(c, R, H, D, rowmap(x_io, D, n, 0), W(c, "head.noisy_w"), EPI_STORE, xh_m), st));
+    KCHK(launch_head_cond(R, H, condp, (const bf16*)c->temb.p + (size_t)s * H, sc, st));
+    // all adaLN modulations of the step in one GEMM: [shift|scale|gate] x L, [shift|scale] final
+    CHK(gemm(c, gemm_args(c, R, (int)MODW, H, rowmap(sc, H), W(c, "head.ada_w"), EPI_STORE, rowmap(mod, MODW)), st));
+    for (int l = 0; l < L; ++l) {
+      const std::string p = "head." + std::to_string(l);
+      const int o = 3 * H * l;
+      CHK(rmsnorm(R, H, xh_m, a_m, W(c, p + ".norm"), k.head_eps, st, mod, MODW, o, o + H));
+      CHK(gemm(c, gemm_args(c, R, 2 * F, H, a_m, W(c, p + ".gu_w"), EPI_SILU_MUL, rowmap(act, F)), st));
+      GemmArgs g = gemm_args(c, R, H, F, rowmap(act, F), W(c, p + ".down_w"), EPI_RES, xh_m);
+      g.epi.res = xh_m;
+      g.epi.gate = rowmap(mod + o + 2 * H, MODW);
+      CHK(gemm(c, g, st));
+    }
+    CHK(rmsnorm(R, H, xh_m, a_m, nullptr, k.head_eps, st, mod, MODW, 3 * H * L, 3 * H * L + H));
+    CHK(gemm(c, gemm_args(c, R, D, H, a_m, W(c, "head.final_w"), EPI_STORE, rowmap(v, D)), st));
+    DpmCoef e = c->coef[s];
+    e.cfg = cfg_scale;
+    KCHK(launch_cfg_dpm(n, D, e, v, (bf16*)x_io, m1, st));
+  }
+  return 0;
+}
+
+static int connector(vv_ctx* c, const char* which, int n, int din, RowMap x, RowMap out, const RowMap* res,
+                     hipStream_t st) {
+  const int H = c->cfg.hidden;
+  const std::string p(which);
+  bf16* t1 = (bf16*)c->codec_ws.p;
+  bf16* t2 = t1 + (size_t)c->cfg.max_batch * H;
+  RowMap t1m = rowmap(t1, H), t2m = rowmap(t2, H);
+  CHK(gemm(c, gemm_args(c, n, H, din, x, W(c, p + ".fc1_w"), EPI_STORE, t1m, W(c, p + ".fc1_b")), st));
+  CHK(rmsnorm(n, H, t1m, t2m, W(c, p + ".norm"), 1e-6f, st));  // LlamaRMSNorm(eps=1e-6) (modeling_vibevoice.py:62)
+  GemmArgs g = gemm_args(c, n, H, H, t2m, W(c, p + ".fc2_w"), res ? EPI_RES : EPI_STORE, out, W(c, p + ".fc2_b"));
+  if (res) g.epi.res = *res;
+  CHK(gemm(c, g, st));
+  return 0;
+}
+
+int vv_connector(vv_ctx* c, int which, int n, const void* x, void* out, vv_stream vst) {
+  hipStream_t st = (hipStream_t)vst;
+  const int H = c->cfg.hidden;
+  const int din = which == 0 ? c->cfg.latent_dim : c->cfg.semantic_dim;
+  // chunk rows through the max_batch-sized connector workspace
+  for (int r0 = 0; r0 < n; r0 += c->cfg.max_batch) {
+    const int m = std::min(c->cfg.max_batch, n - r0);
+    CHK(connector(c, which == 0 ? "conn.ac" : "conn.se", m, din, rowmap((const bf16*)x + (size_t)r0 * din, din),
+                  rowmap((bf16*)out + (size_t)r0 * H, H), nullptr, st));
+  }
+  return 0;
+}
+
+int vv_codec_step(vv_ctx* c, int n, const int* slots, const void* latent, void* audio_out, void* sem_out,
+                  void* embeds_out, const int* embed_rows, vv_stream vst) {
+  hipStream_t st = (hipStream_t)vst;
+  if (!c->finalized) FAIL("vv_codec_step before vv_finalize");
+  if (n <= 0) return 0;
+  if (n > c->cfg.max_batch) FAIL("vv_codec_step: n > max_batch");
+  const int H = c->cfg.hidden, D = c->cfg.latent_dim, S = c->cfg.semantic_dim;
+  ConvNet& dn = c->dec;
+  ConvNet& sn = c->sem;
+  const int hop = dn.T[dn.nst - 1];
+  // decoder input: latent / scaling - bias  (modeling_vibevoice_inference.py:651)
+  KCHK(launch_latent_to_dec(n, D, (const bf16*)latent, W(c, "speech_scaling_factor"), W(c, "speech_bias_factor"),
+                            buf_in_rows(dn.stem, 1, slots), st));
+  // decoder -> audio chunk (also written as the semantic encoder's input rows)
+  CHK(convnet_run(c, dn, n, slots, rowmap(audio_out, 1, hop, hop), buf_in_rows(sn.stem, hop, slots), st));
+  CHK(convnet_roll(dn, n, slots, 0, st));
+  // semantic encoder -> [n, S]
+  bf16* sem = sem_out ? (bf16*)sem_out : (bf16*)c->codec_ws.p + (size_t)c->cfg.max_batch * 2 * H;
+  CHK(convnet_run(c, sn, n, slots, rowmap(sem, S, 1, S), RowMap{}, st));
+  CHK(convnet_roll(sn, n, slots, 0, st));
+  // next input embedding = acoustic_connector(latent) + semantic_connector(sem)  (:682-687)
+  if (embeds_out) {
+    bf16* ac = (bf16*)c->codec_ws.p + (size_t)c->cfg.max_batch * 3 * H;
+    RowMap acm = rowmap(ac, H);
+    CHK(connector(c, "conn.ac", n, D, rowmap(latent, D), acm, nullptr, st));
+    RowMap outm = rowmap(embeds_out, H, 1, H, embed_rows);
+    CHK(connector(c, "conn.se", n, S, rowmap(sem, S), outm, &acm, st));
+  }
+  return 0;
+}
+
+int vv_codec_reset(vv_ctx* c, int n, const int* slots, vv_stream vst) {
+  hipStream_t st = (hipStream_t)vst;
+  if (n <= 0) return 0;
+  CHK(convnet_roll(c->dec, n, slots, 1, st));
+  CHK(convnet_roll(c->sem, n, slots, 1, st));
+  return 0;
+}
+
+int vv_acoustic_encode(vv_ctx* c, int nv, int L, const void* audio, void* mean_out, vv_stream vst) {
+  hipStream_t st = (hipStream_t)vst;
+  if (!c->w.count("aenc.stem_w")) FAIL("acoustic encoder weights not bound");
+  if (nv <= 0 || L <= 0) return 0;
+  ConvNet& net = c->aenc;
+  // (re)layout for this call: nv slots, T0 = L; per-layer right zero padding of
+  // strided-conv inputs reproduces the non-streaming extra padding (:127-133, :398-403)
+  if (net.slots != nv || net.T0 != L) {
+    convnet_shape(c, net, false, "aenc", c->cfg.ac_enc_n_filters, 1, c->cfg.latent_dim, L, nv);
+    CHK(convnet_alloc(net, 7));
+  } else {
+    HIPCHK(hipMemsetAsync(net.state.p, 0, net.state.bytes, st));
+  }
+  CHK(c->slot_scratch.ensure(sizeof(int) * (size_t)std::max(nv, 1024)));
+  std::vector<int> ids(nv);
+  for (int i = 0; i < nv; ++i) ids[i] = i;
+  int* d_ids = (int*)c->slot_scratch.p;
+  HIPCHK(hipMemcpyAsync(d_ids, ids.data(), nv * sizeof(int), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpy2DAsync(net.stem.base + net.stem.ctx, net.stem.sB * sizeof(bf16), audio, (size_t)L * sizeof(bf16),
+                          (size_t)L * sizeof(bf16), nv, hipMemcpyDeviceToDevice, st));
+  const int Tl = net.T[net.nst - 1];
+  CHK(convnet_run(c, net, nv, d_ids, rowmap(mean_out, c->cfg.latent_dim, Tl, (long long)Tl * c->cfg.latent_dim),
+                  RowMap{}, st));
+  HIPCHK(hipStreamSynchronize(st));  // d_ids scratch is reused by the next call
+  return 0;
+}
+
+int vv_vae_features(vv_ctx* c, int nv, int frames, const void* mean, const void* stdv, const void* noise, void* feat,
+                    vv_stream vst) {
+  KCHK(launch_vae_features(nv * frames, c->cfg.latent_dim, frames, (const bf16*)mean, (const bf16*)stdv,
+                           (const bf16*)noise, W(c, "speech_scaling_factor"), W(c, "speech_bias_factor"),
+                           (bf16*)feat, (hipStream_t)vst));
+  return 0;
+}
+
+int vv_scatter_rows(vv_ctx* c, int n, int C, const void* src, int64_t lds, const int* idx, void* dst, int64_t ldd,
+                    vv_stream vst) {
+  (void)c;
+  // dst[idx[i]] = src[i]: a gather with the roles of the maps swapped
+  RowMap dm = rowmap(dst, ldd, 1, ldd, idx);
+  KCHK(launch_gather_rows(n, C, (const bf16*)src, lds, nullptr, dm, (hipStream_t)vst));
+  return 0;
+}
+
+int vv_gemm_bf16(int M, int N, int K, const void* A, int64_t lda, const void* Wt, const void* bias, int epi, void* Y,
+                 int64_t ldy, const void* res, const void* gamma, vv_ctx* c, vv_stream vst) {
+  GemmArgs g;
+  memset(&g, 0, sizeof(g));
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.ksplit = 1;
+  g.a = rowmap(A, lda);
+  g.w = (const bf16*)Wt;
+  g.ldw = K;
+  g.epi.kind = epi;
+  g.epi.bias = (const bf16*)bias;
+  g.epi.out = rowmap(Y, ldy);
+  g.epi.res = rowmap(res, ldy);
+  g.epi.gamma = (const bf16*)gamma;
+  if (c) {
+    g.ws = (float*)c->splitk_ws.p;
+    g.counters = (unsigned*)c->splitk_cnt.p;
+  } else {
+    // standalone calls (tests): a process-wide split-K workspace
+    static DevBuf ws, cnt;
+    if (!cnt.p) {
+      CHK(ws.ensure(64ull << 20));
+      CHK(cnt.ensure(65536 * sizeof(unsigned)));
+      HIPCHK(hipMemset(cnt.p, 0, 65536 * sizeof(unsigned)));
+    }
+    g.ws = (float*)ws.p;
+    g.counters = (unsigned*)cnt.p;
+  }
+  KCHK(launch_gemm(g, (hipStream_t)vst));
+  return 0;
+}
+
+int vv_rmsnorm_bf16(int M, int C, const void* x, int64_t ldx, const void* w, float eps, void* y, int64_t ldy,
+                    vv_stream vst) {
+  return rmsnorm(M, C, rowmap(x, ldx), rowmap(y, ldy), (const bf16*)w, eps, (hipStream_t)vst);
+}
+
+}  // extern "C"

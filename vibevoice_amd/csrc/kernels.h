@@ -1,0 +1,127 @@
+// Kernel argument structs and host launchers shared by the .hip kernel files
+// and the engine (engine.cpp).  See each kernel for the reference it follows.
+#pragma once
+#include "common.h"
+
+struct GemmArgs {
+  int M, N, K;
+  int ksplit;
+  RowMap a;
+  const bf16* w;
+  long long ldw;
+  EpiArgs epi;
+  float* ws;
+  unsigned* counters;
+};
+
+struct NormArgs {
+  int M, C;
+  float eps;
+  int has_mod;
+  RowMap in, out;
+  const bf16* w;
+  const bf16* mod;      // row m: mod + m * mod_ld
+  long long mod_ld;
+  int shift_off, scale_off;
+};
+
+struct DwArgs {
+  int M, C, T, K;    // rows (groups*T), channels, rows per group, kernel size
+  RowMap buf;        // row t of group -> buffer row t (conv window rows t .. t+K-1)
+  RowMap x;
+  const bf16* w;     // [C, K]
+  const bf16* b;     // [C]
+  const bf16* gamma; // [C]
+};
+
+struct Conv1Args {
+  int M, C, K;
+  RowMap buf;
+  const bf16* w;   // [K][C]  (re-packed from [1, C, K])
+  const bf16* b;   // [1]
+  RowMap out, out2;
+};
+
+struct ConvIn1Args {
+  int M, C, K;
+  RowMap buf;      // 1 channel, sT = 1
+  const bf16* w;   // [C, K]
+  const bf16* b;   // [C]
+  RowMap out;
+};
+
+struct RollDesc {
+  bf16* base;
+  long long sB;   // elements per slot
+  int ctx, T, C, pad_;
+};
+
+struct DpmCoef {
+  float cfg;
+  float alpha_s, sigma_s;  // x0 = alpha_s * x - sigma_s * v          (bf16 ops)
+  float c_x, c_d0, c_d1, inv_r0;
+  int order;               // 1: x' = c_x x - bf16(c_d0 x0)
+                           // 2: x' = c_x x - bf16(c_d0 x0) - bf16(c_d1 bf16(inv_r0 bf16(x0 - m1)))
+};
+
+struct KVLayout {
+  bf16* k;
+  bf16* v;
+  long long s_layer, s_slot, s_head;  // elements; s_ctx = d
+  int d, max_ctx;
+};
+
+struct RopeArgs {
+  int R, nh, nkv, layer;
+  const bf16* qkv;
+  long long ld_qkv;
+  bf16* q_out;          // [R][nh*d]
+  const int* slots;     // [R] cache slot of row
+  const int* pos;       // [R] position == cache index written
+  const float* inv_freq;// [d/2]
+  KVLayout kv;
+};
+
+struct AttnArgs {
+  int nq, nh, nkv, layer, nsplit;
+  float scale;
+  const bf16* q;        // [nq][nh*d]
+  bf16* out;            // [nq][nh*d]
+  const int* slots;
+  const int* pos;        // [nq] position of the query; it attends keys [0, pos]
+  KVLayout kv;
+  float* part_o;        // [nq][nh][nsplit][d]
+  float* part_ml;       // [nq][nh][nsplit][2]
+};
+
+int launch_gemm(GemmArgs a, hipStream_t st);
+int launch_rmsnorm(NormArgs a, hipStream_t st);
+int launch_dwconv(DwArgs a, hipStream_t st);
+int launch_conv_cout1(Conv1Args a, hipStream_t st);
+int launch_conv_cin1(ConvIn1Args a, hipStream_t st);
+int launch_roll(const RollDesc* d, int nd, const int* slots, int ns, int mode, hipStream_t st);
+int launch_latent_to_dec(int n, int D, const bf16* lat, const bf16* s, const bf16* b, RowMap out, hipStream_t st);
+int launch_vae_features(int rows, int D, int frames, const bf16* mean, const bf16* stdv, const bf16* noise,
+                        const bf16* s, const bf16* b, bf16* out, hipStream_t st);
+int launch_head_cond(int rows, int H, const bf16* condp, const bf16* temb, bf16* out, hipStream_t st);
+int launch_silu(int n, const bf16* x, bf16* y, hipStream_t st);
+int launch_cfg_dpm(int n, int D, DpmCoef k, const bf16* eps, bf16* x, bf16* m1, hipStream_t st);
+int launch_gather_rows(int n, int C, const bf16* src, long long lds, const int* idx, RowMap dst, hipStream_t st);
+int launch_rope_kv(RopeArgs a, hipStream_t st);
+int attn_nsplit(int max_len);
+int launch_attn(AttnArgs a, hipStream_t st);
+int launch_lmhead_ids(int R, int H, const bf16* h, long long ldh, const bf16* W, const int* ids, int nid, float* out,
+                      hipStream_t st);
+
+// RowMap helpers (host)
+static inline RowMap rowmap(const void* base, long long sT, int T = 1 << 30, long long sB = 0,
+                            const int* idx = nullptr) {
+  RowMap r;
+  r.base = const_cast<void*>(base);
+  r.sB = sB;
+  r.sT = sT;
+  r.T = T;
+  r.pad_ = 0;
+  r.idx = idx;
+  return r;
+}

@@ -1,0 +1,179 @@
+"""Python handle on the native engine (libvibevoice_hip.so).
+
+Thin: converts torch device tensors to pointers, keeps borrowed weights alive,
+and forwards to the C ABI.  No arithmetic happens here.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from .config import VibeVoiceConfig
+from .schedule import Schedule
+from .weights import codec_channels, pack
+
+_VALID_IDS_DEFAULT = None
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def engine_config(cfg: VibeVoiceConfig, max_batch, max_ctx):
+    lm = cfg.decoder_config
+    hc = cfg.diffusion_head_config
+    c = _lib.VVConfig()
+    c.hidden = lm.hidden_size
+    c.n_layers = lm.num_hidden_layers
+    c.n_heads = lm.num_attention_heads
+    c.n_kv_heads = lm.num_key_value_heads
+    c.head_dim = lm.get("head_dim") or lm.hidden_size // lm.num_attention_heads
+    c.intermediate = lm.intermediate_size
+    c.rms_eps = lm.rms_norm_eps
+    c.rope_theta = lm.rope_theta
+    c.head_layers = hc.head_layers
+    c.head_ffn = int(hc.hidden_size * hc.head_ffn_ratio)
+    c.latent_dim = hc.latent_size
+    c.head_eps = hc.rms_norm_eps
+    c.n_stages = len(cfg.dec_depths)
+    for i, r in enumerate(cfg.ratios):
+        c.ratios[i] = r
+    for i, v in enumerate(cfg.dec_depths):
+        c.dec_depths[i] = v
+    for i, v in enumerate(cfg.enc_depths):
+        c.enc_depths[i] = v
+    c.dec_n_filters = cfg.acoustic_tokenizer_config.decoder_n_filters
+    c.sem_n_filters = cfg.semantic_tokenizer_config.encoder_n_filters
+    c.ac_enc_n_filters = cfg.acoustic_tokenizer_config.encoder_n_filters
+    c.semantic_dim = cfg.semantic_vae_dim
+    c.codec_eps = cfg.acoustic_tokenizer_config.layernorm_eps
+    c.max_batch = max_batch
+    c.max_ctx = max_ctx
+    return c
+
+
+class Engine:
+    """One device-resident VibeVoice model instance."""
+
+    def __init__(self, cfg: VibeVoiceConfig, state_dict, device="cuda", max_batch=1, max_ctx=4096,
+                 valid_ids=None):
+        L = _lib.lib()
+        self.cfg = cfg
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("the VibeVoice HIP engine runs on a ROCm GPU device only")
+        self.max_batch = max_batch
+        self.max_ctx = max_ctx
+        self.hidden = cfg.decoder_config.hidden_size
+        self.latent = cfg.diffusion_head_config.latent_size
+        self.hop = cfg.hop
+        with torch.cuda.device(self.device):
+            self.w = pack(state_dict, cfg, self.device)
+            h = ctypes.c_void_p()
+            self._ecfg = engine_config(cfg, max_batch, max_ctx)
+            _lib.check(L.vv_create(ctypes.byref(self._ecfg), self.device.index or 0, ctypes.byref(h)), "create")
+            self.h = h
+            for name, t in self.w.items():
+                shape = (ctypes.c_int64 * max(1, t.dim()))(*t.shape)
+                _lib.check(L.vv_bind_weight(h, name.encode(), _ptr(t), shape, t.dim()), f"bind {name}")
+            _lib.check(L.vv_finalize(h), "finalize")
+            if valid_ids is not None:
+                self.set_valid_ids(valid_ids)
+        self.steps = None
+        self.schedule = Schedule()
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.lib().vv_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------- setup
+    def set_valid_ids(self, ids):
+        arr = (ctypes.c_int * len(ids))(*ids)
+        _lib.check(_lib.lib().vv_set_valid_ids(self.h, len(ids), arr), "set_valid_ids")
+        self.n_valid = len(ids)
+
+    def set_steps(self, steps, stream=None):
+        if steps == self.steps:
+            return
+        _, coef = self.schedule.coefficients(steps)
+        tf = self.schedule.timestep_features(steps).to(self.device)
+        c = (ctypes.c_float * coef.size)(*coef.reshape(-1).tolist())
+        _lib.check(_lib.lib().vv_set_schedule(self.h, steps, c, _ptr(tf), _stream(stream)), "set_schedule")
+        torch.cuda.current_stream().synchronize() if stream is None else stream.synchronize()
+        self.steps = steps
+
+    # ---------------------------------------------------------------- hot path
+    def lm_forward(self, embeds, slots, pos, out_idx, hidden_out=None, logits_out=None, max_pos=None, stream=None):
+        """embeds [ntok, H] bf16; slots/pos/out_idx int32 device tensors."""
+        ntok, nout = embeds.shape[0], out_idx.shape[0]
+        if hidden_out is None:
+            hidden_out = torch.empty(nout, self.hidden, dtype=torch.bfloat16, device=self.device)
+        if logits_out is None:
+            logits_out = torch.empty(nout, self.n_valid, dtype=torch.float32, device=self.device)
+        mp = int(max_pos if max_pos is not None else pos.max().item()) + 1
+        _lib.check(_lib.lib().vv_lm_forward(self.h, ntok, _ptr(embeds), _ptr(slots), _ptr(pos), mp, nout,
+                                            _ptr(out_idx), _ptr(hidden_out), _ptr(logits_out), _stream(stream)),
+                   "lm_forward")
+        return hidden_out, logits_out
+
+    def embed(self, ids, out=None, stream=None):
+        if out is None:
+            out = torch.empty(ids.shape[0], self.hidden, dtype=torch.bfloat16, device=self.device)
+        _lib.check(_lib.lib().vv_embed(self.h, ids.shape[0], _ptr(ids), _ptr(out), _stream(stream)), "embed")
+        return out
+
+    def diffusion_sample(self, pos_h, neg_h, x_io, cfg_scale, stream=None):
+        _lib.check(_lib.lib().vv_diffusion_sample(self.h, pos_h.shape[0], _ptr(pos_h), _ptr(neg_h), _ptr(x_io),
+                                                  float(cfg_scale), _stream(stream)), "diffusion_sample")
+        return x_io
+
+    def codec_step(self, slots, latent, audio_out, sem_out=None, embeds_out=None, embed_rows=None, stream=None):
+        _lib.check(_lib.lib().vv_codec_step(self.h, slots.shape[0], _ptr(slots), _ptr(latent), _ptr(audio_out),
+                                            _ptr(sem_out), _ptr(embeds_out), _ptr(embed_rows), _stream(stream)),
+                   "codec_step")
+
+    def codec_reset(self, slots, stream=None):
+        _lib.check(_lib.lib().vv_codec_reset(self.h, slots.shape[0], _ptr(slots), _stream(stream)), "codec_reset")
+
+    # ---------------------------------------------------------------- prefill helpers
+    def acoustic_encode(self, audio_bf16, stream=None):
+        nv, L = audio_bf16.shape
+        frames = -(-L // self.hop)
+        mean = torch.empty(nv, frames, self.latent, dtype=torch.bfloat16, device=self.device)
+        _lib.check(_lib.lib().vv_acoustic_encode(self.h, nv, L, _ptr(audio_bf16.contiguous()), _ptr(mean),
+                                                 _stream(stream)), "acoustic_encode")
+        return mean
+
+    def vae_features(self, mean, stdv, noise, stream=None):
+        nv, frames, D = mean.shape
+        out = torch.empty_like(mean)
+        _lib.check(_lib.lib().vv_vae_features(self.h, nv, frames, _ptr(mean), _ptr(stdv), _ptr(noise), _ptr(out),
+                                              _stream(stream)), "vae_features")
+        return out
+
+    def connector(self, which, x, stream=None):
+        x = x.contiguous()
+        out = torch.empty(x.shape[0], self.hidden, dtype=torch.bfloat16, device=self.device)
+        _lib.check(_lib.lib().vv_connector(self.h, which, x.shape[0], _ptr(x), _ptr(out), _stream(stream)),
+                   "connector")
+        return out
+
+    def scatter_rows(self, src, idx, dst, stream=None):
+        _lib.check(_lib.lib().vv_scatter_rows(self.h, src.shape[0], src.shape[1], _ptr(src), src.stride(0),
+                                              _ptr(idx), _ptr(dst), dst.stride(0), _stream(stream)), "scatter_rows")
+
+
+def semantic_channels(cfg):
+    return codec_channels(cfg, "encoder", "semantic")

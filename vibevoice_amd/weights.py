@@ -1,0 +1,305 @@
+"""Weights: the reference's checkpoint names -> engine names + layouts.
+
+Checkpoint names are those of VibeVoiceForConditionalGenerationInference's
+state dict (modeling_vibevoice.py:107-142,
+modeling_vibevoice_inference.py:77-80).  `pack()` turns them into the
+layouts the HIP kernels consume (vibevoice_amd/csrc/gemm.hip header):
+
+  * q/k/v projections concatenated -> one [(nh+2nkv)d, H] GEMM (+ bias)
+  * gate/up interleaved in blocks of 8 rows -> one GEMM with a SiLU*up epilogue
+  * all adaLN modulation matrices of the head stacked -> one GEMM per step
+  * causal conv [Co, Ci, k] -> [Co, k*Ci]  (channels-last im2col row order)
+  * ConvTranspose [Ci, Co, 2r] -> 2-tap [r*Co, 2*Ci] (history row, current row)
+
+`synthetic_state_dict()` builds seeded random weights at the reference's
+shapes (no checkpoints are reachable offline).
+"""
+import math
+
+import torch
+
+from .config import VibeVoiceConfig
+
+LM = "model.language_model."
+HEAD = "model.prediction_head."
+
+
+def codec_channels(cfg: VibeVoiceConfig, part, which="acoustic"):
+    t = cfg.acoustic_tokenizer_config if which == "acoustic" else cfg.semantic_tokenizer_config
+    n = len(cfg.enc_depths)
+    if part == "decoder":
+        nf = t.decoder_n_filters
+        return [nf * 2 ** (n - 1 - i) for i in range(n)]
+    nf = t.encoder_n_filters
+    return [nf * 2 ** i for i in range(n)]
+
+
+def _codec_shapes(cfg, prefix, part, which):
+    """(name, shape) of one conv stack, in the reference's naming."""
+    chans = codec_channels(cfg, part, which)
+    t = cfg.acoustic_tokenizer_config if which == "acoustic" else cfg.semantic_tokenizer_config
+    out = []
+    n = len(chans)
+    if part == "decoder":
+        depths, ratios = cfg.dec_depths, cfg.ratios
+        out.append((f"{prefix}decoder.upsample_layers.0.0.conv.conv", [chans[0], t.vae_dim, 7], chans[0]))
+        for i in range(1, n):
+            r = ratios[i - 1]
+            out.append((f"{prefix}decoder.upsample_layers.{i}.0.convtr.convtr", [chans[i - 1], chans[i], 2 * r],
+                        chans[i]))
+        stages = "decoder.stages"
+        out.append((f"{prefix}decoder.head.conv.conv", [1, chans[-1], 7], 1))
+    else:
+        depths, ratios = cfg.enc_depths, list(reversed(cfg.ratios))
+        out.append((f"{prefix}encoder.downsample_layers.0.0.conv.conv", [chans[0], 1, 7], chans[0]))
+        for i in range(1, n):
+            r = ratios[i - 1]
+            out.append((f"{prefix}encoder.downsample_layers.{i}.0.conv.conv", [chans[i], chans[i - 1], 2 * r],
+                        chans[i]))
+        stages = "encoder.stages"
+        out.append((f"{prefix}encoder.head.conv.conv", [t.vae_dim, chans[-1], 7], t.vae_dim))
+    blocks = []
+    for i, dep in enumerate(depths):
+        C = chans[i]
+        for j in range(dep):
+            blocks.append((f"{prefix}{stages}.{i}.{j}.", C))
+    return out, blocks
+
+
+def synthetic_state_dict(cfg: VibeVoiceConfig, seed=0, device="cpu", dtype=torch.bfloat16, mode="bench",
+                         with_acoustic_encoder=True):
+    """Seeded random weights with the reference's names and shapes.
+
+    mode="bench": the reference's own init scales (std 0.02 linears,
+    layer-scale gamma 1e-6, zero biases) so activations behave like an
+    untrained model.  mode="test": larger, fan-in-scaled weights, random
+    norms / gammas / biases so every term of every kernel is exercised.
+    """
+    g = torch.Generator(device=device).manual_seed(seed)
+    sd = {}
+    test = mode == "test"
+
+    def rnd(shape, std):
+        return (torch.randn(shape, generator=g, device=device, dtype=torch.float32) * std).to(dtype)
+
+    def lin(name, shape, bias=None):
+        std = (1.0 / math.sqrt(shape[1] if len(shape) == 2 else shape[1] * shape[2])) if test else 0.02
+        sd[name + ".weight"] = rnd(shape, std)
+        if bias is not None:
+            sd[name + ".bias"] = rnd([bias], 0.1) if test else torch.zeros(bias, device=device, dtype=dtype)
+
+    def norm(name, n):
+        sd[name] = (1.0 + rnd([n], 0.1).float()).to(dtype) if test else torch.ones(n, device=device, dtype=dtype)
+
+    lm = cfg.decoder_config
+    H, nh, nkv = lm.hidden_size, lm.num_attention_heads, lm.num_key_value_heads
+    d = lm.get("head_dim") or H // nh
+    I, V = lm.intermediate_size, lm.vocab_size
+    sd[LM + "embed_tokens.weight"] = rnd([V, H], 0.02 if not test else 1.0)
+    for i in range(lm.num_hidden_layers):
+        p = f"{LM}layers.{i}."
+        lin(p + "self_attn.q_proj", [nh * d, H], nh * d)
+        lin(p + "self_attn.k_proj", [nkv * d, H], nkv * d)
+        lin(p + "self_attn.v_proj", [nkv * d, H], nkv * d)
+        lin(p + "self_attn.o_proj", [H, nh * d])
+        lin(p + "mlp.gate_proj", [I, H])
+        lin(p + "mlp.up_proj", [I, H])
+        lin(p + "mlp.down_proj", [H, I])
+        norm(p + "input_layernorm.weight", H)
+        norm(p + "post_attention_layernorm.weight", H)
+    norm(LM + "norm.weight", H)
+    if cfg.tie_word_embeddings:
+        sd["lm_head.weight"] = sd[LM + "embed_tokens.weight"]
+    else:
+        lin("lm_head", [V, H])
+
+    hc = cfg.diffusion_head_config
+    Hh, F, Dl = hc.hidden_size, int(hc.hidden_size * hc.head_ffn_ratio), hc.latent_size
+    lin(HEAD + "noisy_images_proj", [Hh, Dl])
+    lin(HEAD + "cond_proj", [Hh, Hh])
+    lin(HEAD + "t_embedder.mlp.0", [Hh, 256])
+    lin(HEAD + "t_embedder.mlp.2", [Hh, Hh])
+    for i in range(hc.head_layers):
+        p = f"{HEAD}layers.{i}."
+        lin(p + "ffn.gate_proj", [F, Hh])
+        lin(p + "ffn.up_proj", [F, Hh])
+        lin(p + "ffn.down_proj", [Hh, F])
+        norm(p + "norm.weight", Hh)
+        lin(p + "adaLN_modulation.1", [3 * Hh, Hh])
+    lin(HEAD + "final_layer.linear", [Dl, Hh])
+    lin(HEAD + "final_layer.adaLN_modulation.1", [2 * Hh, Hh])
+
+    for name, din in (("acoustic", cfg.acoustic_vae_dim), ("semantic", cfg.semantic_vae_dim)):
+        p = f"model.{name}_connector."
+        lin(p + "fc1", [H, din], H)
+        norm(p + "norm.weight", H)
+        lin(p + "fc2", [H, H], H)
+    sd["model.speech_scaling_factor"] = torch.tensor(0.2 if not test else 0.75, device=device).to(dtype)
+    sd["model.speech_bias_factor"] = torch.tensor(-0.05 if not test else 0.1, device=device).to(dtype)
+
+    parts = [("model.acoustic_tokenizer.", "decoder", "acoustic"), ("model.semantic_tokenizer.", "encoder", "semantic")]
+    if with_acoustic_encoder:
+        parts.append(("model.acoustic_tokenizer.", "encoder", "acoustic"))
+    wi = cfg.acoustic_tokenizer_config.weight_init_value
+    ls = cfg.acoustic_tokenizer_config.layer_scale_init_value
+    for prefix, part, which in parts:
+        convs, blocks = _codec_shapes(cfg, prefix, part, which)
+        for name, shape, nb in convs:
+            if test:
+                fan = shape[0] * shape[2] if "convtr" in name else shape[1] * shape[2]
+                sd[name + ".weight"] = rnd(shape, 1.0 / math.sqrt(fan) * (2.0 if "convtr" in name else 1.0))
+                sd[name + ".bias"] = rnd([nb], 0.05)
+            else:
+                sd[name + ".weight"] = rnd(shape, wi)
+                sd[name + ".bias"] = torch.zeros(nb, device=device, dtype=dtype)
+        for p, C in blocks:
+            norm(p + "norm.weight", C)
+            norm(p + "ffn_norm.weight", C)
+            if test:
+                sd[p + "mixer.conv.conv.conv.weight"] = rnd([C, 1, 7], 0.4)
+                sd[p + "mixer.conv.conv.conv.bias"] = rnd([C], 0.05)
+                sd[p + "gamma"] = rnd([C], 0.3)
+                sd[p + "ffn_gamma"] = rnd([C], 0.3)
+            else:
+                sd[p + "mixer.conv.conv.conv.weight"] = rnd([C, 1, 7], wi)
+                sd[p + "mixer.conv.conv.conv.bias"] = torch.zeros(C, device=device, dtype=dtype)
+                sd[p + "gamma"] = torch.full([C], ls, device=device).to(dtype)
+                sd[p + "ffn_gamma"] = torch.full([C], ls, device=device).to(dtype)
+            if test:
+                sd[p + "ffn.linear1.weight"] = rnd([4 * C, C], 1.0 / math.sqrt(C))
+                sd[p + "ffn.linear1.bias"] = rnd([4 * C], 0.05)
+                sd[p + "ffn.linear2.weight"] = rnd([C, 4 * C], 1.0 / math.sqrt(4 * C))
+                sd[p + "ffn.linear2.bias"] = rnd([C], 0.05)
+            else:
+                sd[p + "ffn.linear1.weight"] = rnd([4 * C, C], wi)
+                sd[p + "ffn.linear1.bias"] = torch.zeros(4 * C, device=device, dtype=dtype)
+                sd[p + "ffn.linear2.weight"] = rnd([C, 4 * C], wi)
+                sd[p + "ffn.linear2.bias"] = torch.zeros(C, device=device, dtype=dtype)
+    return sd
+
+
+# ------------------------------------------------------------------ packing
+def _gu(gate, up):
+    """Interleave gate/up rows in blocks of 8 (EPI_SILU_MUL tile layout)."""
+    I, H = gate.shape
+    assert I % 8 == 0
+    return torch.stack([gate.reshape(I // 8, 8, H), up.reshape(I // 8, 8, H)], dim=1).reshape(2 * I, H)
+
+
+def _conv_rows(w):
+    """[Co, Ci, k] -> [Co, k*Ci], element (co, j*Ci + ci) = w[co, ci, j]."""
+    Co, Ci, k = w.shape
+    return w.permute(0, 2, 1).reshape(Co, k * Ci)
+
+
+def _convtr_2tap(w, b, r):
+    """[Ci, Co, 2r] -> [r*Co, 2*Ci]: row (j*Co + co) = [w[:, co, j+r] (history) | w[:, co, j] (current)]."""
+    Ci, Co, k = w.shape
+    assert k == 2 * r
+    wp = w.permute(2, 1, 0)  # [k, Co, Ci]
+    packed = torch.cat([wp[r:], wp[:r]], dim=2).reshape(r * Co, 2 * Ci)
+    return packed, b.repeat(r)
+
+
+def rope_inv_freq(theta, d):
+    """Qwen2RotaryEmbedding default inv_freq (transformers modeling_qwen2.py:69-86), fp32."""
+    return 1.0 / (theta ** (torch.arange(0, d, 2, dtype=torch.int64).to(dtype=torch.float) / d))
+
+
+def pack(sd, cfg: VibeVoiceConfig, device, with_acoustic_encoder=True):
+    """Reference state dict -> {engine name: contiguous device tensor}."""
+    dt = torch.bfloat16
+
+    def t(x):
+        return x.to(device=device, dtype=dt).contiguous()
+
+    out = {}
+    lm = cfg.decoder_config
+    H, nh = lm.hidden_size, lm.num_attention_heads
+    d = lm.get("head_dim") or H // nh
+    out["lm.embed"] = t(sd[LM + "embed_tokens.weight"])
+    out["lm.lm_head"] = t(sd["lm_head.weight"]) if "lm_head.weight" in sd else out["lm.embed"]
+    out["lm.norm"] = t(sd[LM + "norm.weight"])
+    out["lm.inv_freq"] = rope_inv_freq(lm.rope_theta, d).to(device)
+    for i in range(lm.num_hidden_layers):
+        p = f"{LM}layers.{i}."
+        e = f"lm.{i}."
+        out[e + "in_norm"] = t(sd[p + "input_layernorm.weight"])
+        out[e + "post_norm"] = t(sd[p + "post_attention_layernorm.weight"])
+        out[e + "qkv_w"] = t(torch.cat([sd[p + f"self_attn.{x}_proj.weight"] for x in "qkv"], 0))
+        out[e + "qkv_b"] = t(torch.cat([sd[p + f"self_attn.{x}_proj.bias"] for x in "qkv"], 0))
+        out[e + "o_w"] = t(sd[p + "self_attn.o_proj.weight"])
+        out[e + "gu_w"] = t(_gu(sd[p + "mlp.gate_proj.weight"], sd[p + "mlp.up_proj.weight"]))
+        out[e + "down_w"] = t(sd[p + "mlp.down_proj.weight"])
+
+    hc = cfg.diffusion_head_config
+    out["head.noisy_w"] = t(sd[HEAD + "noisy_images_proj.weight"])
+    out["head.cond_w"] = t(sd[HEAD + "cond_proj.weight"])
+    out["head.t0_w"] = t(sd[HEAD + "t_embedder.mlp.0.weight"])
+    out["head.t2_w"] = t(sd[HEAD + "t_embedder.mlp.2.weight"])
+    ada = [sd[f"{HEAD}layers.{i}.adaLN_modulation.1.weight"] for i in range(hc.head_layers)]
+    ada.append(sd[HEAD + "final_layer.adaLN_modulation.1.weight"])
+    out["head.ada_w"] = t(torch.cat(ada, 0))
+    for i in range(hc.head_layers):
+        p = f"{HEAD}layers.{i}."
+        out[f"head.{i}.norm"] = t(sd[p + "norm.weight"])
+        out[f"head.{i}.gu_w"] = t(_gu(sd[p + "ffn.gate_proj.weight"], sd[p + "ffn.up_proj.weight"]))
+        out[f"head.{i}.down_w"] = t(sd[p + "ffn.down_proj.weight"])
+    out["head.final_w"] = t(sd[HEAD + "final_layer.linear.weight"])
+
+    for src, dst in (("acoustic", "ac"), ("semantic", "se")):
+        p = f"model.{src}_connector."
+        out[f"conn.{dst}.fc1_w"] = t(sd[p + "fc1.weight"])
+        out[f"conn.{dst}.fc1_b"] = t(sd[p + "fc1.bias"])
+        out[f"conn.{dst}.norm"] = t(sd[p + "norm.weight"])
+        out[f"conn.{dst}.fc2_w"] = t(sd[p + "fc2.weight"])
+        out[f"conn.{dst}.fc2_b"] = t(sd[p + "fc2.bias"])
+    out["speech_scaling_factor"] = t(sd["model.speech_scaling_factor"].reshape(()))
+    out["speech_bias_factor"] = t(sd["model.speech_bias_factor"].reshape(()))
+
+    nets = [("dec", "model.acoustic_tokenizer.", "decoder", "acoustic"),
+            ("sem", "model.semantic_tokenizer.", "encoder", "semantic")]
+    if with_acoustic_encoder and "model.acoustic_tokenizer.encoder.head.conv.conv.weight" in sd:
+        nets.append(("aenc", "model.acoustic_tokenizer.", "encoder", "acoustic"))
+    for e, prefix, part, which in nets:
+        chans = codec_channels(cfg, part, which)
+        n = len(chans)
+        if part == "decoder":
+            w = sd[prefix + "decoder.upsample_layers.0.0.conv.conv.weight"]
+            out[e + ".stem_w"] = t(_conv_rows(w))
+            out[e + ".stem_b"] = t(sd[prefix + "decoder.upsample_layers.0.0.conv.conv.bias"])
+            for i in range(1, n):
+                q = f"{prefix}decoder.upsample_layers.{i}.0.convtr.convtr."
+                pw, pb = _convtr_2tap(sd[q + "weight"], sd[q + "bias"], cfg.ratios[i - 1])
+                out[f"{e}.tr{i}_w"], out[f"{e}.tr{i}_b"] = t(pw), t(pb)
+            hw = sd[prefix + "decoder.head.conv.conv.weight"]
+            out[e + ".head_w"] = t(hw[0].t())
+            out[e + ".head_b"] = t(sd[prefix + "decoder.head.conv.conv.bias"])
+            depths, st = cfg.dec_depths, "decoder.stages"
+        else:
+            w = sd[prefix + "encoder.downsample_layers.0.0.conv.conv.weight"]
+            out[e + ".stem_w"] = t(w.reshape(w.shape[0], w.shape[2]))
+            out[e + ".stem_b"] = t(sd[prefix + "encoder.downsample_layers.0.0.conv.conv.bias"])
+            for i in range(1, n):
+                q = f"{prefix}encoder.downsample_layers.{i}.0.conv.conv."
+                out[f"{e}.tr{i}_w"] = t(_conv_rows(sd[q + "weight"]))
+                out[f"{e}.tr{i}_b"] = t(sd[q + "bias"])
+            out[e + ".head_w"] = t(_conv_rows(sd[prefix + "encoder.head.conv.conv.weight"]))
+            out[e + ".head_b"] = t(sd[prefix + "encoder.head.conv.conv.bias"])
+            depths, st = cfg.enc_depths, "encoder.stages"
+        for i, dep in enumerate(depths):
+            for j in range(dep):
+                p = f"{prefix}{st}.{i}.{j}."
+                b = f"{e}.s{i}.b{j}."
+                C = chans[i]
+                out[b + "norm"] = t(sd[p + "norm.weight"])
+                out[b + "ffn_norm"] = t(sd[p + "ffn_norm.weight"])
+                out[b + "dw_w"] = t(sd[p + "mixer.conv.conv.conv.weight"].reshape(C, 7))
+                out[b + "dw_b"] = t(sd[p + "mixer.conv.conv.conv.bias"])
+                out[b + "gamma"] = t(sd[p + "gamma"])
+                out[b + "ffn_gamma"] = t(sd[p + "ffn_gamma"])
+                out[b + "fc1_w"] = t(sd[p + "ffn.linear1.weight"])
+                out[b + "fc1_b"] = t(sd[p + "ffn.linear1.bias"])
+                out[b + "fc2_w"] = t(sd[p + "ffn.linear2.weight"])
+                out[b + "fc2_b"] = t(sd[p + "ffn.linear2.bias"])
+    return out
