@@ -84,6 +84,9 @@ int vv_set_schedule(vv_ctx* ctx, int steps, const float* coef, const void* tfreq
 int vv_lm_forward(vv_ctx* ctx, int ntok, const void* embeds, const int* slot, const int* pos, int max_pos_p1,
                   int nout, const int* out_idx, void* hidden_out, float* logits_out, vv_stream st);
 
+/* Copy the K/V cache entry src[i] -> dst[i] of slot slots[i] (all layers). */
+int vv_kv_copy(vv_ctx* ctx, int n, const int* slots, const int* src, const int* dst, vv_stream st);
+
 /* embeds_out[i] = embed_tokens[ids[i]] */
 int vv_embed(vv_ctx* ctx, int n, const int* ids, void* embeds_out, vv_stream st);
 

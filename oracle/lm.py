@@ -103,3 +103,53 @@ def forward_rows(sd, cfg, x, kvs, commit=True):
         for r in range(R):
             kvs[r].k, kvs[r].v = new_kv[r]
     return rms(h, sd["norm.weight"], eps)
+
+
+def forward_rows_masked(sd, cfg, x, kvs, masks):
+    """One new token per row with an explicit attention mask, the way the
+    reference runs its negative stream (DynamicCache + attention_mask,
+    modeling_vibevoice_inference.py:591-604).
+
+    masks[r]: bool [len_r + 1] over (existing cache entries, the new token).
+    The new token's position is cumsum(mask)[-1] - 1 (HF 4.51.3
+    prepare_inputs_for_generation); its K/V are always appended.
+    """
+    H = cfg["hidden_size"]
+    nh, nkv = cfg["num_attention_heads"], cfg["num_key_value_heads"]
+    d = cfg.get("head_dim") or H // nh
+    eps, theta = cfg["rms_norm_eps"], cfg["rope_theta"]
+    R = x.shape[0]
+    h = x
+    for li in range(cfg["num_hidden_layers"]):
+        p = f"layers.{li}."
+        a = rms(h, sd[p + "input_layernorm.weight"], eps)
+        q = F.linear(a, sd[p + "self_attn.q_proj.weight"], sd[p + "self_attn.q_proj.bias"])
+        k = F.linear(a, sd[p + "self_attn.k_proj.weight"], sd[p + "self_attn.k_proj.bias"])
+        v = F.linear(a, sd[p + "self_attn.v_proj.weight"], sd[p + "self_attn.v_proj.bias"])
+        outs = []
+        for r in range(R):
+            m = masks[r]
+            pos = torch.tensor([int(m.long().sum()) - 1])
+            cos, sin = rope_cos_sin(pos, d, theta, x.dtype)
+            qr = q[r].view(1, nh, d).transpose(0, 1)
+            kr = k[r].view(1, nkv, d).transpose(0, 1)
+            vr = v[r].view(1, nkv, d).transpose(0, 1)
+            qr = qr * cos + _rot(qr) * sin
+            kr = kr * cos + _rot(kr) * sin
+            kc = kr if kvs[r].k[li] is None else torch.cat([kvs[r].k[li], kr], dim=1)
+            vc = vr if kvs[r].v[li] is None else torch.cat([kvs[r].v[li], vr], dim=1)
+            kvs[r].k[li], kvs[r].v[li] = kc, vc
+            rep = nh // nkv
+            kk = kc.repeat_interleave(rep, dim=0)
+            vv = vc.repeat_interleave(rep, dim=0)
+            s = torch.matmul(qr, kk.transpose(1, 2)) * d ** -0.5
+            bias = torch.zeros(kc.shape[1])
+            bias[~m] = float("-inf")
+            pw = F.softmax(s.float() + bias, dim=-1).to(x.dtype)
+            outs.append(torch.matmul(pw, vv).transpose(0, 1).reshape(1, nh * d))
+        o = F.linear(torch.stack(outs), sd[p + "self_attn.o_proj.weight"])
+        h = h + o
+        a = rms(h, sd[p + "post_attention_layernorm.weight"], eps)
+        h = h + F.linear(F.silu(F.linear(a, sd[p + "mlp.gate_proj.weight"])) * F.linear(a, sd[p + "mlp.up_proj.weight"]),
+                         sd[p + "mlp.down_proj.weight"])
+    return rms(h, sd["norm.weight"], eps)

@@ -1,0 +1,64 @@
+"""End-to-end generate() on the GPU vs the oracle's literal restatement of the
+reference loop (oracle/loop.py: negative stream kept as cache + attention mask
+with the reference's in-place reset / shift, modeling_vibevoice_inference.py:
+563-580, 609-639).
+
+B = 2 left-padded text prompts, forced token schedules that exercise:
+diffusion steps for both samples, speech_end (codec reset), speech_start
+(negative reset) while the other sample diffuses, the skip correction,
+the reference's KV-shift boundary case (a sample with one committed negative
+entry skipped at the next pass), and eos.  Both refresh_negative modes.
+Tolerance: audio / latent rel L2 < 5e-2 and cosine > 0.998 (bf16 model, the
+error compounds through the autoregressive feedback); token sequences equal.
+"""
+import types
+
+import pytest
+import torch
+
+from gpu_util import cos, rel_err
+from oracle import loop as oloop
+from tiny import tiny_config
+from vibevoice_amd.modeling_vibevoice_inference import VibeVoiceForConditionalGenerationInference
+from vibevoice_amd.weights import synthetic_state_dict
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+IDS = dict(eos=151643, start=151652, end=151653, diffusion=151654)
+D, E, S, X = IDS["diffusion"], IDS["end"], IDS["start"], IDS["eos"]
+TOK = types.SimpleNamespace(speech_start_id=S, speech_end_id=E, speech_diffusion_id=D, eos_token_id=X,
+                            bos_token_id=None, pad_token_id=151655)
+
+SCHEDULES = [
+    [D, D, D, D, D, E, S, D, X],
+    [D, E, D, D, S, D, D, X],   # step 1: skip with one committed entry (KV-shift boundary case)
+]
+
+
+@pytest.mark.parametrize("refresh_negative", [True, False])
+def test_generate_matches_reference_loop(refresh_negative):
+    cfg = tiny_config(hidden=256, layers=2, heads=2, kv_heads=1, inter=512)
+    sd = synthetic_state_dict(cfg, seed=21, device="cpu", mode="test", with_acoustic_encoder=False)
+    model = VibeVoiceForConditionalGenerationInference(cfg, sd, dev, max_batch=2, max_ctx=128)
+    model.set_ddpm_inference_steps(5)
+    g = torch.Generator().manual_seed(2)
+    ids = torch.randint(0, 151000, (2, 10), generator=g)
+    mask = torch.ones(2, 10, dtype=torch.long)
+    mask[1, :3] = 0
+    ids[1, :3] = TOK.pad_token_id
+    torch.manual_seed(1234)
+    out = model.generate(input_ids=ids, attention_mask=mask, tokenizer=TOK, cfg_scale=1.3,
+                         forced_tokens=SCHEDULES, refresh_negative=refresh_negative, show_progress_bar=False)
+    torch.cuda.synchronize()
+    torch.manual_seed(1234)
+    rec = {}
+    seqs, audio, reach = oloop.generate(sd, cfg, ids, mask, IDS, ddpm_steps=5, cfg_scale=1.3, forced=SCHEDULES,
+                                        refresh_negative=refresh_negative, record=rec)
+    assert torch.equal(out.sequences, seqs)
+    assert torch.equal(out.reach_max_step_sample.cpu(), reach)
+    for b in range(2):
+        got, ref = out.speech_outputs[b], audio[b]
+        assert got.shape == ref.shape, (got.shape, ref.shape)
+        e, c = rel_err(got, ref), cos(got, ref)
+        print(f"sample {b} audio rel_err {e:.3e} cos {c:.6f} samples {ref.shape[-1]}")
+        assert e < 5e-2 and c > 0.998

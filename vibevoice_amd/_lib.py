@@ -39,6 +39,7 @@ EXPORTS = [
     ("vv_set_valid_ids", I, [P, I, ctypes.POINTER(I)]),
     ("vv_set_schedule", I, [P, I, ctypes.POINTER(F), P, P]),
     ("vv_lm_forward", I, [P, I, P, P, P, I, I, P, P, P, P]),
+    ("vv_kv_copy", I, [P, I, P, P, P, P]),
     ("vv_embed", I, [P, I, P, P, P]),
     ("vv_diffusion_sample", I, [P, I, P, P, P, F, P]),
     ("vv_codec_step", I, [P, I, P, P, P, P, P, P, P]),

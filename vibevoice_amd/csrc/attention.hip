@@ -214,3 +214,29 @@ int launch_lmhead_ids(int R, int H, const bf16* h, long long ldh, const bf16* W,
   hipLaunchKernelGGL(k_lmhead_ids, dim3(R), dim3(256), 0, st, R, H, h, ldh, W, ids, nid, out);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
+
+// ---------------------------------------------------------------- KV entry copy
+// cache[slot][*][dst] = cache[slot][*][src] for every layer / kv head (K and V).
+// Used for the reference's negative-stream shift whose KV boundary test
+// (modeling_vibevoice_inference.py:628) differs from the mask's (:618): when
+// it leaves the KV unshifted, the just-computed entry takes the place of the
+// previous one.
+__global__ void __launch_bounds__(256) k_kv_copy(KVLayout kv, int n_layers, int nkv, const int* slots,
+                                                 const int* src, const int* dst) {
+  const int i = blockIdx.x;
+  const int d = kv.d;
+  const int per = n_layers * nkv * d;
+  for (int e = threadIdx.x; e < per; e += blockDim.x) {
+    const int l = e / (nkv * d), r = e - l * nkv * d, h = r / d, j = r - h * d;
+    const long long b = (long long)l * kv.s_layer + (long long)slots[i] * kv.s_slot + (long long)h * kv.s_head + j;
+    kv.k[b + (long long)dst[i] * d] = kv.k[b + (long long)src[i] * d];
+    kv.v[b + (long long)dst[i] * d] = kv.v[b + (long long)src[i] * d];
+  }
+}
+
+int launch_kv_copy(KVLayout kv, int n_layers, int nkv, int n, const int* slots, const int* src, const int* dst,
+                   hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_kv_copy, dim3(n), dim3(256), 0, st, kv, n_layers, nkv, slots, src, dst);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

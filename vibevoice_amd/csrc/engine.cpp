@@ -620,6 +620,12 @@ int vv_set_schedule(vv_ctx* c, int steps, const float* coef, const void* tfreq, 
   return 0;
 }
 
+int vv_kv_copy(vv_ctx* c, int n, const int* slots, const int* src, const int* dst, vv_stream vst) {
+  if (!c->finalized) FAIL("vv_kv_copy before vv_finalize");
+  KCHK(launch_kv_copy(c->kv, c->cfg.n_layers, c->cfg.n_kv_heads, n, slots, src, dst, (hipStream_t)vst));
+  return 0;
+}
+
 int vv_embed(vv_ctx* c, int n, const int* ids, void* out, vv_stream vst) {
   const int H = c->cfg.hidden;
   KCHK(launch_gather_rows(n, H, W(c, "lm.embed"), H, ids, rowmap(out, H), (hipStream_t)vst));

@@ -110,6 +110,8 @@ int launch_gather_rows(int n, int C, const bf16* src, long long lds, const int* 
 int launch_rope_kv(RopeArgs a, hipStream_t st);
 int attn_nsplit(int max_len);
 int launch_attn(AttnArgs a, hipStream_t st);
+int launch_kv_copy(KVLayout kv, int n_layers, int nkv, int n, const int* slots, const int* src, const int* dst,
+                   hipStream_t st);
 int launch_lmhead_ids(int R, int H, const bf16* h, long long ldh, const bf16* W, const int* ids, int nid, float* out,
                       hipStream_t st);
 

@@ -128,6 +128,10 @@ class Engine:
                    "lm_forward")
         return hidden_out, logits_out
 
+    def kv_copy(self, slots, src, dst, stream=None):
+        _lib.check(_lib.lib().vv_kv_copy(self.h, slots.shape[0], _ptr(slots), _ptr(src), _ptr(dst), _stream(stream)),
+                   "kv_copy")
+
     def embed(self, ids, out=None, stream=None):
         if out is None:
             out = torch.empty(ids.shape[0], self.hidden, dtype=torch.bfloat16, device=self.device)

@@ -189,6 +189,8 @@ class VibeVoiceForConditionalGenerationInference:
         reach_max = torch.zeros(B, dtype=torch.bool)
         pos_len = Li.clone()
         neg_len = torch.zeros(B, dtype=torch.long)
+        correct_cnt = torch.zeros(B, dtype=torch.long)                     # :393
+        neg_passes = 0                                                      # negative cache length (all rows)
         audio_chunks = [[] for _ in range(B)]
         seq = [input_ids.cpu()]
         H = eng.hidden
@@ -244,9 +246,10 @@ class VibeVoiceForConditionalGenerationInference:
                 nxt = torch.tensor(valid)[pick]
             nxt[finished] = eos_id
             seq.append(nxt[:, None])
-            # ---- negative stream when refresh_negative is False (:512-527): committed every step
+            # ---- negative stream when refresh_negative is False (:512-527): run and committed every step
             if not refresh_negative:
                 neg_len += 1
+                neg_passes += 1
             # ---- finish bookkeeping (:530-553)
             new_eos = (nxt == eos_id) & ~finished
             if new_eos.any():
@@ -263,20 +266,27 @@ class VibeVoiceForConditionalGenerationInference:
             if ends.numel():
                 eng.codec_reset(ends.to(**i32))
             starts = ~finished & (nxt == start_id)                          # :563-580
-            if refresh_negative and starts.any():
-                neg_len[starts] = 0
+            if refresh_negative:
+                neg_len[starts] = 0     # mask reset: empty context, next position 0
             next_embeds = eng.embed(nxt.to(**i32))                          # :584
             diff = ~finished & (nxt == diff_id)                             # :588
             if diff.any():
                 didx = torch.nonzero(diff).reshape(-1)
                 n = didx.numel()
-                if refresh_negative:
-                    commit = diff | finished                                # skip correction :609-639
-                    commit &= ~starts
-                    neg_len[commit] += 1
-                else:
-                    undo = ~finished & ~diff                                # correction of the always-run pass
-                    neg_len[undo] -= 1
+                if refresh_negative:                                        # negative pass :591-604
+                    neg_len += 1        # every row appends; rows reset above were computed speculatively
+                    neg_passes += 1     # and are always dropped again below (speech_start != diffusion)
+                # non-diffusion correction (:609-639): drop the entry just appended.  Where the
+                # reference's KV-shift test (:628) skips the shift while the mask shift (:618)
+                # happens (correct_cnt == cache_len - 2), the new entry replaces the previous one.
+                skip = torch.nonzero(~finished & ~diff).reshape(-1)
+                quirk = [b for b in skip.tolist()
+                         if int(correct_cnt[b]) == neg_passes - 2 and int(neg_len[b]) == 2]
+                neg_len[skip] -= 1
+                correct_cnt[skip] += 1
+                if quirk:
+                    q = torch.tensor(quirk)
+                    eng.kv_copy((q + B).to(**i32), torch.ones_like(q).to(**i32), torch.zeros_like(q).to(**i32))
                 pos_h = hid[didx.to(dev)]
                 neg_h = hid[(didx + B).to(dev)]
                 noise = torch.randn(2 * n, self.config.acoustic_vae_dim)    # CPU generator (:716)
