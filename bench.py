@@ -1,0 +1,240 @@
+"""Throughput of VibeVoice's next-token-diffusion generate loop on MI355X.
+
+One bench "step" = one iteration of the reference's generate loop
+(vibevoice/modular/modeling_vibevoice_inference.py:432-690) for every sample
+of the batch, through the product path (GenerateSession.step -> the C-ABI of
+libvibevoice_hip.so): positive + negative Qwen2 decode (batched rows), the
+constrained argmax read back to the host, S-step CFG DPM-Solver++ diffusion
+head, streaming acoustic decode + semantic encode, connectors.  The token
+schedule is forced to `speech_diffusion` (random weights emit arbitrary control
+tokens), so every step emits one 3200-sample audio frame per sample.
+
+Default workload = BASELINE.json configs[1]: VibeVoice-1.5B bf16, 1 speaker
+(3 s voice prompt + 1-sentence script), 10 diffusion steps, TP=1, one MI355X.
+`--batch 8 --speakers 2` is configs[2].  With `--gpus N` (torchrun, one rank
+per GPU) every rank runs its own independent dialogues: DP replicas, no
+collective on the data path (DESIGN.md "Multi-GPU").
+
+Prints ONE JSON line on rank 0 (metric contract: BASELINE.json / SURVEY.md §8d).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+SR, HOP = 24000, 3200
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "audio-sec/wall-sec (RTF) + acoustic tokens/sec, VibeVoice-1.5B at 1/2/4/8 GPU"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=1, help="dialogues per GPU")
+    ap.add_argument("--speakers", type=int, default=1)
+    ap.add_argument("--ddpm-steps", type=int, default=10)
+    ap.add_argument("--model", default="1.5B", choices=["1.5B", "Large"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-tokens", type=int, default=8, help="timed tokens of the CPU oracle sample")
+    return ap.parse_args()
+
+
+# ------------------------------------------------------------------ algorithmic bytes
+def weight_bytes(w):
+    """Bytes of the packed device weights by role (SURVEY.md §8d conventions)."""
+    def sz(pred):
+        return sum(t.numel() * t.element_size() for k, t in w.items() if pred(k))
+    H = w["lm.norm"].numel()
+    return dict(
+        lm=sz(lambda k: k.startswith("lm.") and k.split(".")[1].isdigit()) + sz(lambda k: k == "lm.norm"),
+        lm_head4=4 * H * 2,
+        head_step=sz(lambda k: k.startswith("head.") and k not in ("head.cond_w", "head.t0_w", "head.t2_w")),
+        head_token=sz(lambda k: k == "head.cond_w"),
+        codec=sz(lambda k: k.startswith("dec.") or k.startswith("sem.")),
+        conn=sz(lambda k: k.startswith("conn.")),
+    )
+
+
+def bytes_per_token(wb, cfg, B, S, ctx_pos, ctx_neg):
+    lmc = cfg.decoder_config
+    d = lmc.get("head_dim") or lmc.hidden_size // lmc.num_attention_heads
+    kv_pos = lmc.num_hidden_layers * 2 * lmc.num_key_value_heads * d * 2      # 28,672 B at 1.5B
+    shared = wb["lm"] + wb["lm_head4"] + S * wb["head_step"] + wb["head_token"] + wb["codec"] + wb["conn"]
+    return shared / B + kv_pos * (ctx_pos + ctx_neg + 2)
+
+
+# ------------------------------------------------------------------ dominant kernel, live
+def measure_gemv(model, B, iters=6):
+    """The LM MLP gate|up weight-streaming GEMV (k_gemv, EPI_SILU_MUL): the
+    largest single launch of the loop (2I x H bf16 = 55 MB at 1.5B, 28 per LM
+    pass).  Timed with HIP events on the stream it is launched on, rotating
+    over the 28 layers' weights so the Infinity Cache cannot serve it."""
+    from vibevoice_amd import _lib
+    eng = model.engine
+    lmc = model.config.decoder_config
+    H, I, nl = lmc.hidden_size, lmc.intermediate_size, lmc.num_hidden_layers
+    M = 2 * B
+    A = torch.randn(M, H, device=model.device).bfloat16()
+    Y = torch.empty(M, I, device=model.device, dtype=torch.bfloat16)
+    stream = torch.cuda.current_stream()
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    L = _lib.lib()
+    Ws = [eng.w[f"lm.{l}.gu_w"] for l in range(nl)]
+
+    def run():
+        for Wt in Ws:
+            _lib.check(L.vv_gemm_bf16(M, 2 * I, H, ctypes.c_void_p(A.data_ptr()), H, ctypes.c_void_p(Wt.data_ptr()),
+                                      None, _lib.EPI["silu_mul"], ctypes.c_void_p(Y.data_ptr()), I, None, None,
+                                      eng.h, sp), "gemv")
+    run()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(iters):
+        run()
+    e1.record(stream)
+    e1.synchronize()
+    avg_s = e0.elapsed_time(e1) / 1e3 / (iters * nl)
+    alg = 2 * I * H * 2 + M * H * 2 + M * I * 2
+    ach = alg / avg_s / 1e9
+    return dict(kernel="k_gemv (LM gate|up, EPI_SILU_MUL)", shape=f"M={M} N={2 * I} K={H}", bound="hbm",
+                achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
+                traffic=None, avg_us=round(avg_s * 1e6, 2), alg_bytes_per_launch=alg)
+
+
+# ------------------------------------------------------------------ CPU baseline (oracle)
+def cpu_baseline(cfg, tokens, S):
+    """The oracle's fp32 eager restatement of the reference loop (the
+    reference's own CPU path runs fp32 + eager/sdpa attention,
+    demo/inference_from_file.py:268) on the host cores: text prompt, forced
+    diffusion tokens.  Per-token time = (T(1 + k tokens) - T(1 token)) / k."""
+    from oracle import loop as oloop
+    from vibevoice_amd.weights import synthetic_state_dict
+    from vibevoice_amd.synthetic import synthetic_inputs, tokenizer_ids
+    torch.manual_seed(0)
+    sd = synthetic_state_dict(cfg, seed=0, device="cpu", dtype=torch.float32, with_acoustic_encoder=False)
+    inp = synthetic_inputs(batch=1, speakers=1, voice_seconds=0, text_tokens=16, seed=1)
+    tk = tokenizer_ids()
+    ids = dict(eos=tk.eos_token_id, start=tk.speech_start_id, end=tk.speech_end_id, diffusion=tk.speech_diffusion_id)
+
+    def run(k):
+        forced = [[tk.speech_diffusion_id] * k + [tk.eos_token_id]]
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            oloop.generate(sd, cfg, inp["input_ids"], inp["attention_mask"], ids, ddpm_steps=S, cfg_scale=1.3,
+                           forced=forced, dtype=torch.float32)
+        return time.perf_counter() - t0
+    run(1)                                   # warm-up (allocator, thread pool)
+    t1 = run(1)
+    tk_ = run(1 + tokens)
+    per = (tk_ - t1) / tokens
+    tps = 1.0 / per
+    return dict(value=round(tps * HOP / SR, 4), unit="audio-sec/wall-sec", tokens_per_s=round(tps, 3),
+                cores=torch.get_num_threads(), kind="port",
+                sample=f"oracle/loop.py fp32 eager on CPU, VibeVoice-1.5B shapes (seeded random weights), "
+                       f"B=1, S={S}, {tokens} timed diffusion tokens after a 1-token run (difference of two runs)")
+
+
+# ------------------------------------------------------------------ main
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from vibevoice_amd.modeling_vibevoice_inference import VibeVoiceForConditionalGenerationInference
+    from vibevoice_amd.synthetic import synthetic_inputs, tokenizer_ids
+
+    B, S, K, W = args.batch, args.ddpm_steps, args.steps, args.warmup
+    inp = synthetic_inputs(batch=B, speakers=args.speakers, voice_seconds=3.0, text_tokens=64, seed=100 + rank)
+    L = inp["input_ids"].shape[1]
+    total = W + K + 4
+    model = VibeVoiceForConditionalGenerationInference.from_pretrained(
+        f"synthetic:{args.model}", device_map=str(dev), synthetic_seed=0, max_batch=B, max_ctx=L + total + 8)
+    model.set_ddpm_inference_steps(S)
+    tk = tokenizer_ids()
+    forced = [[tk.speech_diffusion_id] * total for _ in range(B)]
+    torch.manual_seed(1234)
+    sess = model.generate_session(**inp, tokenizer=tk, cfg_scale=1.3, generation_config={"do_sample": False},
+                                  forced_tokens=forced, max_length_times=total / L + 1, max_new_tokens=total + 2)
+    for _ in range(W):
+        assert sess.step()
+    ctx0 = int(sess.pos_len.float().mean())
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        assert sess.step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    barrier()
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+    ctx1 = int(sess.pos_len.float().mean())
+
+    tokens = B * K * world
+    tps = tokens / dt
+    audio_per_s = tps * HOP / SR
+    wb = weight_bytes(model.engine.w)
+    ctx_avg = (ctx0 + ctx1) / 2
+    bpt = bytes_per_token(wb, model.config, B, S, ctx_avg, (ctx0 + ctx1) / 2 - L)
+    step_ach = bpt * B / (dt / K) / 1e9
+    roof = measure_gemv(model, B)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(model.config, args.cpu_tokens, S)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(audio_per_s, 3),
+            "unit": "audio-sec/wall-sec",
+            "acoustic_tokens_per_sec": round(tps, 2),
+            "rtf_wall_per_audio": round(1.0 / audio_per_s, 5),
+            "n_gpus": world, "steps": K, "warmup": W,
+            "ms_per_step": round(dt / K * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic: seeded random-init VibeVoice weights at real shapes, seeded -25 dBFS noise voice "
+                    "prompt (3 s/speaker), random script ids in the processor's prompt layout, forced "
+                    "speech_diffusion schedule (constrained argmax still computed and read back each step)",
+            "config": {"workload": f"VibeVoice-{args.model} bf16, {B} dialogue(s)/GPU x {args.speakers} speaker(s), "
+                                   f"{S} diffusion steps, TP=1, prompt {L} tokens",
+                       "model": f"VibeVoice-{args.model}", "global_batch": B * world, "seq_len": L,
+                       "diffusion_steps": S, "parallelism": f"dp{world} (independent replicas), tp1"},
+            "roofline": roof,
+            "step_roofline": {"bound": "hbm", "achieved": round(step_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(step_ach / HBM_PEAK_GBS, 4),
+                              "alg_bytes_per_token": int(bpt), "note": "whole loop iteration, SURVEY.md §8d bytes"},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

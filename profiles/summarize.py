@@ -1,0 +1,59 @@
+"""Summarise a rocprofv3 --kernel-trace CSV of `bench.py` per generate-loop step.
+
+Steps are delimited by the restricted lm_head launch (k_lmhead_ids, one per LM
+pass).  For the last N steps it reports GPU busy time, wall time, idle gap and
+the per-kernel (name, grid) breakdown, plus each kernel's average duration.
+Usage: python profiles/summarize.py <run_kernel_trace.csv> [n_steps]
+"""
+import collections
+import csv
+import sys
+
+
+def short(name):
+    n = name.split("(")[0]
+    if n.startswith("void "):
+        n = n[5:]
+    if "at::native" in n:
+        n = "torch:" + n.split("::")[-1][:40]
+    return n[:60]
+
+
+def main(path, n_steps=None):
+    rows = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]),
+                         (int(r["Grid_Size_X"]), int(r["Grid_Size_Y"]))))
+    rows.sort()
+    marks = [i for i, r in enumerate(rows) if r[2] == "k_lmhead_ids"]
+    steps = list(zip(marks[:-1], marks[1:]))
+    # the bench's timed steps are the last ones before the standalone gemv measurement
+    if n_steps:
+        steps = steps[-n_steps:]
+    busy = wall = 0
+    per = collections.defaultdict(lambda: [0, 0])
+    for a, b in steps:
+        seg = rows[a + 1:b + 1]
+        wall += rows[b][0] - rows[a + 1][0]
+        for s, e, n, g in seg[:-1]:
+            busy += e - s
+            per[(n, g)][0] += 1
+            per[(n, g)][1] += e - s
+    k = len(steps)
+    print(f"steps {k}: wall/step {wall / k / 1e3:.1f} us, GPU busy/step {busy / k / 1e3:.1f} us, "
+          f"launches/step {sum(v[0] for v in per.values()) / k:.0f}")
+    byname = collections.defaultdict(lambda: [0, 0])
+    for (n, g), (c, t) in per.items():
+        byname[n][0] += c
+        byname[n][1] += t
+    print(f"{'kernel':60s} {'calls/step':>10s} {'us/step':>9s} {'avg us':>8s}")
+    for n, (c, t) in sorted(byname.items(), key=lambda x: -x[1][1]):
+        print(f"{n:60s} {c / k:10.1f} {t / k / 1e3:9.1f} {t / c / 1e3:8.2f}")
+    print("\nby (kernel, grid), top 30:")
+    for (n, g), (c, t) in sorted(per.items(), key=lambda x: -x[1][1])[:30]:
+        print(f"{n:40s} {str(g):>16s} {c / k:8.1f}/step {t / k / 1e3:9.1f} us/step  avg {t / c / 1e3:8.2f} us")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else None)

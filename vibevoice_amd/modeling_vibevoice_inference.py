@@ -146,162 +146,248 @@ class VibeVoiceForConditionalGenerationInference:
     def generate(self, inputs=None, generation_config=None, audio_streamer=None, speech_tensors=None,
                  speech_masks=None, speech_input_mask=None, return_speech=True, cfg_scale=1.0,
                  stop_check_fn=None, **kwargs):
+        """The reference's generate() (modeling_vibevoice_inference.py:327-710), same
+        arguments and return type.  Extra keyword (bench / tests only):
+        `forced_tokens` = per-sample token schedule that replaces the constrained
+        argmax (the argmax is still computed and read back every step)."""
+        verbose = kwargs.get("verbose", False)
+        sess = self.generate_session(inputs, generation_config, audio_streamer, speech_tensors, speech_masks,
+                                     speech_input_mask, cfg_scale, stop_check_fn, **kwargs)
+        rng = range(sess.max_steps)
+        if kwargs.get("show_progress_bar", True) and verbose:
+            from tqdm import tqdm
+            rng = tqdm(rng, desc="Generating", leave=True, ncols=100, mininterval=0.5)
+        for _ in rng:
+            if not sess.step():
+                break
+        return sess.result(return_speech)
+
+    @torch.no_grad()
+    def generate_session(self, inputs=None, generation_config=None, audio_streamer=None, speech_tensors=None,
+                         speech_masks=None, speech_input_mask=None, cfg_scale=1.0, stop_check_fn=None, **kwargs):
+        """generate() split into prefill (done here) + one `step()` per loop iteration."""
+        return GenerateSession(self, inputs, generation_config, audio_streamer, speech_tensors, speech_masks,
+                               speech_input_mask, cfg_scale, stop_check_fn, **kwargs)
+
+
+class _Staging:
+    """Pinned host ring -> device copies for the loop's small per-step operands
+    (positions, slot lists, noise).  One async H2D each; the ring is drained
+    (stream sync) only when it wraps."""
+
+    def __init__(self, dev, dtype, n):
+        self.host = torch.empty(n, dtype=dtype, pin_memory=True)
+        self.dev = torch.empty(n, dtype=dtype, device=dev)
+        self.n, self.off = n, 0
+
+    def put(self, values):
+        t = torch.as_tensor(values).reshape(-1).to(self.host.dtype)
+        k = t.numel()
+        if k > self.n:
+            raise ValueError("staging ring too small")
+        if self.off + k > self.n:
+            torch.cuda.current_stream().synchronize()
+            self.off = 0
+        h = self.host[self.off:self.off + k]
+        h.copy_(t)
+        d = self.dev[self.off:self.off + k]
+        d.copy_(h, non_blocking=True)
+        self.off = (self.off + k + 63) // 64 * 64
+        return d
+
+
+class GenerateSession:
+    """State of one generate() call (modeling_vibevoice_inference.py:327-710).
+
+    Host side holds only the reference's control state (finished / reach_max /
+    per-sample lengths / token ids); every tensor of the loop body lives on the
+    device and every op on it is a libvibevoice_hip.so call.
+    """
+
+    def __init__(self, model, inputs, generation_config, audio_streamer, speech_tensors, speech_masks,
+                 speech_input_mask, cfg_scale, stop_check_fn, **kwargs):
         tokenizer = kwargs.pop("tokenizer", None)
         kwargs.pop("parsed_scripts", None)
         kwargs.pop("all_speakers_list", None)
-        max_length_times = kwargs.pop("max_length_times", 2)
-        refresh_negative = kwargs.get("refresh_negative", True)
-        verbose = kwargs.get("verbose", False)
-        forced = kwargs.get("forced_tokens", None)      # bench / test hook: fixed token schedule
+        self.m = model
+        self.max_length_times = kwargs.pop("max_length_times", 2)
+        self.refresh_negative = kwargs.get("refresh_negative", True)
+        self.forced = kwargs.get("forced_tokens", None)
+        self.cfg_scale = cfg_scale
+        self.stop_check_fn = stop_check_fn
+        self.audio_streamer = audio_streamer
         input_ids = kwargs["input_ids"] if inputs is None else inputs
         attention_mask = kwargs.get("attention_mask")
         if attention_mask is None:
             attention_mask = torch.ones_like(input_ids)
         gen = dict(generation_config or {})
-        do_sample = bool(gen.get("do_sample", False))
+        self.do_sample = bool(gen.get("do_sample", False))
 
-        dev, eng = self.device, self.engine
+        dev, eng = model.device, model.engine
+        self.dev, self.eng = dev, eng
         B, L = input_ids.shape
-        lmc = self.config.decoder_config
+        self.B, self.L = B, L
+        lmc = model.config.decoder_config
         max_new = kwargs.get("max_new_tokens")
         if max_new is None:
             max_new = lmc.max_position_embeddings - L                      # :371-372
-        max_length = gen.get("max_length") or (L + max_new)
+        self.max_length = gen.get("max_length") or (L + max_new)
         Li = attention_mask.sum(-1).cpu().long()
-        max_steps = min(max_length - L, int(max_length_times * L))          # :421
-        per_sample_max = torch.minimum(max_length - Li, (max_length_times * Li).long())  # :422
+        self.max_steps = min(self.max_length - L, int(self.max_length_times * L))        # :421
+        self.per_sample_max = torch.minimum(self.max_length - Li, (self.max_length_times * Li).long())  # :422
 
-        start_id, end_id = tokenizer.speech_start_id, tokenizer.speech_end_id
-        diff_id, eos_id = tokenizer.speech_diffusion_id, tokenizer.eos_token_id
-        valid = [start_id, end_id, diff_id, eos_id]                          # :405-413
+        self.start_id, self.end_id = tokenizer.speech_start_id, tokenizer.speech_end_id
+        self.diff_id, self.eos_id = tokenizer.speech_diffusion_id, tokenizer.eos_token_id
+        self.valid = [self.start_id, self.end_id, self.diff_id, self.eos_id]                # :405-413
         bos = getattr(tokenizer, "bos_token_id", None)
         if bos is not None:
             raise NotImplementedError("a bos id in the constrained set (Qwen tokenizers have none)")
-        order = sorted(range(4), key=lambda j: valid[j])                    # argmax ties -> lowest id
-        eng.set_valid_ids(valid)
-        eng.set_steps(self.ddpm_inference_steps)
-        need_ctx = int(Li.max()) + max_steps + 2
+        self.order = sorted(range(4), key=lambda j: self.valid[j])         # argmax ties -> lowest id
+        eng.set_valid_ids(self.valid)
+        eng.set_steps(model.ddpm_inference_steps)
+        need_ctx = int(Li.max()) + self.max_steps + 2
         if need_ctx > eng.max_ctx or B > eng.max_batch:
             raise RuntimeError(f"engine capacity (batch {eng.max_batch}, ctx {eng.max_ctx}) < request "
                                f"(batch {B}, ctx {need_ctx}); construct with larger max_batch/max_ctx")
 
-        finished = torch.zeros(B, dtype=torch.bool)
-        reach_max = torch.zeros(B, dtype=torch.bool)
-        pos_len = Li.clone()
-        neg_len = torch.zeros(B, dtype=torch.long)
-        correct_cnt = torch.zeros(B, dtype=torch.long)                     # :393
-        neg_passes = 0                                                      # negative cache length (all rows)
-        audio_chunks = [[] for _ in range(B)]
-        seq = [input_ids.cpu()]
-        H = eng.hidden
+        self.finished = torch.zeros(B, dtype=torch.bool)
+        self.reach_max = torch.zeros(B, dtype=torch.bool)
+        self.pos_len = Li.clone()
+        self.neg_len = torch.zeros(B, dtype=torch.long)
+        self.correct_cnt = torch.zeros(B, dtype=torch.long)                # :393
+        self.neg_passes = 0                                                # negative cache length (all rows)
+        self.audio_chunks = [[] for _ in range(B)]
+        self.seq = [input_ids.cpu()]
+        self.step_idx = 0
+        self.done = False
         i32 = dict(device=dev, dtype=torch.int32)
+        self.ints = _Staging(dev, torch.int32, 1 << 16)
+        self.lat = _Staging(dev, model.dtype, 1 << 16)
+        self.rows2 = torch.arange(2 * B, **i32)                           # LM rows: [positive B | negative B]
+        self.valid_t = torch.tensor(self.valid)
+        self.order_t = torch.tensor(self.order)
 
         # ---- step 0: positive prefill rows + speculative negative [speech_start] rows
-        emb = self._prompt_embeds(input_ids.to(dev), attention_mask.to(dev), speech_tensors, speech_masks,
-                                  speech_input_mask)
-        neg_in = eng.embed(torch.full((B,), start_id, **i32))
+        emb = model._prompt_embeds(input_ids.to(dev), attention_mask.to(dev), speech_tensors, speech_masks,
+                                   speech_input_mask)
+        neg_in = eng.embed(torch.full((B,), self.start_id, **i32))
         ntok = emb.shape[0]
         tok_slot = torch.cat([torch.repeat_interleave(torch.arange(B), Li), torch.arange(B, 2 * B)])
         tok_pos = torch.cat([torch.cat([torch.arange(int(n)) for n in Li]), torch.zeros(B, dtype=torch.long)])
         last = torch.cumsum(Li, 0) - 1
         out_idx = torch.cat([last, torch.arange(ntok, ntok + B)])
         step_in = torch.cat([emb, neg_in], 0)
-        hid, logits = eng.lm_forward(step_in, tok_slot.to(**i32), tok_pos.to(**i32), out_idx.to(**i32),
-                                     max_pos=int(tok_pos.max()))
-        inputs_embeds = None
-        rng = range(max_steps)
-        if kwargs.get("show_progress_bar", True) and verbose:
-            from tqdm import tqdm
-            rng = tqdm(rng, desc="Generating", leave=True, ncols=100, mininterval=0.5)
-        for step in rng:
-            if stop_check_fn is not None and stop_check_fn():                # :434-440
-                if audio_streamer is not None:
-                    audio_streamer.end()
-                break
-            if audio_streamer is not None and any(getattr(audio_streamer, "finished_flags", [])):
-                break
-            if bool(finished.all()):
-                break
-            if L + step >= max_length:                                      # :454-459
-                reach_max[~finished] = True
-                break
-            if step > 0:
-                slots = torch.cat([torch.arange(B), torch.arange(B, 2 * B)])
-                pos = torch.cat([pos_len, neg_len])
-                in2 = torch.cat([inputs_embeds, inputs_embeds], 0)          # negative consumes the same input
-                hid, logits = eng.lm_forward(in2, slots.to(**i32), pos.to(**i32), torch.arange(2 * B).to(**i32),
-                                             max_pos=int(pos.max()))
-                pos_len += 1
-            # ---- token choice (:494-509)
-            if forced is not None:
-                nxt = torch.tensor([forced[b][step] if step < len(forced[b]) else eos_id for b in range(B)])
+        self.hid, self.logits = eng.lm_forward(step_in, tok_slot.to(**i32), tok_pos.to(**i32), out_idx.to(**i32),
+                                               max_pos=int(tok_pos.max()))
+        self.inputs_embeds = None
+
+    # ---------------------------------------------------------------- one iteration
+    def step(self):
+        """One iteration of the reference loop (:432-690).  Returns False (and
+        does nothing) once the loop has ended."""
+        if self.done or self.step_idx >= self.max_steps:
+            self.done = True
+            return False
+        B, eng, dev, step = self.B, self.eng, self.dev, self.step_idx
+        st = self.audio_streamer
+        if self.stop_check_fn is not None and self.stop_check_fn():       # :434-440
+            if st is not None:
+                st.end()
+            self.done = True
+            return False
+        if st is not None and any(getattr(st, "finished_flags", [])):     # :443-447
+            self.done = True
+            return False
+        if bool(self.finished.all()):                                      # :449
+            self.done = True
+            return False
+        if self.L + step >= self.max_length:                               # :454-459
+            self.reach_max[~self.finished] = True
+            self.done = True
+            return False
+        if step > 0:
+            pos = torch.cat([self.pos_len, self.neg_len])
+            in2 = torch.cat([self.inputs_embeds, self.inputs_embeds], 0)   # negative consumes the same input
+            self.hid, self.logits = eng.lm_forward(in2, self.rows2, self.ints.put(pos), self.rows2,
+                                                   max_pos=int(pos.max()))
+            self.pos_len += 1
+        # ---- token choice (:494-509); the argmax is always read back, as in the reference
+        lg = self.logits[:B].float().cpu()
+        if self.do_sample:
+            pick = torch.multinomial(torch.softmax(lg, -1), 1).squeeze(1)
+        else:
+            pick = self.order_t[lg[:, self.order].argmax(-1)]
+        nxt = self.valid_t[pick]
+        if self.forced is not None:
+            nxt = torch.tensor([f[step] if step < len(f) else self.eos_id for f in self.forced])
+        finished = self.finished
+        nxt[finished] = self.eos_id
+        self.seq.append(nxt[:, None])
+        # ---- negative stream when refresh_negative is False (:512-527): run and committed every step
+        if not self.refresh_negative:
+            self.neg_len += 1
+            self.neg_passes += 1
+        # ---- finish bookkeeping (:530-553)
+        new_eos = (nxt == self.eos_id) & ~finished
+        if new_eos.any():
+            finished |= new_eos
+            if st is not None:
+                st.end(torch.nonzero(new_eos).reshape(-1))
+        hit_max = (step >= self.per_sample_max) & ~finished
+        if hit_max.any():
+            finished |= hit_max
+            self.reach_max |= hit_max
+            if st is not None:
+                st.end(torch.nonzero(hit_max).reshape(-1))
+        ends = torch.nonzero(nxt == self.end_id).reshape(-1)              # :556-560
+        if ends.numel():
+            eng.codec_reset(self.ints.put(ends))
+        starts = ~finished & (nxt == self.start_id)                         # :563-580
+        if self.refresh_negative:
+            self.neg_len[starts] = 0     # mask reset: empty context, next position 0
+        next_embeds = eng.embed(self.ints.put(nxt))                        # :584
+        diff = ~finished & (nxt == self.diff_id)                            # :588
+        if diff.any():
+            didx = torch.nonzero(diff).reshape(-1)
+            n = didx.numel()
+            if self.refresh_negative:                                       # negative pass :591-604
+                self.neg_len += 1    # every row appends; rows reset above were computed speculatively
+                self.neg_passes += 1  # and are always dropped again below (speech_start != diffusion)
+            # non-diffusion correction (:609-639): drop the entry just appended.  Where the
+            # reference's KV-shift test (:628) skips the shift while the mask shift (:618)
+            # happens (correct_cnt == cache_len - 2), the new entry replaces the previous one.
+            skip = torch.nonzero(~finished & ~diff).reshape(-1)
+            quirk = [b for b in skip.tolist()
+                     if int(self.correct_cnt[b]) == self.neg_passes - 2 and int(self.neg_len[b]) == 2]
+            self.neg_len[skip] -= 1
+            self.correct_cnt[skip] += 1
+            if quirk:
+                q = torch.tensor(quirk)
+                eng.kv_copy(self.ints.put(q + B), self.ints.put(torch.ones_like(q)),
+                            self.ints.put(torch.zeros_like(q)))
+            d32 = self.ints.put(didx)
+            if n == B:
+                pos_h, neg_h = self.hid[:B], self.hid[B:]
             else:
-                lg = logits[:B].float().cpu()
-                if do_sample:
-                    pr = torch.softmax(lg, -1)
-                    pick = torch.multinomial(pr, 1).squeeze(1)
-                else:
-                    lg_sorted = lg[:, order]
-                    pick = torch.tensor(order)[lg_sorted.argmax(-1)]
-                nxt = torch.tensor(valid)[pick]
-            nxt[finished] = eos_id
-            seq.append(nxt[:, None])
-            # ---- negative stream when refresh_negative is False (:512-527): run and committed every step
-            if not refresh_negative:
-                neg_len += 1
-                neg_passes += 1
-            # ---- finish bookkeeping (:530-553)
-            new_eos = (nxt == eos_id) & ~finished
-            if new_eos.any():
-                finished |= new_eos
-                if audio_streamer is not None:
-                    audio_streamer.end(torch.nonzero(new_eos).reshape(-1))
-            hit_max = (step >= per_sample_max) & ~finished
-            if hit_max.any():
-                finished |= hit_max
-                reach_max |= hit_max
-                if audio_streamer is not None:
-                    audio_streamer.end(torch.nonzero(hit_max).reshape(-1))
-            ends = torch.nonzero(nxt == end_id).reshape(-1)                # :556-560
-            if ends.numel():
-                eng.codec_reset(ends.to(**i32))
-            starts = ~finished & (nxt == start_id)                          # :563-580
-            if refresh_negative:
-                neg_len[starts] = 0     # mask reset: empty context, next position 0
-            next_embeds = eng.embed(nxt.to(**i32))                          # :584
-            diff = ~finished & (nxt == diff_id)                             # :588
-            if diff.any():
-                didx = torch.nonzero(diff).reshape(-1)
-                n = didx.numel()
-                if refresh_negative:                                        # negative pass :591-604
-                    neg_len += 1        # every row appends; rows reset above were computed speculatively
-                    neg_passes += 1     # and are always dropped again below (speech_start != diffusion)
-                # non-diffusion correction (:609-639): drop the entry just appended.  Where the
-                # reference's KV-shift test (:628) skips the shift while the mask shift (:618)
-                # happens (correct_cnt == cache_len - 2), the new entry replaces the previous one.
-                skip = torch.nonzero(~finished & ~diff).reshape(-1)
-                quirk = [b for b in skip.tolist()
-                         if int(correct_cnt[b]) == neg_passes - 2 and int(neg_len[b]) == 2]
-                neg_len[skip] -= 1
-                correct_cnt[skip] += 1
-                if quirk:
-                    q = torch.tensor(quirk)
-                    eng.kv_copy((q + B).to(**i32), torch.ones_like(q).to(**i32), torch.zeros_like(q).to(**i32))
-                pos_h = hid[didx.to(dev)]
-                neg_h = hid[(didx + B).to(dev)]
-                noise = torch.randn(2 * n, self.config.acoustic_vae_dim)    # CPU generator (:716)
-                x = noise[:n].to(device=dev, dtype=self.dtype).contiguous()
-                eng.diffusion_sample(pos_h.contiguous(), neg_h.contiguous(), x, cfg_scale)
-                audio = torch.empty(n, eng.hop, dtype=self.dtype, device=dev)
-                d32 = didx.to(**i32)
-                eng.codec_step(d32, x, audio, embeds_out=next_embeds, embed_rows=d32)
-                for i, b in enumerate(didx.tolist()):
-                    audio_chunks[b].append(audio[i:i + 1])
-                if audio_streamer is not None:
-                    audio_streamer.put(audio[:, None, :], didx)
-            inputs_embeds = next_embeds
-        if audio_streamer is not None:
-            audio_streamer.end()
-        outs = [torch.cat(c, dim=-1) if c else None for c in audio_chunks]
-        return VibeVoiceGenerationOutput(sequences=torch.cat(seq, dim=1), speech_outputs=outs if return_speech else None,
-                                         reach_max_step_sample=reach_max)
+                pos_h = self.hid.index_select(0, d32)
+                neg_h = self.hid.index_select(0, d32 + B)
+            noise = torch.randn(2 * n, self.m.config.acoustic_vae_dim)    # CPU generator (:716)
+            x = self.lat.put(noise[:n].to(self.m.dtype)).view(n, -1)
+            eng.diffusion_sample(pos_h, neg_h, x, self.cfg_scale)
+            audio = torch.empty(n, eng.hop, dtype=self.m.dtype, device=dev)
+            eng.codec_step(d32, x, audio, embeds_out=next_embeds, embed_rows=d32)
+            for i, b in enumerate(didx.tolist()):
+                self.audio_chunks[b].append(audio[i:i + 1])
+            if st is not None:
+                st.put(audio[:, None, :], didx)
+        self.inputs_embeds = next_embeds
+        self.step_idx += 1
+        return True
+
+    def result(self, return_speech=True):
+        if self.audio_streamer is not None:
+            self.audio_streamer.end()
+        outs = [torch.cat(c, dim=-1) if c else None for c in self.audio_chunks]
+        return VibeVoiceGenerationOutput(sequences=torch.cat(self.seq, dim=1),
+                                         speech_outputs=outs if return_speech else None,
+                                         reach_max_step_sample=self.reach_max)
