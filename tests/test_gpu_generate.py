@@ -62,3 +62,25 @@ def test_generate_matches_reference_loop(refresh_negative):
         e, c = rel_err(got, ref), cos(got, ref)
         print(f"sample {b} audio rel_err {e:.3e} cos {c:.6f} samples {ref.shape[-1]}")
         assert e < 5e-2 and c > 0.998
+
+
+def test_graph_replay_matches_eager():
+    """The hipGraph-captured loop body replays exactly the eager kernel sequence."""
+    cfg = tiny_config(hidden=256, layers=2, heads=2, kv_heads=1, inter=512)
+    sd = synthetic_state_dict(cfg, seed=5, device="cpu", mode="test", with_acoustic_encoder=False)
+    model = VibeVoiceForConditionalGenerationInference(cfg, sd, dev, max_batch=2, max_ctx=128)
+    model.set_ddpm_inference_steps(5)
+    g = torch.Generator().manual_seed(3)
+    ids = torch.randint(0, 151000, (2, 12), generator=g)
+    mask = torch.ones(2, 12, dtype=torch.long)
+    sched = [[D] * 6 + [E, S] + [D] * 4 + [X], [D] * 3 + [S] + [D] * 8 + [X]]
+    outs = []
+    for graphs in (False, True, True):
+        torch.manual_seed(77)
+        outs.append(model.generate(input_ids=ids, attention_mask=mask, tokenizer=TOK, cfg_scale=1.3,
+                                   forced_tokens=sched, use_graphs=graphs, show_progress_bar=False))
+    assert len(model._graph_cache) >= 2
+    for o in outs[1:]:
+        assert torch.equal(o.sequences, outs[0].sequences)
+        for b in range(2):
+            assert torch.equal(o.speech_outputs[b].cpu(), outs[0].speech_outputs[b].cpu())

@@ -44,128 +44,202 @@ __global__ void __launch_bounds__(256) k_rope_kv(RopeArgs a) {
 }
 
 // ---------------------------------------------------------------- attention
-// One workgroup = (query row, kv head, key split).  Query row i attends to keys
-// [0, len[i]) of cache slot slots[i].  softmax(q k^T / sqrt(d)) in fp32.
-constexpr int ATT_CHUNK = 256;
+// Grid (query row x kv head, split).  A workgroup owns keys [k0, k1) of its
+// split, walks them in 64-key sub-chunks with an online softmax (running max /
+// sum per query head, fp32), and all ATT_GMAX <= 8 query heads of the kv head
+// share each K/V load (GQA).  Thread t owns dims dl = 8*(t&15) and keys
+// kr + 16j (kr = t>>4, j < 4) of a sub-chunk: 4 x 16-B K loads and 4 x 16-B V
+// loads per thread, all issued together and the next sub-chunk prefetched.
+// With nsplit > 1 every split stores (o, m, l) partials and the last arriver of
+// the (row, kv head) group — agent-scope release / ticket / acquire
+// (cdna_hip_programming.md Guideline 16) — merges them, so decode attention is
+// one launch per layer.
+constexpr int ATT_KC = 64;
 constexpr int ATT_GMAX = 8;
 
-
+template <int G>
 __global__ void __launch_bounds__(256) k_attn(AttnArgs a) {
-  __shared__ float sc[ATT_GMAX][ATT_CHUNK];
-  __shared__ float ored[4][ATT_GMAX][128];
-  __shared__ float mrow[ATT_GMAX], lrow[ATT_GMAX];
-  const int d = 128;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ float sc[G][ATT_KC];
+  __shared__ float red[4][G][128];
+  __shared__ float mrun[G], lrun[G], alpha[G];
+  __shared__ unsigned last_flag;
+  constexpr int d = 128;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int qi = blockIdx.x / a.nkv, kh = blockIdx.x - qi * a.nkv, split = blockIdx.y;
-  const int G = a.nh / a.nkv;
   const int len = a.pos[qi] + 1;
-  const int k0 = split * ATT_CHUNK;
-  const int nk = min(ATT_CHUNK, len - k0);
+  // this row's split size: >= a.chunk (the launch plan's floor), all nsplit
+  // splits cover len; splits past the row's last key exit at once
+  int chunk = (len + a.nsplit - 1) / a.nsplit;
+  chunk = max(a.chunk, (chunk + ATT_KC - 1) / ATT_KC * ATT_KC);
+  const int nact = (len + chunk - 1) / chunk;
+  if (split >= nact) return;
+  const int k0 = split * chunk;
+  const int k1 = min(len, k0 + chunk);
   const long long cbase = (long long)a.layer * a.kv.s_layer + (long long)a.slots[qi] * a.kv.s_slot +
                           (long long)kh * a.kv.s_head;
   const bf16* K = a.kv.k + cbase;
   const bf16* V = a.kv.v + cbase;
+  const int dl = (t & 15) * 8, kr = t >> 4;
 
-  if (nk > 0) {
-    // phase 1: scores; 16 lanes per key, 8 dims per lane
-    const int sub = lane >> 4, dl = (lane & 15) * 8;
-    float qv[ATT_GMAX][8];
+  float qv[G][8];
 #pragma unroll
-    for (int h = 0; h < ATT_GMAX; ++h) {
-      if (h >= G) break;
-      bf16x8 t = *(const bf16x8*)(a.q + (long long)qi * a.nh * d + (kh * G + h) * d + dl);
+  for (int h = 0; h < G; ++h) {
+    const bf16x8 q8 = *(const bf16x8*)(a.q + (long long)qi * a.nh * d + (kh * G + h) * d + dl);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) qv[h][j] = bf(t[j]);
+    for (int e = 0; e < 8; ++e) qv[h][e] = bf(q8[e]) * a.scale;
+  }
+  float o[G][8];
+#pragma unroll
+  for (int h = 0; h < G; ++h)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[h][e] = 0.f;
+  if (t < G) {
+    mrun[t] = -INFINITY;
+    lrun[t] = 0.f;
+  }
+  const bf16x8 z8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+  bf16x8 kf[4], vf[4];
+  auto load = [&](int c0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int key = c0 + kr + 16 * j;
+      const bool ok = key < k1;
+      kf[j] = ok ? *(const bf16x8*)(K + (long long)key * d + dl) : z8;
+      vf[j] = ok ? *(const bf16x8*)(V + (long long)key * d + dl) : z8;
     }
-    for (int kk = wave * 4 + sub; kk < nk; kk += 16) {
-      bf16x8 kv8 = *(const bf16x8*)(K + (long long)(k0 + kk) * d + dl);
-      float kf[8];
+  };
+  if (k0 < k1) load(k0);
+  for (int c0 = k0; c0 < k1; c0 += ATT_KC) {
+    const int nk = min(ATT_KC, k1 - c0);
+    bf16x8 kc[4], vc[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) kf[j] = bf(kv8[j]);
+    for (int j = 0; j < 4; ++j) {
+      kc[j] = kf[j];
+      vc[j] = vf[j];
+    }
+    if (c0 + ATT_KC < k1) load(c0 + ATT_KC);   // prefetch the next sub-chunk
+    // scores s[h][key] = (q*scale) . k
 #pragma unroll
-      for (int h = 0; h < ATT_GMAX; ++h) {
-        if (h >= G) break;
+    for (int j = 0; j < 4; ++j) {
+      float kx[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) kx[e] = bf(kc[j][e]);
+#pragma unroll
+      for (int h = 0; h < G; ++h) {
         float s = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s += qv[h][j] * kf[j];
+        for (int e = 0; e < 8; ++e) s += qv[h][e] * kx[e];
         s += __shfl_xor(s, 8);
         s += __shfl_xor(s, 4);
         s += __shfl_xor(s, 2);
         s += __shfl_xor(s, 1);
-        if ((lane & 15) == 0) sc[h][kk] = s * a.scale;
+        if ((t & 15) == 0) sc[h][kr + 16 * j] = s;
       }
     }
-  }
-  __syncthreads();
-  // phase 2: per-head max / exp / sum over this chunk
-  for (int h = wave; h < G; h += 4) {
-    float mx = -INFINITY;
-    for (int k = lane; k < nk; k += 64) mx = fmaxf(mx, sc[h][k]);
-    mx = wave_max(mx);
-    float sum = 0.f;
-    for (int k = lane; k < nk; k += 64) {
-      const float p = __expf(sc[h][k] - mx);
-      sc[h][k] = p;
-      sum += p;
+    __syncthreads();
+    // online softmax update, one wave per head
+    for (int h = wave; h < G; h += 4) {
+      const float s = lane < nk ? sc[h][lane] : -INFINITY;
+      const float mnew = fmaxf(mrun[h], wave_max(s));
+      const float p = lane < nk ? __expf(s - mnew) : 0.f;
+      sc[h][lane] = p;
+      const float sum = wave_sum(p);
+      if (lane == 0) {
+        const float al = __expf(mrun[h] - mnew);
+        alpha[h] = al;
+        lrun[h] = lrun[h] * al + sum;
+        mrun[h] = mnew;
+      }
     }
-    sum = wave_sum(sum);
-    if (lane == 0) { mrow[h] = mx; lrow[h] = sum; }
-  }
-  __syncthreads();
-  // phase 3: o[h][dim] = sum_k p[h][k] v[k][dim]; lane owns dims 2l, 2l+1; waves split keys
-  float o[ATT_GMAX][2];
+    __syncthreads();
 #pragma unroll
-  for (int h = 0; h < ATT_GMAX; ++h) o[h][0] = o[h][1] = 0.f;
-  for (int k = wave; k < nk; k += 4) {
-    const bf16* vr = V + (long long)(k0 + k) * d + 2 * lane;
-    const float v0 = bf(vr[0]), v1 = bf(vr[1]);
+    for (int h = 0; h < G; ++h) {
+      const float al = alpha[h];
 #pragma unroll
-    for (int h = 0; h < ATT_GMAX; ++h) {
-      if (h >= G) break;
-      const float p = sc[h][k];
-      o[h][0] += p * v0;
-      o[h][1] += p * v1;
+      for (int e = 0; e < 8; ++e) o[h][e] *= al;
     }
-  }
 #pragma unroll
-  for (int h = 0; h < ATT_GMAX; ++h) {
-    if (h >= G) break;
-    ored[wave][h][2 * lane] = o[h][0];
-    ored[wave][h][2 * lane + 1] = o[h][1];
+    for (int j = 0; j < 4; ++j) {
+      const int kk = kr + 16 * j;
+      if (kk < nk) {
+        float vx[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vx[e] = bf(vc[j][e]);
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+          const float p = sc[h][kk];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[h][e] += p * vx[e];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // reduce the 16 key rows: 4 inside the wave (lanes +16, +32), 4 waves via LDS
+#pragma unroll
+  for (int h = 0; h < G; ++h)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = o[h][e];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      o[h][e] = v;
+    }
+  if (lane < 16) {
+#pragma unroll
+    for (int h = 0; h < G; ++h)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[wave][h][dl + e] = o[h][e];
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < G * d; e += blockDim.x) {
+  if (nact == 1) {
+    for (int e = t; e < G * d; e += 256) {
+      const int h = e / d, j = e - h * d;
+      const float s = red[0][h][j] + red[1][h][j] + red[2][h][j] + red[3][h][j];
+      a.out[(long long)qi * a.nh * d + (kh * G + h) * d + j] = tobf(s / lrun[h]);
+    }
+    return;
+  }
+  for (int e = t; e < G * d; e += 256) {
     const int h = e / d, j = e - h * d;
-    const float s = ored[0][h][j] + ored[1][h][j] + ored[2][h][j] + ored[3][h][j];
-    const int hh = kh * G + h;
-    if (a.nsplit == 1) {
-      a.out[(long long)qi * a.nh * d + hh * d + j] = tobf(s / lrow[h]);
-    } else {
-      const long long pidx = ((long long)qi * a.nh + hh) * a.nsplit + split;
-      a.part_o[pidx * d + j] = s;
-      if (j == 0) {
-        a.part_ml[pidx * 2] = nk > 0 ? mrow[h] : -INFINITY;
-        a.part_ml[pidx * 2 + 1] = nk > 0 ? lrow[h] : 0.f;
-      }
+    const long long pidx = ((long long)qi * a.nh + kh * G + h) * a.nsplit + split;
+    a.part_o[pidx * d + j] = red[0][h][j] + red[1][h][j] + red[2][h][j] + red[3][h][j];
+    if (j == 0) {
+      a.part_ml[pidx * 2] = mrun[h];
+      a.part_ml[pidx * 2 + 1] = lrun[h];
     }
   }
-}
-
-__global__ void __launch_bounds__(128) k_attn_combine(AttnArgs a) {
-  const int qi = blockIdx.x / a.nh, hh = blockIdx.x - qi * a.nh;
-  const int j = threadIdx.x;
-  const long long p0 = ((long long)qi * a.nh + hh) * a.nsplit;
-  float M = -INFINITY;
-  for (int s = 0; s < a.nsplit; ++s) M = fmaxf(M, a.part_ml[(p0 + s) * 2]);
-  float num = 0.f, den = 0.f;
-  for (int s = 0; s < a.nsplit; ++s) {
-    const float m = a.part_ml[(p0 + s) * 2];
-    if (m == -INFINITY) continue;
-    const float w = __expf(m - M);
-    num += w * a.part_o[(p0 + s) * 128 + j];
-    den += w * a.part_ml[(p0 + s) * 2 + 1];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned* ctr = a.counters + blockIdx.x;
+    const unsigned tk = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_flag = tk == (unsigned)(nact - 1);
+    if (last_flag) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
-  a.out[(long long)qi * a.nh * 128 + hh * 128 + j] = tobf(num / den);
+  __syncthreads();
+  if (!last_flag) return;
+  // merge the splits: out = sum_s e^{m_s - M} o_s / sum_s e^{m_s - M} l_s
+  for (int e = t; e < G * d; e += 256) {
+    const int h = e / d, j = e - h * d;
+    const long long p0 = ((long long)qi * a.nh + kh * G + h) * a.nsplit;
+    float M = -INFINITY;
+    for (int s = 0; s < nact; ++s) M = fmaxf(M, a.part_ml[(p0 + s) * 2]);
+    float num = 0.f, den = 0.f;
+    for (int s = 0; s < nact; ++s) {
+      const float m = a.part_ml[(p0 + s) * 2];
+      const float w = __expf(m - M);
+      num += w * a.part_o[(p0 + s) * d + j];
+      den += w * a.part_ml[(p0 + s) * 2 + 1];
+    }
+    a.out[(long long)qi * a.nh * d + (kh * G + h) * d + j] = tobf(num / den);
+  }
 }
 
 // ---------------------------------------------------------------- restricted lm_head
@@ -197,13 +271,37 @@ int launch_rope_kv(RopeArgs a, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
-int attn_nsplit(int max_len) { return max_len <= ATT_CHUNK ? 1 : (max_len + ATT_CHUNK - 1) / ATT_CHUNK; }
+// Launch plan for keys up to max_len: aim for ~1024 workgroups over
+// (rows x kv heads x splits), never below 64 keys per split, at most 64
+// splits (merge cost).  Each row then sizes its own splits from its length
+// (k_attn), so a plan made for max_ctx serves every step of a captured graph.
+int attn_plan(int nq, int nkv, int max_len, int* chunk) {
+  const int groups = nq * nkv;
+  int want = 1024 / groups;
+  if (want < 1) want = 1;
+  int ns = (max_len + ATT_KC - 1) / ATT_KC;
+  if (ns > want) ns = want;
+  if (ns > 64) ns = 64;
+  if (ns < 1) ns = 1;
+  *chunk = ATT_KC;
+  return ns;
+}
 
 int launch_attn(AttnArgs a, hipStream_t st) {
   if (a.nq <= 0) return 0;
-  if (a.kv.d != 128 || a.nh % a.nkv || a.nh / a.nkv > ATT_GMAX) return 1;
-  hipLaunchKernelGGL(k_attn, dim3(a.nq * a.nkv, a.nsplit), dim3(256), 0, st, a);
-  if (a.nsplit > 1) hipLaunchKernelGGL(k_attn_combine, dim3(a.nq * a.nh), dim3(128), 0, st, a);
+  if (a.kv.d != 128 || a.nh % a.nkv || a.nh / a.nkv > ATT_GMAX || a.chunk % ATT_KC) return 1;
+  if (a.nsplit > 1 && (!a.part_o || !a.part_ml || !a.counters)) return 1;
+  dim3 grid(a.nq * a.nkv, a.nsplit);
+  switch (a.nh / a.nkv) {
+    case 1: hipLaunchKernelGGL(k_attn<1>, grid, dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL(k_attn<2>, grid, dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL(k_attn<3>, grid, dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL(k_attn<4>, grid, dim3(256), 0, st, a); break;
+    case 5: hipLaunchKernelGGL(k_attn<5>, grid, dim3(256), 0, st, a); break;
+    case 6: hipLaunchKernelGGL(k_attn<6>, grid, dim3(256), 0, st, a); break;
+    case 7: hipLaunchKernelGGL(k_attn<7>, grid, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL(k_attn<8>, grid, dim3(256), 0, st, a); break;
+  }
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -115,7 +115,7 @@ struct vv_ctx {
   KVLayout kv;
   DevBuf lm_ws;  // h, a, qkv, q, att, act
   size_t lm_ws_tokens = 0;
-  DevBuf attn_part;
+  DevBuf attn_part, attn_cnt;
   DevBuf valid_ids;
   int n_valid = 0;
   // split-K
@@ -469,7 +469,7 @@ void vv_destroy(vv_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
-  DevBuf* bufs[] = {&c->kv_k, &c->kv_v, &c->lm_ws, &c->attn_part, &c->valid_ids, &c->splitk_ws, &c->splitk_cnt,
+  DevBuf* bufs[] = {&c->kv_k, &c->kv_v, &c->lm_ws, &c->attn_part, &c->attn_cnt, &c->valid_ids, &c->splitk_ws, &c->splitk_cnt,
                     &c->temb, &c->tfreq_tmp, &c->head_ws, &c->codec_ws, &c->slot_scratch};
   for (DevBuf* b : bufs) b->release();
   ConvNet* nets[] = {&c->dec, &c->sem, &c->aenc};
@@ -573,6 +573,10 @@ int vv_finalize(vv_ctx* c) {
   CHK(c->kv_v.ensure(kvb));
   c->kv.k = (bf16*)c->kv_k.p;
   c->kv.v = (bf16*)c->kv_v.p;
+  // ---- attention split partials for decode (2 * max_batch rows, <= 64 splits) + tickets
+  CHK(c->attn_part.ensure((size_t)2 * k.max_batch * k.n_heads * 64 * (d + 2) * sizeof(float)));
+  CHK(c->attn_cnt.ensure(65536 * sizeof(unsigned)));
+  HIPCHK(hipMemset(c->attn_cnt.p, 0, 65536 * sizeof(unsigned)));
   // ---- split-K slabs + tickets
   CHK(c->splitk_ws.ensure(64ull << 20));
   CHK(c->splitk_cnt.ensure(65536 * sizeof(unsigned)));
@@ -609,8 +613,9 @@ int vv_set_schedule(vv_ctx* c, int steps, const float* coef, const void* tfreq, 
     e.order = (int)q[6];
     e.cfg = 0.f;
   }
-  CHK(c->temb.ensure((size_t)steps * H * sizeof(bf16)));
-  CHK(c->tfreq_tmp.ensure((size_t)steps * H * sizeof(bf16)));
+  // sized for the largest schedule once, so captured graphs keep valid pointers
+  CHK(c->temb.ensure((size_t)1000 * H * sizeof(bf16)));
+  CHK(c->tfreq_tmp.ensure((size_t)1000 * H * sizeof(bf16)));
   // t_emb = Linear2(SiLU(Linear0(t_freq)))  (TimestepEmbedder.forward, diffusion_head.py:90-93)
   bf16* t1 = (bf16*)c->tfreq_tmp.p;
   CHK(gemm(c, gemm_args(c, steps, H, 256, rowmap(tfreq, 256), W(c, "head.t0_w"), EPI_STORE, rowmap(t1, H)), st));
@@ -653,8 +658,12 @@ int vv_lm_forward(vv_ctx* c, int ntok, const void* embeds, const int* slot, cons
   bf16* att = q + (size_t)ntok * nhd;
   bf16* act = att + (size_t)ntok * nhd;
   bf16* fin = act + (size_t)ntok * I;
-  const int nsplit = attn_nsplit(max_pos_p1);
-  if (nsplit > 1) CHK(c->attn_part.ensure((size_t)ntok * k.n_heads * nsplit * (d + 2) * sizeof(float)));
+  int chunk = 0;
+  const int nsplit = attn_plan(ntok, k.n_kv_heads, max_pos_p1, &chunk);
+  if (nsplit > 1) {
+    if ((size_t)ntok * k.n_kv_heads > 65536) FAIL("attention split tickets exhausted");
+    CHK(c->attn_part.ensure((size_t)ntok * k.n_heads * nsplit * (d + 2) * sizeof(float)));
+  }
   HIPCHK(hipMemcpyAsync(h, embeds, (size_t)ntok * H * sizeof(bf16), hipMemcpyDeviceToDevice, st));
   RowMap hm = rowmap(h, H), am = rowmap(a, H);
   for (int l = 0; l < k.n_layers; ++l) {
@@ -681,6 +690,8 @@ int vv_lm_forward(vv_ctx* c, int ntok, const void* embeds, const int* slot, cons
     at.nkv = k.n_kv_heads;
     at.layer = l;
     at.nsplit = nsplit;
+    at.chunk = chunk;
+    at.counters = (unsigned*)c->attn_cnt.p;
     at.scale = 1.0f / sqrtf((float)d);
     at.q = q;
     at.out = att;

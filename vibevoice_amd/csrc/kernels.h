@@ -84,6 +84,7 @@ struct RopeArgs {
 
 struct AttnArgs {
   int nq, nh, nkv, layer, nsplit;
+  int chunk;            // keys per split (multiple of 64)
   float scale;
   const bf16* q;        // [nq][nh*d]
   bf16* out;            // [nq][nh*d]
@@ -92,6 +93,7 @@ struct AttnArgs {
   KVLayout kv;
   float* part_o;        // [nq][nh][nsplit][d]
   float* part_ml;       // [nq][nh][nsplit][2]
+  unsigned* counters;   // [nq * nkv] split tickets (zero between launches)
 };
 
 int launch_gemm(GemmArgs a, hipStream_t st);
@@ -108,7 +110,7 @@ int launch_silu(int n, const bf16* x, bf16* y, hipStream_t st);
 int launch_cfg_dpm(int n, int D, DpmCoef k, const bf16* eps, bf16* x, bf16* m1, hipStream_t st);
 int launch_gather_rows(int n, int C, const bf16* src, long long lds, const int* idx, RowMap dst, hipStream_t st);
 int launch_rope_kv(RopeArgs a, hipStream_t st);
-int attn_nsplit(int max_len);
+int attn_plan(int nq, int nkv, int max_len, int* chunk);
 int launch_attn(AttnArgs a, hipStream_t st);
 int launch_kv_copy(KVLayout kv, int n_layers, int nkv, int n, const int* slots, const int* src, const int* dst,
                    hipStream_t st);

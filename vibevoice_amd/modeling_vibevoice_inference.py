@@ -84,6 +84,30 @@ class VibeVoiceForConditionalGenerationInference:
                              max_ctx=min(max_ctx, config.decoder_config.max_position_embeddings))
         self.ddpm_inference_steps = config.diffusion_head_config.ddpm_num_inference_steps
         self.model = _ModelView(self)
+        self.use_graphs = True          # capture the steady-state loop body into hipGraphs
+        self._bufs = {}
+        self._graph_cache, self._graph_seen = {}, set()
+
+    def _step_buffers(self, B):
+        """Static device operands of the loop body for batch B (shared by every
+        generate call of that batch size, so captured graphs stay valid)."""
+        if B not in self._bufs:
+            dev, eng, dt = self.device, self.engine, self.dtype
+            H, D = eng.hidden, self.config.acoustic_vae_dim
+            i32 = dict(device=dev, dtype=torch.int32)
+            self._bufs[B] = dict(
+                rows2=torch.arange(2 * B, **i32),
+                x_in2=torch.zeros(2 * B, H, device=dev, dtype=dt),
+                hid=torch.zeros(2 * B, H, device=dev, dtype=dt),
+                logits=torch.zeros(2 * B, 4, device=dev, dtype=torch.float32),
+                pos_dev=torch.zeros(2 * B, **i32), ids_dev=torch.zeros(B, **i32), didx_dev=torch.zeros(B, **i32),
+                noise_dev=torch.zeros(B, D, device=dev, dtype=dt),
+                audio_dev=torch.zeros(B, eng.hop, device=dev, dtype=dt),
+                pos_pin=torch.zeros(2 * B, dtype=torch.int32, pin_memory=True),
+                ids_pin=torch.zeros(B, dtype=torch.int32, pin_memory=True),
+                didx_pin=torch.zeros(B, dtype=torch.int32, pin_memory=True),
+                noise_pin=torch.zeros(B, D, dtype=dt, pin_memory=True))
+        return self._bufs[B]
 
     # ------------------------------------------------------------ loading
     @classmethod
@@ -262,11 +286,19 @@ class GenerateSession:
         self.done = False
         i32 = dict(device=dev, dtype=torch.int32)
         self.ints = _Staging(dev, torch.int32, 1 << 16)
-        self.lat = _Staging(dev, model.dtype, 1 << 16)
-        self.rows2 = torch.arange(2 * B, **i32)                           # LM rows: [positive B | negative B]
         self.valid_t = torch.tensor(self.valid)
         self.order_t = torch.tensor(self.order)
+        # static device operands of the loop body (graph-capturable): LM rows are
+        # [positive B | negative B]; the negative rows consume the same input (:594-596)
+        sb = model._step_buffers(B)
+        for k, v in sb.items():
+            setattr(self, k, v)
+        self.use_graphs = kwargs.get("use_graphs", model.use_graphs)
+        self.graphs = model._graph_cache
+        self.seen = model._graph_seen
 
+        # fresh streaming codec caches per call (VibeVoiceTokenizerStreamingCache() x2, :387-388)
+        eng.codec_reset(torch.arange(B, **i32))
         # ---- step 0: positive prefill rows + speculative negative [speech_start] rows
         emb = model._prompt_embeds(input_ids.to(dev), attention_mask.to(dev), speech_tensors, speech_masks,
                                    speech_input_mask)
@@ -277,9 +309,58 @@ class GenerateSession:
         last = torch.cumsum(Li, 0) - 1
         out_idx = torch.cat([last, torch.arange(ntok, ntok + B)])
         step_in = torch.cat([emb, neg_in], 0)
-        self.hid, self.logits = eng.lm_forward(step_in, tok_slot.to(**i32), tok_pos.to(**i32), out_idx.to(**i32),
-                                               max_pos=int(tok_pos.max()))
-        self.inputs_embeds = None
+        eng.lm_forward(step_in, tok_slot.to(**i32), tok_pos.to(**i32), out_idx.to(**i32), hidden_out=self.hid,
+                       logits_out=self.logits, max_pos=int(tok_pos.max()))
+
+    # ---------------------------------------------------------------- device phases
+    def _replay(self, key, fn):
+        """Run `fn` (device work only, on static buffers).  With graphs on, the
+        second occurrence of `key` is captured into a hipGraph (the first runs
+        eagerly so every kernel is loaded) and later ones replay it."""
+        if not self.use_graphs:
+            return fn()
+        full = (self.B, self.m.engine.steps, float(self.cfg_scale)) + key
+        g = self.graphs.get(full)
+        if g is None:
+            if full not in self.seen:
+                self.seen.add(full)
+                return fn()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                fn()
+            self.graphs[full] = g
+        g.replay()
+
+    def _lm_phase(self):
+        """Positive + negative decode rows in one pass (:483-486, :598-600)."""
+        B, eng = self.B, self.eng
+
+        def body():
+            self.x_in2[B:].copy_(self.x_in2[:B])
+            eng.lm_forward(self.x_in2, self.rows2, self.pos_dev, self.rows2, hidden_out=self.hid,
+                           logits_out=self.logits, max_pos=eng.max_ctx - 1)
+        self._replay(("lm",), body)
+
+    def _token_phase(self, n):
+        """next_embeds = embed(next tokens) (:584); for the n diffusion rows:
+        CFG diffusion sampling (:644, 712-725), streaming decode / encode and the
+        connectors (:651-687), overwriting those rows' embeddings."""
+        B, eng = self.B, self.eng
+
+        def body():
+            eng.embed(self.ids_dev, out=self.x_in2)
+            if n == 0:
+                return
+            d = self.didx_dev[:n]
+            if n == B:
+                pos_h, neg_h = self.hid[:B], self.hid[B:]
+            else:
+                pos_h = self.hid.index_select(0, d)
+                neg_h = self.hid.index_select(0, d + B)
+            x = self.noise_dev[:n]
+            eng.diffusion_sample(pos_h, neg_h, x, self.cfg_scale)
+            eng.codec_step(d, x, self.audio_dev[:n], embeds_out=self.x_in2, embed_rows=d)
+        self._replay(("token", n), body)
 
     # ---------------------------------------------------------------- one iteration
     def step(self):
@@ -306,10 +387,10 @@ class GenerateSession:
             self.done = True
             return False
         if step > 0:
-            pos = torch.cat([self.pos_len, self.neg_len])
-            in2 = torch.cat([self.inputs_embeds, self.inputs_embeds], 0)   # negative consumes the same input
-            self.hid, self.logits = eng.lm_forward(in2, self.rows2, self.ints.put(pos), self.rows2,
-                                                   max_pos=int(pos.max()))
+            self.pos_pin[:B].copy_(self.pos_len)
+            self.pos_pin[B:].copy_(self.neg_len)
+            self.pos_dev.copy_(self.pos_pin, non_blocking=True)
+            self._lm_phase()
             self.pos_len += 1
         # ---- token choice (:494-509); the argmax is always read back, as in the reference
         lg = self.logits[:B].float().cpu()
@@ -345,7 +426,8 @@ class GenerateSession:
         starts = ~finished & (nxt == self.start_id)                         # :563-580
         if self.refresh_negative:
             self.neg_len[starts] = 0     # mask reset: empty context, next position 0
-        next_embeds = eng.embed(self.ints.put(nxt))                        # :584
+        self.ids_pin.copy_(nxt)
+        self.ids_dev.copy_(self.ids_pin, non_blocking=True)
         diff = ~finished & (nxt == self.diff_id)                            # :588
         if diff.any():
             didx = torch.nonzero(diff).reshape(-1)
@@ -365,22 +447,19 @@ class GenerateSession:
                 q = torch.tensor(quirk)
                 eng.kv_copy(self.ints.put(q + B), self.ints.put(torch.ones_like(q)),
                             self.ints.put(torch.zeros_like(q)))
-            d32 = self.ints.put(didx)
-            if n == B:
-                pos_h, neg_h = self.hid[:B], self.hid[B:]
-            else:
-                pos_h = self.hid.index_select(0, d32)
-                neg_h = self.hid.index_select(0, d32 + B)
+            self.didx_pin[:n].copy_(didx)
+            self.didx_dev.copy_(self.didx_pin, non_blocking=True)
             noise = torch.randn(2 * n, self.m.config.acoustic_vae_dim)    # CPU generator (:716)
-            x = self.lat.put(noise[:n].to(self.m.dtype)).view(n, -1)
-            eng.diffusion_sample(pos_h, neg_h, x, self.cfg_scale)
-            audio = torch.empty(n, eng.hop, dtype=self.m.dtype, device=dev)
-            eng.codec_step(d32, x, audio, embeds_out=next_embeds, embed_rows=d32)
+            self.noise_pin[:n].copy_(noise[:n])
+            self.noise_dev.copy_(self.noise_pin, non_blocking=True)
+            self._token_phase(n)
+            audio = self.audio_dev[:n].clone()
             for i, b in enumerate(didx.tolist()):
                 self.audio_chunks[b].append(audio[i:i + 1])
             if st is not None:
                 st.put(audio[:, None, :], didx)
-        self.inputs_embeds = next_embeds
+        else:
+            self._token_phase(0)
         self.step_idx += 1
         return True
 
