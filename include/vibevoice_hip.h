@@ -118,9 +118,14 @@ int vv_connector(vv_ctx* ctx, int which, int n, const void* x, void* out, vv_str
 int vv_scatter_rows(vv_ctx* ctx, int n, int C, const void* src, int64_t lds, const int* idx, void* dst,
                     int64_t ldd, vv_stream st);
 
-/* Low-level kernel entry points (used by the parity tests). */
+/* Low-level kernel entry points (used by the parity tests).  W is [N, K] in the
+ * MFMA-packed order of vibevoice_amd/weights.py:mfma_pack (csrc/gemm.hip). */
 int vv_gemm_bf16(int M, int N, int K, const void* A, int64_t lda, const void* W, const void* bias, int epi,
                  void* Y, int64_t ldy, const void* res, const void* gamma, vv_ctx* ws_ctx, vv_stream st);
+/* Tuning hook (benchmarks only): override the GEMV launch plan — waves per
+ * workgroup, split-K workgroups, split-K hand-off form (0 fences, 1 sc1),
+ * target waves per launch.  0 / -1 restore the built-in plan. */
+int vv_gemv_tune(int nw, int ks, int handoff, int target_waves);
 int vv_rmsnorm_bf16(int M, int C, const void* x, int64_t ldx, const void* w, float eps, void* y, int64_t ldy,
                     vv_stream st);
 

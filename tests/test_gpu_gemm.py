@@ -11,6 +11,7 @@ import torch
 
 from gpu_util import max_rel, rel_err
 from vibevoice_amd import _lib
+from vibevoice_amd.weights import mfma_pack
 
 pytestmark = pytest.mark.gpu
 dev = "cuda"
@@ -29,7 +30,8 @@ def run(M, N, K, epi, bias=True, res=False, gamma=False, ws_ctx=None):
     Y = torch.empty(M, outN, device=dev, dtype=torch.float32 if epi == "f32" else torch.bfloat16)
     R = torch.randn(M, outN, device=dev, generator=g).bfloat16() if res else None
     G = torch.randn(outN, device=dev, generator=g).bfloat16() if gamma else None
-    rc = _lib.lib().vv_gemm_bf16(M, N, K, P(A), K, P(W), P(b), _lib.EPI[epi], P(Y), outN, P(R), P(G), ws_ctx,
+    Wp = mfma_pack(W) if N % 16 == 0 and K % 32 == 0 else W
+    rc = _lib.lib().vv_gemm_bf16(M, N, K, P(A), K, P(Wp), P(b), _lib.EPI[epi], P(Y), outN, P(R), P(G), ws_ctx,
                                  ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
     _lib.check(rc, "gemm")
     torch.cuda.synchronize()

@@ -1,0 +1,122 @@
+"""Sweep the GEMV launch plan (waves / workgroup, split-K, hand-off form) over
+the generate loop's weight-streaming shapes on the MI355X, checking every
+configuration against a torch fp32 reference.  Weights rotate over enough
+copies (> 512 MB) that the Infinity Cache cannot serve them.
+
+usage: python tools/gemv_sweep.py [--quick]   (prints one line per shape/config)
+"""
+import ctypes
+import itertools
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vibevoice_amd import _lib  # noqa: E402
+from vibevoice_amd.weights import mfma_pack  # noqa: E402
+
+SHAPES = [  # name, M, N, K, epi
+    ("lm.qkv", 2, 2048, 1536, "store"), ("lm.o", 2, 1536, 1536, "res"), ("lm.gu", 2, 17920, 1536, "silu_mul"),
+    ("lm.down", 2, 1536, 8960, "res"), ("head.ada", 2, 21504, 1536, "store"), ("head.gu", 2, 9216, 1536, "silu_mul"),
+    ("head.down", 2, 1536, 4608, "res"), ("head.final", 2, 64, 1536, "store"),
+    ("codec.fc1", 1, 8192, 2048, "gelu"), ("codec.fc2", 1, 2048, 8192, "res"),
+    ("lm.gu.b8", 16, 17920, 1536, "silu_mul"), ("lm.down.b8", 16, 1536, 8960, "res"),
+]
+
+
+def P(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def main():
+    quick = "--quick" in sys.argv
+    L = _lib.lib()
+    dev = "cuda"
+    torch.manual_seed(0)
+    def sp_():
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    results = []
+    for name, M, N, K, epi in SHAPES:
+        ncopy = max(2, (512 << 20) // (N * K * 2) + 1)
+        Ws = [(torch.randn(N, K, device=dev) / K ** 0.5).bfloat16() for _ in range(ncopy)]
+        A = torch.randn(M, K, device=dev).bfloat16()
+        outN = N // 2 if epi == "silu_mul" else N
+        Y = torch.empty(M, outN, device=dev, dtype=torch.bfloat16)
+        R = torch.randn(M, outN, device=dev).bfloat16() if epi == "res" else None
+        ref = A.float() @ Ws[0].float().t()
+        Ws = [mfma_pack(w) for w in Ws]
+        if epi == "silu_mul":
+            a = ref.view(M, N // 16, 2, 8)
+            gte, up = a[:, :, 0].reshape(M, -1), a[:, :, 1].reshape(M, -1)
+            ref = torch.nn.functional.silu(gte.bfloat16().float()) * up.bfloat16().float()
+        elif epi == "gelu":
+            ref = torch.nn.functional.gelu(ref.bfloat16().float())
+        elif epi == "res":
+            ref = R.float() + ref.bfloat16().float()
+
+        def run(W):
+            _lib.check(L.vv_gemm_bf16(M, N, K, P(A), K, P(W), None, _lib.EPI[epi], P(Y), outN, P(R), None, None, sp_()))
+
+        def measure():
+            # graph-captured back-to-back launches: GPU time incl. kernel boundaries, no host overhead
+            reps = max(16, 2 * len(Ws))
+            for W in Ws[:2]:
+                run(W)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for i in range(reps):
+                    run(Ws[i % len(Ws)])
+            g.replay()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            g.replay()
+            g.replay()
+            e1.record()
+            e1.synchronize()
+            return e0.elapsed_time(e1) * 1e3 / (2 * reps)
+
+        def check():
+            run(Ws[0])
+            torch.cuda.synchronize()
+            return ((Y.float() - ref).norm() / ref.norm()).item()
+
+        configs = [(0, 0, -1, 0)]
+        if not quick:
+            configs += [(0, 0, h, t) for h in (0, 1) for t in (1024, 2048, 4096, 8192)]
+            configs += [(nw, ks, h, 0) for nw, ks, h in itertools.product((1, 2, 4), (1, 2, 3, 4, 6, 8, 12, 16), (0, 1))]
+        best = None
+        for nw, ks, h, tw in configs:
+            L.vv_gemv_tune(nw, ks, h, tw)
+            try:
+                err = check()
+                us = measure()
+            except RuntimeError as e:
+                print(name, (nw, ks, h, tw), "error", e)
+                continue
+            gbs = (N * K * 2 + M * K * 2 + M * outN * 2) / us / 1e3
+            rec = dict(shape=name, M=M, N=N, K=K, nw=nw, ks=ks, handoff=h, target=tw, us=round(us, 2),
+                       gbs=round(gbs, 1), err=err)
+            results.append(rec)
+            ok = err < 1e-2
+            if ok and (best is None or us < best["us"]):
+                best = rec
+            if not ok:
+                print("BAD", json.dumps(rec), flush=True)
+        L.vv_gemv_tune(0, 0, -1, 0)
+        dflt = [r for r in results if r["shape"] == name and r["nw"] == 0 and r["ks"] == 0 and r["target"] == 0
+                and r["handoff"] == -1][0]
+        print(f"{name:12s} M={M:2d} N={N:6d} K={K:5d} default {dflt['us']:7.2f} us {dflt['gbs']:7.1f} GB/s | "
+              f"best {best['us']:7.2f} us {best['gbs']:7.1f} GB/s nw={best['nw']} ks={best['ks']} "
+              f"h={best['handoff']} target={best['target']}", flush=True)
+        del Ws
+        torch.cuda.empty_cache()
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/gemv_sweep.json", "w") as f:
+        json.dump(results, f)
+
+
+if __name__ == "__main__":
+    main()

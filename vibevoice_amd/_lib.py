@@ -50,6 +50,7 @@ EXPORTS = [
     ("vv_scatter_rows", I, [P, I, I, P, I64, P, P, I64, P]),
     ("vv_gemm_bf16", I, [I, I, I, P, I64, P, P, I, P, I64, P, P, P, P]),
     ("vv_rmsnorm_bf16", I, [I, I, P, I64, P, F, P, I64, P]),
+    ("vv_gemv_tune", I, [I, I, I, I]),
 ]
 
 EPI = {"store": 0, "gelu": 1, "silu_mul": 2, "res": 3, "f32": 4}

@@ -64,6 +64,15 @@ enum {
   EPI_SILU_MUL = 2,  // W rows packed [gate 8 | up 8] per 16: y = bf16(bf16(silu(bf16 g)) * bf16 u)
   EPI_RES = 3,       // y = bf16(res + bf16(s * bf16(acc + bias)))  s: none / gamma[n] / gate[m,n]
   EPI_F32 = 4,       // y(float) = acc + bias
+  EPI_ROPE = 5,      // Qwen2 q|k|v rows (rope-paired packing): RoPE q -> q_out, RoPE k / v -> KV cache
+  EPI_CFG_DPM = 6,   // diffusion-head final rows [cond n | uncond n]: CFG combine + DPM-Solver++ step
+};
+
+// Transforms applied to the A operand as it is loaded (fused producers):
+enum {
+  XF_NONE = 0,
+  XF_NORM = 1,       // a = RMSNorm(row)[*w][modulate(shift, scale)]   (row = whole K)
+  XF_SILU_ADD = 2,   // a = bf16(silu(bf16(row + vec)))
 };
 
 struct EpiArgs {

@@ -170,6 +170,20 @@ static GemmArgs gemm_args(vv_ctx* c, int M, int N, int K, RowMap a, const bf16* 
   return g;
 }
 
+static ATransform xf_norm(const bf16* w, float eps, const bf16* mod = nullptr, long long mod_ld = 0, int shift_off = 0,
+                          int scale_off = 0) {
+  ATransform x;
+  memset(&x, 0, sizeof(x));
+  x.kind = XF_NORM;
+  x.eps = eps;
+  x.w = w;
+  x.mod = mod;
+  x.mod_ld = mod_ld;
+  x.shift_off = shift_off;
+  x.scale_off = scale_off;
+  return x;
+}
+
 static int gemm(vv_ctx* c, GemmArgs g, hipStream_t st) {
   if (!g.w) FAIL("gemm: null weight");
   KCHK(launch_gemm(g, st));
@@ -404,10 +418,11 @@ static int convnet_run(vv_ctx* c, ConvNet& net, int n, const int* slots, RowMap 
       d.gamma = W(c, b + ".gamma");
       KCHK(launch_dwconv(d, st));
       // ffn
-      RowMap Am = rowmap(net.A, C);
+      // ffn: ConvRMSNorm fused into fc1's A load
       RowMap Fm = rowmap(net.F, 4LL * C);
-      CHK(rmsnorm(n * T, C, X, Am, W(c, b + ".ffn_norm"), eps, st));
-      CHK(gemm(c, gemm_args(c, n * T, 4 * C, C, Am, W(c, b + ".fc1_w"), EPI_GELU, Fm, W(c, b + ".fc1_b")), st));
+      GemmArgs g1 = gemm_args(c, n * T, 4 * C, C, X, W(c, b + ".fc1_w"), EPI_GELU, Fm, W(c, b + ".fc1_b"));
+      g1.xf = xf_norm(W(c, b + ".ffn_norm"), eps);
+      CHK(gemm(c, g1, st));
       RowMap o = X;
       const bool last = j == net.depth[i] - 1;
       if (last) {
@@ -665,25 +680,24 @@ int vv_lm_forward(vv_ctx* c, int ntok, const void* embeds, const int* slot, cons
     CHK(c->attn_part.ensure((size_t)ntok * k.n_heads * nsplit * (d + 2) * sizeof(float)));
   }
   HIPCHK(hipMemcpyAsync(h, embeds, (size_t)ntok * H * sizeof(bf16), hipMemcpyDeviceToDevice, st));
-  RowMap hm = rowmap(h, H), am = rowmap(a, H);
+  RowMap hm = rowmap(h, H);
+  const float* inv_freq = (const float*)W(c, "lm.inv_freq");
   for (int l = 0; l < k.n_layers; ++l) {
     const std::string p = "lm." + std::to_string(l);
-    CHK(rmsnorm(ntok, H, hm, am, W(c, p + ".in_norm"), k.rms_eps, st));
-    CHK(gemm(c, gemm_args(c, ntok, c->qkv_n, H, am, W(c, p + ".qkv_w"), EPI_STORE, rowmap(qkv, c->qkv_n),
-                          W(c, p + ".qkv_b")), st));
-    RopeArgs r;
-    r.R = ntok;
-    r.nh = k.n_heads;
-    r.nkv = k.n_kv_heads;
-    r.layer = l;
-    r.qkv = qkv;
-    r.ld_qkv = c->qkv_n;
-    r.q_out = q;
-    r.slots = slot;
-    r.pos = pos;
-    r.inv_freq = (const float*)c->w["lm.inv_freq"].p;
-    r.kv = c->kv;
-    KCHK(launch_rope_kv(r, st));
+    // input_layernorm -> q|k|v projection (+bias) -> RoPE -> q / KV cache, one launch
+    {
+      GemmArgs g = gemm_args(c, ntok, c->qkv_n, H, hm, W(c, p + ".qkv_w"), EPI_ROPE, RowMap{}, W(c, p + ".qkv_b"));
+      g.xf = xf_norm(W(c, p + ".in_norm"), k.rms_eps);
+      g.rope.nh = k.n_heads;
+      g.rope.nkv = k.n_kv_heads;
+      g.rope.layer = l;
+      g.rope.q_out = q;
+      g.rope.slots = slot;
+      g.rope.pos = pos;
+      g.rope.inv_freq = inv_freq;
+      g.rope.kv = c->kv;
+      CHK(gemm(c, g, st));
+    }
     AttnArgs at;
     at.nq = ntok;
     at.nh = k.n_heads;
@@ -704,8 +718,10 @@ int vv_lm_forward(vv_ctx* c, int ntok, const void* embeds, const int* slot, cons
     GemmArgs g = gemm_args(c, ntok, H, nhd, rowmap(att, nhd), W(c, p + ".o_w"), EPI_RES, hm);
     g.epi.res = hm;
     CHK(gemm(c, g, st));
-    CHK(rmsnorm(ntok, H, hm, am, W(c, p + ".post_norm"), k.rms_eps, st));
-    CHK(gemm(c, gemm_args(c, ntok, 2 * I, H, am, W(c, p + ".gu_w"), EPI_SILU_MUL, rowmap(act, I)), st));
+    // post_attention_layernorm fused into gate|up's A load
+    g = gemm_args(c, ntok, 2 * I, H, hm, W(c, p + ".gu_w"), EPI_SILU_MUL, rowmap(act, I));
+    g.xf = xf_norm(W(c, p + ".post_norm"), k.rms_eps);
+    CHK(gemm(c, g, st));
     g = gemm_args(c, ntok, H, I, rowmap(act, I), W(c, p + ".down_w"), EPI_RES, hm);
     g.epi.res = hm;
     CHK(gemm(c, g, st));
@@ -747,24 +763,42 @@ int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, 
   for (int s = 0; s < c->steps; ++s) {
     // x = noisy_images_proj(cat[x, x])  -- both halves read the same n latent rows
     CHK(gemm(c, gemm_args(c, R, H, D, rowmap(x_io, D, n, 0), W(c, "head.noisy_w"), EPI_STORE, xh_m), st));
-    KCHK(launch_head_cond(R, H, condp, (const bf16*)c->temb.p + (size_t)s * H, sc, st));
-    // all adaLN modulations of the step in one GEMM: [shift|scale|gate] x L, [shift|scale] final
-    CHK(gemm(c, gemm_args(c, R, (int)MODW, H, rowmap(sc, H), W(c, "head.ada_w"), EPI_STORE, rowmap(mod, MODW)), st));
+    // all adaLN modulations of the step in one GEMM: [shift|scale|gate] x L, [shift|scale] final;
+    // its A operand silu(cond_proj(c) + t_emb[s]) is formed on load
+    {
+      GemmArgs g = gemm_args(c, R, (int)MODW, H, rowmap(condp, H), W(c, "head.ada_w"), EPI_STORE, rowmap(mod, MODW));
+      g.xf.kind = XF_SILU_ADD;
+      g.xf.vec = (const bf16*)c->temb.p + (size_t)s * H;
+      CHK(gemm(c, g, st));
+    }
     for (int l = 0; l < L; ++l) {
       const std::string p = "head." + std::to_string(l);
       const int o = 3 * H * l;
-      CHK(rmsnorm(R, H, xh_m, a_m, W(c, p + ".norm"), k.head_eps, st, mod, MODW, o, o + H));
-      CHK(gemm(c, gemm_args(c, R, 2 * F, H, a_m, W(c, p + ".gu_w"), EPI_SILU_MUL, rowmap(act, F)), st));
-      GemmArgs g = gemm_args(c, R, H, F, rowmap(act, F), W(c, p + ".down_w"), EPI_RES, xh_m);
+      // modulate(norm(x), shift, scale) fused into gate|up's A load
+      GemmArgs g = gemm_args(c, R, 2 * F, H, xh_m, W(c, p + ".gu_w"), EPI_SILU_MUL, rowmap(act, F));
+      g.xf = xf_norm(W(c, p + ".norm"), k.head_eps, mod, MODW, o, o + H);
+      CHK(gemm(c, g, st));
+      g = gemm_args(c, R, H, F, rowmap(act, F), W(c, p + ".down_w"), EPI_RES, xh_m);
       g.epi.res = xh_m;
       g.epi.gate = rowmap(mod + o + 2 * H, MODW);
       CHK(gemm(c, g, st));
     }
-    CHK(rmsnorm(R, H, xh_m, a_m, nullptr, k.head_eps, st, mod, MODW, 3 * H * L, 3 * H * L + H));
-    CHK(gemm(c, gemm_args(c, R, D, H, a_m, W(c, "head.final_w"), EPI_STORE, rowmap(v, D)), st));
+    // final layer: modulate(norm_final(x)) -> linear -> CFG + DPM-Solver++ step on x
     DpmCoef e = c->coef[s];
     e.cfg = cfg_scale;
-    KCHK(launch_cfg_dpm(n, D, e, v, (bf16*)x_io, m1, st));
+    GemmArgs g = gemm_args(c, R, D, H, xh_m, W(c, "head.final_w"), EPI_STORE, rowmap(v, D));
+    g.xf = xf_norm(nullptr, k.head_eps, mod, MODW, 3 * H * L, 3 * H * L + H);
+    if (R <= 16) {
+      g.epi.kind = EPI_CFG_DPM;
+      g.dpm.n = n;
+      g.dpm.k = e;
+      g.dpm.x = (bf16*)x_io;
+      g.dpm.m1 = m1;
+      CHK(gemm(c, g, st));
+    } else {
+      CHK(gemm(c, g, st));
+      KCHK(launch_cfg_dpm(n, D, e, v, (bf16*)x_io, m1, st));
+    }
   }
   return 0;
 }
@@ -777,8 +811,9 @@ static int connector(vv_ctx* c, const char* which, int n, int din, RowMap x, Row
   bf16* t2 = t1 + (size_t)c->cfg.max_batch * H;
   RowMap t1m = rowmap(t1, H), t2m = rowmap(t2, H);
   CHK(gemm(c, gemm_args(c, n, H, din, x, W(c, p + ".fc1_w"), EPI_STORE, t1m, W(c, p + ".fc1_b")), st));
-  CHK(rmsnorm(n, H, t1m, t2m, W(c, p + ".norm"), 1e-6f, st));  // LlamaRMSNorm(eps=1e-6) (modeling_vibevoice.py:62)
-  GemmArgs g = gemm_args(c, n, H, H, t2m, W(c, p + ".fc2_w"), res ? EPI_RES : EPI_STORE, out, W(c, p + ".fc2_b"));
+  // LlamaRMSNorm(eps=1e-6) (modeling_vibevoice.py:62) fused into fc2's A load
+  GemmArgs g = gemm_args(c, n, H, H, t1m, W(c, p + ".fc2_w"), res ? EPI_RES : EPI_STORE, out, W(c, p + ".fc2_b"));
+  g.xf = xf_norm(W(c, p + ".norm"), 1e-6f);
   if (res) g.epi.res = *res;
   CHK(gemm(c, g, st));
   return 0;

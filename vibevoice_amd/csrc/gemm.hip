@@ -1,7 +1,11 @@
-// bf16 MFMA GEMMs for gfx950:  Y[m, n] = epi( sum_k A[m, k] * W[n, k] )
+// bf16 MFMA GEMMs for gfx950:  Y[m, n] = epi( sum_k xf(A)[m, k] * W[n, k] )
 //
-// W is a PyTorch Linear weight [N, K] (K contiguous), or a conv weight that the
-// loader re-packed to the same [N, K] form (see vibevoice_amd/weights.py):
+// W is a PyTorch Linear weight [N, K], or a conv weight that the loader
+// re-packed to the same [N, K] form (see vibevoice_amd/weights.py), stored in
+// MFMA-fragment order ("mfma_pack"): the 16 x 32 block (tile t, chunk c) is 1 KB
+// contiguous at (t * K/32 + c) * 512 elements, lane l's 8 elements at l * 8 =
+// W[16t + (l & 15)][32c + 8(l >> 4) .. +7] — every wave load is one coalesced
+// 1 KB read instead of 16 row fragments of 64 B.
 //   * causal conv k, stride s, channels-last input buffer with (k - s) history
 //     rows in front:  A row t = buffer + t*s*C_in, K = k*C_in  (lda = s*C_in),
 //   * 2-tap ConvTranspose (k = 2r, stride r): A row t = rows [t-1, t] of the
@@ -9,34 +13,192 @@
 //     consecutive channels-last output rows.
 // so every linear / conv layer on the hot path is this one kernel family.
 //
+// Fusions (the producer / consumer of each GEMM folded into it):
+//   * A transform (XF_*): RMSNorm (+ weight, + adaLN modulate) of the A rows, or
+//     SiLU(row + vec), applied to each A fragment as it is loaded.  The inverse
+//     RMS of the block's rows is computed in a prologue (every workgroup redoes
+//     it: at M <= 64 that is a few KB of L2 reads against MBs of weights).
+//   * epilogues (EPI_*): bias, GELU, SiLU(gate)*up, gated / layer-scaled
+//     residual, RoPE + KV-cache append, CFG + DPM-Solver++ update.
+//
 // Two shapes:
 //   k_gemv : M <= 64 (LM decode rows, diffusion-head rows, codec stage at T=1).
 //            HBM-bound weight stream.  MFMA 16x16x32 with W as the A operand
 //            (16 weight rows = the MFMA M dim) and the <=16*MREP activation rows
-//            as the B operand; each wave streams a contiguous K range straight
-//            to VGPRs (no LDS: the "GEMV / M <= 16" row of the guide), waves of a
-//            workgroup split K and reduce through LDS, and workgroups may split
-//            K further with an agent-scope release/acquire ticket (last arriver
-//            reduces the fp32 slabs and runs the epilogue).
+//            as the B operand.  One workgroup per 16 weight rows; up to 16 waves
+//            split K and each wave issues U chunks (U x 1 KB per wave) of weight
+//            loads before its first MFMA, so a 16-wave workgroup keeps >100 KB in
+//            flight (the "GEMV / M <= 16" row of cdna_hip_programming.md: no LDS
+//            staging).  Waves reduce through LDS.  Cross-workgroup split-K (agent
+//            release / ticket / acquire, Guideline 16) only for few-tile shapes.
 //   k_gemm : M > 64 (codec stages at T >= 8, LM prefill).  64 x BN workgroup
 //            tile, 4 waves of 32 x BN/2, operands straight from L2.
 #include "kernels.h"
 
+DEV f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
 
-// ---- epilogue on one 16(n) x 16(m) MFMA tile held in the C/D layout:
-// lane l holds m = m0 + (l & 15), n = n0 + 4*(l >> 4) + i, i = 0..3.
-DEV void epi_tile(const EpiArgs& e, int M, int N, int m, int n0, int lane, const float v_in[4]) {
+// ------------------------------------------------------------------ A transform
+// Inverse RMS of rows [m0, m0 + nrows) (local index i -> inv_s[i]); same
+// summation order as k_rmsnorm (lane-strided 8-element chunks, wave sum).
+DEV void row_inv(const GemmArgs& a, int m0, int nrows, float* inv_s, int wave, int NW, int lane) {
+  const int nch = a.K >> 3;
+  for (int i = wave; i < nrows; i += NW) {
+    const int m = m0 + i;
+    float ss = 0.f;
+    if (m < a.M) {
+      const bf16* x = rm_bf(a.a, m);
+      for (int c = lane; c < nch; c += 64) {
+        const bf16x8 v = *(const bf16x8*)(x + c * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += bf(v[j]) * bf(v[j]);
+      }
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) inv_s[i] = rsqrtf(ss / (float)a.K + a.xf.eps);
+  }
+}
+
+template <int XF>
+DEV bf16x8 xform(const GemmArgs& a, bf16x8 x, int m, int k, float inv) {
+  bf16x8 o;
+  if (XF == XF_NORM) {
+    bf16x8 wv, sh, sc;
+    if (a.xf.w) wv = *(const bf16x8*)(a.xf.w + k);
+    const bf16* md = a.xf.mod ? a.xf.mod + (long long)m * a.xf.mod_ld : nullptr;
+    if (md) {
+      sh = *(const bf16x8*)(md + a.xf.shift_off + k);
+      sc = *(const bf16x8*)(md + a.xf.scale_off + k);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = rb(bf(x[j]) * inv);
+      if (a.xf.w) t = rb(t * bf(wv[j]));
+      if (md) t = rb(rb(t * rb(1.0f + bf(sc[j]))) + bf(sh[j]));
+      o[j] = tobf(t);
+    }
+  } else if (XF == XF_SILU_ADD) {
+    const bf16x8 v = *(const bf16x8*)(a.xf.vec + k);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = tobf(silu_f(rb(bf(x[j]) + bf(v[j]))));
+  } else {
+    o = x;
+  }
+  return o;
+}
+
+// ------------------------------------------------------------------ epilogues
+// One 16(n) x 16(m) MFMA tile in the C/D layout: lane l holds m = m0 + (l & 15),
+// n = n0 + 4*(l >> 4) + i, i = 0..3.  Every lane of the wave must call this
+// (cross-lane exchanges), rows m >= M are dropped inside.
+
+// RoPE epilogue (Qwen2 q/k/v projection + apply_rotary_pos_emb + cache append;
+// transformers modeling_qwen2.py:99-134, 195-247).  Packed q/k rows: tile tt of
+// head h holds dims [8tt, 8tt+8) in rows 0..7 and [64+8tt, 64+8tt+8) in rows
+// 8..15 (weights.py: _rope_pack); v rows are in natural order.
+DEV void epi_rope(const GemmArgs& a, int m, int n0, int lane, float v[4]) {
+  const RopeEpi& R = a.rope;
+  constexpr int d = 128;
+  const int g = lane >> 4;
+  if (a.epi.bias) {
+    const bf16x4 b = *(const bf16x4*)(a.epi.bias + n0 + 4 * g);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] += bf(b[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = rb(v[i]);  // q/k/v_proj output (bf16)
+  const int h = n0 / d, tt = (n0 % d) >> 4;
+  if (h < R.nh + R.nkv) {
+    float u[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) u[i] = __shfl_xor(v[i], 32);
+    if (g >= 2 || m >= a.M) return;
+    const int j = 8 * tt + 4 * g;
+    const int p = R.pos[m];
+    bf16x4 o1, o2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float f = (float)p * R.inv_freq[j + i];
+      const float cs = rb(cosf(f)), sn = rb(sinf(f));
+      o1[i] = tobf(rb(v[i] * cs) + rb(-u[i] * sn));
+      o2[i] = tobf(rb(u[i] * cs) + rb(v[i] * sn));
+    }
+    bf16* dst = h < R.nh ? R.q_out + (long long)m * R.nh * d + h * d
+                         : R.kv.k + (long long)R.layer * R.kv.s_layer + (long long)R.slots[m] * R.kv.s_slot +
+                               (long long)(h - R.nh) * R.kv.s_head + (long long)p * d;
+    *(bf16x4*)(dst + j) = o1;
+    *(bf16x4*)(dst + j + 64) = o2;
+  } else {
+    if (m >= a.M) return;
+    const int hv = h - R.nh - R.nkv;
+    bf16* dst = R.kv.v + (long long)R.layer * R.kv.s_layer + (long long)R.slots[m] * R.kv.s_slot +
+                (long long)hv * R.kv.s_head + (long long)R.pos[m] * d + (n0 % d) + 4 * g;
+    bf16x4 o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = tobf(v[i]);
+    *(bf16x4*)dst = o;
+  }
+}
+
+// CFG combine + DPM-Solver++ update (sample_speech_tokens,
+// modeling_vibevoice_inference.py:717-724; DPMSolverMultistepScheduler.step,
+// dpm_solver.py:935-1022) on the final linear's rows: rows [0, n) are the
+// conditional and [n, 2n) the unconditional v-predictions, 2n <= 16 so row r and
+// its partner r + n sit in the same 16-lane group.
+DEV void epi_dpm(const GemmArgs& a, int n0, int lane, const float v[4]) {
+  const DpmEpi& P = a.dpm;
+  const int g = lane >> 4, r = lane & 15, n = P.n;
+  float e[4], u[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) e[i] = rb(v[i]);  // final_layer.linear output (bf16, no bias)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) u[i] = __shfl(e[i], (lane + n) & 63);
+  if (r >= n) return;
+  const DpmCoef& k = P.k;
+  const long long off = (long long)r * a.N + n0 + 4 * g;
+  const bf16x4 xv = *(const bf16x4*)(P.x + off);
+  const bf16x4 mv = *(const bf16x4*)(P.m1 + off);
+  bf16x4 xo, mo;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float c = e[i], un = u[i];
+    const float vv = rb(un + rb(k.cfg * rb(c - un)));
+    const float xs = bf(xv[i]);
+    const float x0 = rb(rb(k.alpha_s * xs) - rb(k.sigma_s * vv));
+    float out = k.c_x * xs - rb(k.c_d0 * x0);
+    if (k.order == 2) {
+      const float d1 = rb(k.inv_r0 * rb(x0 - bf(mv[i])));
+      out = out - rb(k.c_d1 * d1);
+    }
+    xo[i] = tobf(out);
+    mo[i] = tobf(x0);
+  }
+  *(bf16x4*)(P.x + off) = xo;
+  *(bf16x4*)(P.m1 + off) = mo;
+}
+
+DEV void epi_tile(const GemmArgs& a, int m, int n0, int lane, const float v_in[4]) {
+  const EpiArgs& e = a.epi;
   float v[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) v[i] = v_in[i];
   const int g = lane >> 4;
+  if (e.kind == EPI_ROPE) {
+    epi_rope(a, m, n0, lane, v);
+    return;
+  }
+  if (e.kind == EPI_CFG_DPM) {
+    epi_dpm(a, n0, lane, v);
+    return;
+  }
   if (e.kind == EPI_SILU_MUL) {
     // rows 0..7 of the tile are gate, 8..15 the matching up rows; lane g<2 holds
     // gate rows 4g+i, lane g+2 holds up rows 8+4g+i
     float u[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) u[i] = __shfl_xor(v[i], 32);
-    if (g >= 2 || m >= M) return;
+    if (g >= 2 || m >= a.M) return;
     const int col = (n0 >> 1) + 4 * g;
     bf16x4 o;
 #pragma unroll
@@ -44,7 +206,7 @@ DEV void epi_tile(const EpiArgs& e, int M, int N, int m, int n0, int lane, const
     *(bf16x4*)(rm_bfw(e.out, m) + col) = o;
     return;
   }
-  if (m >= M) return;
+  if (m >= a.M) return;
   const int n = n0 + 4 * g;
   if (e.bias) {
     bf16x4 b = *(const bf16x4*)(e.bias + n);
@@ -89,134 +251,254 @@ DEV void epi_tile(const EpiArgs& e, int M, int N, int m, int n0, int lane, const
   *(bf16x4*)(rm_bfw(e.out, m) + n) = o;
 }
 
-DEV f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+// ------------------------------------------------------------------ GEMV
+// Split-K hand-off of the 16 x (16*MREP) fp32 tile between the workgroups of one
+// tile column: every split stores its slab, takes a ticket, the last arriver
+// sums the slabs in split order (deterministic) and runs the epilogue.
+//   handoff 0: plain stores + agent release / acquire fences (Guideline 16 R1)
+//   handoff 1: sc1 (write-through) 4-B stores, vmcnt(0) in every storing wave,
+//              one agent atomic per workgroup, sc1 loads by the last arriver
+//              (MI355X_MICROARCH.md "Valid forms", first table row)
+// Returns true in the workgroup that must run the epilogue (red[] = sums).
+DEV bool splitk_handoff(const GemmArgs& a, float* red, int TILE, unsigned* last_flag) {
+  float* slab = a.ws + ((long long)blockIdx.x * a.ksplit + blockIdx.y) * TILE;
+  const int t = threadIdx.x;
+  if (a.handoff == 1) {
+    for (int e = t; e < TILE; e += blockDim.x) __hip_atomic_store(slab + e, red[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    for (int e = t; e < TILE; e += blockDim.x) slab[e] = red[e];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    if (a.handoff != 1) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const unsigned tk = __hip_atomic_fetch_add(&a.counters[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *last_flag = tk == (unsigned)(a.ksplit - 1) ? 1u : 0u;
+    if (*last_flag) {
+      if (a.handoff != 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __hip_atomic_store(&a.counters[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  if (!*last_flag) return false;
+  const float* slabs = a.ws + (long long)blockIdx.x * a.ksplit * TILE;
+  for (int e = t; e < TILE; e += blockDim.x) {
+    float s = 0.f;
+    if (a.handoff == 1) {
+      for (int k = 0; k < a.ksplit; ++k) s += __hip_atomic_load(slabs + k * TILE + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      for (int k = 0; k < a.ksplit; ++k) s += slabs[k * TILE + e];
+    }
+    red[e] = s;
+  }
+  __syncthreads();
+  return true;
 }
 
-// ------------------------------------------------------------------ GEMV
-template <int MREP, int U>
-__global__ void __launch_bounds__(1024) k_gemv(GemmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float red[];
+// M <= 16: the workgroup's A rows (its K range, transformed) are staged once in
+// LDS; each wave streams its weight chunks with a two-deep register ping-pong
+// (U chunks = U KB per wave in flight while the previous U are multiplied).
+template <int U, int XF>
+__global__ void __launch_bounds__(256) k_gemv1(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ float inv_s[16];
+  __shared__ float red[4 * 256];
+  __shared__ unsigned last_flag;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, NW = blockDim.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int n0 = blockIdx.x * 16;
   const int nchunk = a.K >> 5;
-  const int gw = blockIdx.y * NW + wave, GW = gridDim.y * NW;
-  const int c0 = (int)((long long)nchunk * gw / GW);
-  const int c1 = (int)((long long)nchunk * (gw + 1) / GW);
+  // this workgroup's chunk range, then each wave's
+  const int b0 = (int)((long long)nchunk * blockIdx.y / a.ksplit);
+  const int b1 = (int)((long long)nchunk * (blockIdx.y + 1) / a.ksplit);
+  const int c0 = b0 + (int)((long long)(b1 - b0) * wave / NW);
+  const int c1 = b0 + (int)((long long)(b1 - b0) * (wave + 1) / NW);
+  const bf16* wrow = a.w + (long long)(n0 >> 4) * a.K * 16 + lane * 8;  // MFMA-packed W
+  const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
 
-  const bf16* wrow = a.w + (long long)(n0 + r) * a.ldw + 8 * g;
+  // first weight chunks go out before the A staging (they do not depend on it)
+  bf16x8 wa[U], wb[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) wa[u] = *(const bf16x8*)(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
+
+  // ---- stage A rows [0, M) x chunks [b0, b1) into LDS (row stride padded 16 B)
+  const int kw = (b1 - b0) * 32;         // elements staged per row
+  const int lds_ld = kw + 8;
+  bf16* xs = (bf16*)smem;
+  if (XF == XF_NORM) {
+    row_inv(a, 0, a.M, inv_s, wave, NW, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  for (int e = threadIdx.x; e < a.M * (kw >> 3); e += blockDim.x) {
+    const int m = e / (kw >> 3), k8 = (e - m * (kw >> 3)) * 8;
+    const int k = b0 * 32 + k8;
+    bf16x8 x = *(const bf16x8*)(rm_bf(a.a, m) + k);
+    if (XF != XF_NONE) x = xform<XF>(a, x, m, k, XF == XF_NORM ? inv_s[m] : 0.f);
+    *(bf16x8*)(xs + m * lds_ld + k8) = x;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+  f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const bool xok = r < a.M;
+  const bf16* xrow = xs + r * lds_ld + 8 * g - b0 * 32;
+  auto compute = [&](bf16x8 (&wf)[U], int c) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool ok = c + u < c1;
+      const bf16x8 w = ok ? wf[u] : zero8;
+      const bf16x8 x = (xok && ok) ? *(const bf16x8*)(xrow + (c + u) * 32) : zero8;
+      acc = mfma(w, x, acc);
+    }
+  };
+  auto load = [&](bf16x8 (&wf)[U], int c) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) wf[u] = *(const bf16x8*)(wrow + min(c + u, max(c1 - 1, 0)) * 512);
+  };
+  for (int c = c0; c < c1; c += 2 * U) {
+    load(wb, c + U);
+    compute(wa, c);
+    load(wa, c + 2 * U);
+    compute(wb, c + U);
+  }
+
+  // ---- reduce the waves of this workgroup
+#pragma unroll
+  for (int i = 0; i < 4; ++i) red[(wave * 4 + i) * 64 + lane] = acc[i];
+  __syncthreads();
+  if (NW > 1) {
+    for (int e = threadIdx.x; e < 256; e += blockDim.x) {
+      float s = 0.f;
+      for (int w = 1; w < NW; ++w) s += red[w * 256 + e];
+      red[e] += s;
+    }
+    __syncthreads();
+  }
+  if (a.ksplit > 1 && !splitk_handoff(a, red, 256, &last_flag)) return;
+  if (wave == 0) {
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = red[i * 64 + lane];
+    epi_tile(a, r, n0, lane, v);
+  }
+}
+
+// 16 < M <= 64: A fragments loaded straight from global / L2, transform per
+// chunk; weights ping-ponged as in k_gemv1.
+template <int MREP, int U, int XF>
+__global__ void __launch_bounds__(256) k_gemv(GemmArgs a) {
+  __shared__ float red[4 * MREP * 256];
+  __shared__ float inv_s[64];
+  __shared__ unsigned last_flag;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, NW = blockDim.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * 16;
+  const int nchunk = a.K >> 5;
+  const int b0 = (int)((long long)nchunk * blockIdx.y / a.ksplit);
+  const int b1 = (int)((long long)nchunk * (blockIdx.y + 1) / a.ksplit);
+  const int c0 = b0 + (int)((long long)(b1 - b0) * wave / NW);
+  const int c1 = b0 + (int)((long long)(b1 - b0) * (wave + 1) / NW);
+  const bf16* wrow = a.w + (long long)(n0 >> 4) * a.K * 16 + lane * 8;  // MFMA-packed W
+  const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+  bf16x8 wa[U], wb[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) wa[u] = *(const bf16x8*)(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
+  if (XF == XF_NORM) {
+    row_inv(a, 0, 16 * MREP, inv_s, wave, NW, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
   const bf16* xrow[MREP];
   bool xok[MREP];
+  float inv[MREP];
 #pragma unroll
   for (int mr = 0; mr < MREP; ++mr) {
     const int m = r + 16 * mr;
     xok[mr] = m < a.M;
     xrow[mr] = xok[mr] ? rm_bf(a.a, m) + 8 * g : nullptr;
+    inv[mr] = XF == XF_NORM ? inv_s[m] : 0.f;
   }
   f32x4 acc[MREP];
 #pragma unroll
   for (int mr = 0; mr < MREP; ++mr) acc[mr] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-
-  int c = c0;
-  for (; c + U <= c1; c += U) {
-    bf16x8 wf[U], xf[U][MREP];
+  auto compute = [&](bf16x8 (&wf)[U], int c) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) wf[u] = *(const bf16x8*)(wrow + (c + u) * 32);
+    for (int u = 0; u < U; ++u) {
+      const bool ok = c + u < c1;
+      const int cc = min(c + u, max(c1 - 1, 0));
+      const bf16x8 w = ok ? wf[u] : zero8;
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int mr = 0; mr < MREP; ++mr)
-        xf[u][mr] = xok[mr] ? *(const bf16x8*)(xrow[mr] + (c + u) * 32) : zero8;
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int mr = 0; mr < MREP; ++mr) acc[mr] = mfma(wf[u], xf[u][mr], acc[mr]);
-  }
-  for (; c < c1; ++c) {
-    bf16x8 wf = *(const bf16x8*)(wrow + c * 32);
-#pragma unroll
-    for (int mr = 0; mr < MREP; ++mr) {
-      bf16x8 xf = xok[mr] ? *(const bf16x8*)(xrow[mr] + c * 32) : zero8;
-      acc[mr] = mfma(wf, xf, acc[mr]);
+      for (int mr = 0; mr < MREP; ++mr) {
+        bf16x8 x = (xok[mr] && ok) ? *(const bf16x8*)(xrow[mr] + cc * 32) : zero8;
+        if (XF != XF_NONE && xok[mr] && ok) x = xform<XF>(a, x, r + 16 * mr, cc * 32 + 8 * g, inv[mr]);
+        acc[mr] = mfma(w, x, acc[mr]);
+      }
     }
+  };
+  auto load = [&](bf16x8 (&wf)[U], int c) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) wf[u] = *(const bf16x8*)(wrow + min(c + u, max(c1 - 1, 0)) * 512);
+  };
+  for (int c = c0; c < c1; c += 2 * U) {
+    load(wb, c + U);
+    compute(wa, c);
+    load(wa, c + 2 * U);
+    compute(wb, c + U);
   }
-
-  // ---- reduce the NW waves of this workgroup:  red[wave][mr*4 + i][lane]
   const int TILE = MREP * 256;
 #pragma unroll
   for (int mr = 0; mr < MREP; ++mr)
 #pragma unroll
     for (int i = 0; i < 4; ++i) red[(wave * MREP * 4 + mr * 4 + i) * 64 + lane] = acc[mr][i];
   __syncthreads();
-  for (int e = threadIdx.x; e < TILE; e += blockDim.x) {
-    float s = 0.f;
-    for (int w = 1; w < NW; ++w) s += red[w * TILE + e];
-    red[e] += s;
-  }
-  __syncthreads();
-
-  if (a.ksplit > 1) {
-    // ---- cross-workgroup split-K: plain slab stores, agent release, ticket;
-    // the last arriver acquires and reduces (cdna_hip_programming.md §5,
-    // "In-launch split-K reduction"; Guideline 16).
-    __shared__ unsigned last_flag;
-    float* slab = a.ws + ((long long)blockIdx.x * a.ksplit + blockIdx.y) * TILE;
-    for (int e = threadIdx.x; e < TILE; e += blockDim.x) slab[e] = red[e];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      unsigned t = __hip_atomic_fetch_add(&a.counters[blockIdx.x], 1u, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-      last_flag = (t == (unsigned)(a.ksplit - 1)) ? 1u : 0u;
-      if (last_flag) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    }
-    __syncthreads();
-    if (!last_flag) return;
-    const float* slabs = a.ws + (long long)blockIdx.x * a.ksplit * TILE;
+  if (NW > 1) {
     for (int e = threadIdx.x; e < TILE; e += blockDim.x) {
       float s = 0.f;
-      for (int k = 0; k < a.ksplit; ++k) s += slabs[k * TILE + e];
-      red[e] = s;
+      for (int w = 1; w < NW; ++w) s += red[w * TILE + e];
+      red[e] += s;
     }
-    if (threadIdx.x == 0)
-      __hip_atomic_store(&a.counters[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
   }
-  // ---- epilogue: wave mr handles MFMA tile mr (lane layout preserved)
+  if (a.ksplit > 1 && !splitk_handoff(a, red, TILE, &last_flag)) return;
   for (int mr = wave; mr < MREP; mr += NW) {
     float v[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = red[(mr * 4 + i) * 64 + lane];
-    epi_tile(a.epi, a.M, a.N, r + 16 * mr, n0, lane, v);
+    epi_tile(a, r + 16 * mr, n0, lane, v);
   }
 }
 
 // ------------------------------------------------------------------ tiled GEMM (M > 64)
-template <int BN>
+template <int BN, int XF>
 __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
   constexpr int NT = BN / 32;  // 16-wide n tiles per wave (wave covers BN/2 columns)
+  __shared__ float inv_s[64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m_base = blockIdx.x * 64 + wm * 32;
+  const int m_blk = blockIdx.x * 64;
+  const int m_base = m_blk + wm * 32;
   const int n_base = blockIdx.y * BN + wn * (BN / 2);
+  if (XF == XF_NORM) {
+    row_inv(a, m_blk, 64, inv_s, wave, 4, lane);
+    __syncthreads();
+  }
   const bf16* wrow[NT];
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) wrow[nt] = a.w + (long long)(n_base + nt * 16 + r) * a.ldw + 8 * g;
+  for (int nt = 0; nt < NT; ++nt) wrow[nt] = a.w + (long long)((n_base >> 4) + nt) * a.K * 16 + lane * 8;
   const bf16* xrow[2];
   bool xok[2];
+  float inv[2];
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
     const int m = m_base + mt * 16 + r;
     xok[mt] = m < a.M;
     xrow[mt] = xok[mt] ? rm_bf(a.a, m) + 8 * g : nullptr;
+    inv[mt] = XF == XF_NORM ? inv_s[m - m_blk] : 0.f;
   }
   f32x4 acc[2][NT];
 #pragma unroll
@@ -225,89 +507,147 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
     for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
   const int nk = a.K >> 5;
-  int c = 0;
-  for (; c + 2 <= nk; c += 2) {
+  for (int c = 0; c < nk; c += 2) {
     bf16x8 wf[2][NT], xf[2][2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
+      const int cc = min(c + u, nk - 1);
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) wf[u][nt] = *(const bf16x8*)(wrow[nt] + (c + u) * 32);
+      for (int nt = 0; nt < NT; ++nt) wf[u][nt] = *(const bf16x8*)(wrow[nt] + cc * 512);
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) xf[u][mt] = xok[mt] ? *(const bf16x8*)(xrow[mt] + (c + u) * 32) : zero8;
+      for (int mt = 0; mt < 2; ++mt) xf[u][mt] = xok[mt] ? *(const bf16x8*)(xrow[mt] + cc * 32) : zero8;
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < 2; ++u) {
+      if (c + u >= nk) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) wf[u][nt] = zero8;
+      }
+      if (XF != XF_NONE) {
+        const int k = min(c + u, nk - 1) * 32 + 8 * g;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+          if (xok[mt]) xf[u][mt] = xform<XF>(a, xf[u][mt], m_base + mt * 16 + r, k, inv[mt]);
+      }
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma(wf[u][nt], xf[u][mt], acc[mt][nt]);
-  }
-  for (; c < nk; ++c) {
-    bf16x8 wf[NT], xf[2];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) wf[nt] = *(const bf16x8*)(wrow[nt] + c * 32);
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) xf[mt] = xok[mt] ? *(const bf16x8*)(xrow[mt] + c * 32) : zero8;
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma(wf[nt], xf[mt], acc[mt][nt]);
+    }
   }
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       float v[4] = {acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]};
-      epi_tile(a.epi, a.M, a.N, m_base + mt * 16 + r, n_base + nt * 16, lane, v);
+      epi_tile(a, m_base + mt * 16 + r, n_base + nt * 16, lane, v);
     }
 }
 
 // ------------------------------------------------------------------ host launch
+static int g_tune_nw = 0, g_tune_ks = 0, g_tune_handoff = -1, g_tune_waves = 0;
+
+extern "C" int vv_gemv_tune(int nw, int ks, int handoff, int target_waves) {
+  g_tune_nw = nw;
+  g_tune_ks = ks;
+  g_tune_handoff = handoff;
+  g_tune_waves = target_waves;
+  return 0;
+}
+
 struct GemmPlan { int nw, ksplit; };
 
+// Measured on MI355X (tools/gemv_sweep.py, profiles/r01_gemv_sweep.txt): four
+// waves per workgroup and NO cross-workgroup split-K is fastest or within 3 %
+// for every decode shape of the loop — a split-K hand-off costs >= 2 us (sc1
+// form) to 30 us (fence form), more than the extra CUs it brings.
 static GemmPlan gemv_plan(int N, int K) {
-  const int tiles = N / 16, chunks = K / 32;
-  int wpt = (2048 + tiles - 1) / tiles;
-  int maxw = chunks / 4 > 0 ? chunks / 4 : 1;
-  if (wpt > maxw) wpt = maxw;
-  if (wpt < 1) wpt = 1;
-  int ks = (256 + tiles - 1) / tiles;
-  if (ks > wpt) ks = wpt;
-  if (ks < 1) ks = 1;
-  int nw = (wpt + ks - 1) / ks;
-  if (nw > 16) nw = 16;
+  (void)N;
+  int nw = 4, ks = 1;
+  const int chunks = K / 32;
+  if (g_tune_waves > 0) {
+    const int tiles = N / 16;
+    int wpt = (g_tune_waves + tiles - 1) / tiles;
+    const int maxw = (chunks + 3) / 4;
+    if (wpt > maxw) wpt = maxw;
+    if (wpt < 1) wpt = 1;
+    nw = wpt < 4 ? wpt : 4;
+    ks = (wpt + nw - 1) / nw;
+  }
+  if (g_tune_nw > 0) nw = g_tune_nw;
+  if (g_tune_ks > 0) ks = g_tune_ks;
+  if (ks > chunks) ks = chunks;
   return {nw, ks};
+}
+
+// k_gemv1 stages the A slice in LDS (<= 64 KB)
+static bool gemv1_fits(const GemmArgs& a) {
+  const int nchunk = a.K >> 5;
+  return (size_t)a.M * (((nchunk + a.ksplit - 1) / a.ksplit) * 32 + 8) * 2 <= 65536;
+}
+
+template <int XF>
+static void launch_gemv_xf(const GemmArgs& a, int mrep, dim3 grid, dim3 block, hipStream_t st) {
+  if (mrep == 1 && !gemv1_fits(a)) {
+    hipLaunchKernelGGL((k_gemv<1, 8, XF>), grid, block, 0, st, a);
+    return;
+  }
+  if (mrep == 1) {
+    const int nchunk = a.K >> 5;
+    const int kw = ((nchunk + a.ksplit - 1) / a.ksplit) * 32;
+    const size_t lds = (size_t)a.M * (kw + 8) * sizeof(bf16);
+    hipLaunchKernelGGL((k_gemv1<8, XF>), grid, block, lds, st, a);
+    return;
+  }
+  switch (mrep) {
+    case 2: hipLaunchKernelGGL((k_gemv<2, 4, XF>), grid, block, 0, st, a); break;
+    case 3: hipLaunchKernelGGL((k_gemv<3, 2, XF>), grid, block, 0, st, a); break;
+    default: hipLaunchKernelGGL((k_gemv<4, 2, XF>), grid, block, 0, st, a); break;
+  }
+}
+
+template <int XF>
+static int launch_gemm_xf(const GemmArgs& a, hipStream_t st) {
+  if (a.N % 64 == 0) {
+    dim3 grid((a.M + 63) / 64, a.N / 64);
+    hipLaunchKernelGGL((k_gemm<64, XF>), grid, dim3(256), 0, st, a);
+  } else if (a.N % 32 == 0) {
+    dim3 grid((a.M + 63) / 64, a.N / 32);
+    hipLaunchKernelGGL((k_gemm<32, XF>), grid, dim3(256), 0, st, a);
+  } else {
+    return 1;
+  }
+  return 0;
 }
 
 // returns 0 ok, else an error code (see engine.cpp)
 int launch_gemm(GemmArgs a, hipStream_t st) {
   if (a.M <= 0) return 0;
   if (a.K % 32 != 0 || a.N % 16 != 0) return 1;
-  if (a.epi.kind == EPI_SILU_MUL && a.N % 16 != 0) return 1;
+  if (a.xf.kind == XF_NORM && a.K % 8 != 0) return 1;
+  if (a.epi.kind == EPI_ROPE && (a.rope.kv.d != 128 || !a.rope.pos || !a.rope.slots)) return 1;
+  if (a.epi.kind == EPI_CFG_DPM && (a.M > 16 || 2 * a.dpm.n != a.M)) return 1;
   if (a.M <= 64) {
-    GemmPlan p = gemv_plan(a.N, a.K);
     const int mrep = (a.M + 15) / 16;
+    GemmPlan p = gemv_plan(a.N, a.K);
     a.ksplit = p.ksplit;
-    if (a.ksplit > 1 && (!a.ws || !a.counters)) a.ksplit = 1;
+    if (a.ksplit > 1 && (!a.ws || !a.counters || a.N / 16 > 65536)) a.ksplit = 1;
+    a.handoff = g_tune_handoff >= 0 ? g_tune_handoff : 1;
     dim3 grid(a.N / 16, a.ksplit), block(64 * p.nw);
-    size_t lds = (size_t)p.nw * mrep * 256 * sizeof(float);
-    if (lds < (size_t)mrep * 256 * sizeof(float)) lds = (size_t)mrep * 256 * sizeof(float);
-    switch (mrep) {
-      case 1: hipLaunchKernelGGL((k_gemv<1, 8>), grid, block, lds, st, a); break;
-      case 2: hipLaunchKernelGGL((k_gemv<2, 4>), grid, block, lds, st, a); break;
-      case 3: hipLaunchKernelGGL((k_gemv<3, 4>), grid, block, lds, st, a); break;
-      default: hipLaunchKernelGGL((k_gemv<4, 2>), grid, block, lds, st, a); break;
+    switch (a.xf.kind) {
+      case XF_NORM: launch_gemv_xf<XF_NORM>(a, mrep, grid, block, st); break;
+      case XF_SILU_ADD: launch_gemv_xf<XF_SILU_ADD>(a, mrep, grid, block, st); break;
+      default: launch_gemv_xf<XF_NONE>(a, mrep, grid, block, st); break;
     }
   } else {
-    if (a.N % 64 == 0) {
-      dim3 grid((a.M + 63) / 64, a.N / 64);
-      hipLaunchKernelGGL((k_gemm<64>), grid, dim3(256), 0, st, a);
-    } else if (a.N % 32 == 0) {
-      dim3 grid((a.M + 63) / 64, a.N / 32);
-      hipLaunchKernelGGL((k_gemm<32>), grid, dim3(256), 0, st, a);
-    } else {
-      return 1;
+    if (a.epi.kind == EPI_CFG_DPM) return 1;
+    int rc;
+    switch (a.xf.kind) {
+      case XF_NORM: rc = launch_gemm_xf<XF_NORM>(a, st); break;
+      case XF_SILU_ADD: rc = launch_gemm_xf<XF_SILU_ADD>(a, st); break;
+      default: rc = launch_gemm_xf<XF_NONE>(a, st); break;
     }
+    if (rc) return rc;
   }
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

@@ -3,13 +3,62 @@
 #pragma once
 #include "common.h"
 
+struct DpmCoef {
+  float cfg;
+  float alpha_s, sigma_s;  // x0 = alpha_s * x - sigma_s * v          (bf16 ops)
+  float c_x, c_d0, c_d1, inv_r0;
+  int order;               // 1: x' = c_x x - bf16(c_d0 x0)
+                           // 2: x' = c_x x - bf16(c_d0 x0) - bf16(c_d1 bf16(inv_r0 bf16(x0 - m1)))
+};
+
+struct KVLayout {
+  bf16* k;
+  bf16* v;
+  long long s_layer, s_slot, s_head;  // elements; s_ctx = d
+  int d, max_ctx;
+};
+
+// A-operand transform (XF_*).  XF_NORM: inverse RMS of each A row over K, then
+// bf16(bf16(x * inv) * w) (w optional) and optionally the adaLN modulate
+// bf16(bf16(y * bf16(1 + scale)) + shift) with shift/scale read from `mod` rows.
+struct ATransform {
+  int kind;
+  float eps;
+  const bf16* w;
+  const bf16* mod;
+  long long mod_ld;
+  int shift_off, scale_off;
+  const bf16* vec;      // XF_SILU_ADD
+};
+
+struct RopeEpi {         // EPI_ROPE
+  int nh, nkv, layer, pad_;
+  bf16* q_out;           // [M][nh*d]
+  const int* slots;      // [M] KV slot of row
+  const int* pos;        // [M] position == cache index written
+  const float* inv_freq; // [d/2]
+  KVLayout kv;
+};
+
+struct DpmEpi {          // EPI_CFG_DPM
+  int n, pad_;
+  DpmCoef k;
+  bf16* x;               // [n][N] latent, updated in place
+  bf16* m1;              // [n][N] previous x0 (2nd-order history)
+};
+
 struct GemmArgs {
   int M, N, K;
   int ksplit;
+  int handoff;            // split-K hand-off form (gemm.hip: splitk_handoff)
+  int pad_;
   RowMap a;
   const bf16* w;
   long long ldw;
   EpiArgs epi;
+  ATransform xf;
+  RopeEpi rope;
+  DpmEpi dpm;
   float* ws;
   unsigned* counters;
 };
@@ -56,20 +105,7 @@ struct RollDesc {
   int ctx, T, C, pad_;
 };
 
-struct DpmCoef {
-  float cfg;
-  float alpha_s, sigma_s;  // x0 = alpha_s * x - sigma_s * v          (bf16 ops)
-  float c_x, c_d0, c_d1, inv_r0;
-  int order;               // 1: x' = c_x x - bf16(c_d0 x0)
-                           // 2: x' = c_x x - bf16(c_d0 x0) - bf16(c_d1 bf16(inv_r0 bf16(x0 - m1)))
-};
 
-struct KVLayout {
-  bf16* k;
-  bf16* v;
-  long long s_layer, s_slot, s_head;  // elements; s_ctx = d
-  int d, max_ctx;
-};
 
 struct RopeArgs {
   int R, nh, nkv, layer;

@@ -186,6 +186,36 @@ def _gu(gate, up):
     return torch.stack([gate.reshape(I // 8, 8, H), up.reshape(I // 8, 8, H)], dim=1).reshape(2 * I, H)
 
 
+def mfma_pack(w):
+    """[N, K] -> the same shape in MFMA-fragment order (csrc/gemm.hip header):
+    block (tile t, chunk c) of 16 rows x 32 columns is 1 KB contiguous, lane l
+    holding W[16t + (l & 15)][32c + 8(l >> 4) .. +7]."""
+    N, K = w.shape
+    assert N % 16 == 0 and K % 32 == 0, (N, K)
+    return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().reshape(N, K)
+
+
+def mfma_unpack(w):
+    N, K = w.shape
+    return w.reshape(N // 16, K // 32, 4, 16, 8).permute(0, 3, 1, 2, 4).contiguous().reshape(N, K)
+
+
+def is_gemm_weight(name):
+    """Engine weights consumed by the MFMA GEMM / GEMV kernels (MFMA-packed)."""
+    if not name.endswith("_w") or name.endswith(".dw_w"):
+        return False
+    return name not in ("dec.head_w", "sem.stem_w", "aenc.stem_w")
+
+
+def _rope_pack(x, nheads, d=128):
+    """Reorder q or k projection rows (or bias) so each 16-row MFMA tile holds
+    8 rotary pairs: tile t of a head = dims [8t, 8t+8) then [d/2+8t, d/2+8t+8)
+    (EPI_ROPE layout, csrc/gemm.hip)."""
+    rest = x.shape[1:]
+    y = x.reshape(nheads, 2, d // 16, 8, *rest).transpose(1, 2)
+    return y.reshape(nheads * d, *rest)
+
+
 def _conv_rows(w):
     """[Co, Ci, k] -> [Co, k*Ci], element (co, j*Ci + ci) = w[co, ci, j]."""
     Co, Ci, k = w.shape
@@ -226,8 +256,11 @@ def pack(sd, cfg: VibeVoiceConfig, device, with_acoustic_encoder=True):
         e = f"lm.{i}."
         out[e + "in_norm"] = t(sd[p + "input_layernorm.weight"])
         out[e + "post_norm"] = t(sd[p + "post_attention_layernorm.weight"])
-        out[e + "qkv_w"] = t(torch.cat([sd[p + f"self_attn.{x}_proj.weight"] for x in "qkv"], 0))
-        out[e + "qkv_b"] = t(torch.cat([sd[p + f"self_attn.{x}_proj.bias"] for x in "qkv"], 0))
+        nkv = lm.num_key_value_heads
+        q, k, v = (sd[p + f"self_attn.{x}_proj.weight"] for x in "qkv")
+        qb, kb, vb = (sd[p + f"self_attn.{x}_proj.bias"] for x in "qkv")
+        out[e + "qkv_w"] = t(torch.cat([_rope_pack(q, nh, d), _rope_pack(k, nkv, d), v], 0))
+        out[e + "qkv_b"] = t(torch.cat([_rope_pack(qb, nh, d), _rope_pack(kb, nkv, d), vb], 0))
         out[e + "o_w"] = t(sd[p + "self_attn.o_proj.weight"])
         out[e + "gu_w"] = t(_gu(sd[p + "mlp.gate_proj.weight"], sd[p + "mlp.up_proj.weight"]))
         out[e + "down_w"] = t(sd[p + "mlp.down_proj.weight"])
@@ -302,4 +335,7 @@ def pack(sd, cfg: VibeVoiceConfig, device, with_acoustic_encoder=True):
                 out[b + "fc1_b"] = t(sd[p + "ffn.linear1.bias"])
                 out[b + "fc2_w"] = t(sd[p + "ffn.linear2.weight"])
                 out[b + "fc2_b"] = t(sd[p + "ffn.linear2.bias"])
+    for k in list(out):
+        if is_gemm_weight(k):
+            out[k] = mfma_pack(out[k])
     return out
