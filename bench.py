@@ -74,7 +74,7 @@ def bytes_per_token(wb, cfg, B, S, ctx_pos, ctx_neg):
 
 # ------------------------------------------------------------------ dominant kernel, live
 def measure_gemv(model, B, iters=6):
-    """The LM MLP gate|up weight-streaming GEMV (k_gemv, EPI_SILU_MUL): the
+    """The LM MLP gate|up weight-streaming GEMV (k_gemv1<8, XF_NORM>, EPI_SILU_MUL): the
     largest single launch of the loop (2I x H bf16 = 55 MB at 1.5B, 28 per LM
     pass).  Timed with HIP events on the stream it is launched on, rotating
     over the 28 layers' weights so the Infinity Cache cannot serve it."""
@@ -84,6 +84,7 @@ def measure_gemv(model, B, iters=6):
     H, I, nl = lmc.hidden_size, lmc.intermediate_size, lmc.num_hidden_layers
     M = 2 * B
     A = torch.randn(M, H, device=model.device).bfloat16()
+    norm_w = [eng.w[f"lm.{l}.post_norm"] for l in range(nl)]
     Y = torch.empty(M, I, device=model.device, dtype=torch.bfloat16)
     stream = torch.cuda.current_stream()
     sp = ctypes.c_void_p(stream.cuda_stream)
@@ -91,10 +92,11 @@ def measure_gemv(model, B, iters=6):
     Ws = [eng.w[f"lm.{l}.gu_w"] for l in range(nl)]
 
     def run():
-        for Wt in Ws:
-            _lib.check(L.vv_gemm_bf16(M, 2 * I, H, ctypes.c_void_p(A.data_ptr()), H, ctypes.c_void_p(Wt.data_ptr()),
-                                      None, _lib.EPI["silu_mul"], ctypes.c_void_p(Y.data_ptr()), I, None, None,
-                                      eng.h, sp), "gemv")
+        for Wt, nw_ in zip(Ws, norm_w):   # the in-loop variant: post_attention_layernorm fused on load
+            _lib.check(L.vv_gemm_bf16_norm(M, 2 * I, H, ctypes.c_void_p(A.data_ptr()), H,
+                                           ctypes.c_void_p(nw_.data_ptr()), float(lmc.rms_norm_eps),
+                                           ctypes.c_void_p(Wt.data_ptr()), _lib.EPI["silu_mul"],
+                                           ctypes.c_void_p(Y.data_ptr()), I, eng.h, sp), "gemv")
     run()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
@@ -105,7 +107,7 @@ def measure_gemv(model, B, iters=6):
     avg_s = e0.elapsed_time(e1) / 1e3 / (iters * nl)
     alg = 2 * I * H * 2 + M * H * 2 + M * I * 2
     ach = alg / avg_s / 1e9
-    return dict(kernel="k_gemv (LM gate|up, EPI_SILU_MUL)", shape=f"M={M} N={2 * I} K={H}", bound="hbm",
+    return dict(kernel="k_gemv1<8, 1> (LM post-norm + gate|up + SiLU*up)", shape=f"M={M} N={2 * I} K={H}", bound="hbm",
                 achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
                 traffic=None, avg_us=round(avg_s * 1e6, 2), alg_bytes_per_launch=alg)
 
@@ -143,18 +145,53 @@ def cpu_baseline(cfg, tokens, S):
                        f"B=1, S={S}, {tokens} timed diffusion tokens after a 1-token run (difference of two runs)")
 
 
-# ------------------------------------------------------------------ main
-def main():
-    args = parse()
+# ------------------------------------------------------------------ multi-rank plumbing
+def dist_setup():
+    """One process per GPU (torchrun env).  Returns (world, rank, local, device).
+    Backend: RCCL ("nccl") on the GPUs; gloo when no GPU is visible (CPU tests)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    gpu = torch.cuda.is_available()
+    dev = torch.device("cuda", local) if gpu else torch.device("cpu")
+    if gpu:
+        torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+        if gpu:
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    return world, rank, local, dev
+
+
+def barrier(world):
+    if world > 1:
+        torch.distributed.barrier()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+def max_over_ranks(x, world, dev):
+    """The job's time is the slowest rank's (contract: max over ranks)."""
+    if world == 1:
+        return float(x)
+    t = torch.tensor([float(x)], device=dev, dtype=torch.float64)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t.item())
+
+
+def throughput(dt, batch, steps, world):
+    """Whole-job acoustic tokens/s and audio-sec/wall-sec (weak scaling: every
+    rank serves `batch` dialogues, one frame per dialogue per step)."""
+    tps = batch * steps * world / dt
+    return tps, tps * HOP / SR
+
+
+# ------------------------------------------------------------------ main
+def main():
+    args = parse()
+    world, rank, local, dev = dist_setup()
 
     from vibevoice_amd.modeling_vibevoice_inference import VibeVoiceForConditionalGenerationInference
     from vibevoice_amd.synthetic import synthetic_inputs, tokenizer_ids
@@ -175,26 +212,16 @@ def main():
         assert sess.step()
     ctx0 = int(sess.pos_len.float().mean())
 
-    def barrier():
-        if world > 1:
-            torch.distributed.barrier()
-        torch.cuda.synchronize()
-    barrier()
+    barrier(world)
     t0 = time.perf_counter()
     for _ in range(K):
         assert sess.step()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    barrier()
-    if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = float(t.item())
+    barrier(world)
+    dt = max_over_ranks(dt, world, dev)
     ctx1 = int(sess.pos_len.float().mean())
-
-    tokens = B * K * world
-    tps = tokens / dt
-    audio_per_s = tps * HOP / SR
+    tps, audio_per_s = throughput(dt, B, K, world)
     wb = weight_bytes(model.engine.w)
     ctx_avg = (ctx0 + ctx1) / 2
     bpt = bytes_per_token(wb, model.config, B, S, ctx_avg, (ctx0 + ctx1) / 2 - L)

@@ -76,12 +76,14 @@ int vv_set_valid_ids(vv_ctx* ctx, int n, const int* host_ids);
  * bf16[steps, 256] sinusoidal timestep features. */
 int vv_set_schedule(vv_ctx* ctx, int steps, const float* coef, const void* tfreq, vv_stream st);
 
-/* Token rows through the Qwen2 decoder.  Token i has KV slot slot[i] and
+/* Token rows through the Qwen2 decoder.  Token i reads embedding row
+ * i % embed_rows of embeds (embed_rows <= 0: ntok), has KV slot slot[i] and
  * position pos[i]; its K/V are written at cache index pos[i] of that slot and
  * it attends to cache entries [0, pos[i]].  max_pos_p1 = 1 + max(pos).
  * For the nout rows listed in out_idx the final-norm hidden state is written to
  * hidden_out[nout, H] and the valid-id logits to logits_out[nout, n_valid]. */
-int vv_lm_forward(vv_ctx* ctx, int ntok, const void* embeds, const int* slot, const int* pos, int max_pos_p1,
+int vv_lm_forward(vv_ctx* ctx, int ntok, const void* embeds, int embed_rows, const int* slot, const int* pos,
+                  int max_pos_p1,
                   int nout, const int* out_idx, void* hidden_out, float* logits_out, vv_stream st);
 
 /* Copy the K/V cache entry src[i] -> dst[i] of slot slots[i] (all layers). */
@@ -122,6 +124,11 @@ int vv_scatter_rows(vv_ctx* ctx, int n, int C, const void* src, int64_t lds, con
  * MFMA-packed order of vibevoice_amd/weights.py:mfma_pack (csrc/gemm.hip). */
 int vv_gemm_bf16(int M, int N, int K, const void* A, int64_t lda, const void* W, const void* bias, int epi,
                  void* Y, int64_t ldy, const void* res, const void* gamma, vv_ctx* ws_ctx, vv_stream st);
+/* The same with the A operand RMS-normalised on load (x * rsqrt(mean(x^2) + eps),
+ * bf16, times norm_w when not NULL): the fused input_layernorm / ConvRMSNorm
+ * producer of the loop's GEMMs (no bias / residual epilogues). */
+int vv_gemm_bf16_norm(int M, int N, int K, const void* A, int64_t lda, const void* norm_w, float eps, const void* W,
+                      int epi, void* Y, int64_t ldy, vv_ctx* ws_ctx, vv_stream st);
 /* Tuning hook (benchmarks only): override the GEMV launch plan — waves per
  * workgroup, split-K workgroups, split-K hand-off form (0 fences, 1 sc1),
  * target waves per launch.  0 / -1 restore the built-in plan. */

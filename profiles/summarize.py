@@ -1,16 +1,20 @@
 """Summarise a rocprofv3 --kernel-trace CSV of `bench.py` per generate-loop step.
 
-Steps are delimited by the restricted lm_head launch (k_lmhead_ids, one per LM
+Steps are delimited by the restricted lm_head launch (k_final_head, one per LM
 pass).  For the last N steps it reports GPU busy time, wall time, idle gap and
 the per-kernel (name, grid) breakdown, plus each kernel's average duration.
 Usage: python profiles/summarize.py <run_kernel_trace.csv> [n_steps]
 """
 import collections
 import csv
+import re
 import sys
 
 
 def short(name):
+    m = re.match(r"_Z(\d+)(\w+)", name)
+    if m:                                   # un-demangled (bf16 argument types)
+        return m.group(2)[:int(m.group(1))]
     n = name.split("(")[0]
     if n.startswith("void "):
         n = n[5:]
@@ -26,7 +30,7 @@ def main(path, n_steps=None):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]),
                          (int(r["Grid_Size_X"]), int(r["Grid_Size_Y"]))))
     rows.sort()
-    marks = [i for i, r in enumerate(rows) if r[2] == "k_lmhead_ids"]
+    marks = [i for i, r in enumerate(rows) if r[2] in ("k_lmhead_ids", "k_final_head")]
     steps = list(zip(marks[:-1], marks[1:]))
     # the bench's timed steps are the last ones before the standalone gemv measurement
     if n_steps:

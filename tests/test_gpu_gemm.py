@@ -80,3 +80,28 @@ def test_epilogues(M, epi):
 def test_shape_rejected():
     with pytest.raises(RuntimeError):
         run(4, 100, 64, "store")
+
+
+@pytest.mark.parametrize("M,N,K,weighted", [(2, 17920, 1536, True), (16, 1024, 2048, True), (5, 64, 1536, False),
+                                            (40, 256, 512, True), (96, 256, 256, True)])
+def test_fused_rmsnorm_producer(M, N, K, weighted):
+    """XF_NORM A transform (input_layernorm / ConvRMSNorm / adaLN-free final norm)
+    vs torch: y = bf16(bf16(x * rsqrt(mean(x^2) + eps)) * w), then the GEMM."""
+    g = torch.Generator(device=dev).manual_seed(M + N + K)
+    A = (3 * torch.randn(M, K, device=dev, generator=g)).bfloat16()
+    W = (torch.randn(N, K, device=dev, generator=g) / K ** 0.5).bfloat16()
+    nw = (1 + 0.2 * torch.randn(K, device=dev, generator=g)).bfloat16() if weighted else None
+    eps = 1e-6
+    Y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    rc = _lib.lib().vv_gemm_bf16_norm(M, N, K, P(A), K, P(nw), eps, P(mfma_pack(W)), _lib.EPI["store"], P(Y), N,
+                                      None, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    _lib.check(rc, "gemm_norm")
+    torch.cuda.synchronize()
+    xf = A.float()
+    a = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)).bfloat16()
+    if nw is not None:
+        a = (a.float() * nw.float()).bfloat16()
+    ref = (a.float() @ W.float().t()).bfloat16()
+    e = rel_err(Y, ref)
+    print(M, N, K, e)
+    assert e < 4e-3

@@ -15,8 +15,10 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vibevoice_amd import _lib  # noqa: E402
-from vibevoice_amd.weights import mfma_pack  # noqa: E402
+from vibevoice_amd.weights import mfma_pack, mfma_unpack  # noqa: E402
 
+SHAPES_NORM = [("lm.qkv+norm", 2, 2048, 1536, "store"), ("lm.gu+norm", 2, 17920, 1536, "silu_mul"),
+               ("head.gu+norm", 2, 9216, 1536, "silu_mul"), ("codec.fc1+norm", 1, 8192, 2048, "gelu")]
 SHAPES = [  # name, M, N, K, epi
     ("lm.qkv", 2, 2048, 1536, "store"), ("lm.o", 2, 1536, 1536, "res"), ("lm.gu", 2, 17920, 1536, "silu_mul"),
     ("lm.down", 2, 1536, 8960, "res"), ("head.ada", 2, 21504, 1536, "store"), ("head.gu", 2, 9216, 1536, "silu_mul"),
@@ -38,7 +40,8 @@ def main():
     def sp_():
         return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     results = []
-    for name, M, N, K, epi in SHAPES:
+    shapes = SHAPES_NORM + SHAPES if "--norm" not in sys.argv else SHAPES_NORM
+    for name, M, N, K, epi in shapes:
         ncopy = max(2, (512 << 20) // (N * K * 2) + 1)
         Ws = [(torch.randn(N, K, device=dev) / K ** 0.5).bfloat16() for _ in range(ncopy)]
         A = torch.randn(M, K, device=dev).bfloat16()
@@ -56,7 +59,27 @@ def main():
         elif epi == "res":
             ref = R.float() + ref.bfloat16().float()
 
+        norm = name.endswith("+norm")
+        nw_ = (1 + 0.1 * torch.randn(K, device=dev)).bfloat16() if norm else None
+        if norm:
+            xf = A.float()
+            an = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-6)).bfloat16()
+            an = (an.float() * nw_.float()).bfloat16()
+            ref0 = an.float() @ mfma_unpack(Ws[0]).float().t()
+            if epi == "silu_mul":
+                a_ = ref0.view(M, N // 16, 2, 8)
+                ref = torch.nn.functional.silu(a_[:, :, 0].reshape(M, -1).bfloat16().float()) * \
+                    a_[:, :, 1].reshape(M, -1).bfloat16().float()
+            elif epi == "gelu":
+                ref = torch.nn.functional.gelu(ref0.bfloat16().float())
+            else:
+                ref = ref0
+
         def run(W):
+            if norm:
+                _lib.check(L.vv_gemm_bf16_norm(M, N, K, P(A), K, P(nw_), 1e-6, P(W), _lib.EPI[epi], P(Y), outN, None,
+                                               sp_()))
+                return
             _lib.check(L.vv_gemm_bf16(M, N, K, P(A), K, P(W), None, _lib.EPI[epi], P(Y), outN, P(R), None, None, sp_()))
 
         def measure():
@@ -85,8 +108,8 @@ def main():
 
         configs = [(0, 0, -1, 0)]
         if not quick:
-            configs += [(0, 0, h, t) for h in (0, 1) for t in (1024, 2048, 4096, 8192)]
-            configs += [(nw, ks, h, 0) for nw, ks, h in itertools.product((1, 2, 4), (1, 2, 3, 4, 6, 8, 12, 16), (0, 1))]
+            
+            configs += [(nw, ks, h, 0) for nw, ks, h in itertools.product((1, 2, 4, 8, 16), (1, 2, 4), (1,))]
         best = None
         for nw, ks, h, tw in configs:
             L.vv_gemv_tune(nw, ks, h, tw)
@@ -106,6 +129,9 @@ def main():
             if not ok:
                 print("BAD", json.dumps(rec), flush=True)
         L.vv_gemv_tune(0, 0, -1, 0)
+        if best is None:
+            print(name, "no valid configuration")
+            continue
         dflt = [r for r in results if r["shape"] == name and r["nw"] == 0 and r["ks"] == 0 and r["target"] == 0
                 and r["handoff"] == -1][0]
         print(f"{name:12s} M={M:2d} N={N:6d} K={K:5d} default {dflt['us']:7.2f} us {dflt['gbs']:7.1f} GB/s | "

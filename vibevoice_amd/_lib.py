@@ -38,7 +38,7 @@ EXPORTS = [
     ("vv_finalize", I, [P]),
     ("vv_set_valid_ids", I, [P, I, ctypes.POINTER(I)]),
     ("vv_set_schedule", I, [P, I, ctypes.POINTER(F), P, P]),
-    ("vv_lm_forward", I, [P, I, P, P, P, I, I, P, P, P, P]),
+    ("vv_lm_forward", I, [P, I, P, I, P, P, I, I, P, P, P, P]),
     ("vv_kv_copy", I, [P, I, P, P, P, P]),
     ("vv_embed", I, [P, I, P, P, P]),
     ("vv_diffusion_sample", I, [P, I, P, P, P, F, P]),
@@ -50,6 +50,7 @@ EXPORTS = [
     ("vv_scatter_rows", I, [P, I, I, P, I64, P, P, I64, P]),
     ("vv_gemm_bf16", I, [I, I, I, P, I64, P, P, I, P, I64, P, P, P, P]),
     ("vv_rmsnorm_bf16", I, [I, I, P, I64, P, F, P, I64, P]),
+    ("vv_gemm_bf16_norm", I, [I, I, I, P, I64, P, F, P, I, P, I64, P, P]),
     ("vv_gemv_tune", I, [I, I, I, I]),
 ]
 

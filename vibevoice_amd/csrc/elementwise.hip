@@ -127,19 +127,28 @@ __global__ void __launch_bounds__(256) k_conv_cin1(ConvIn1Args a) {
 // rows [T, T+ctx) -> [0, ctx).  mode 1 zeroes rows [0, ctx) instead
 // (VibeVoiceTokenizerStreamingCache.set_to_zero, :234-241).
 
+// Forward copy row by row is safe when the regions overlap (T < ctx): row i is
+// read before any later iteration overwrites it.  8 channels per thread.
 __global__ void __launch_bounds__(256) k_roll(const RollDesc* d, const int* slots, int mode) {
   const RollDesc r = d[blockIdx.x];
   const int slot = slots[blockIdx.y];
   bf16* base = r.base + (long long)slot * r.sB;
-  for (int c = threadIdx.x; c < r.C; c += blockDim.x) {
-    bf16 v[16];
-    if (mode == 0) {
-      for (int i = 0; i < r.ctx; ++i) v[i] = base[(long long)(r.T + i) * r.C + c];
-    } else {
-      for (int i = 0; i < r.ctx; ++i) v[i] = tobf(0.f);
+  const bf16x8 z8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+  if ((r.C & 7) == 0) {
+    const int n8 = r.C >> 3;
+    for (int e = threadIdx.x; e < r.ctx * n8; e += blockDim.x) {
+      const int i = e / n8, c = (e - i * n8) * 8;
+      if (r.T >= r.ctx || mode == 1) {
+        *(bf16x8*)(base + (long long)i * r.C + c) =
+            mode == 0 ? *(const bf16x8*)(base + (long long)(r.T + i) * r.C + c) : z8;
+      }
     }
-    for (int i = 0; i < r.ctx; ++i) base[(long long)i * r.C + c] = v[i];
+    if (r.T >= r.ctx || mode == 1) return;
   }
+  // narrow or overlapping buffers: one thread per channel, rows in order
+  for (int c = threadIdx.x; c < r.C; c += blockDim.x)
+    for (int i = 0; i < r.ctx; ++i)
+      base[(long long)i * r.C + c] = mode == 0 ? base[(long long)(r.T + i) * r.C + c] : tobf(0.f);
 }
 
 // ---------------------------------------------------------------- small element-wise ops

@@ -418,10 +418,16 @@ static int convnet_run(vv_ctx* c, ConvNet& net, int n, const int* slots, RowMap 
       d.gamma = W(c, b + ".gamma");
       KCHK(launch_dwconv(d, st));
       // ffn
-      // ffn: ConvRMSNorm fused into fc1's A load
+      // ffn: ConvRMSNorm fused into fc1's A load for GEMV-shaped steps (M <= 64);
+      // tiled GEMMs normalise in their own launch (cheaper than a per-tile prologue)
       RowMap Fm = rowmap(net.F, 4LL * C);
-      GemmArgs g1 = gemm_args(c, n * T, 4 * C, C, X, W(c, b + ".fc1_w"), EPI_GELU, Fm, W(c, b + ".fc1_b"));
-      g1.xf = xf_norm(W(c, b + ".ffn_norm"), eps);
+      RowMap fin = X;
+      if (n * T > 64) {
+        fin = rowmap(net.A, C);
+        CHK(rmsnorm(n * T, C, X, fin, W(c, b + ".ffn_norm"), eps, st));
+      }
+      GemmArgs g1 = gemm_args(c, n * T, 4 * C, C, fin, W(c, b + ".fc1_w"), EPI_GELU, Fm, W(c, b + ".fc1_b"));
+      if (n * T <= 64) g1.xf = xf_norm(W(c, b + ".ffn_norm"), eps);
       CHK(gemm(c, g1, st));
       RowMap o = X;
       const bool last = j == net.depth[i] - 1;
@@ -652,8 +658,8 @@ int vv_embed(vv_ctx* c, int n, const int* ids, void* out, vv_stream vst) {
   return 0;
 }
 
-int vv_lm_forward(vv_ctx* c, int ntok, const void* embeds, const int* slot, const int* pos, int max_pos_p1, int nout,
-                  const int* out_idx, void* hidden_out, float* logits_out, vv_stream vst) {
+int vv_lm_forward(vv_ctx* c, int ntok, const void* embeds, int embed_rows, const int* slot, const int* pos,
+                  int max_pos_p1, int nout, const int* out_idx, void* hidden_out, float* logits_out, vv_stream vst) {
   hipStream_t st = (hipStream_t)vst;
   if (!c->finalized) FAIL("vv_lm_forward before vv_finalize");
   if (ntok <= 0) return 0;
@@ -679,14 +685,18 @@ int vv_lm_forward(vv_ctx* c, int ntok, const void* embeds, const int* slot, cons
     if ((size_t)ntok * k.n_kv_heads > 65536) FAIL("attention split tickets exhausted");
     CHK(c->attn_part.ensure((size_t)ntok * k.n_heads * nsplit * (d + 2) * sizeof(float)));
   }
-  HIPCHK(hipMemcpyAsync(h, embeds, (size_t)ntok * H * sizeof(bf16), hipMemcpyDeviceToDevice, st));
+  // token row m reads embeds row m % embed_rows (the negative CFG rows consume the
+  // positive rows' embeddings, :594-596); layer 0's attention residual writes h
+  if (embed_rows <= 0 || embed_rows > ntok) embed_rows = ntok;
+  const RowMap in_m = rowmap(embeds, H, embed_rows, 0);
   RowMap hm = rowmap(h, H);
   const float* inv_freq = (const float*)W(c, "lm.inv_freq");
   for (int l = 0; l < k.n_layers; ++l) {
     const std::string p = "lm." + std::to_string(l);
     // input_layernorm -> q|k|v projection (+bias) -> RoPE -> q / KV cache, one launch
     {
-      GemmArgs g = gemm_args(c, ntok, c->qkv_n, H, hm, W(c, p + ".qkv_w"), EPI_ROPE, RowMap{}, W(c, p + ".qkv_b"));
+      GemmArgs g = gemm_args(c, ntok, c->qkv_n, H, l == 0 ? in_m : hm, W(c, p + ".qkv_w"), EPI_ROPE, RowMap{},
+                             W(c, p + ".qkv_b"));
       g.xf = xf_norm(W(c, p + ".in_norm"), k.rms_eps);
       g.rope.nh = k.n_heads;
       g.rope.nkv = k.n_kv_heads;
@@ -716,7 +726,7 @@ int vv_lm_forward(vv_ctx* c, int ntok, const void* embeds, const int* slot, cons
     at.part_ml = at.part_o ? at.part_o + (size_t)ntok * k.n_heads * nsplit * d : nullptr;
     KCHK(launch_attn(at, st));
     GemmArgs g = gemm_args(c, ntok, H, nhd, rowmap(att, nhd), W(c, p + ".o_w"), EPI_RES, hm);
-    g.epi.res = hm;
+    g.epi.res = l == 0 ? in_m : hm;
     CHK(gemm(c, g, st));
     // post_attention_layernorm fused into gate|up's A load
     g = gemm_args(c, ntok, 2 * I, H, hm, W(c, p + ".gu_w"), EPI_SILU_MUL, rowmap(act, I));
@@ -727,11 +737,9 @@ int vv_lm_forward(vv_ctx* c, int ntok, const void* embeds, const int* slot, cons
     CHK(gemm(c, g, st));
   }
   if (nout > 0) {
-    KCHK(launch_gather_rows(nout, H, h, H, out_idx, rowmap(fin, H), st));
-    CHK(rmsnorm(nout, H, rowmap(fin, H), rowmap(hidden_out, H), W(c, "lm.norm"), k.rms_eps, st));
-    if (logits_out && c->n_valid > 0)
-      KCHK(launch_lmhead_ids(nout, H, (const bf16*)hidden_out, H, W(c, "lm.lm_head"), (const int*)c->valid_ids.p,
-                             c->n_valid, logits_out, st));
+    // gather the output rows + final norm + the valid-id lm_head rows, one launch
+    KCHK(launch_final_head(nout, H, h, out_idx, W(c, "lm.norm"), k.rms_eps, (bf16*)hidden_out, W(c, "lm.lm_head"),
+                           (const int*)c->valid_ids.p, logits_out ? c->n_valid : 0, logits_out, st));
   }
   return 0;
 }
@@ -755,10 +763,15 @@ int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, 
   bf16* act = mod + (size_t)R * MODW;
   bf16* v = act + (size_t)R * F;
   bf16* m1 = v + (size_t)R * D;
-  HIPCHK(hipMemcpyAsync(cat, pos_h, (size_t)n * H * sizeof(bf16), hipMemcpyDeviceToDevice, st));
-  HIPCHK(hipMemcpyAsync(cat + (size_t)n * H, neg_h, (size_t)n * H * sizeof(bf16), hipMemcpyDeviceToDevice, st));
+  // condition rows cat[pos_h, neg_h]: used in place when the caller's rows are adjacent
+  const bf16* cond = (const bf16*)pos_h;
+  if ((const bf16*)neg_h != (const bf16*)pos_h + (size_t)n * H) {
+    HIPCHK(hipMemcpyAsync(cat, pos_h, (size_t)n * H * sizeof(bf16), hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(cat + (size_t)n * H, neg_h, (size_t)n * H * sizeof(bf16), hipMemcpyDeviceToDevice, st));
+    cond = cat;
+  }
   // cond_proj is step-invariant: computed once per token (bit-identical to per step)
-  CHK(gemm(c, gemm_args(c, R, H, H, rowmap(cat, H), W(c, "head.cond_w"), EPI_STORE, rowmap(condp, H)), st));
+  CHK(gemm(c, gemm_args(c, R, H, H, rowmap(cond, H), W(c, "head.cond_w"), EPI_STORE, rowmap(condp, H)), st));
   RowMap xh_m = rowmap(xh, H), a_m = rowmap(a, H);
   for (int s = 0; s < c->steps; ++s) {
     // x = noisy_images_proj(cat[x, x])  -- both halves read the same n latent rows
@@ -944,6 +957,28 @@ int vv_gemm_bf16(int M, int N, int K, const void* A, int64_t lda, const void* Wt
     }
     g.ws = (float*)ws.p;
     g.counters = (unsigned*)cnt.p;
+  }
+  KCHK(launch_gemm(g, (hipStream_t)vst));
+  return 0;
+}
+
+int vv_gemm_bf16_norm(int M, int N, int K, const void* A, int64_t lda, const void* norm_w, float eps, const void* Wt,
+                      int epi, void* Y, int64_t ldy, vv_ctx* c, vv_stream vst) {
+  GemmArgs g;
+  memset(&g, 0, sizeof(g));
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.ksplit = 1;
+  g.a = rowmap(A, lda);
+  g.w = (const bf16*)Wt;
+  g.ldw = K;
+  g.epi.kind = epi;
+  g.epi.out = rowmap(Y, ldy);
+  g.xf = xf_norm((const bf16*)norm_w, eps);
+  if (c) {
+    g.ws = (float*)c->splitk_ws.p;
+    g.counters = (unsigned*)c->splitk_cnt.p;
   }
   KCHK(launch_gemm(g, (hipStream_t)vst));
   return 0;

@@ -305,10 +305,10 @@ DEV bool splitk_handoff(const GemmArgs& a, float* red, int TILE, unsigned* last_
 // LDS; each wave streams its weight chunks with a two-deep register ping-pong
 // (U chunks = U KB per wave in flight while the previous U are multiplied).
 template <int U, int XF>
-__global__ void __launch_bounds__(256) k_gemv1(GemmArgs a) {
+__global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ float inv_s[16];
-  __shared__ float red[4 * 256];
+  __shared__ float red[8 * 256];
   __shared__ unsigned last_flag;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, NW = blockDim.x >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -322,25 +322,136 @@ __global__ void __launch_bounds__(256) k_gemv1(GemmArgs a) {
   const bf16* wrow = a.w + (long long)(n0 >> 4) * a.K * 16 + lane * 8;  // MFMA-packed W
   const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
 
-  // first weight chunks go out before the A staging (they do not depend on it)
-  bf16x8 wa[U], wb[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) wa[u] = *(const bf16x8*)(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
-
-  // ---- stage A rows [0, M) x chunks [b0, b1) into LDS (row stride padded 16 B)
+  // ---- A staging into LDS (rows [0, M) x chunks [b0, b1), row stride padded
+  // 16 B), overlapped with the first weight chunks.  vmcnt waits are in issue
+  // order, so every A-side load (row chunk + its transform operands) is issued
+  // BEFORE the weight loads: the prologue then waits only for its own bytes and
+  // the weight stream stays in flight through the norm math.
   const int kw = (b1 - b0) * 32;         // elements staged per row
   const int lds_ld = kw + 8;
+  const int n8 = kw >> 3;
   bf16* xs = (bf16*)smem;
-  if (XF == XF_NORM) {
-    row_inv(a, 0, a.M, inv_s, wave, NW, lane);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  }
-  for (int e = threadIdx.x; e < a.M * (kw >> 3); e += blockDim.x) {
-    const int m = e / (kw >> 3), k8 = (e - m * (kw >> 3)) * 8;
-    const int k = b0 * 32 + k8;
-    bf16x8 x = *(const bf16x8*)(rm_bf(a.a, m) + k);
-    if (XF != XF_NONE) x = xform<XF>(a, x, m, k, XF == XF_NORM ? inv_s[m] : 0.f);
-    *(bf16x8*)(xs + m * lds_ld + k8) = x;
+  float* part = (float*)(smem + (((size_t)a.M * lds_ld * 2 + 15) & ~(size_t)15));
+  bf16x8 wa[U], wb[U];
+  constexpr int Q = 4;                   // A items per thread on the fast path
+  const bool fast = a.M * n8 <= Q * (int)blockDim.x;
+  if (fast) {
+    bf16x8 xv[Q], wv[Q], sh[Q], sc[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int e = threadIdx.x + q * blockDim.x;
+      if (e < a.M * n8) {
+        const int m = e / n8, k = b0 * 32 + (e - m * n8) * 8;
+        xv[q] = *(const bf16x8*)(rm_bf(a.a, m) + k);
+        if (XF == XF_NORM) {
+          if (a.xf.w) wv[q] = *(const bf16x8*)(a.xf.w + k);
+          if (a.xf.mod) {
+            const bf16* md = a.xf.mod + (long long)m * a.xf.mod_ld;
+            sh[q] = *(const bf16x8*)(md + a.xf.shift_off + k);
+            sc[q] = *(const bf16x8*)(md + a.xf.scale_off + k);
+          }
+        } else if (XF == XF_SILU_ADD) {
+          wv[q] = *(const bf16x8*)(a.xf.vec + k);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) wa[u] = *(const bf16x8*)(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
+    if (XF == XF_NORM) {
+      // per-item sums of squares -> LDS, rows reduced in a fixed order
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int e = threadIdx.x + q * blockDim.x;
+        if (e < a.M * n8) {
+          float ss = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss += bf(xv[q][j]) * bf(xv[q][j]);
+          part[e] = ss;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (a.ksplit == 1) {
+        for (int m = wave; m < a.M; m += NW) {
+          float ss = 0.f;
+          for (int c = lane; c < n8; c += 64) ss += part[m * n8 + c];
+          ss = wave_sum(ss);
+          if (lane == 0) inv_s[m] = rsqrtf(ss / (float)a.K + a.xf.eps);
+        }
+      } else {
+        row_inv(a, 0, a.M, inv_s, wave, NW, lane);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int e = threadIdx.x + q * blockDim.x;
+      if (e < a.M * n8) {
+        const int m = e / n8, k8 = (e - m * n8) * 8;
+        bf16x8 o = xv[q];
+        if (XF == XF_NORM) {
+          const float inv = inv_s[m];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float t = rb(bf(xv[q][j]) * inv);
+            if (a.xf.w) t = rb(t * bf(wv[q][j]));
+            if (a.xf.mod) t = rb(rb(t * rb(1.0f + bf(sc[q][j]))) + bf(sh[q][j]));
+            o[j] = tobf(t);
+          }
+        } else if (XF == XF_SILU_ADD) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = tobf(silu_f(rb(bf(xv[q][j]) + bf(wv[q][j]))));
+        }
+        *(bf16x8*)(xs + m * lds_ld + k8) = o;
+      }
+    }
+  } else {
+    // many rows (B >= 8 batches): weights first, then the A rows in batches
+#pragma unroll
+    for (int u = 0; u < U; ++u) wa[u] = *(const bf16x8*)(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
+    for (int e0 = threadIdx.x; e0 < a.M * n8; e0 += 4 * blockDim.x) {
+      bf16x8 xv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e = e0 + q * blockDim.x;
+        if (e < a.M * n8) {
+          const int m = e / n8, k8 = (e - m * n8) * 8;
+          xv[q] = *(const bf16x8*)(rm_bf(a.a, m) + b0 * 32 + k8);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e = e0 + q * blockDim.x;
+        if (e < a.M * n8) {
+          const int m = e / n8, k8 = (e - m * n8) * 8;
+          *(bf16x8*)(xs + m * lds_ld + k8) = xv[q];
+        }
+      }
+    }
+    if (XF != XF_NONE) {
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (XF == XF_NORM) {
+        if (a.ksplit == 1) {
+          for (int m = wave; m < a.M; m += NW) {
+            float ss = 0.f;
+            for (int c = lane; c < n8; c += 64) {
+              const bf16x8 v = *(const bf16x8*)(xs + m * lds_ld + c * 8);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) ss += bf(v[j]) * bf(v[j]);
+            }
+            ss = wave_sum(ss);
+            if (lane == 0) inv_s[m] = rsqrtf(ss / (float)a.K + a.xf.eps);
+          }
+        } else {
+          row_inv(a, 0, a.M, inv_s, wave, NW, lane);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      }
+      for (int e = threadIdx.x; e < a.M * n8; e += blockDim.x) {
+        const int m = e / n8, k8 = (e - m * n8) * 8;
+        bf16x8* px = (bf16x8*)(xs + m * lds_ld + k8);
+        *px = xform<XF>(a, *px, m, b0 * 32 + k8, XF == XF_NORM ? inv_s[m] : 0.f);
+      }
+    }
   }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
@@ -391,8 +502,8 @@ __global__ void __launch_bounds__(256) k_gemv1(GemmArgs a) {
 // 16 < M <= 64: A fragments loaded straight from global / L2, transform per
 // chunk; weights ping-ponged as in k_gemv1.
 template <int MREP, int U, int XF>
-__global__ void __launch_bounds__(256) k_gemv(GemmArgs a) {
-  __shared__ float red[4 * MREP * 256];
+__global__ void __launch_bounds__(512) k_gemv(GemmArgs a) {
+  __shared__ float red[(MREP == 1 ? 8 : 4) * MREP * 256];
   __shared__ float inv_s[64];
   __shared__ unsigned last_flag;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, NW = blockDim.x >> 6;
@@ -563,8 +674,8 @@ struct GemmPlan { int nw, ksplit; };
 // form) to 30 us (fence form), more than the extra CUs it brings.
 static GemmPlan gemv_plan(int N, int K) {
   (void)N;
-  int nw = 4, ks = 1;
   const int chunks = K / 32;
+  int nw = chunks >= 200 ? 8 : 4, ks = 1;   // long rows (LM down, codec fc2): 8 waves
   if (g_tune_waves > 0) {
     const int tiles = N / 16;
     int wpt = (g_tune_waves + tiles - 1) / tiles;
@@ -580,10 +691,13 @@ static GemmPlan gemv_plan(int N, int K) {
   return {nw, ks};
 }
 
+static int max_waves(int mrep) { return mrep == 1 ? 8 : 4; }
+
 // k_gemv1 stages the A slice in LDS (<= 64 KB)
 static bool gemv1_fits(const GemmArgs& a) {
   const int nchunk = a.K >> 5;
-  return (size_t)a.M * (((nchunk + a.ksplit - 1) / a.ksplit) * 32 + 8) * 2 <= 65536;
+  const size_t kw = ((nchunk + a.ksplit - 1) / a.ksplit) * 32;
+  return (((size_t)a.M * (kw + 8) * 2 + 15) & ~(size_t)15) + (size_t)a.M * (kw / 8) * 4 <= 65536;
 }
 
 template <int XF>
@@ -595,7 +709,8 @@ static void launch_gemv_xf(const GemmArgs& a, int mrep, dim3 grid, dim3 block, h
   if (mrep == 1) {
     const int nchunk = a.K >> 5;
     const int kw = ((nchunk + a.ksplit - 1) / a.ksplit) * 32;
-    const size_t lds = (size_t)a.M * (kw + 8) * sizeof(bf16);
+    const size_t xs_bytes = ((size_t)a.M * (kw + 8) * sizeof(bf16) + 15) & ~(size_t)15;
+    const size_t lds = xs_bytes + (size_t)a.M * (kw / 8) * sizeof(float);
     hipLaunchKernelGGL((k_gemv1<8, XF>), grid, block, lds, st, a);
     return;
   }
@@ -630,6 +745,7 @@ int launch_gemm(GemmArgs a, hipStream_t st) {
   if (a.M <= 64) {
     const int mrep = (a.M + 15) / 16;
     GemmPlan p = gemv_plan(a.N, a.K);
+    if (p.nw > max_waves(mrep)) p.nw = max_waves(mrep);
     a.ksplit = p.ksplit;
     if (a.ksplit > 1 && (!a.ws || !a.counters || a.N / 16 > 65536)) a.ksplit = 1;
     a.handoff = g_tune_handoff >= 0 ? g_tune_handoff : 1;

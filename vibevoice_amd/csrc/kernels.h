@@ -150,6 +150,8 @@ int attn_plan(int nq, int nkv, int max_len, int* chunk);
 int launch_attn(AttnArgs a, hipStream_t st);
 int launch_kv_copy(KVLayout kv, int n_layers, int nkv, int n, const int* slots, const int* src, const int* dst,
                    hipStream_t st);
+int launch_final_head(int R, int H, const bf16* h, const int* idx, const bf16* norm_w, float eps, bf16* hidden_out,
+                      const bf16* W, const int* ids, int nid, float* logits, hipStream_t st);
 int launch_lmhead_ids(int R, int H, const bf16* h, long long ldh, const bf16* W, const int* ids, int nid, float* out,
                       hipStream_t st);
 

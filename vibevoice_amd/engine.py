@@ -115,15 +115,19 @@ class Engine:
         self.steps = steps
 
     # ---------------------------------------------------------------- hot path
-    def lm_forward(self, embeds, slots, pos, out_idx, hidden_out=None, logits_out=None, max_pos=None, stream=None):
-        """embeds [ntok, H] bf16; slots/pos/out_idx int32 device tensors."""
-        ntok, nout = embeds.shape[0], out_idx.shape[0]
+    def lm_forward(self, embeds, slots, pos, out_idx, hidden_out=None, logits_out=None, max_pos=None, stream=None,
+                   ntok=None):
+        """embeds [rows, H] bf16 (token i reads row i % rows; ntok defaults to rows);
+        slots/pos/out_idx int32 device tensors of ntok / nout entries."""
+        rows = embeds.shape[0]
+        ntok = rows if ntok is None else ntok
+        nout = out_idx.shape[0]
         if hidden_out is None:
             hidden_out = torch.empty(nout, self.hidden, dtype=torch.bfloat16, device=self.device)
         if logits_out is None:
             logits_out = torch.empty(nout, self.n_valid, dtype=torch.float32, device=self.device)
         mp = int(max_pos if max_pos is not None else pos.max().item()) + 1
-        _lib.check(_lib.lib().vv_lm_forward(self.h, ntok, _ptr(embeds), _ptr(slots), _ptr(pos), mp, nout,
+        _lib.check(_lib.lib().vv_lm_forward(self.h, ntok, _ptr(embeds), rows, _ptr(slots), _ptr(pos), mp, nout,
                                             _ptr(out_idx), _ptr(hidden_out), _ptr(logits_out), _stream(stream)),
                    "lm_forward")
         return hidden_out, logits_out

@@ -336,9 +336,8 @@ class GenerateSession:
         B, eng = self.B, self.eng
 
         def body():
-            self.x_in2[B:].copy_(self.x_in2[:B])
-            eng.lm_forward(self.x_in2, self.rows2, self.pos_dev, self.rows2, hidden_out=self.hid,
-                           logits_out=self.logits, max_pos=eng.max_ctx - 1)
+            eng.lm_forward(self.x_in2[:B], self.rows2, self.pos_dev, self.rows2, hidden_out=self.hid,
+                           logits_out=self.logits, max_pos=eng.max_ctx - 1, ntok=2 * B)
         self._replay(("lm",), body)
 
     def _token_phase(self, n):
@@ -354,9 +353,9 @@ class GenerateSession:
             d = self.didx_dev[:n]
             if n == B:
                 pos_h, neg_h = self.hid[:B], self.hid[B:]
-            else:
-                pos_h = self.hid.index_select(0, d)
-                neg_h = self.hid.index_select(0, d + B)
+            else:   # one gather keeps [pos | neg] adjacent (used in place by the engine)
+                both = self.hid.index_select(0, torch.cat([d, d + B]))
+                pos_h, neg_h = both[:n], both[n:]
             x = self.noise_dev[:n]
             eng.diffusion_sample(pos_h, neg_h, x, self.cfg_scale)
             eng.codec_step(d, x, self.audio_dev[:n], embeds_out=self.x_in2, embed_rows=d)
