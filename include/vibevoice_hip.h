@@ -129,6 +129,14 @@ int vv_gemm_bf16(int M, int N, int K, const void* A, int64_t lda, const void* W,
  * producer of the loop's GEMMs (no bias / residual epilogues). */
 int vv_gemm_bf16_norm(int M, int N, int K, const void* A, int64_t lda, const void* norm_w, float eps, const void* W,
                       int epi, void* Y, int64_t ldy, vv_ctx* ws_ctx, vv_stream st);
+/* GQA attention of nq query rows (q [nq, nh*128] bf16, RoPE applied) over a
+ * caller-owned cache in the engine layout ([slot][kv_head][ctx][128], strides
+ * in elements): row i attends keys [0, pos[i]] of slot slots[i] -> out
+ * [nq, nh*128].  max_pos_p1 bounds pos + 1 (launch plan); ws_ctx supplies the
+ * split-merge workspace.  (Kernel entry for tests / benchmarks.) */
+int vv_attention_bf16(int nq, int nh, int nkv, const void* q, const void* k_cache, const void* v_cache,
+                      int64_t s_slot, int64_t s_head, const int* slots, const int* pos, int max_pos_p1, void* out,
+                      vv_ctx* ws_ctx, vv_stream st);
 /* Tuning hook (benchmarks only): override the GEMV launch plan — waves per
  * workgroup, split-K workgroups, split-K hand-off form (0 fences, 1 sc1),
  * target waves per launch.  0 / -1 restore the built-in plan. */

@@ -1,0 +1,68 @@
+"""Decode / prefill attention kernel (k_attn via vv_attention_bf16) vs a plain
+PyTorch fp32 reference (softmax(q k^T / sqrt(128)) v, GQA), at the 1.5B head
+layout (12 q / 2 kv heads) and the Large layout (28 / 4), cache in the engine's
+layout (K [slot][kv_head][ctx][128], V transposed [slot][kv_head][128][ctx]): single-workgroup
+contexts, the in-launch split merge (> 1024 keys), ragged rows sharing a
+launch, and length-1 rows.  Tolerance: rel L2 < 1e-2 (bf16 output)."""
+import ctypes
+
+import pytest
+import torch
+
+from gpu_util import rel_err
+from tests_engine import tiny_engine
+from vibevoice_amd import _lib
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def P(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def run_attention(eng, q, K, V, slots, pos, max_pos_p1):
+    nq, nh = q.shape[0], q.shape[1] // 128
+    nslot, nkv, ctx, _ = K.shape
+    out = torch.empty_like(q)
+    VT = V.transpose(2, 3).contiguous()          # engine layout: V transposed per head, [dim][ctx]
+    rc = _lib.lib().vv_attention_bf16(nq, nh, nkv, P(q), P(K), P(VT), nkv * ctx * 128, ctx * 128, P(slots), P(pos),
+                                      max_pos_p1, P(out), eng.h,
+                                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    _lib.check(rc, "attention")
+    return out
+
+
+def reference(q, K, V, slots, pos):
+    nq, nh = q.shape[0], q.shape[1] // 128
+    nkv = K.shape[1]
+    G = nh // nkv
+    out = torch.empty(nq, nh * 128)
+    for i in range(nq):
+        s, L = int(slots[i]), int(pos[i]) + 1
+        qi = q[i].float().view(nh, 128)
+        k = K[s, :, :L].float().repeat_interleave(G, 0)       # [nh, L, 128]
+        v = V[s, :, :L].float().repeat_interleave(G, 0)
+        p = torch.softmax((k @ qi[:, :, None])[..., 0] / 128 ** 0.5, -1)
+        out[i] = (p[:, None, :] @ v)[:, 0].reshape(-1)
+    return out
+
+
+@pytest.mark.parametrize("nh,nkv,lens", [(12, 2, [1, 37, 170, 1024]), (12, 2, [1025, 3000, 64]),
+                                         (28, 4, [300, 5000]), (12, 2, [65536 // 8])])
+def test_attention_vs_torch(nh, nkv, lens):
+    eng = tiny_engine()
+    g = torch.Generator(device=dev).manual_seed(sum(lens) + nh)
+    nslot = len(lens)
+    ctx = max(lens)
+    K = torch.randn(nslot, nkv, ctx, 128, device=dev, generator=g).bfloat16()
+    V = torch.randn(nslot, nkv, ctx, 128, device=dev, generator=g).bfloat16()
+    q = torch.randn(len(lens), nh * 128, device=dev, generator=g).bfloat16()
+    slots = torch.arange(nslot, device=dev, dtype=torch.int32)
+    pos = torch.tensor([n - 1 for n in lens], device=dev, dtype=torch.int32)
+    out = run_attention(eng, q, K, V, slots, pos, ctx)
+    torch.cuda.synchronize()
+    ref = reference(q.cpu(), K.cpu(), V.cpu(), slots.cpu(), pos.cpu())
+    e = rel_err(out, ref)
+    print(lens, e)
+    assert e < 1e-2

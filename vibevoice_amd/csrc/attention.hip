@@ -4,68 +4,45 @@
 // (modeling_qwen2.py:99-134, 150-173, 195-247) as called by VibeVoiceModel.forward
 // (vibevoice/modular/modeling_vibevoice.py:169-209).
 //
-// KV cache layout (one buffer for K, one for V):  [layer][slot][kv_head][ctx][d]
-// A row's cache holds only the entries its attention mask keeps, in order, so
-// cache index == RoPE position.
+// KV cache layout: K [layer][slot][kv_head][ctx][d]; V transposed per head,
+// [layer][slot][kv_head][d][ctx], so both MFMA operands of the kernel below
+// (K as the key-column operand of Q.K^T, V as the key-row operand of P.V) are
+// contiguous 16-byte loads.  A row's cache holds only the entries its
+// attention mask keeps, in order, so cache index == RoPE position (SURVEY.md
+// §8a rows a3, a7).
 #include "kernels.h"
 
 
-// ---------------------------------------------------------------- RoPE + append
-// qkv row: [q (nh*d) | k (nkv*d) | v (nkv*d)] (biases already added, bf16).
-// q_embed = bf16(bf16(q*cos) + bf16(rotate_half(q)*sin)), cos/sin = bf16(fp32 cos/sin)
-
-__global__ void __launch_bounds__(256) k_rope_kv(RopeArgs a) {
-  const int i = blockIdx.x;
-  const int d = a.kv.d, half = d >> 1;
-  const bf16* row = a.qkv + (long long)i * a.ld_qkv;
-  const int slot = a.slots[i], p = a.pos[i];
-  const long long base = (long long)a.layer * a.kv.s_layer + (long long)slot * a.kv.s_slot + (long long)p * d;
-  const int nrot = (a.nh + a.nkv) * half;
-  for (int e = threadIdx.x; e < nrot; e += blockDim.x) {
-    const int h = e / half, j = e - h * half;
-    const float f = (float)p * a.inv_freq[j];
-    const float cs = rb(cosf(f)), sn = rb(sinf(f));
-    const float x1 = bf(row[h * d + j]), x2 = bf(row[h * d + j + half]);
-    const bf16 o1 = tobf(rb(x1 * cs) + rb(-x2 * sn));
-    const bf16 o2 = tobf(rb(x2 * cs) + rb(x1 * sn));
-    if (h < a.nh) {
-      a.q_out[(long long)i * a.nh * d + h * d + j] = o1;
-      a.q_out[(long long)i * a.nh * d + h * d + j + half] = o2;
-    } else {
-      bf16* kp = a.kv.k + base + (long long)(h - a.nh) * a.kv.s_head;
-      kp[j] = o1;
-      kp[j + half] = o2;
-    }
-  }
-  for (int e = threadIdx.x; e < a.nkv * d; e += blockDim.x) {
-    const int h = e / d, j = e - h * d;
-    a.kv.v[base + (long long)h * a.kv.s_head + j] = row[(a.nh + a.nkv) * d + e];
-  }
-}
-
 // ---------------------------------------------------------------- attention
 // Grid (query row x kv head, split); a workgroup of ATT_NW waves owns keys
-// [k0, k1) of its split and hands each WAVE a contiguous sub-range, so short
-// contexts need no cross-workgroup merge at all.  Inside a wave: lane = (key
-// row kr = lane >> 4, dims dl = 8 * (lane & 15)); 8 keys per sub-chunk (2 per
-// key row), K and V of the next sub-chunk prefetched; all G <= 8 query heads of
-// the kv head share every K/V load (GQA).  Online softmax (running max / sum,
-// fp32) per wave; the waves' (m, l, o) merge through LDS; with nsplit > 1 the
-// splits' partials merge in the last-arriving workgroup (agent release /
-// ticket / acquire, cdna_hip_programming.md Guideline 16).
-constexpr int ATT_NW = 8;           // waves per workgroup (256 VGPRs each: G <= 8 heads fit)
+// [k0, k1) of its split and hands each wave a contiguous sub-range, merged in
+// LDS — short contexts need no cross-workgroup merge.  Per wave, 32 keys per
+// step on the matrix cores (mfma 16x16x32 bf16):
+//   S[16 heads x 16 keys] = Q[heads x 128] . K^T   (2 tiles, 4 MFMAs each; the
+//       G <= 8 query heads of the kv head are the rows, padded to 16)
+//   online softmax on S in registers (row = head spread over 16 lanes)
+//   P (bf16, as the reference's eager path rounds it) -> per-wave LDS tile ->
+//   O[heads x 128] += P[heads x 32 keys] . V[32 keys x 128] (8 MFMAs, V^T cache)
+// K / V of the next step are prefetched while the current one computes.  With
+// nsplit > 1 the splits' (m, l, O) merge in the last-arriving workgroup (agent
+// release / ticket / acquire, cdna_hip_programming.md Guideline 16).
+constexpr int ATT_NW = 8;           // waves per workgroup
 constexpr int ATT_KEYS = 1024;      // keys per workgroup before the launch splits
 constexpr int ATT_GMAX = 8;
 constexpr int ATT_KC = 64;          // per-row split granularity
+
+DEV f32x4 amfma(bf16x8 a, bf16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
 
 template <int G>
 __global__ void __launch_bounds__(64 * ATT_NW) k_attn(AttnArgs a) {
   __shared__ float wm[ATT_NW][G], wl[ATT_NW][G];
   __shared__ float wo[ATT_NW][G][128];
+  __shared__ __attribute__((aligned(16))) bf16 pt[ATT_NW][16][32];
   __shared__ float fm[G], fl[G];
   __shared__ unsigned last_flag;
   constexpr int d = 128;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int r = lane & 15, g = lane >> 4;
   const int qi = blockIdx.x / a.nkv, kh = blockIdx.x - qi * a.nkv, split = blockIdx.y;
   const int len = a.pos[qi] + 1;
   // this row's split size: >= a.chunk, all nsplit splits cover len; splits past
@@ -76,108 +53,123 @@ __global__ void __launch_bounds__(64 * ATT_NW) k_attn(AttnArgs a) {
   if (split >= nact) return;
   const int k0 = split * chunk;
   const int k1 = min(len, k0 + chunk);
-  // this wave's keys
-  const int per = (k1 - k0 + ATT_NW - 1) / ATT_NW;
+  // this wave's keys, in 32-key steps
+  const int per = ((k1 - k0 + ATT_NW - 1) / ATT_NW + 31) / 32 * 32;
   const int w0 = k0 + wave * per;
   const int w1 = min(k1, w0 + per);
   const long long cbase = (long long)a.layer * a.kv.s_layer + (long long)a.slots[qi] * a.kv.s_slot +
                           (long long)kh * a.kv.s_head;
-  const bf16* K = a.kv.k + cbase;
-  const bf16* V = a.kv.v + cbase;
-  const int dl = (lane & 15) * 8, kr = lane >> 4;
-
-  float qv[G][8];
-#pragma unroll
-  for (int h = 0; h < G; ++h) {
-    const bf16x8 q8 = *(const bf16x8*)(a.q + (long long)qi * a.nh * d + (kh * G + h) * d + dl);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) qv[h][e] = bf(q8[e]) * a.scale;
-  }
-  float o[G][8], m[G], l[G];
-#pragma unroll
-  for (int h = 0; h < G; ++h) {
-    m[h] = -INFINITY;
-    l[h] = 0.f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[h][e] = 0.f;
-  }
+  const bf16* K = a.kv.k + cbase;             // [ctx][128]
+  const bf16* VT = a.kv.v + cbase;            // [128][max_ctx]
+  const int ldv = a.kv.max_ctx;
   const bf16x8 z8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-  bf16x8 kf[2], vf[2];
+
+  // Q fragments (A operand): row = head r (zero past G), k = dims 32c + 8g .. +7;
+  // the fp32 scores are scaled by 1/sqrt(d) after the MFMA
+  bf16x8 qf[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if (r < G) {
+      const bf16x8 q8 = *(const bf16x8*)(a.q + (long long)qi * a.nh * d + (kh * G + r) * d + 32 * c + 8 * g);
+      qf[c] = q8;
+    } else {
+      qf[c] = z8;
+    }
+  }
+  f32x4 o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m[4], l[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    m[i] = -INFINITY;
+    l[i] = 0.f;
+  }
+  bf16x8 kf[2][4], vf[8];
   auto load = [&](int c0) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int key = c0 + kr + 4 * j;
+    for (int tt = 0; tt < 2; ++tt) {
+      const int key = c0 + 16 * tt + r;       // B operand of S: col = key
       const bool ok = key < w1;
-      kf[j] = ok ? *(const bf16x8*)(K + (long long)key * d + dl) : z8;
-      vf[j] = ok ? *(const bf16x8*)(V + (long long)key * d + dl) : z8;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) kf[tt][c] = ok ? *(const bf16x8*)(K + (long long)key * d + 32 * c + 8 * g) : z8;
+    }
+    const int kb = c0 + 8 * g;                 // B operand of O: k = keys kb .. kb+7, col = dim
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bf16x8 v = kb < w1 ? *(const bf16x8*)(VT + (long long)(16 * j + r) * ldv + kb) : z8;
+      if (kb + 8 > w1) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (kb + e >= w1) v[e] = (bf16)0.f;
+      }
+      vf[j] = v;
     }
   };
   if (w0 < w1) load(w0);
-  for (int c0 = w0; c0 < w1; c0 += 8) {
-    bf16x8 kc[2], vc[2];
+  for (int c0 = w0; c0 < w1; c0 += 32) {
+    bf16x8 kc[2][4], vc[8];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      kc[j] = kf[j];
-      vc[j] = vf[j];
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) kc[tt][c] = kf[tt][c];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vc[j] = vf[j];
+    if (c0 + 32 < w1) load(c0 + 32);
+    // S tiles: lane holds S[head 4g+i][key c0 + 16tt + r]
+    f32x4 sacc[2];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      sacc[tt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) sacc[tt] = amfma(qf[c], kc[tt][c], sacc[tt]);
     }
-    if (c0 + 8 < w1) load(c0 + 8);
-    float sc[G][2];
+    float p[2][4];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      float kx[8];
+    for (int i = 0; i < 4; ++i) {
+      float s0 = c0 + r < w1 ? sacc[0][i] * a.scale : -INFINITY;
+      float s1 = c0 + 16 + r < w1 ? sacc[1][i] * a.scale : -INFINITY;
+      float mx = fmaxf(s0, s1);
+      mx = fmaxf(mx, __shfl_xor(mx, 1));
+      mx = fmaxf(mx, __shfl_xor(mx, 2));
+      mx = fmaxf(mx, __shfl_xor(mx, 4));
+      mx = fmaxf(mx, __shfl_xor(mx, 8));
+      const float mnew = fmaxf(m[i], mx);
+      const float al = __expf(m[i] - mnew);
+      p[0][i] = __expf(s0 - mnew);
+      p[1][i] = __expf(s1 - mnew);
+      float ps = p[0][i] + p[1][i];
+      ps += __shfl_xor(ps, 1);
+      ps += __shfl_xor(ps, 2);
+      ps += __shfl_xor(ps, 4);
+      ps += __shfl_xor(ps, 8);
+      l[i] = l[i] * al + ps;
+      m[i] = mnew;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) kx[e] = bf(kc[j][e]);
-      const bool ok = c0 + kr + 4 * j < w1;
+      for (int j = 0; j < 8; ++j) o[j][i] *= al;
+    }
+    // P -> LDS [head][key] -> A operand (row = head r, k = keys 8g .. 8g+7)
 #pragma unroll
-      for (int h = 0; h < G; ++h) {
-        float s = 0.f;
+    for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) s += qv[h][e] * kx[e];
-        s += __shfl_xor(s, 8);
-        s += __shfl_xor(s, 4);
-        s += __shfl_xor(s, 2);
-        s += __shfl_xor(s, 1);
-        sc[h][j] = ok ? s : -INFINITY;
+      for (int i = 0; i < 4; ++i) pt[wave][4 * g + i][16 * tt + r] = (bf16)p[tt][i];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const bf16x8 pa = *(const bf16x8*)&pt[wave][r][8 * g];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = amfma(pa, vc[j], o[j]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  // this wave's (m, l, O): lane holds O[head 4g+i][dim 16j + r]
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int h = 4 * g + i;
+    if (h < G) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) wo[wave][h][16 * j + r] = o[j][i];
+      if (r == 0) {
+        wm[wave][h] = m[i];
+        wl[wave][h] = l[i];
       }
-    }
-#pragma unroll
-    for (int h = 0; h < G; ++h) {
-      float mx = fmaxf(sc[h][0], sc[h][1]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16));
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
-      const float mnew = fmaxf(m[h], mx);
-      const float al = __expf(m[h] - mnew);
-      const float p0 = __expf(sc[h][0] - mnew), p1 = __expf(sc[h][1] - mnew);
-      float ps = p0 + p1;
-      ps += __shfl_xor(ps, 16);
-      ps += __shfl_xor(ps, 32);
-      l[h] = l[h] * al + ps;
-      m[h] = mnew;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[h][e] = o[h][e] * al + p0 * bf(vc[0][e]) + p1 * bf(vc[1][e]);
-    }
-  }
-  // this wave's (m, l, o): sum o over the 4 key rows (lanes +16, +32)
-#pragma unroll
-  for (int h = 0; h < G; ++h)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float v = o[h][e];
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
-      o[h][e] = v;
-    }
-  if (lane < 16) {
-#pragma unroll
-    for (int h = 0; h < G; ++h)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) wo[wave][h][dl + e] = o[h][e];
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int h = 0; h < G; ++h) {
-      wm[wave][h] = m[h];
-      wl[wave][h] = l[h];
     }
   }
   __syncthreads();
@@ -191,31 +183,41 @@ __global__ void __launch_bounds__(64 * ATT_NW) k_attn(AttnArgs a) {
     fl[t] = L;
   }
   __syncthreads();
-  float res[(G * 128 + 64 * ATT_NW - 1) / (64 * ATT_NW)];
-  int ne = 0;
-  for (int e = t; e < G * d; e += 64 * ATT_NW, ++ne) {
-    const int h = e / d, j = e - h * d;
-    float s = 0.f;
-    for (int w = 0; w < ATT_NW; ++w)
-      if (wm[w][h] != -INFINITY) s += __expf(wm[w][h] - fm[h]) * wo[w][h][j];
-    res[ne] = s;
+  constexpr int NE = (G * 128 + 64 * ATT_NW - 1) / (64 * ATT_NW);
+  float res[NE];
+#pragma unroll
+  for (int q = 0; q < NE; ++q) {
+    const int e = t + q * 64 * ATT_NW;
+    float sum = 0.f;
+    if (e < G * d) {
+      const int h = e / d, j = e - h * d;
+      for (int w = 0; w < ATT_NW; ++w)
+        if (wm[w][h] != -INFINITY) sum += __expf(wm[w][h] - fm[h]) * wo[w][h][j];
+    }
+    res[q] = sum;
   }
   if (nact == 1) {
-    ne = 0;
-    for (int e = t; e < G * d; e += 64 * ATT_NW, ++ne) {
-      const int h = e / d, j = e - h * d;
-      a.out[(long long)qi * a.nh * d + (kh * G + h) * d + j] = tobf(res[ne] / fl[h]);
+#pragma unroll
+    for (int q = 0; q < NE; ++q) {
+      const int e = t + q * 64 * ATT_NW;
+      if (e < G * d) {
+        const int h = e / d, j = e - h * d;
+        a.out[(long long)qi * a.nh * d + (kh * G + h) * d + j] = tobf(res[q] / fl[h]);
+      }
     }
     return;
   }
-  ne = 0;
-  for (int e = t; e < G * d; e += 64 * ATT_NW, ++ne) {
-    const int h = e / d, j = e - h * d;
-    const long long pidx = ((long long)qi * a.nh + kh * G + h) * a.nsplit + split;
-    a.part_o[pidx * d + j] = res[ne];
-    if (j == 0) {
-      a.part_ml[pidx * 2] = fm[h];
-      a.part_ml[pidx * 2 + 1] = fl[h];
+#pragma unroll
+  for (int q = 0; q < NE; ++q) {
+    const int e = t + q * 64 * ATT_NW;
+    if (e < G * d) {
+      const int h = e / d, j = e - h * d;
+      const long long pidx = ((long long)qi * a.nh + kh * G + h) * a.nsplit + split;
+      a.part_o[pidx * d + j] = res[q];
+      if (j == 0) {
+        a.part_ml[pidx * 2] = fm[h];
+        a.part_ml[pidx * 2 + 1] = fl[h];
+      }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -332,12 +334,6 @@ int launch_final_head(int R, int H, const bf16* h, const int* idx, const bf16* n
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
-int launch_rope_kv(RopeArgs a, hipStream_t st) {
-  if (a.R <= 0) return 0;
-  if (a.kv.d != 128) return 1;
-  hipLaunchKernelGGL(k_rope_kv, dim3(a.R), dim3(256), 0, st, a);
-  return hipGetLastError() == hipSuccess ? 0 : 2;
-}
 
 // Launch plan for keys up to max_len: aim for ~1024 workgroups over
 // (rows x kv heads x splits), never below 64 keys per split, at most 64
@@ -399,7 +395,9 @@ __global__ void __launch_bounds__(256) k_kv_copy(KVLayout kv, int n_layers, int 
     const int l = e / (nkv * d), r = e - l * nkv * d, h = r / d, j = r - h * d;
     const long long b = (long long)l * kv.s_layer + (long long)slots[i] * kv.s_slot + (long long)h * kv.s_head + j;
     kv.k[b + (long long)dst[i] * d] = kv.k[b + (long long)src[i] * d];
-    kv.v[b + (long long)dst[i] * d] = kv.v[b + (long long)src[i] * d];
+    // V^T: element (dim j, position p) at head base + j * max_ctx + p
+    const long long bv = b - j + (long long)j * kv.max_ctx;
+    kv.v[bv + dst[i]] = kv.v[bv + src[i]];
   }
 }
 

@@ -96,6 +96,7 @@ struct ConvNet {
   DevBuf state;               // all ConvBufs
   DevBuf work;                // X stages + A + F
   bf16* X[VV_MAX_STAGES] = {};
+  bf16* Y[VV_MAX_STAGES] = {};   // residual ping-pong partner of X (k_mix output)
   bf16* A = nullptr;
   bf16* F = nullptr;
   std::vector<RollDesc> rolls;
@@ -291,11 +292,13 @@ static int convnet_alloc(ConvNet& n, int kernel) {
     aw = std::max(aw, (size_t)n.T[i] * n.chans[i]);
     fw = std::max(fw, (size_t)n.T[i] * n.chans[i] * 4);
   }
-  const size_t per = xw + aw + fw;
+  const size_t per = 2 * xw + aw + fw;
   CHK(n.work.ensure(per * n.nmax * sizeof(bf16)));
   bf16* q = (bf16*)n.work.p;
   for (int i = 0; i < n.nst; ++i) {
     n.X[i] = q;
+    q += (size_t)n.T[i] * n.chans[i] * n.nmax;
+    n.Y[i] = q;
     q += (size_t)n.T[i] * n.chans[i] * n.nmax;
   }
   n.A = q;
@@ -404,31 +407,30 @@ static int convnet_run(vv_ctx* c, ConvNet& net, int n, const int* slots, RowMap 
     for (int j = 0; j < net.depth[i]; ++j) {
       const std::string b = p + ".s" + std::to_string(i) + ".b" + std::to_string(j);
       const ConvBuf& mb = net.mix[i][j];
-      // norm -> mixer buffer (this step's rows), depthwise conv + gamma + residual
-      CHK(rmsnorm(n * T, C, X, buf_in_rows(mb, T, slots), W(c, b + ".norm"), eps, st));
-      DwArgs d;
-      d.M = n * T;
-      d.C = C;
-      d.T = T;
-      d.K = k;
-      d.buf = rowmap(mb.base, C, T, mb.sB, slots);
-      d.x = X;
-      d.w = W(c, b + ".dw_w");
-      d.b = W(c, b + ".dw_b");
-      d.gamma = W(c, b + ".gamma");
-      KCHK(launch_dwconv(d, st));
-      // ffn
-      // ffn: ConvRMSNorm fused into fc1's A load for GEMV-shaped steps (M <= 64);
-      // tiled GEMMs normalise in their own launch (cheaper than a per-tile prologue)
+      // mixer norm + depthwise conv + gamma residual (X -> Y) + ffn_norm (-> A), one launch
+      MixArgs mx;
+      mx.n = n;
+      mx.T = T;
+      mx.C = C;
+      mx.R = std::max(1, std::min(T, 2048 / C));
+      mx.eps = eps;
+      mx.ctx = mb.ctx;
+      mx.x = net.X[i];
+      mx.y = net.Y[i];
+      mx.a = net.A;
+      mx.buf = mb.base;
+      mx.buf_sB = mb.sB;
+      mx.slots = slots;
+      mx.norm_w = W(c, b + ".norm");
+      mx.dw_w = W(c, b + ".dw_w");
+      mx.dw_b = W(c, b + ".dw_b");
+      mx.gamma = W(c, b + ".gamma");
+      mx.ffn_norm_w = W(c, b + ".ffn_norm");
+      KCHK(launch_mix(mx, st));
+      RowMap Y = rowmap(net.Y[i], C, T, (long long)T * C);
       RowMap Fm = rowmap(net.F, 4LL * C);
-      RowMap fin = X;
-      if (n * T > 64) {
-        fin = rowmap(net.A, C);
-        CHK(rmsnorm(n * T, C, X, fin, W(c, b + ".ffn_norm"), eps, st));
-      }
-      GemmArgs g1 = gemm_args(c, n * T, 4 * C, C, fin, W(c, b + ".fc1_w"), EPI_GELU, Fm, W(c, b + ".fc1_b"));
-      if (n * T <= 64) g1.xf = xf_norm(W(c, b + ".ffn_norm"), eps);
-      CHK(gemm(c, g1, st));
+      CHK(gemm(c, gemm_args(c, n * T, 4 * C, C, rowmap(net.A, C), W(c, b + ".fc1_w"), EPI_GELU, Fm,
+                            W(c, b + ".fc1_b")), st));
       RowMap o = X;
       const bool last = j == net.depth[i] - 1;
       if (last) {
@@ -436,7 +438,7 @@ static int convnet_run(vv_ctx* c, ConvNet& net, int n, const int* slots, RowMap 
         o = buf_in_rows(nb, T, slots);
       }
       GemmArgs g = gemm_args(c, n * T, C, 4 * C, Fm, W(c, b + ".fc2_w"), EPI_RES, o, W(c, b + ".fc2_b"));
-      g.epi.res = X;
+      g.epi.res = Y;
       g.epi.gamma = W(c, b + ".ffn_gamma");
       CHK(gemm(c, g, st));
     }
@@ -591,7 +593,7 @@ int vv_finalize(vv_ctx* c) {
   c->kv.s_layer = c->kv.s_slot * c->lm_slots;
   const size_t kvb = (size_t)c->kv.s_layer * k.n_layers * sizeof(bf16);
   CHK(c->kv_k.ensure(kvb));
-  CHK(c->kv_v.ensure(kvb));
+  CHK(c->kv_v.ensure(kvb + 256));   // V^T rows are read 16 B at a time: pad the tail
   c->kv.k = (bf16*)c->kv_k.p;
   c->kv.v = (bf16*)c->kv_v.p;
   // ---- attention split partials for decode (2 * max_batch rows, <= 64 splits) + tickets
@@ -981,6 +983,44 @@ int vv_gemm_bf16_norm(int M, int N, int K, const void* A, int64_t lda, const voi
     g.counters = (unsigned*)c->splitk_cnt.p;
   }
   KCHK(launch_gemm(g, (hipStream_t)vst));
+  return 0;
+}
+
+int vv_attention_bf16(int nq, int nh, int nkv, const void* q, const void* k_cache, const void* v_cache,
+                      int64_t s_slot, int64_t s_head, const int* slots, const int* pos, int max_pos_p1, void* out,
+                      vv_ctx* c, vv_stream vst) {
+  if (!c) FAIL("vv_attention_bf16: needs an engine for split workspaces");
+  KVLayout kv;
+  kv.k = (bf16*)k_cache;
+  kv.v = (bf16*)v_cache;
+  kv.s_layer = 0;
+  kv.s_slot = s_slot;
+  kv.s_head = s_head;
+  kv.d = 128;
+  kv.max_ctx = (int)(s_head / 128);
+  AttnArgs at;
+  memset(&at, 0, sizeof(at));
+  int chunk = 0;
+  at.nsplit = attn_plan(nq, nkv, max_pos_p1, &chunk);
+  if (at.nsplit > 1) {
+    if ((size_t)nq * nkv > 65536) FAIL("attention split tickets exhausted");
+    CHK(c->attn_part.ensure((size_t)nq * nh * at.nsplit * (128 + 2) * sizeof(float)));
+  }
+  at.nq = nq;
+  at.nh = nh;
+  at.nkv = nkv;
+  at.layer = 0;
+  at.chunk = chunk;
+  at.scale = 1.0f / sqrtf(128.f);
+  at.q = (const bf16*)q;
+  at.out = (bf16*)out;
+  at.slots = slots;
+  at.pos = pos;
+  at.kv = kv;
+  at.counters = (unsigned*)c->attn_cnt.p;
+  at.part_o = (float*)c->attn_part.p;
+  at.part_ml = at.part_o + (size_t)nq * nh * at.nsplit * 128;
+  KCHK(launch_attn(at, (hipStream_t)vst));
   return 0;
 }
 

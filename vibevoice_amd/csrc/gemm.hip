@@ -131,13 +131,12 @@ DEV void epi_rope(const GemmArgs& a, int m, int n0, int lane, float v[4]) {
     *(bf16x4*)(dst + j + 64) = o2;
   } else {
     if (m >= a.M) return;
+    // V cache is transposed per head ([dim][ctx], attention.hip)
     const int hv = h - R.nh - R.nkv;
     bf16* dst = R.kv.v + (long long)R.layer * R.kv.s_layer + (long long)R.slots[m] * R.kv.s_slot +
-                (long long)hv * R.kv.s_head + (long long)R.pos[m] * d + (n0 % d) + 4 * g;
-    bf16x4 o;
+                (long long)hv * R.kv.s_head + (long long)((n0 % d) + 4 * g) * R.kv.max_ctx + R.pos[m];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = tobf(v[i]);
-    *(bf16x4*)dst = o;
+    for (int i = 0; i < 4; ++i) dst[(long long)i * R.kv.max_ctx] = tobf(v[i]);
   }
 }
 

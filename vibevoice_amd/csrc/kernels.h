@@ -83,6 +83,24 @@ struct DwArgs {
   const bf16* gamma; // [C]
 };
 
+// Block1D mixer + FFN pre-norm, fused (elementwise.hip: k_mix)
+struct MixArgs {
+  int n, T, C, R;          // samples, rows per sample, channels, rows per workgroup
+  float eps;
+  int ctx;                 // history rows in front of the conv buffer (k - 1)
+  const bf16* x;           // residual in  [n][T][C]
+  bf16* y;                 // residual out [n][T][C]
+  bf16* a;                 // ffn_norm(y)  [n][T][C]
+  bf16* buf;               // conv buffer, slot s at buf + s * buf_sB: rows [ctx + t] = norm(x)[t]
+  long long buf_sB;
+  const int* slots;
+  const bf16* norm_w;      // [C]
+  const bf16* dw_w;        // [C][7]
+  const bf16* dw_b;        // [C]
+  const bf16* gamma;       // [C]
+  const bf16* ffn_norm_w;  // [C]
+};
+
 struct Conv1Args {
   int M, C, K;
   RowMap buf;
@@ -107,16 +125,6 @@ struct RollDesc {
 
 
 
-struct RopeArgs {
-  int R, nh, nkv, layer;
-  const bf16* qkv;
-  long long ld_qkv;
-  bf16* q_out;          // [R][nh*d]
-  const int* slots;     // [R] cache slot of row
-  const int* pos;       // [R] position == cache index written
-  const float* inv_freq;// [d/2]
-  KVLayout kv;
-};
 
 struct AttnArgs {
   int nq, nh, nkv, layer, nsplit;
@@ -135,6 +143,7 @@ struct AttnArgs {
 int launch_gemm(GemmArgs a, hipStream_t st);
 int launch_rmsnorm(NormArgs a, hipStream_t st);
 int launch_dwconv(DwArgs a, hipStream_t st);
+int launch_mix(MixArgs a, hipStream_t st);
 int launch_conv_cout1(Conv1Args a, hipStream_t st);
 int launch_conv_cin1(ConvIn1Args a, hipStream_t st);
 int launch_roll(const RollDesc* d, int nd, const int* slots, int ns, int mode, hipStream_t st);
@@ -145,7 +154,6 @@ int launch_head_cond(int rows, int H, const bf16* condp, const bf16* temb, bf16*
 int launch_silu(int n, const bf16* x, bf16* y, hipStream_t st);
 int launch_cfg_dpm(int n, int D, DpmCoef k, const bf16* eps, bf16* x, bf16* m1, hipStream_t st);
 int launch_gather_rows(int n, int C, const bf16* src, long long lds, const int* idx, RowMap dst, hipStream_t st);
-int launch_rope_kv(RopeArgs a, hipStream_t st);
 int attn_plan(int nq, int nkv, int max_len, int* chunk);
 int launch_attn(AttnArgs a, hipStream_t st);
 int launch_kv_copy(KVLayout kv, int n_layers, int nkv, int n, const int* slots, const int* src, const int* dst,
