@@ -139,8 +139,9 @@ int vv_attention_bf16(int nq, int nh, int nkv, const void* q, const void* k_cach
                       vv_ctx* ws_ctx, vv_stream st);
 /* Tuning hook (benchmarks only): override the GEMV launch plan — waves per
  * workgroup, split-K workgroups, split-K hand-off form (0 fences, 1 sc1),
- * target waves per launch.  0 / -1 restore the built-in plan. */
-int vv_gemv_tune(int nw, int ks, int handoff, int target_waves);
+ * target waves per launch, weight chunks in flight per wave (2/4/8).
+ * 0 / -1 restore the built-in plan. */
+int vv_gemv_tune(int nw, int ks, int handoff, int target_waves, int u);
 int vv_rmsnorm_bf16(int M, int C, const void* x, int64_t ldx, const void* w, float eps, void* y, int64_t ldy,
                     vv_stream st);
 

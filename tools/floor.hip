@@ -15,3 +15,36 @@ extern "C" int fl_launch(int kind, int blocks, int threads, void* x, void* y, in
   else hipLaunchKernelGGL(k_load, dim3(blocks), dim3(threads), 0, s, (const float*)x, (float*)y, n);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
+
+// Pure read stream: G workgroups x W waves; each wave reads its contiguous share
+// in 1 KB wave-loads with U loads in flight (ping-pong), checksum to one word.
+template <int U>
+__global__ void k_stream(const uint4* __restrict__ p, long long n16_per_wave, unsigned* out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long long w = (long long)blockIdx.x * (blockDim.x >> 6) + wave;
+  const uint4* q = p + w * n16_per_wave + lane;
+  unsigned acc = 0;
+  uint4 a[U], b[U];
+  const long long steps = n16_per_wave / 64;      // 1 KB pieces
+#pragma unroll
+  for (int u = 0; u < U; ++u) a[u] = q[(long long)(u < steps ? u : steps - 1) * 64];
+  for (long long s = 0; s < steps; s += 2 * U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) { long long i = s + U + u; b[u] = q[(i < steps ? i : steps - 1) * 64]; }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= a[u].x ^ a[u].y ^ a[u].z ^ a[u].w;
+#pragma unroll
+    for (int u = 0; u < U; ++u) { long long i = s + 2 * U + u; a[u] = q[(i < steps ? i : steps - 1) * 64]; }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= b[u].x ^ b[u].y ^ b[u].z ^ b[u].w;
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+extern "C" int fl_stream(int G, int W, int U, void* p, long long bytes, void* out, void* st) {
+  const long long n16 = bytes / 16 / ((long long)G * W);
+  hipStream_t s = (hipStream_t)st;
+  if (U == 4) hipLaunchKernelGGL(k_stream<4>, dim3(G), dim3(64 * W), 0, s, (const uint4*)p, n16, (unsigned*)out);
+  else if (U == 8) hipLaunchKernelGGL(k_stream<8>, dim3(G), dim3(64 * W), 0, s, (const uint4*)p, n16, (unsigned*)out);
+  else hipLaunchKernelGGL(k_stream<16>, dim3(G), dim3(64 * W), 0, s, (const uint4*)p, n16, (unsigned*)out);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}

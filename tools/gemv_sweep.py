@@ -106,13 +106,12 @@ def main():
             torch.cuda.synchronize()
             return ((Y.float() - ref).norm() / ref.norm()).item()
 
-        configs = [(0, 0, -1, 0)]
+        configs = [(0, 0, -1, 0, 0)]
         if not quick:
-            
-            configs += [(nw, ks, h, 0) for nw, ks, h in itertools.product((1, 2, 4, 8, 16), (1, 2, 4), (1,))]
+            configs += [(nw, 1, 1, 0, u) for nw, u in itertools.product((1, 2, 4, 8), (2, 4, 8))]
         best = None
-        for nw, ks, h, tw in configs:
-            L.vv_gemv_tune(nw, ks, h, tw)
+        for nw, ks, h, tw, u in configs:
+            L.vv_gemv_tune(nw, ks, h, tw, u)
             try:
                 err = check()
                 us = measure()
@@ -120,7 +119,7 @@ def main():
                 print(name, (nw, ks, h, tw), "error", e)
                 continue
             gbs = (N * K * 2 + M * K * 2 + M * outN * 2) / us / 1e3
-            rec = dict(shape=name, M=M, N=N, K=K, nw=nw, ks=ks, handoff=h, target=tw, us=round(us, 2),
+            rec = dict(shape=name, M=M, N=N, K=K, nw=nw, ks=ks, handoff=h, target=tw, u=u, us=round(us, 2),
                        gbs=round(gbs, 1), err=err)
             results.append(rec)
             ok = err < 1e-2
@@ -128,7 +127,7 @@ def main():
                 best = rec
             if not ok:
                 print("BAD", json.dumps(rec), flush=True)
-        L.vv_gemv_tune(0, 0, -1, 0)
+        L.vv_gemv_tune(0, 0, -1, 0, 0)
         if best is None:
             print(name, "no valid configuration")
             continue
@@ -136,7 +135,7 @@ def main():
                 and r["handoff"] == -1][0]
         print(f"{name:12s} M={M:2d} N={N:6d} K={K:5d} default {dflt['us']:7.2f} us {dflt['gbs']:7.1f} GB/s | "
               f"best {best['us']:7.2f} us {best['gbs']:7.1f} GB/s nw={best['nw']} ks={best['ks']} "
-              f"h={best['handoff']} target={best['target']}", flush=True)
+              f"u={best['u']}", flush=True)
         del Ws
         torch.cuda.empty_cache()
     os.makedirs("gpurun_out", exist_ok=True)

@@ -655,26 +655,27 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
 }
 
 // ------------------------------------------------------------------ host launch
-static int g_tune_nw = 0, g_tune_ks = 0, g_tune_handoff = -1, g_tune_waves = 0;
+static int g_tune_nw = 0, g_tune_ks = 0, g_tune_handoff = -1, g_tune_waves = 0, g_tune_u = 0;
 
-extern "C" int vv_gemv_tune(int nw, int ks, int handoff, int target_waves) {
+extern "C" int vv_gemv_tune(int nw, int ks, int handoff, int target_waves, int u) {
   g_tune_nw = nw;
   g_tune_ks = ks;
   g_tune_handoff = handoff;
   g_tune_waves = target_waves;
+  g_tune_u = u;
   return 0;
 }
 
 struct GemmPlan { int nw, ksplit; };
 
-// Measured on MI355X (tools/gemv_sweep.py, profiles/r01_gemv_sweep.txt): four
-// waves per workgroup and NO cross-workgroup split-K is fastest or within 3 %
-// for every decode shape of the loop — a split-K hand-off costs >= 2 us (sc1
-// form) to 30 us (fence form), more than the extra CUs it brings.
-static GemmPlan gemv_plan(int N, int K) {
-  (void)N;
-  const int chunks = K / 32;
-  int nw = chunks >= 200 ? 8 : 4, ks = 1;   // long rows (LM down, codec fc2): 8 waves
+// Measured on MI355X (tools/gemv_sweep.py, profiles/r01_gemv_sweep*.txt): NO
+// cross-workgroup split-K (a hand-off costs >= 2 us in the sc1 form, up to 30 us
+// with fences — more than the extra CUs bring), 4 waves per workgroup, 8 for
+// few-tile long-row shapes and for M >= 8, 4 weight chunks in flight per wave.
+static GemmPlan gemv_plan(int N, int K, int M) {
+  const int chunks = K / 32, tiles = N / 16;
+  // few tiles with long rows (LM / head down, codec fc2), or many rows: 8 waves
+  int nw = ((tiles <= 128 && chunks >= 128) || M >= 8) ? 8 : 4, ks = 1;
   if (g_tune_waves > 0) {
     const int tiles = N / 16;
     int wpt = (g_tune_waves + tiles - 1) / tiles;
@@ -710,7 +711,10 @@ static void launch_gemv_xf(const GemmArgs& a, int mrep, dim3 grid, dim3 block, h
     const int kw = ((nchunk + a.ksplit - 1) / a.ksplit) * 32;
     const size_t xs_bytes = ((size_t)a.M * (kw + 8) * sizeof(bf16) + 15) & ~(size_t)15;
     const size_t lds = xs_bytes + (size_t)a.M * (kw / 8) * sizeof(float);
-    hipLaunchKernelGGL((k_gemv1<8, XF>), grid, block, lds, st, a);
+    const int u = g_tune_u > 0 ? g_tune_u : 4;   // 4 x 1 KB in flight per wave (tools/gemv_sweep.py)
+    if (u == 4) hipLaunchKernelGGL((k_gemv1<4, XF>), grid, block, lds, st, a);
+    else if (u == 2) hipLaunchKernelGGL((k_gemv1<2, XF>), grid, block, lds, st, a);
+    else hipLaunchKernelGGL((k_gemv1<8, XF>), grid, block, lds, st, a);
     return;
   }
   switch (mrep) {
@@ -743,7 +747,7 @@ int launch_gemm(GemmArgs a, hipStream_t st) {
   if (a.epi.kind == EPI_CFG_DPM && (a.M > 16 || 2 * a.dpm.n != a.M)) return 1;
   if (a.M <= 64) {
     const int mrep = (a.M + 15) / 16;
-    GemmPlan p = gemv_plan(a.N, a.K);
+    GemmPlan p = gemv_plan(a.N, a.K, a.M);
     if (p.nw > max_waves(mrep)) p.nw = max_waves(mrep);
     a.ksplit = p.ksplit;
     if (a.ksplit > 1 && (!a.ws || !a.counters || a.N / 16 > 65536)) a.ksplit = 1;
