@@ -153,12 +153,15 @@ def dist_setup():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     gpu = torch.cuda.is_available()
-    dev = torch.device("cuda", local) if gpu else torch.device("cpu")
+    # VV_BENCH_BACKEND=gloo rehearses the multi-rank path with every rank on
+    # the visible GPU(s) (RCCL needs one GPU per rank)
+    backend = os.environ.get("VV_BENCH_BACKEND", "nccl" if gpu else "gloo")
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count())) if gpu else torch.device("cpu")
     if gpu:
         torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
-        if gpu:
+        if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
@@ -176,7 +179,8 @@ def max_over_ranks(x, world, dev):
     """The job's time is the slowest rank's (contract: max over ranks)."""
     if world == 1:
         return float(x)
-    t = torch.tensor([float(x)], device=dev, dtype=torch.float64)
+    gloo = torch.distributed.get_backend() == "gloo"
+    t = torch.tensor([float(x)], device="cpu" if gloo else dev, dtype=torch.float64)
     torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     return float(t.item())
 

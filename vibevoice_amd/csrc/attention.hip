@@ -283,15 +283,19 @@ __global__ void __launch_bounds__(256) k_final_head(int H, const bf16* h, const 
   const int i = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const bf16* x = h + (long long)(idx ? idx[i] : i) * H;
   const int nch = H >> 3;
-  // one workgroup per row, thread t owns elements [8t, 8t+8)
-  float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // one workgroup per row; thread t owns 8-element chunks t, t + 256, ... (H <= 8192)
+  float v[4][8];
   float ss = 0.f;
-  if (t < nch) {
-    const bf16x8 x8 = *(const bf16x8*)(x + t * 8);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      v[j] = bf(x8[j]);
-      ss += v[j] * v[j];
+  for (int q = 0; q < 4; ++q) {
+    const int c = t + 256 * q;
+    if (c < nch) {
+      const bf16x8 x8 = *(const bf16x8*)(x + c * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[q][j] = bf(x8[j]);
+        ss += v[q][j] * v[q][j];
+      }
     }
   }
   ss = wave_sum(ss);
@@ -300,25 +304,29 @@ __global__ void __launch_bounds__(256) k_final_head(int H, const bf16* h, const 
   ss = red[0][0] + red[1][0] + red[2][0] + red[3][0];
   const float inv = rsqrtf(ss / (float)H + eps);
   float part[4] = {0.f, 0.f, 0.f, 0.f};
-  if (t < nch) {
-    const bf16x8 w8 = *(const bf16x8*)(norm_w + t * 8);
-    bf16x8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      v[j] = rb(rb(v[j] * inv) * bf(w8[j]));
-      o[j] = tobf(v[j]);
-    }
-    *(bf16x8*)(hid + (long long)i * H + t * 8) = o;
-    for (int q = 0; q < nid; ++q) {
-      const bf16x8 l8 = *(const bf16x8*)(W + (long long)ids[q] * H + t * 8);
+  for (int q = 0; q < 4; ++q) {
+    const int c = t + 256 * q;
+    if (c < nch) {
+      const bf16x8 w8 = *(const bf16x8*)(norm_w + c * 8);
+      bf16x8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) part[q] += v[j] * bf(l8[j]);
+      for (int j = 0; j < 8; ++j) {
+        v[q][j] = rb(rb(v[q][j] * inv) * bf(w8[j]));
+        o[j] = tobf(v[q][j]);
+      }
+      *(bf16x8*)(hid + (long long)i * H + c * 8) = o;
+      for (int k = 0; k < nid; ++k) {
+        const bf16x8 l8 = *(const bf16x8*)(W + (long long)ids[k] * H + c * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) part[k] += v[q][j] * bf(l8[j]);
+      }
     }
   }
   __syncthreads();
-  for (int q = 0; q < nid; ++q) {
-    const float s = wave_sum(part[q]);
-    if (lane == 0) red[wave][1 + q] = s;
+  for (int k = 0; k < nid; ++k) {
+    const float sk = wave_sum(part[k]);
+    if (lane == 0) red[wave][1 + k] = sk;
   }
   __syncthreads();
   if (t < nid) logits[i * nid + t] = rb(red[0][1 + t] + red[1][1 + t] + red[2][1 + t] + red[3][1 + t]);
@@ -328,7 +336,7 @@ __global__ void __launch_bounds__(256) k_final_head(int H, const bf16* h, const 
 int launch_final_head(int R, int H, const bf16* h, const int* idx, const bf16* norm_w, float eps, bf16* hidden_out,
                       const bf16* W, const int* ids, int nid, float* logits, hipStream_t st) {
   if (R <= 0) return 0;
-  if (H % 8 || H / 8 > 256 || nid > 4 || (nid > 0 && (!W || !ids || !logits))) return 1;
+  if (H % 8 || H / 8 > 1024 || nid > 4 || (nid > 0 && (!W || !ids || !logits))) return 1;
   hipLaunchKernelGGL(k_final_head, dim3(R), dim3(256), 0, st, H, h, idx, norm_w, eps, hidden_out, W, ids, nid,
                      logits);
   return hipGetLastError() == hipSuccess ? 0 : 2;
