@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--speakers", type=int, default=1)
     ap.add_argument("--ddpm-steps", type=int, default=10)
     ap.add_argument("--model", default="1.5B", choices=["1.5B", "Large"])
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel ranks per model replica (RCCL)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-tokens", type=int, default=8, help="timed tokens of the CPU oracle sample")
     return ap.parse_args()
@@ -201,11 +202,20 @@ def main():
     from vibevoice_amd.synthetic import synthetic_inputs, tokenizer_ids
 
     B, S, K, W = args.batch, args.ddpm_steps, args.steps, args.warmup
-    inp = synthetic_inputs(batch=B, speakers=args.speakers, voice_seconds=3.0, text_tokens=64, seed=100 + rank)
+    T = args.tp
+    if world % T:
+        raise SystemExit(f"--tp {T} must divide the {world} ranks")
+    tp_group = None
+    if T > 1:   # consecutive ranks form one TP group; groups are DP replicas
+        groups = [torch.distributed.new_group(list(range(g * T, (g + 1) * T))) for g in range(world // T)]
+        tp_group = groups[rank // T]
+    replicas = world // T
+    inp = synthetic_inputs(batch=B, speakers=args.speakers, voice_seconds=3.0, text_tokens=64, seed=100 + rank // T)
     L = inp["input_ids"].shape[1]
     total = W + K + 4
     model = VibeVoiceForConditionalGenerationInference.from_pretrained(
-        f"synthetic:{args.model}", device_map=str(dev), synthetic_seed=0, max_batch=B, max_ctx=L + total + 8)
+        f"synthetic:{args.model}", device_map=str(dev), synthetic_seed=0, max_batch=B, max_ctx=L + total + 8,
+        tp_group=tp_group)
     model.set_ddpm_inference_steps(S)
     tk = tokenizer_ids()
     forced = [[tk.speech_diffusion_id] * total for _ in range(B)]
@@ -225,7 +235,7 @@ def main():
     barrier(world)
     dt = max_over_ranks(dt, world, dev)
     ctx1 = int(sess.pos_len.float().mean())
-    tps, audio_per_s = throughput(dt, B, K, world)
+    tps, audio_per_s = throughput(dt, B, K, replicas)
     wb = weight_bytes(model.engine.w)
     ctx_avg = (ctx0 + ctx1) / 2
     bpt = bytes_per_token(wb, model.config, B, S, ctx_avg, (ctx0 + ctx1) / 2 - L)
@@ -233,7 +243,7 @@ def main():
     roof = measure_gemv(model, B)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:   # bounded CPU sample, N=1 only
         cpu = cpu_baseline(model.config, args.cpu_tokens, S)
 
     if rank == 0:
@@ -252,10 +262,10 @@ def main():
             "data": "synthetic: seeded random-init VibeVoice weights at real shapes, seeded -25 dBFS noise voice "
                     "prompt (3 s/speaker), random script ids in the processor's prompt layout, forced "
                     "speech_diffusion schedule (constrained argmax still computed and read back each step)",
-            "config": {"workload": f"VibeVoice-{args.model} bf16, {B} dialogue(s)/GPU x {args.speakers} speaker(s), "
-                                   f"{S} diffusion steps, TP=1, prompt {L} tokens",
-                       "model": f"VibeVoice-{args.model}", "global_batch": B * world, "seq_len": L,
-                       "diffusion_steps": S, "parallelism": f"dp{world} (independent replicas), tp1"},
+            "config": {"workload": f"VibeVoice-{args.model} bf16, {B} dialogue(s)/replica x {args.speakers} "
+                                   f"speaker(s), {S} diffusion steps, TP={T}, prompt {L} tokens",
+                       "model": f"VibeVoice-{args.model}", "global_batch": B * replicas, "seq_len": L,
+                       "diffusion_steps": S, "parallelism": f"dp{replicas} (independent replicas), tp{T}"},
             "roofline": roof,
             "step_roofline": {"bound": "hbm", "achieved": round(step_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(step_ach / HBM_PEAK_GBS, 4),

@@ -86,6 +86,24 @@ int vv_lm_forward(vv_ctx* ctx, int ntok, const void* embeds, int embed_rows, con
                   int max_pos_p1,
                   int nout, const int* out_idx, void* hidden_out, float* logits_out, vv_stream st);
 
+/* Tensor parallelism of the Qwen2 backbone (Megatron split declared at
+ * configuration_vibevoice.py:175-183: q/k/v/gate/up column-parallel, o/down
+ * row-parallel).  The engine is created with its rank's LOCAL head /
+ * intermediate counts and bound to its shard of the weights; the residual
+ * stream is all-reduced (RCCL, sum, bf16, in place) after o_proj and down_proj,
+ * rank 0 alone carrying the residual into the sum.
+ *   vv_tp_unique_id: ncclGetUniqueId into out (returns its size)
+ *   vv_tp_init:      rank / size; unique_id NULL = no communicator (a
+ *                    single-process group driven by vv_lm_forward_group)
+ *   vv_lm_forward_group: the ranks of one group on ONE device, interleaved
+ *                    layer by layer with a device-side sum as the all-reduce
+ *                    (tests / single-GPU emulation); outputs from rank 0. */
+int vv_tp_unique_id(void* out, int nbytes);
+int vv_tp_init(vv_ctx* ctx, int rank, int size, const void* unique_id);
+int vv_lm_forward_group(int n, vv_ctx* const* ctxs, int ntok, const void* embeds, int embed_rows, const int* slot,
+                        const int* pos, int max_pos_p1, int nout, const int* out_idx, void* hidden_out,
+                        float* logits_out, vv_stream st);
+
 /* Copy the K/V cache entry src[i] -> dst[i] of slot slots[i] (all layers). */
 int vv_kv_copy(vv_ctx* ctx, int n, const int* slots, const int* src, const int* dst, vv_stream st);
 

@@ -326,7 +326,31 @@ __global__ void k_gather_rows(int n, int C, const bf16* src, long long lds, cons
   *(bf16x8*)(rm_bfw(dst, i) + c8) = *(const bf16x8*)(src + (long long)(idx ? idx[i] : i) * lds + c8);
 }
 
+// sum of the tensor-parallel partial residual streams, written back to every
+// rank (the all-reduce of a single-process TP group; fp32 sum, one rounding)
+__global__ void k_sum_rows(SumRows s, long long n8) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n8) return;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int r = 0; r < s.n; ++r) {
+    const bf16x8 v = *(const bf16x8*)(s.p[r] + i * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += bf(v[j]);
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = tobf(acc[j]);
+  for (int r = 0; r < s.n; ++r) *(bf16x8*)(s.p[r] + i * 8) = o;
+}
+
 // ================================================================ host launchers
+int launch_sum_rows(SumRows s, long long count, hipStream_t st) {
+  if (count % 8 || s.n < 1 || s.n > 8) return 1;
+  const long long n8 = count / 8;
+  hipLaunchKernelGGL(k_sum_rows, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, st, s, n8);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
 static inline int nblk(long long n, int b) { return (int)((n + b - 1) / b); }
 
 int launch_rmsnorm(NormArgs a, hipStream_t st) {

@@ -6,6 +6,7 @@
 // stream (no host sync, no allocation after vv_finalize except the grow-only
 // prefill / voice-prompt workspaces).  C ABI: include/vibevoice_hip.h.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -130,6 +131,11 @@ struct vv_ctx {
   ConvNet dec, sem, aenc;
   DevBuf codec_ws;  // connectors
   DevBuf slot_scratch;
+  // tensor parallelism of the LM (Megatron split, configuration_vibevoice.py:175-183):
+  // this engine holds rank tp_rank's shard; the residual stream is all-reduced
+  // after o_proj and down_proj
+  int tp_rank = 0, tp_size = 1;
+  ncclComm_t comm = nullptr;
 };
 
 // ------------------------------------------------------------------ helpers
@@ -501,6 +507,7 @@ void vv_destroy(vv_ctx* c) {
     n->work.release();
     n->d_rolls.release();
   }
+  if (c->comm) (void)ncclCommDestroy(c->comm);
   delete c;
 }
 
@@ -660,89 +667,200 @@ int vv_embed(vv_ctx* c, int n, const int* ids, void* out, vv_stream vst) {
   return 0;
 }
 
-int vv_lm_forward(vv_ctx* c, int ntok, const void* embeds, int embed_rows, const int* slot, const int* pos,
-                  int max_pos_p1, int nout, const int* out_idx, void* hidden_out, float* logits_out, vv_stream vst) {
-  hipStream_t st = (hipStream_t)vst;
+// ------------------------------------------------------------------ LM pass
+// One forward of ntok token rows, split so that a tensor-parallel group can
+// interleave its ranks layer by layer (vv_lm_forward_group) or all-reduce over
+// RCCL between the halves (vv_lm_forward).
+struct LmPass {
+  int ntok = 0, nsplit = 1, chunk = 64;
+  bf16 *h = nullptr, *q = nullptr, *att = nullptr, *act = nullptr;
+  RowMap in_m, hm;
+  const int *slot = nullptr, *pos = nullptr;
+  const float* inv_freq = nullptr;
+};
+
+static int lm_begin(vv_ctx* c, LmPass& P, int ntok, const void* embeds, int embed_rows, const int* slot,
+                    const int* pos, int max_pos_p1) {
   if (!c->finalized) FAIL("vv_lm_forward before vv_finalize");
-  if (ntok <= 0) return 0;
   if (max_pos_p1 > c->cfg.max_ctx) FAIL("position beyond max_ctx");
   const vv_config& k = c->cfg;
   const int H = k.hidden, d = k.head_dim, I = k.intermediate, nhd = k.n_heads * d;
-  // workspace
   const size_t per = (size_t)H * 3 + c->qkv_n + nhd * 2 + I;
   if ((size_t)ntok > c->lm_ws_tokens) {
     CHK(c->lm_ws.ensure(per * ntok * sizeof(bf16) + 256));
     c->lm_ws_tokens = ntok;
   }
-  bf16* h = (bf16*)c->lm_ws.p;
-  bf16* a = h + (size_t)ntok * H;
+  P.ntok = ntok;
+  P.h = (bf16*)c->lm_ws.p;
+  bf16* a = P.h + (size_t)ntok * H;
   bf16* qkv = a + (size_t)ntok * H;
-  bf16* q = qkv + (size_t)ntok * c->qkv_n;
-  bf16* att = q + (size_t)ntok * nhd;
-  bf16* act = att + (size_t)ntok * nhd;
-  bf16* fin = act + (size_t)ntok * I;
-  int chunk = 0;
-  const int nsplit = attn_plan(ntok, k.n_kv_heads, max_pos_p1, &chunk);
-  if (nsplit > 1) {
+  P.q = qkv + (size_t)ntok * c->qkv_n;
+  P.att = P.q + (size_t)ntok * nhd;
+  P.act = P.att + (size_t)ntok * nhd;
+  P.nsplit = attn_plan(ntok, k.n_kv_heads, max_pos_p1, &P.chunk);
+  if (P.nsplit > 1) {
     if ((size_t)ntok * k.n_kv_heads > 65536) FAIL("attention split tickets exhausted");
-    CHK(c->attn_part.ensure((size_t)ntok * k.n_heads * nsplit * (d + 2) * sizeof(float)));
+    CHK(c->attn_part.ensure((size_t)ntok * k.n_heads * P.nsplit * (d + 2) * sizeof(float)));
   }
   // token row m reads embeds row m % embed_rows (the negative CFG rows consume the
   // positive rows' embeddings, :594-596); layer 0's attention residual writes h
   if (embed_rows <= 0 || embed_rows > ntok) embed_rows = ntok;
-  const RowMap in_m = rowmap(embeds, H, embed_rows, 0);
-  RowMap hm = rowmap(h, H);
-  const float* inv_freq = (const float*)W(c, "lm.inv_freq");
-  for (int l = 0; l < k.n_layers; ++l) {
-    const std::string p = "lm." + std::to_string(l);
+  P.in_m = rowmap(embeds, H, embed_rows, 0);
+  P.hm = rowmap(P.h, H);
+  P.slot = slot;
+  P.pos = pos;
+  P.inv_freq = (const float*)W(c, "lm.inv_freq");
+  return 0;
+}
+
+// residual epilogue of a row-parallel projection: rank 0 adds the residual,
+// the other ranks contribute their partial only (the all-reduce sums them)
+static void tp_residual(vv_ctx* c, GemmArgs& g, const RowMap& res) {
+  if (c->tp_rank == 0) {
+    g.epi.kind = EPI_RES;
+    g.epi.res = res;
+  } else {
+    g.epi.kind = EPI_STORE;
+  }
+}
+
+// input_layernorm .. o_proj (+ residual on rank 0)
+static int lm_attn_half(vv_ctx* c, LmPass& P, int l, hipStream_t st) {
+  const vv_config& k = c->cfg;
+  const int H = k.hidden, d = k.head_dim, nhd = k.n_heads * d;
+  const std::string p = "lm." + std::to_string(l);
+  {
     // input_layernorm -> q|k|v projection (+bias) -> RoPE -> q / KV cache, one launch
-    {
-      GemmArgs g = gemm_args(c, ntok, c->qkv_n, H, l == 0 ? in_m : hm, W(c, p + ".qkv_w"), EPI_ROPE, RowMap{},
-                             W(c, p + ".qkv_b"));
-      g.xf = xf_norm(W(c, p + ".in_norm"), k.rms_eps);
-      g.rope.nh = k.n_heads;
-      g.rope.nkv = k.n_kv_heads;
-      g.rope.layer = l;
-      g.rope.q_out = q;
-      g.rope.slots = slot;
-      g.rope.pos = pos;
-      g.rope.inv_freq = inv_freq;
-      g.rope.kv = c->kv;
-      CHK(gemm(c, g, st));
-    }
-    AttnArgs at;
-    at.nq = ntok;
-    at.nh = k.n_heads;
-    at.nkv = k.n_kv_heads;
-    at.layer = l;
-    at.nsplit = nsplit;
-    at.chunk = chunk;
-    at.counters = (unsigned*)c->attn_cnt.p;
-    at.scale = 1.0f / sqrtf((float)d);
-    at.q = q;
-    at.out = att;
-    at.slots = slot;
-    at.pos = pos;
-    at.kv = c->kv;
-    at.part_o = (float*)c->attn_part.p;
-    at.part_ml = at.part_o ? at.part_o + (size_t)ntok * k.n_heads * nsplit * d : nullptr;
-    KCHK(launch_attn(at, st));
-    GemmArgs g = gemm_args(c, ntok, H, nhd, rowmap(att, nhd), W(c, p + ".o_w"), EPI_RES, hm);
-    g.epi.res = l == 0 ? in_m : hm;
-    CHK(gemm(c, g, st));
-    // post_attention_layernorm fused into gate|up's A load
-    g = gemm_args(c, ntok, 2 * I, H, hm, W(c, p + ".gu_w"), EPI_SILU_MUL, rowmap(act, I));
-    g.xf = xf_norm(W(c, p + ".post_norm"), k.rms_eps);
-    CHK(gemm(c, g, st));
-    g = gemm_args(c, ntok, H, I, rowmap(act, I), W(c, p + ".down_w"), EPI_RES, hm);
-    g.epi.res = hm;
+    GemmArgs g = gemm_args(c, P.ntok, c->qkv_n, H, l == 0 ? P.in_m : P.hm, W(c, p + ".qkv_w"), EPI_ROPE, RowMap{},
+                           W(c, p + ".qkv_b"));
+    g.xf = xf_norm(W(c, p + ".in_norm"), k.rms_eps);
+    g.rope.nh = k.n_heads;
+    g.rope.nkv = k.n_kv_heads;
+    g.rope.layer = l;
+    g.rope.q_out = P.q;
+    g.rope.slots = P.slot;
+    g.rope.pos = P.pos;
+    g.rope.inv_freq = P.inv_freq;
+    g.rope.kv = c->kv;
     CHK(gemm(c, g, st));
   }
-  if (nout > 0) {
-    // gather the output rows + final norm + the valid-id lm_head rows, one launch
-    KCHK(launch_final_head(nout, H, h, out_idx, W(c, "lm.norm"), k.rms_eps, (bf16*)hidden_out, W(c, "lm.lm_head"),
-                           (const int*)c->valid_ids.p, logits_out ? c->n_valid : 0, logits_out, st));
+  AttnArgs at;
+  at.nq = P.ntok;
+  at.nh = k.n_heads;
+  at.nkv = k.n_kv_heads;
+  at.layer = l;
+  at.nsplit = P.nsplit;
+  at.chunk = P.chunk;
+  at.counters = (unsigned*)c->attn_cnt.p;
+  at.scale = 1.0f / sqrtf((float)d);
+  at.q = P.q;
+  at.out = P.att;
+  at.slots = P.slot;
+  at.pos = P.pos;
+  at.kv = c->kv;
+  at.part_o = (float*)c->attn_part.p;
+  at.part_ml = at.part_o ? at.part_o + (size_t)P.ntok * k.n_heads * P.nsplit * d : nullptr;
+  KCHK(launch_attn(at, st));
+  GemmArgs g = gemm_args(c, P.ntok, H, nhd, rowmap(P.att, nhd), W(c, p + ".o_w"), EPI_RES, P.hm);
+  tp_residual(c, g, l == 0 ? P.in_m : P.hm);
+  CHK(gemm(c, g, st));
+  return 0;
+}
+
+// post_attention_layernorm .. down_proj (+ residual on rank 0)
+static int lm_mlp_half(vv_ctx* c, LmPass& P, int l, hipStream_t st) {
+  const vv_config& k = c->cfg;
+  const int H = k.hidden, I = k.intermediate;
+  const std::string p = "lm." + std::to_string(l);
+  // post_attention_layernorm fused into gate|up's A load
+  GemmArgs g = gemm_args(c, P.ntok, 2 * I, H, P.hm, W(c, p + ".gu_w"), EPI_SILU_MUL, rowmap(P.act, I));
+  g.xf = xf_norm(W(c, p + ".post_norm"), k.rms_eps);
+  CHK(gemm(c, g, st));
+  g = gemm_args(c, P.ntok, H, I, rowmap(P.act, I), W(c, p + ".down_w"), EPI_RES, P.hm);
+  tp_residual(c, g, P.hm);
+  CHK(gemm(c, g, st));
+  return 0;
+}
+
+static int tp_allreduce(vv_ctx* c, LmPass& P, hipStream_t st) {
+  if (!c->comm) {
+    if (c->tp_size > 1) FAIL("tensor-parallel engine without a communicator (vv_tp_init)");
+    return 0;
   }
+  const ncclResult_t r = ncclAllReduce(P.h, P.h, (size_t)P.ntok * c->cfg.hidden, ncclBfloat16, ncclSum, c->comm, st);
+  if (r != ncclSuccess) FAIL(std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  return 0;
+}
+
+static int lm_end(vv_ctx* c, LmPass& P, int nout, const int* out_idx, void* hidden_out, float* logits_out,
+                  hipStream_t st) {
+  if (nout <= 0) return 0;
+  const vv_config& k = c->cfg;
+  // gather the output rows + final norm + the valid-id lm_head rows, one launch
+  KCHK(launch_final_head(nout, k.hidden, P.h, out_idx, W(c, "lm.norm"), k.rms_eps, (bf16*)hidden_out,
+                         W(c, "lm.lm_head"), (const int*)c->valid_ids.p, logits_out ? c->n_valid : 0, logits_out,
+                         st));
+  return 0;
+}
+
+int vv_lm_forward(vv_ctx* c, int ntok, const void* embeds, int embed_rows, const int* slot, const int* pos,
+                  int max_pos_p1, int nout, const int* out_idx, void* hidden_out, float* logits_out, vv_stream vst) {
+  hipStream_t st = (hipStream_t)vst;
+  if (ntok <= 0) return 0;
+  LmPass P;
+  CHK(lm_begin(c, P, ntok, embeds, embed_rows, slot, pos, max_pos_p1));
+  for (int l = 0; l < c->cfg.n_layers; ++l) {
+    CHK(lm_attn_half(c, P, l, st));
+    CHK(tp_allreduce(c, P, st));
+    CHK(lm_mlp_half(c, P, l, st));
+    CHK(tp_allreduce(c, P, st));
+  }
+  return lm_end(c, P, nout, out_idx, hidden_out, logits_out, st);
+}
+
+int vv_lm_forward_group(int n, vv_ctx* const* ctxs, int ntok, const void* embeds, int embed_rows, const int* slot,
+                        const int* pos, int max_pos_p1, int nout, const int* out_idx, void* hidden_out,
+                        float* logits_out, vv_stream vst) {
+  hipStream_t st = (hipStream_t)vst;
+  if (n < 1 || n > 8) FAIL("vv_lm_forward_group: 1..8 ranks");
+  if (ntok <= 0) return 0;
+  std::vector<LmPass> P(n);
+  SumRows sr;
+  sr.n = n;
+  for (int r = 0; r < n; ++r) {
+    if (ctxs[r]->tp_rank != r || ctxs[r]->tp_size != n) FAIL("vv_lm_forward_group: engine r must be TP rank r of n");
+    CHK(lm_begin(ctxs[r], P[r], ntok, embeds, embed_rows, slot, pos, max_pos_p1));
+    sr.p[r] = P[r].h;
+  }
+  const long long count = (long long)ntok * ctxs[0]->cfg.hidden;
+  for (int l = 0; l < ctxs[0]->cfg.n_layers; ++l) {
+    for (int r = 0; r < n; ++r) CHK(lm_attn_half(ctxs[r], P[r], l, st));
+    KCHK(launch_sum_rows(sr, count, st));
+    for (int r = 0; r < n; ++r) CHK(lm_mlp_half(ctxs[r], P[r], l, st));
+    KCHK(launch_sum_rows(sr, count, st));
+  }
+  return lm_end(ctxs[0], P[0], nout, out_idx, hidden_out, logits_out, st);
+}
+
+int vv_tp_unique_id(void* out, int nbytes) {
+  if (nbytes < (int)sizeof(ncclUniqueId)) FAIL("vv_tp_unique_id: buffer smaller than ncclUniqueId");
+  ncclUniqueId id;
+  const ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) FAIL(std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  memcpy(out, &id, sizeof(id));
+  return (int)sizeof(id);
+}
+
+int vv_tp_init(vv_ctx* c, int rank, int size, const void* unique_id) {
+  if (size < 1 || rank < 0 || rank >= size) FAIL("vv_tp_init: bad rank / size");
+  c->tp_rank = rank;
+  c->tp_size = size;
+  if (!unique_id) return 0;  // group emulation in one process: no communicator
+  HIPCHK(hipSetDevice(c->device));
+  ncclUniqueId id;
+  memcpy(&id, unique_id, sizeof(id));
+  const ncclResult_t r = ncclCommInitRank(&c->comm, size, id, rank);
+  if (r != ncclSuccess) FAIL(std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
   return 0;
 }
 

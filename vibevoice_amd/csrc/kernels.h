@@ -140,7 +140,14 @@ struct AttnArgs {
   unsigned* counters;   // [nq * nkv] split tickets (zero between launches)
 };
 
+// out_r = sum_r in_r for every r (single-process tensor-parallel group)
+struct SumRows {
+  int n, pad_;
+  bf16* p[8];
+};
+
 int launch_gemm(GemmArgs a, hipStream_t st);
+int launch_sum_rows(SumRows s, long long count, hipStream_t st);
 int launch_rmsnorm(NormArgs a, hipStream_t st);
 int launch_dwconv(DwArgs a, hipStream_t st);
 int launch_mix(MixArgs a, hipStream_t st);

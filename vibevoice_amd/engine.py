@@ -24,16 +24,18 @@ def _stream(stream=None):
     return ctypes.c_void_p(s.cuda_stream)
 
 
-def engine_config(cfg: VibeVoiceConfig, max_batch, max_ctx):
+def engine_config(cfg: VibeVoiceConfig, max_batch, max_ctx, tp_size=1):
+    """vv_config of one engine; with tensor parallelism the LM head and
+    intermediate counts are this rank's local ones."""
     lm = cfg.decoder_config
     hc = cfg.diffusion_head_config
     c = _lib.VVConfig()
     c.hidden = lm.hidden_size
     c.n_layers = lm.num_hidden_layers
-    c.n_heads = lm.num_attention_heads
-    c.n_kv_heads = lm.num_key_value_heads
+    c.n_heads = lm.num_attention_heads // tp_size
+    c.n_kv_heads = lm.num_key_value_heads // tp_size
     c.head_dim = lm.get("head_dim") or lm.hidden_size // lm.num_attention_heads
-    c.intermediate = lm.intermediate_size
+    c.intermediate = lm.intermediate_size // tp_size
     c.rms_eps = lm.rms_norm_eps
     c.rope_theta = lm.rope_theta
     c.head_layers = hc.head_layers
@@ -61,7 +63,10 @@ class Engine:
     """One device-resident VibeVoice model instance."""
 
     def __init__(self, cfg: VibeVoiceConfig, state_dict, device="cuda", max_batch=1, max_ctx=4096,
-                 valid_ids=None):
+                 valid_ids=None, tp_rank=0, tp_size=1, tp_unique_id=None):
+        """tp_size > 1: rank tp_rank's shard of the LM; tp_unique_id (bytes of
+        vv_tp_unique_id, shared by the group) creates its RCCL communicator, None
+        leaves it for a single-process group (lm_forward_group)."""
         L = _lib.lib()
         self.cfg = cfg
         self.device = torch.device(device)
@@ -72,12 +77,17 @@ class Engine:
         self.hidden = cfg.decoder_config.hidden_size
         self.latent = cfg.diffusion_head_config.latent_size
         self.hop = cfg.hop
+        self.tp_rank, self.tp_size = tp_rank, tp_size
         with torch.cuda.device(self.device):
-            self.w = pack(state_dict, cfg, self.device)
+            self.w = pack(state_dict, cfg, self.device, tp_rank=tp_rank, tp_size=tp_size)
             h = ctypes.c_void_p()
-            self._ecfg = engine_config(cfg, max_batch, max_ctx)
+            self._ecfg = engine_config(cfg, max_batch, max_ctx, tp_size)
             _lib.check(L.vv_create(ctypes.byref(self._ecfg), self.device.index or 0, ctypes.byref(h)), "create")
             self.h = h
+            if tp_size > 1 or tp_unique_id is not None:
+                uid = None if tp_unique_id is None else ctypes.create_string_buffer(bytes(tp_unique_id),
+                                                                                   len(tp_unique_id))
+                _lib.check(L.vv_tp_init(h, tp_rank, tp_size, uid), "tp_init")
             for name, t in self.w.items():
                 shape = (ctypes.c_int64 * max(1, t.dim()))(*t.shape)
                 _lib.check(L.vv_bind_weight(h, name.encode(), _ptr(t), shape, t.dim()), f"bind {name}")
@@ -100,6 +110,7 @@ class Engine:
 
     # ---------------------------------------------------------------- setup
     def set_valid_ids(self, ids):
+        self._valid = list(ids)
         arr = (ctypes.c_int * len(ids))(*ids)
         _lib.check(_lib.lib().vv_set_valid_ids(self.h, len(ids), arr), "set_valid_ids")
         self.n_valid = len(ids)
@@ -131,6 +142,35 @@ class Engine:
                                             _ptr(out_idx), _ptr(hidden_out), _ptr(logits_out), _stream(stream)),
                    "lm_forward")
         return hidden_out, logits_out
+
+    def lm_forward_group(self, peers, embeds, slots, pos, out_idx, hidden_out=None, logits_out=None,
+                         max_pos=None, stream=None, ntok=None):
+        """Run the TP group [self] + peers (ranks 0..n-1, same device) layer by
+        layer with an on-device all-reduce; outputs of rank 0 (= self)."""
+        rows = embeds.shape[0]
+        ntok = rows if ntok is None else ntok
+        nout = out_idx.shape[0]
+        if hidden_out is None:
+            hidden_out = torch.empty(nout, self.hidden, dtype=torch.bfloat16, device=self.device)
+        if logits_out is None:
+            logits_out = torch.empty(nout, self.n_valid, dtype=torch.float32, device=self.device)
+        if getattr(self, "_valid", None):
+            for p in peers:
+                p.set_valid_ids(self._valid)
+        mp = int(max_pos if max_pos is not None else pos.max().item()) + 1
+        ctxs = (ctypes.c_void_p * (1 + len(peers)))(self.h, *[p.h for p in peers])
+        _lib.check(_lib.lib().vv_lm_forward_group(1 + len(peers), ctxs, ntok, _ptr(embeds), rows, _ptr(slots),
+                                                  _ptr(pos), mp, nout, _ptr(out_idx), _ptr(hidden_out),
+                                                  _ptr(logits_out), _stream(stream)), "lm_forward_group")
+        return hidden_out, logits_out
+
+    @staticmethod
+    def tp_unique_id():
+        buf = ctypes.create_string_buffer(256)
+        n = _lib.lib().vv_tp_unique_id(buf, 256)
+        if n <= 0:
+            _lib.check(-1, "tp_unique_id")
+        return buf.raw[:n]
 
     def kv_copy(self, slots, src, dst, stream=None):
         _lib.check(_lib.lib().vv_kv_copy(self.h, slots.shape[0], _ptr(slots), _ptr(src), _ptr(dst), _stream(stream)),

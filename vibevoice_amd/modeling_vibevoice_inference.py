@@ -74,14 +74,28 @@ def load_state_dict(path):
 
 class VibeVoiceForConditionalGenerationInference:
     def __init__(self, config: VibeVoiceConfig, state_dict, device="cuda", attn_implementation="hip",
-                 max_batch=8, max_ctx=8192):
+                 max_batch=8, max_ctx=8192, tp_group=None):
+        """tp_group: a torch.distributed process group whose ranks (one per GPU)
+        tensor-parallel-shard the Qwen2 backbone over RCCL; every
+        rank then runs generate() on the same inputs (SPMD) and gets the same
+        result.  None: the whole model on this GPU."""
         self.config = config
         self.attn_implementation = attn_implementation
         self.device = torch.device(device)
         self.dtype = torch.bfloat16
         self._sd = state_dict
+        tp_rank, tp_size, uid = 0, 1, None
+        if tp_group is not None:
+            import torch.distributed as dist
+            tp_rank, tp_size = dist.get_rank(tp_group), dist.get_world_size(tp_group)
+            if tp_size > 1:
+                box = [Engine.tp_unique_id() if tp_rank == 0 else None]
+                dist.broadcast_object_list(box, src=dist.get_global_rank(tp_group, 0), group=tp_group)
+                uid = box[0]
+        self.tp_rank, self.tp_size = tp_rank, tp_size
         self.engine = Engine(config, state_dict, self.device, max_batch=max_batch,
-                             max_ctx=min(max_ctx, config.decoder_config.max_position_embeddings))
+                             max_ctx=min(max_ctx, config.decoder_config.max_position_embeddings),
+                             tp_rank=tp_rank, tp_size=tp_size, tp_unique_id=uid)
         self.ddpm_inference_steps = config.diffusion_head_config.ddpm_num_inference_steps
         self.model = _ModelView(self)
         self.use_graphs = True          # capture the steady-state loop body into hipGraphs

@@ -236,9 +236,25 @@ def rope_inv_freq(theta, d):
     return 1.0 / (theta ** (torch.arange(0, d, 2, dtype=torch.int64).to(dtype=torch.float) / d))
 
 
-def pack(sd, cfg: VibeVoiceConfig, device, with_acoustic_encoder=True):
-    """Reference state dict -> {engine name: contiguous device tensor}."""
+def tp_check(cfg: VibeVoiceConfig, tp_size):
+    """Where the backbone shards cleanly: whole kv heads per
+    rank (1.5B: 2 kv heads -> TP <= 2; Large: 4 -> TP <= 4)."""
+    lm = cfg.decoder_config
+    nh, nkv, inter = lm.num_attention_heads, lm.num_key_value_heads, lm.intermediate_size
+    if nkv % tp_size or nh % tp_size or inter % (16 * tp_size):
+        raise ValueError(f"TP={tp_size} does not shard {nh} q / {nkv} kv heads / intermediate {inter} cleanly")
+
+
+def pack(sd, cfg: VibeVoiceConfig, device, with_acoustic_encoder=True, tp_rank=0, tp_size=1):
+    """Reference state dict -> {engine name: contiguous device tensor}.
+
+    tp_size > 1: this rank's Megatron shard of the Qwen2 layers
+    (configuration_vibevoice.py:175-183): q/k/v rows of its heads and
+    gate/up rows of its intermediate slice (column-parallel), the matching
+    o_proj / down_proj input columns (row-parallel).  Embedding, norms,
+    lm_head, diffusion head, codec and connectors are replicated."""
     dt = torch.bfloat16
+    tp_check(cfg, tp_size)
 
     def t(x):
         return x.to(device=device, dtype=dt).contiguous()
@@ -257,13 +273,17 @@ def pack(sd, cfg: VibeVoiceConfig, device, with_acoustic_encoder=True):
         out[e + "in_norm"] = t(sd[p + "input_layernorm.weight"])
         out[e + "post_norm"] = t(sd[p + "post_attention_layernorm.weight"])
         nkv = lm.num_key_value_heads
+        nhl, nkvl, il = nh // tp_size, nkv // tp_size, lm.intermediate_size // tp_size
+        qs = slice(tp_rank * nhl * d, (tp_rank + 1) * nhl * d)
+        ks = slice(tp_rank * nkvl * d, (tp_rank + 1) * nkvl * d)
+        fs = slice(tp_rank * il, (tp_rank + 1) * il)
         q, k, v = (sd[p + f"self_attn.{x}_proj.weight"] for x in "qkv")
         qb, kb, vb = (sd[p + f"self_attn.{x}_proj.bias"] for x in "qkv")
-        out[e + "qkv_w"] = t(torch.cat([_rope_pack(q, nh, d), _rope_pack(k, nkv, d), v], 0))
-        out[e + "qkv_b"] = t(torch.cat([_rope_pack(qb, nh, d), _rope_pack(kb, nkv, d), vb], 0))
-        out[e + "o_w"] = t(sd[p + "self_attn.o_proj.weight"])
-        out[e + "gu_w"] = t(_gu(sd[p + "mlp.gate_proj.weight"], sd[p + "mlp.up_proj.weight"]))
-        out[e + "down_w"] = t(sd[p + "mlp.down_proj.weight"])
+        out[e + "qkv_w"] = t(torch.cat([_rope_pack(q[qs], nhl, d), _rope_pack(k[ks], nkvl, d), v[ks]], 0))
+        out[e + "qkv_b"] = t(torch.cat([_rope_pack(qb[qs], nhl, d), _rope_pack(kb[ks], nkvl, d), vb[ks]], 0))
+        out[e + "o_w"] = t(sd[p + "self_attn.o_proj.weight"][:, qs])
+        out[e + "gu_w"] = t(_gu(sd[p + "mlp.gate_proj.weight"][fs], sd[p + "mlp.up_proj.weight"][fs]))
+        out[e + "down_w"] = t(sd[p + "mlp.down_proj.weight"][:, fs])
 
     hc = cfg.diffusion_head_config
     out["head.noisy_w"] = t(sd[HEAD + "noisy_images_proj.weight"])
