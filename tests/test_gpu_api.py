@@ -1,0 +1,122 @@
+"""The reference's plugin surface around generate() (GPU):
+
+* from_pretrained(<dir>) loads a HF-style checkpoint directory (config.json +
+  sharded *.safetensors with the reference's state-dict names, untied lm_head
+  dropped -> tied to the embedding as modeling_vibevoice_inference.py:120-129)
+  and produces exactly what the in-memory state dict produces;
+* audio_streamer: put() receives every chunk of speech_outputs per sample,
+  end() is called for a finished sample, and — as in the reference
+  (modeling_vibevoice_inference.py:443-447) — the loop stops at the next step
+  once any streamer flag is set;
+* stop_check_fn stops the loop and ends the streamer (:434-440);
+* model.model.language_model.config._attn_implementation exists
+  (demo/inference_from_file.py:315-316).
+"""
+import json
+import os
+
+import pytest
+import torch
+from safetensors.torch import save_file
+
+from tiny import tiny_config, tiny_dict
+from vibevoice_amd.modeling_vibevoice_inference import VibeVoiceForConditionalGenerationInference
+from vibevoice_amd.synthetic import tokenizer_ids
+from vibevoice_amd.weights import synthetic_state_dict
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+TOK = tokenizer_ids()
+D, E, S, X = TOK.speech_diffusion_id, TOK.speech_end_id, TOK.speech_start_id, TOK.eos_token_id
+
+
+class RecordingStreamer:
+    """Duck-typed AudioStreamer (vibevoice/modular/streamer.py:13-76)."""
+
+    def __init__(self, batch):
+        self.chunks = [[] for _ in range(batch)]
+        self.finished_flags = [False] * batch
+        self.ended = []
+
+    def put(self, audio_chunks, sample_indices):
+        for i, idx in enumerate(sample_indices.tolist()):
+            if not self.finished_flags[idx]:
+                self.chunks[idx].append(audio_chunks[i].detach().cpu())
+
+    def end(self, sample_indices=None):
+        idx = range(len(self.finished_flags)) if sample_indices is None else sample_indices.tolist()
+        for i in idx:
+            if not self.finished_flags[i]:
+                self.finished_flags[i] = True
+                self.ended.append(i)
+
+
+def _model(sd, cfg):
+    m = VibeVoiceForConditionalGenerationInference(cfg, sd, dev, max_batch=2, max_ctx=128)
+    m.set_ddpm_inference_steps(3)
+    return m
+
+
+def _inputs():
+    g = torch.Generator().manual_seed(4)
+    return torch.randint(0, 151000, (2, 12), generator=g), torch.ones(2, 12, dtype=torch.long)
+
+
+def test_from_pretrained_checkpoint_dir(tmp_path):
+    cfg = tiny_config(hidden=256, layers=2, heads=2, kv_heads=1, inter=512)
+    sd = synthetic_state_dict(cfg, seed=9, device="cpu", mode="test", with_acoustic_encoder=True)
+    names = sorted(k for k in sd if k != "lm_head.weight")           # tied: not saved
+    half = len(names) // 2
+    for i, part in enumerate((names[:half], names[half:])):
+        save_file({k: sd[k].contiguous() for k in part}, os.path.join(tmp_path, f"model-0000{i + 1}-of-00002.safetensors"))
+    with open(os.path.join(tmp_path, "config.json"), "w") as f:
+        json.dump(tiny_dict(hidden=256, layers=2, heads=2, kv_heads=1, inter=512), f)
+    a = VibeVoiceForConditionalGenerationInference.from_pretrained(str(tmp_path), torch_dtype=torch.bfloat16,
+                                                                   device_map="cuda",
+                                                                   attn_implementation="flash_attention_2",
+                                                                   max_batch=2, max_ctx=128)
+    assert a.model.language_model.config._attn_implementation == "flash_attention_2"
+    b = _model(sd, cfg)
+    a.set_ddpm_inference_steps(3)
+    ids, mask = _inputs()
+    sched = [[D, D, D, X], [D, D, E, X]]
+    outs = []
+    for m in (a, b):
+        torch.manual_seed(5)
+        outs.append(m.generate(input_ids=ids, attention_mask=mask, tokenizer=TOK, cfg_scale=1.3,
+                               forced_tokens=sched, show_progress_bar=False))
+    assert torch.equal(outs[0].sequences, outs[1].sequences)
+    for i in range(2):
+        assert torch.equal(outs[0].speech_outputs[i].cpu(), outs[1].speech_outputs[i].cpu())
+
+
+def test_streamer_and_stop_check():
+    cfg = tiny_config(hidden=256, layers=2, heads=2, kv_heads=1, inter=512)
+    sd = synthetic_state_dict(cfg, seed=10, device="cpu", mode="test", with_acoustic_encoder=False)
+    m = _model(sd, cfg)
+    ids, mask = _inputs()
+    # sample 1 emits eos at step 2: the streamer ends it, the loop stops at step 3
+    sched = [[D] * 8 + [X], [D, D, X]]
+    st = RecordingStreamer(2)
+    torch.manual_seed(6)
+    out = m.generate(input_ids=ids, attention_mask=mask, tokenizer=TOK, cfg_scale=1.3, forced_tokens=sched,
+                     audio_streamer=st, show_progress_bar=False)
+    assert out.sequences.shape[1] == 12 + 3
+    assert st.ended[0] == 1 and sorted(st.ended) == [0, 1]
+    for b in range(2):
+        got = torch.cat(st.chunks[b], dim=-1)
+        assert torch.equal(got.reshape(-1), out.speech_outputs[b].cpu().reshape(-1))
+    # external stop after 4 steps
+    calls = {"n": 0}
+
+    def stop():
+        calls["n"] += 1
+        return calls["n"] > 4
+    st2 = RecordingStreamer(2)
+    torch.manual_seed(6)
+    out2 = m.generate(input_ids=ids, attention_mask=mask, tokenizer=TOK, cfg_scale=1.3,
+                      forced_tokens=[[D] * 8 + [X]] * 2, audio_streamer=st2, stop_check_fn=stop,
+                      show_progress_bar=False)
+    assert out2.sequences.shape[1] == 12 + 4
+    assert sorted(st2.ended) == [0, 1]
+    assert out2.speech_outputs[0].shape[-1] == 4 * m.engine.hop

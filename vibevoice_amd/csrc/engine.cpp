@@ -418,7 +418,7 @@ static int convnet_run(vv_ctx* c, ConvNet& net, int n, const int* slots, RowMap 
       mx.n = n;
       mx.T = T;
       mx.C = C;
-      mx.R = std::max(1, std::min(T, 2048 / C));
+      mx.R = std::max(1, std::min(T, 2048 / C));   // R * C / 8 = 256 conv items: one per thread
       mx.eps = eps;
       mx.ctx = mb.ctx;
       mx.x = net.X[i];
