@@ -160,6 +160,14 @@ int vv_attention_bf16(int nq, int nh, int nkv, const void* q, const void* k_cach
  * target waves per launch, weight chunks in flight per wave (2/4/8).
  * 0 / -1 restore the built-in plan. */
 int vv_gemv_tune(int nw, int ks, int handoff, int target_waves, int u);
+/* Diagnostic (benchmarks only): M <= 16 GEMV launches write 4 s_memrealtime
+ * stamps per workgroup (start, A staged, weights streamed, epilogue stored) to
+ * buf (uint64[grid * 4]); NULL turns it off. */
+int vv_gemv_stamps(void* buf);
+/* Test switch: 1 (default) folds each codec Block1D's mixer (norm, depthwise
+ * conv, gamma residual, FFN norm) into its fc1 GEMV when <= 16 rows fit; 0
+ * runs the separate k_mix launch everywhere.  Results are bit-identical. */
+int vv_codec_mix_fusion(int on);
 int vv_rmsnorm_bf16(int M, int C, const void* x, int64_t ldx, const void* w, float eps, void* y, int64_t ldy,
                     vv_stream st);
 

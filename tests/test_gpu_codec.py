@@ -72,3 +72,38 @@ def test_codec_stream_real_shapes():
             eng.codec_reset(torch.tensor([0], dtype=torch.int32, device=dev))
             st_a.zero(torch.tensor([0]))
             st_s.zero(torch.tensor([0]))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_mix_fusion_bit_exact(n):
+    """The codec Block1D mixer folded into fc1's prologue (XF_MIX, rows <= 16)
+    must give the separate k_mix + fc1 path's bits, state included: three
+    streamed frames per mode, then audio / semantic features / embeddings and
+    the next frame compared exactly.  n = 3 exceeds the fused form's LDS and
+    runs unfused in both modes (the control)."""
+    from vibevoice_amd import _lib
+    cfg = tiny_config(ratios=(8, 5, 5, 4, 2, 2), depths="3-3-3-3-3-3-8", nf=32)
+    sd = synthetic_state_dict(cfg, seed=3, device="cpu", mode="test", with_acoustic_encoder=False)
+    eng = Engine(cfg, sd, dev, max_batch=3, max_ctx=64)
+    H = cfg.decoder_config.hidden_size
+    g = torch.Generator().manual_seed(7)
+    lats = [torch.randn(n, 64, generator=g).bfloat16().to(dev) for _ in range(4)]
+    slots = torch.arange(n, dtype=torch.int32, device=dev)
+    outs = {}
+    try:
+        for fuse in (0, 1):
+            _lib.lib().vv_codec_mix_fusion(fuse)
+            eng.codec_reset(slots)
+            res = []
+            for lat in lats:
+                audio = torch.empty(n, cfg.hop, dtype=torch.bfloat16, device=dev)
+                sem = torch.empty(n, 128, dtype=torch.bfloat16, device=dev)
+                emb = torch.zeros(n, H, dtype=torch.bfloat16, device=dev)
+                eng.codec_step(slots, lat, audio, sem, emb, slots)
+                res += [audio, sem, emb]
+            torch.cuda.synchronize()
+            outs[fuse] = res
+    finally:
+        _lib.lib().vv_codec_mix_fusion(1)
+    for i, (a, b) in enumerate(zip(outs[0], outs[1])):
+        assert torch.equal(a, b), (n, i, (a.float() - b.float()).abs().max().item())

@@ -1,0 +1,16 @@
+"""A/B a library switch on one box: python tools/ab_bench.py <switch> <value> [bench args]
+(switch: codec_mix_fusion).  Runs bench.py's main with the switch set first."""
+import os
+import sys
+
+import torch  # noqa: F401  (torch first: the library binds to its HIP runtime)
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vibevoice_amd import _lib  # noqa: E402
+
+name, val = sys.argv[1], int(sys.argv[2])
+getattr(_lib.lib(), "vv_" + name)(val)
+sys.argv = ["bench.py"] + sys.argv[3:]
+import bench  # noqa: E402
+
+bench.main()

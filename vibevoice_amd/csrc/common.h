@@ -73,6 +73,7 @@ enum {
   XF_NONE = 0,
   XF_NORM = 1,       // a = RMSNorm(row)[*w][modulate(shift, scale)]   (row = whole K)
   XF_SILU_ADD = 2,   // a = bf16(silu(bf16(row + vec)))
+  XF_MIX = 3,        // a = ffn_norm(x + gamma * dwconv(norm(x)))  (codec Block1D, M <= 16)
 };
 
 struct EpiArgs {

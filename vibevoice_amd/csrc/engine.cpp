@@ -363,6 +363,14 @@ static RowMap buf_in_rows(const ConvBuf& b, int T, const int* slots) {
   return rowmap(b.base + (long long)b.ctx * b.C, b.C, T, b.sB, slots);
 }
 
+// Codec Block1D front half folded into fc1's prologue where it fits (XF_MIX);
+// off only for the bit-exactness test against the k_mix path.
+static bool g_mix_fusion = true;
+extern "C" int vv_codec_mix_fusion(int on) {
+  g_mix_fusion = on != 0;
+  return 0;
+}
+
 // One block stack + transitions.  n active samples (slots[n]); input rows already
 // in `stem` (rows [ctx, ctx+T0)).  Decoder: writes audio to out (+ out2).
 // Encoder: writes [n, out_ch] features to out.
@@ -413,6 +421,26 @@ static int convnet_run(vv_ctx* c, ConvNet& net, int n, const int* slots, RowMap 
     for (int j = 0; j < net.depth[i]; ++j) {
       const std::string b = p + ".s" + std::to_string(i) + ".b" + std::to_string(j);
       const ConvBuf& mb = net.mix[i][j];
+      RowMap Y = rowmap(net.Y[i], C, T, (long long)T * C);
+      RowMap Fm = rowmap(net.F, 4LL * C);
+      if (g_mix_fusion && gemv_mix_lds(n * T, T, C)) {
+        // few rows (T = 1, 8 stages at small batch): the mix runs in fc1's prologue
+        GemmArgs g = gemm_args(c, n * T, 4 * C, C, X, W(c, b + ".fc1_w"), EPI_GELU, Fm, W(c, b + ".fc1_b"));
+        g.xf.kind = XF_MIX;
+        g.xf.eps = eps;
+        g.xf.w = W(c, b + ".norm");
+        g.xf.T = T;
+        g.xf.ctx = mb.ctx;
+        g.xf.buf = mb.base;
+        g.xf.buf_sB = mb.sB;
+        g.xf.slots = slots;
+        g.xf.dw_w = W(c, b + ".dw_w");
+        g.xf.dw_b = W(c, b + ".dw_b");
+        g.xf.gamma = W(c, b + ".gamma");
+        g.xf.ffn_w = W(c, b + ".ffn_norm");
+        g.xf.y = net.Y[i];
+        CHK(gemm(c, g, st));
+      } else {
       // mixer norm + depthwise conv + gamma residual (X -> Y) + ffn_norm (-> A), one launch
       MixArgs mx;
       mx.n = n;
@@ -433,10 +461,9 @@ static int convnet_run(vv_ctx* c, ConvNet& net, int n, const int* slots, RowMap 
       mx.gamma = W(c, b + ".gamma");
       mx.ffn_norm_w = W(c, b + ".ffn_norm");
       KCHK(launch_mix(mx, st));
-      RowMap Y = rowmap(net.Y[i], C, T, (long long)T * C);
-      RowMap Fm = rowmap(net.F, 4LL * C);
       CHK(gemm(c, gemm_args(c, n * T, 4 * C, C, rowmap(net.A, C), W(c, b + ".fc1_w"), EPI_GELU, Fm,
                             W(c, b + ".fc1_b")), st));
+      }
       RowMap o = X;
       const bool last = j == net.depth[i] - 1;
       if (last) {

@@ -35,6 +35,16 @@
 //            tile, 4 waves of 32 x BN/2, operands straight from L2.
 #include "kernels.h"
 
+// Diagnostic timestamps (tools/gemv_stamps.py): 100 MHz real-time clock, one
+// lane per workgroup, to a buffer nothing else reads (a.stamps == nullptr in
+// every product call).
+DEV void stamp(const GemmArgs& a, int which) {
+  if (a.stamps && threadIdx.x == 0) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    a.stamps[((long long)blockIdx.y * gridDim.x + blockIdx.x) * 4 + which] = t;
+  }
+}
+
 DEV f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -309,6 +319,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   __shared__ float inv_s[16];
   __shared__ float red[8 * 256];
   __shared__ unsigned last_flag;
+  stamp(a, 0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, NW = blockDim.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int n0 = blockIdx.x * 16;
@@ -334,7 +345,136 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   bf16x8 wa[U], wb[U];
   constexpr int Q = 4;                   // A items per thread on the fast path
   const bool fast = a.M * n8 <= Q * (int)blockDim.x;
-  if (fast) {
+  if (XF == XF_MIX) {
+    // Codec Block1D front half for the M = ns * T rows (k_mix's math and
+    // summation order, elementwise.hip): every workgroup recomputes it (a few
+    // tens of KB of L2 reads next to its weight slice); workgroup 0 also stores
+    // the conv-buffer rows and y.  One dependent global round trip: operands,
+    // x rows and history rows are issued together ahead of the weight stream
+    // (the slot ids come through the scalar cache), the raw x rows stay in LDS
+    // (xs) and are overwritten by y, then by fc1's normalised input.
+    const int C = a.K, T = a.xf.T, ctx = a.xf.ctx, ns = a.M / T, NT = blockDim.x;
+    bf16* nrm = (bf16*)part;                                 // [ns][ctx + T][C] conv input rows
+    float* ssp = (float*)(nrm + (size_t)ns * (ctx + T) * C); // [M][n8] partial sums of squares
+    const bool writer = blockIdx.x == 0;
+    const int c2 = threadIdx.x % n8;                         // fixed: NT % n8 == 0
+    bf16x8 wk[7], bb, gv, wf, wn;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) wk[k] = *(const bf16x8*)(a.xf.dw_w + (size_t)c2 * 56 + k * 8);
+    bb = *(const bf16x8*)(a.xf.dw_b + c2 * 8);
+    gv = *(const bf16x8*)(a.xf.gamma + c2 * 8);
+    wf = *(const bf16x8*)(a.xf.ffn_w + c2 * 8);
+    wn = *(const bf16x8*)(a.xf.w + c2 * 8);
+    long long sbase[4];                                      // ns <= 4 (host check)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sbase[q] = q < ns ? (long long)a.xf.slots[q] * a.xf.buf_sB : 0;
+    // items [0, M*n8): x row m; [M*n8, (M + ns*ctx)*n8): history row h of sample s
+    const int nx = a.M * n8, nitem = (a.M + ns * ctx) * n8;
+    for (int e0 = threadIdx.x, first = 1; e0 < nitem; e0 += 8 * NT, first = 0) {
+      bf16x8 v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int e = e0 + q * NT;
+        if (e < nx) {
+          v[q] = *(const bf16x8*)(rm_bf(a.a, e / n8) + c2 * 8);
+        } else if (e < nitem) {
+          const int hr = (e - nx) / n8, s_ = hr / ctx;
+          long long sb = sbase[0];
+#pragma unroll
+          for (int q2 = 1; q2 < 4; ++q2) sb = s_ == q2 ? sbase[q2] : sb;
+          v[q] = *(const bf16x8*)(a.xf.buf + sb + (long long)(hr - s_ * ctx) * C + c2 * 8);
+        }
+      }
+      if (first) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) wa[u] = *(const bf16x8*)(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int e = e0 + q * NT;
+        if (e < nx) {
+          const int m = e / n8;
+          *(bf16x8*)(xs + m * lds_ld + c2 * 8) = v[q];
+          float ss = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss += bf(v[q][j]) * bf(v[q][j]);
+          ssp[e] = ss;
+        } else if (e < nitem) {
+          const int hr = (e - nx) / n8, s_ = hr / ctx;
+          *(bf16x8*)(nrm + ((size_t)s_ * (ctx + T) + (hr - s_ * ctx)) * C + c2 * 8) = v[q];
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    for (int m = wave; m < a.M; m += NW) {                   // k_mix's row-sum order (64 lanes)
+      float ss = 0.f;
+      for (int c = lane; c < n8; c += 64) ss += ssp[m * n8 + c];
+      ss = wave_sum(ss);
+      if (lane == 0) inv_s[m] = rsqrtf(ss / (float)C + a.xf.eps);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // mixer norm of the new rows -> conv input rows; workgroup 0 appends them to the buffer
+    for (int e = threadIdx.x; e < nx; e += NT) {
+      const int m = e / n8, s_ = m / T, t = m - s_ * T;
+      const bf16x8 v = *(const bf16x8*)(xs + m * lds_ld + c2 * 8);
+      const float rr = inv_s[m];
+      bf16x8 o8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o8[j] = tobf(rb(rb(bf(v[j]) * rr) * bf(wn[j])));
+      *(bf16x8*)(nrm + ((size_t)s_ * (ctx + T) + ctx + t) * C + c2 * 8) = o8;
+      if (writer) {
+        long long sb = sbase[0];
+#pragma unroll
+        for (int q2 = 1; q2 < 4; ++q2) sb = s_ == q2 ? sbase[q2] : sb;
+        *(bf16x8*)(a.xf.buf + sb + (long long)(ctx + t) * C + c2 * 8) = o8;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // depthwise conv + gamma residual: y over the raw x in xs (workgroup 0 stores y)
+    for (int e = threadIdx.x; e < nx; e += NT) {
+      const int m = e / n8, s_ = m / T, t = m - s_ * T;
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        const bf16x8 v = *(const bf16x8*)(nrm + ((size_t)s_ * (ctx + T) + t + k) * C + c2 * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int f = j * 7 + k;
+          acc[j] += bf(wk[f >> 3][f & 7]) * bf(v[j]);
+        }
+      }
+      bf16x8* px = (bf16x8*)(xs + m * lds_ld + c2 * 8);
+      const bf16x8 xv = *px;
+      bf16x8 y8;
+      float ss = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        y8[j] = tobf(bf(xv[j]) + rb(rb(acc[j] + bf(bb[j])) * bf(gv[j])));
+        ss += bf(y8[j]) * bf(y8[j]);
+      }
+      if (writer) *(bf16x8*)(a.xf.y + (long long)m * C + c2 * 8) = y8;
+      *px = y8;
+      ssp[e] = ss;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    for (int m = wave; m < a.M; m += NW) {
+      float ss = 0.f;
+      for (int c = lane; c < n8; c += 64) ss += ssp[m * n8 + c];
+      ss = wave_sum(ss);
+      if (lane == 0) inv_s[m] = rsqrtf(ss / (float)C + a.xf.eps);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    for (int e = threadIdx.x; e < nx; e += NT) {             // FFN pre-norm, in place
+      const int m = e / n8;
+      bf16x8* px = (bf16x8*)(xs + m * lds_ld + c2 * 8);
+      const bf16x8 y8 = *px;
+      const float rr = inv_s[m];
+      bf16x8 o8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o8[j] = tobf(rb(rb(bf(y8[j]) * rr) * bf(wf[j])));
+      *px = o8;
+    }
+  } else if (fast) {
     bf16x8 xv[Q], wv[Q], sh[Q], sc[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
@@ -453,6 +593,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  stamp(a, 1);
 
   f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
   const bool xok = r < a.M;
@@ -476,6 +617,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     load(wa, c + 2 * U);
     compute(wb, c + U);
   }
+  stamp(a, 2);
 
   // ---- reduce the waves of this workgroup
 #pragma unroll
@@ -495,6 +637,10 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = red[i * 64 + lane];
     epi_tile(a, r, n0, lane, v);
+    if (a.stamps) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      stamp(a, 3);
+    }
   }
 }
 
@@ -656,6 +802,13 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
 
 // ------------------------------------------------------------------ host launch
 static int g_tune_nw = 0, g_tune_ks = 0, g_tune_handoff = -1, g_tune_waves = 0, g_tune_u = 0;
+static unsigned long long* g_stamps = nullptr;
+
+// diagnostic: GEMV launches record per-workgroup timestamps into buf (nullptr: off)
+extern "C" int vv_gemv_stamps(void* buf) {
+  g_stamps = (unsigned long long*)buf;
+  return 0;
+}
 
 extern "C" int vv_gemv_tune(int nw, int ks, int handoff, int target_waves, int u) {
   g_tune_nw = nw;
@@ -738,6 +891,17 @@ static int launch_gemm_xf(const GemmArgs& a, hipStream_t st) {
   return 0;
 }
 
+// LDS of the XF_MIX GEMV (A rows + history/new rows + partial sums), 0 when
+// the fused form does not apply (rows > 16, rows not whole samples, C outside
+// [512, 2048] — k_mix's summation order needs >= 64 chunks — or > 64 KB)
+size_t gemv_mix_lds(int M, int T, int C) {
+  if (M <= 0 || M > 16 || T <= 0 || M % T || M / T > 4 || C < 512 || C > 2048 || C % 256) return 0;
+  const int rows = (M / T) * (6 + T), n8 = C / 8;
+  const size_t xs = ((size_t)M * (C + 8) * 2 + 15) & ~(size_t)15;
+  const size_t lds = xs + (size_t)rows * C * 2 + (size_t)M * n8 * 4;
+  return lds <= 98304 ? lds : 0;
+}
+
 // returns 0 ok, else an error code (see engine.cpp)
 int launch_gemm(GemmArgs a, hipStream_t st) {
   if (a.M <= 0) return 0;
@@ -745,6 +909,7 @@ int launch_gemm(GemmArgs a, hipStream_t st) {
   if (a.xf.kind == XF_NORM && a.K % 8 != 0) return 1;
   if (a.epi.kind == EPI_ROPE && (a.rope.kv.d != 128 || !a.rope.pos || !a.rope.slots)) return 1;
   if (a.epi.kind == EPI_CFG_DPM && (a.M > 16 || 2 * a.dpm.n != a.M)) return 1;
+  a.stamps = g_stamps;
   if (a.M <= 64) {
     const int mrep = (a.M + 15) / 16;
     GemmPlan p = gemv_plan(a.N, a.K, a.M);
@@ -753,6 +918,19 @@ int launch_gemm(GemmArgs a, hipStream_t st) {
     if (a.ksplit > 1 && (!a.ws || !a.counters || a.N / 16 > 65536)) a.ksplit = 1;
     a.handoff = g_tune_handoff >= 0 ? g_tune_handoff : 1;
     dim3 grid(a.N / 16, a.ksplit), block(64 * p.nw);
+    if (a.xf.kind == XF_MIX) {
+      const size_t lds = gemv_mix_lds(a.M, a.xf.T, a.K);
+      if (mrep != 1 || a.ksplit != 1 || !lds || (64 * p.nw) % (a.K / 8) || a.xf.ctx != 6) return 1;
+      static bool attr = false;   // > 64 KB of dynamic LDS needs the opt-in (one workgroup may hold 160 KiB)
+      if (!attr) {
+        if (hipFuncSetAttribute((const void*)k_gemv1<4, XF_MIX>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                98304) != hipSuccess)
+          return 2;
+        attr = true;
+      }
+      hipLaunchKernelGGL((k_gemv1<4, XF_MIX>), grid, block, lds, st, a);
+      return hipGetLastError() == hipSuccess ? 0 : 2;
+    }
     switch (a.xf.kind) {
       case XF_NORM: launch_gemv_xf<XF_NORM>(a, mrep, grid, block, st); break;
       case XF_SILU_ADD: launch_gemv_xf<XF_SILU_ADD>(a, mrep, grid, block, st); break;

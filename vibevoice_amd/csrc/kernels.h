@@ -29,6 +29,14 @@ struct ATransform {
   long long mod_ld;
   int shift_off, scale_off;
   const bf16* vec;      // XF_SILU_ADD
+  // XF_MIX: the codec Block1D front half of k_mix computed in the GEMV prologue
+  // (A rows = the x rows of M/T samples x T steps; w = mixer norm weight)
+  int T, ctx;
+  bf16* buf;             // conv history buffer (slot stride buf_sB), rows ctx + t written
+  long long buf_sB;
+  const int* slots;
+  const bf16 *dw_w, *dw_b, *gamma, *ffn_w;
+  bf16* y;               // residual rows y (fc2's residual), [M][K]
 };
 
 struct RopeEpi {         // EPI_ROPE
@@ -61,6 +69,7 @@ struct GemmArgs {
   DpmEpi dpm;
   float* ws;
   unsigned* counters;
+  unsigned long long* stamps;  // diagnostic builds only: 4 s_memrealtime stamps per workgroup
 };
 
 struct NormArgs {
@@ -146,6 +155,7 @@ struct SumRows {
   bf16* p[8];
 };
 
+size_t gemv_mix_lds(int M, int T, int C);
 int launch_gemm(GemmArgs a, hipStream_t st);
 int launch_sum_rows(SumRows s, long long count, hipStream_t st);
 int launch_rmsnorm(NormArgs a, hipStream_t st);
