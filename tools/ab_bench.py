@@ -1,5 +1,6 @@
 """A/B a library switch on one box: python tools/ab_bench.py <switch> <value> [bench args]
-(switch: codec_mix_fusion).  Runs bench.py's main with the switch set first."""
+(switch: codec_mix_fusion; or "lib" <path> to load another build of the
+library, e.g. a -DVV_W_NT=0 variant).  Runs bench.py's main with it set first."""
 import os
 import sys
 
@@ -8,8 +9,12 @@ import torch  # noqa: F401  (torch first: the library binds to its HIP runtime)
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vibevoice_amd import _lib  # noqa: E402
 
-name, val = sys.argv[1], int(sys.argv[2])
-getattr(_lib.lib(), "vv_" + name)(val)
+name, val = sys.argv[1], sys.argv[2]
+if name == "lib":
+    _lib.LIB_PATH = os.path.abspath(val)
+    _lib.lib()
+else:
+    getattr(_lib.lib(), "vv_" + name)(int(val))
 sys.argv = ["bench.py"] + sys.argv[3:]
 import bench  # noqa: E402
 

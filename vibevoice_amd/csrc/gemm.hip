@@ -33,6 +33,9 @@
 //            release / ticket / acquire, Guideline 16) only for few-tile shapes.
 //   k_gemm : M > 64 (codec stages at T >= 8, LM prefill).  64 x BN workgroup
 //            tile, 4 waves of 32 x BN/2, operands straight from L2.
+#include <cstdio>
+#include <cstdlib>
+
 #include "kernels.h"
 
 // Diagnostic timestamps (tools/gemv_stamps.py): 100 MHz real-time clock, one
@@ -43,6 +46,20 @@ DEV void stamp(const GemmArgs& a, int which) {
     const unsigned long long t = __builtin_amdgcn_s_memrealtime();
     a.stamps[((long long)blockIdx.y * gridDim.x + blockIdx.x) * 4 + which] = t;
   }
+}
+
+// Weight-stream load.  Decode weights are read once per step (GBs against a
+// 256 MB Infinity Cache), so they go out non-temporal (MI355X_MICROARCH.md
+// "nt-weights"); VV_W_NT=0 builds the default-policy variant for A/B runs.
+#ifndef VV_W_NT
+#define VV_W_NT 1
+#endif
+DEV bf16x8 ldw(const bf16* p) {
+#if VV_W_NT
+  return __builtin_nontemporal_load((const bf16x8*)p);
+#else
+  return *(const bf16x8*)p;
+#endif
 }
 
 DEV f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
@@ -387,7 +404,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
       }
       if (first) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) wa[u] = *(const bf16x8*)(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
+        for (int u = 0; u < U; ++u) wa[u] = ldw(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
       }
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -495,7 +512,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
       }
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) wa[u] = *(const bf16x8*)(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
+    for (int u = 0; u < U; ++u) wa[u] = ldw(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
     if (XF == XF_NORM) {
       // per-item sums of squares -> LDS, rows reduced in a fixed order
 #pragma unroll
@@ -546,7 +563,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   } else {
     // many rows (B >= 8 batches): weights first, then the A rows in batches
 #pragma unroll
-    for (int u = 0; u < U; ++u) wa[u] = *(const bf16x8*)(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
+    for (int u = 0; u < U; ++u) wa[u] = ldw(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
     for (int e0 = threadIdx.x; e0 < a.M * n8; e0 += 4 * blockDim.x) {
       bf16x8 xv[4];
 #pragma unroll
@@ -609,7 +626,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   };
   auto load = [&](bf16x8 (&wf)[U], int c) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) wf[u] = *(const bf16x8*)(wrow + min(c + u, max(c1 - 1, 0)) * 512);
+    for (int u = 0; u < U; ++u) wf[u] = ldw(wrow + min(c + u, max(c1 - 1, 0)) * 512);
   };
   for (int c = c0; c < c1; c += 2 * U) {
     load(wb, c + U);
@@ -663,7 +680,7 @@ __global__ void __launch_bounds__(512) k_gemv(GemmArgs a) {
   const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
   bf16x8 wa[U], wb[U];
 #pragma unroll
-  for (int u = 0; u < U; ++u) wa[u] = *(const bf16x8*)(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
+  for (int u = 0; u < U; ++u) wa[u] = ldw(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
   if (XF == XF_NORM) {
     row_inv(a, 0, 16 * MREP, inv_s, wave, NW, lane);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -697,7 +714,7 @@ __global__ void __launch_bounds__(512) k_gemv(GemmArgs a) {
   };
   auto load = [&](bf16x8 (&wf)[U], int c) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) wf[u] = *(const bf16x8*)(wrow + min(c + u, max(c1 - 1, 0)) * 512);
+    for (int u = 0; u < U; ++u) wf[u] = ldw(wrow + min(c + u, max(c1 - 1, 0)) * 512);
   };
   for (int c = c0; c < c1; c += 2 * U) {
     load(wb, c + U);
@@ -769,7 +786,7 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
     for (int u = 0; u < 2; ++u) {
       const int cc = min(c + u, nk - 1);
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) wf[u][nt] = *(const bf16x8*)(wrow[nt] + cc * 512);
+      for (int nt = 0; nt < NT; ++nt) wf[u][nt] = *(const bf16x8*)(wrow[nt] + cc * 512);   // re-read across row tiles: default policy
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) xf[u][mt] = xok[mt] ? *(const bf16x8*)(xrow[mt] + cc * 32) : zero8;
     }
@@ -803,6 +820,7 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
 // ------------------------------------------------------------------ host launch
 static int g_tune_nw = 0, g_tune_ks = 0, g_tune_handoff = -1, g_tune_waves = 0, g_tune_u = 0;
 static unsigned long long* g_stamps = nullptr;
+static const bool g_shape_log = getenv("VV_GEMM_LOG") != nullptr;
 
 // diagnostic: GEMV launches record per-workgroup timestamps into buf (nullptr: off)
 extern "C" int vv_gemv_stamps(void* buf) {
@@ -910,6 +928,9 @@ int launch_gemm(GemmArgs a, hipStream_t st) {
   if (a.epi.kind == EPI_ROPE && (a.rope.kv.d != 128 || !a.rope.pos || !a.rope.slots)) return 1;
   if (a.epi.kind == EPI_CFG_DPM && (a.M > 16 || 2 * a.dpm.n != a.M)) return 1;
   a.stamps = g_stamps;
+  if (g_shape_log) {   // VV_GEMM_LOG=1: one line per launch (shape census for profiles/)
+    fprintf(stderr, "vv_gemm M=%d N=%d K=%d xf=%d epi=%d\n", a.M, a.N, a.K, a.xf.kind, a.epi.kind);
+  }
   if (a.M <= 64) {
     const int mrep = (a.M + 15) / 16;
     GemmPlan p = gemv_plan(a.N, a.K, a.M);
