@@ -665,7 +665,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
 // chunk; weights ping-ponged as in k_gemv1.
 template <int MREP, int U, int XF>
 __global__ void __launch_bounds__(512) k_gemv(GemmArgs a) {
-  __shared__ float red[(MREP == 1 ? 8 : 4) * MREP * 256];
+  __shared__ float red[8 * MREP * 256];
   __shared__ float inv_s[64];
   __shared__ unsigned last_flag;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, NW = blockDim.x >> 6;
@@ -678,9 +678,6 @@ __global__ void __launch_bounds__(512) k_gemv(GemmArgs a) {
   const int c1 = b0 + (int)((long long)(b1 - b0) * (wave + 1) / NW);
   const bf16* wrow = a.w + (long long)(n0 >> 4) * a.K * 16 + lane * 8;  // MFMA-packed W
   const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-  bf16x8 wa[U], wb[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) wa[u] = ldw(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
   if (XF == XF_NORM) {
     row_inv(a, 0, 16 * MREP, inv_s, wave, NW, lane);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -698,7 +695,19 @@ __global__ void __launch_bounds__(512) k_gemv(GemmArgs a) {
   f32x4 acc[MREP];
 #pragma unroll
   for (int mr = 0; mr < MREP; ++mr) acc[mr] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  auto compute = [&](bf16x8 (&wf)[U], int c) {
+  // each chunk's A fragments travel with its weight chunk (vmcnt waits are in
+  // issue order: loading A inside compute would wait for the next batch too)
+  bf16x8 wa[U], wb[U], xa[U][MREP], xb[U][MREP];
+  auto load = [&](bf16x8 (&wf)[U], bf16x8 (&xf)[U][MREP], int c) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int cc = min(c + u, max(c1 - 1, 0));
+#pragma unroll
+      for (int mr = 0; mr < MREP; ++mr) xf[u][mr] = xok[mr] ? *(const bf16x8*)(xrow[mr] + cc * 32) : zero8;
+      wf[u] = ldw(wrow + cc * 512);
+    }
+  };
+  auto compute = [&](bf16x8 (&wf)[U], bf16x8 (&xf)[U][MREP], int c) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const bool ok = c + u < c1;
@@ -706,21 +715,18 @@ __global__ void __launch_bounds__(512) k_gemv(GemmArgs a) {
       const bf16x8 w = ok ? wf[u] : zero8;
 #pragma unroll
       for (int mr = 0; mr < MREP; ++mr) {
-        bf16x8 x = (xok[mr] && ok) ? *(const bf16x8*)(xrow[mr] + cc * 32) : zero8;
+        bf16x8 x = (xok[mr] && ok) ? xf[u][mr] : zero8;
         if (XF != XF_NONE && xok[mr] && ok) x = xform<XF>(a, x, r + 16 * mr, cc * 32 + 8 * g, inv[mr]);
         acc[mr] = mfma(w, x, acc[mr]);
       }
     }
   };
-  auto load = [&](bf16x8 (&wf)[U], int c) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) wf[u] = ldw(wrow + min(c + u, max(c1 - 1, 0)) * 512);
-  };
+  load(wa, xa, c0);
   for (int c = c0; c < c1; c += 2 * U) {
-    load(wb, c + U);
-    compute(wa, c);
-    load(wa, c + 2 * U);
-    compute(wb, c + U);
+    load(wb, xb, c + U);
+    compute(wa, xa, c);
+    load(wa, xa, c + 2 * U);
+    compute(wb, xb, c + U);
   }
   const int TILE = MREP * 256;
 #pragma unroll
@@ -862,7 +868,7 @@ static GemmPlan gemv_plan(int N, int K, int M) {
   return {nw, ks};
 }
 
-static int max_waves(int mrep) { return mrep == 1 ? 8 : 4; }
+static int max_waves(int) { return 8; }
 
 // k_gemv1 stages the A slice in LDS (<= 64 KB)
 static bool gemv1_fits(const GemmArgs& a) {
