@@ -110,12 +110,22 @@ def main():
         if not quick:
             configs += [(nw, 1, 1, 0, u) for nw, u in itertools.product((1, 2, 4, 8), (2, 4, 8))]
         best = None
+        # two passes, min per config: the first launches of a shape run on a cold clock
+        times = {}
+        for _ in range(2):
+            for cf in configs:
+                L.vv_gemv_tune(*cf)
+                try:
+                    t = measure()
+                except RuntimeError:
+                    continue
+                times[cf] = min(times.get(cf, 1e9), t)
         for nw, ks, h, tw, u in configs:
             L.vv_gemv_tune(nw, ks, h, tw, u)
             try:
                 err = check()
-                us = measure()
-            except RuntimeError as e:
+                us = times[(nw, ks, h, tw, u)]
+            except (RuntimeError, KeyError) as e:
                 print(name, (nw, ks, h, tw), "error", e)
                 continue
             gbs = (N * K * 2 + M * K * 2 + M * outN * 2) / us / 1e3

@@ -843,18 +843,34 @@ extern "C" int vv_gemv_tune(int nw, int ks, int handoff, int target_waves, int u
   return 0;
 }
 
-struct GemmPlan { int nw, ksplit; };
+struct GemmPlan { int nw, ksplit, u; };
 
-// Measured on MI355X (tools/gemv_sweep.py, profiles/r01_gemv_sweep*.txt): NO
-// cross-workgroup split-K (a hand-off costs >= 2 us in the sc1 form, up to 30 us
-// with fences — more than the extra CUs bring), 4 waves per workgroup, 8 for
-// few-tile long-row shapes and for M >= 8, 4 weight chunks in flight per wave.
+// Measured on MI355X (tools/gemv_sweep.py two-pass min, profiles/r01_gemv_sweep*.txt).
+// NO cross-workgroup split-K (a hand-off costs >= 2 us in the sc1 form, up to
+// 30 us with fences — more than the extra CUs bring).  Waves per workgroup (nw)
+// and weight chunks in flight per wave (u):
+//   * >= 1024 tiles (LM gate|up, head adaLN): 2 waves — every workgroup resident
+//     in the first round (4-wave groups left a second-round tail: 16.7 -> 14.0 us)
+//   * few tiles, long rows (LM / head down): 8 waves x 4; at M >= 8, 2 waves
+//     (B = 8 LM down 22.5 -> 18.6 us); 128 tiles x K >= 8192 (codec fc2): 4 x 8
+//   * few tiles, short rows (qkv, o_proj): 4 x 8, all chunks in flight at once
+//   * M >= 8 otherwise: 8 x 2
 static GemmPlan gemv_plan(int N, int K, int M) {
   const int chunks = K / 32, tiles = N / 16;
-  // few tiles with long rows (LM / head down, codec fc2), or many rows: 8 waves
-  int nw = ((tiles <= 128 && chunks >= 128) || M >= 8) ? 8 : 4, ks = 1;
+  int nw = 4, ks = 1, u = 4;
+  if (tiles <= 128 && chunks >= 128) {
+    if (M >= 8) nw = 2;
+    else if (tiles == 128 && chunks >= 256) u = 8;
+    else nw = 8;
+  } else if (M >= 8) {
+    nw = 8;
+    u = 2;
+  } else if (tiles >= 1024) {
+    nw = 2;
+  } else if (tiles <= 128) {
+    u = 8;
+  }
   if (g_tune_waves > 0) {
-    const int tiles = N / 16;
     int wpt = (g_tune_waves + tiles - 1) / tiles;
     const int maxw = (chunks + 3) / 4;
     if (wpt > maxw) wpt = maxw;
@@ -864,8 +880,9 @@ static GemmPlan gemv_plan(int N, int K, int M) {
   }
   if (g_tune_nw > 0) nw = g_tune_nw;
   if (g_tune_ks > 0) ks = g_tune_ks;
+  if (g_tune_u > 0) u = g_tune_u;
   if (ks > chunks) ks = chunks;
-  return {nw, ks};
+  return {nw, ks, u};
 }
 
 static int max_waves(int) { return 8; }
@@ -878,7 +895,7 @@ static bool gemv1_fits(const GemmArgs& a) {
 }
 
 template <int XF>
-static void launch_gemv_xf(const GemmArgs& a, int mrep, dim3 grid, dim3 block, hipStream_t st) {
+static void launch_gemv_xf(const GemmArgs& a, int mrep, int u, dim3 grid, dim3 block, hipStream_t st) {
   if (mrep == 1 && !gemv1_fits(a)) {
     hipLaunchKernelGGL((k_gemv<1, 8, XF>), grid, block, 0, st, a);
     return;
@@ -888,7 +905,6 @@ static void launch_gemv_xf(const GemmArgs& a, int mrep, dim3 grid, dim3 block, h
     const int kw = ((nchunk + a.ksplit - 1) / a.ksplit) * 32;
     const size_t xs_bytes = ((size_t)a.M * (kw + 8) * sizeof(bf16) + 15) & ~(size_t)15;
     const size_t lds = xs_bytes + (size_t)a.M * (kw / 8) * sizeof(float);
-    const int u = g_tune_u > 0 ? g_tune_u : 4;   // 4 x 1 KB in flight per wave (tools/gemv_sweep.py)
     if (u == 4) hipLaunchKernelGGL((k_gemv1<4, XF>), grid, block, lds, st, a);
     else if (u == 2) hipLaunchKernelGGL((k_gemv1<2, XF>), grid, block, lds, st, a);
     else hipLaunchKernelGGL((k_gemv1<8, XF>), grid, block, lds, st, a);
@@ -959,9 +975,9 @@ int launch_gemm(GemmArgs a, hipStream_t st) {
       return hipGetLastError() == hipSuccess ? 0 : 2;
     }
     switch (a.xf.kind) {
-      case XF_NORM: launch_gemv_xf<XF_NORM>(a, mrep, grid, block, st); break;
-      case XF_SILU_ADD: launch_gemv_xf<XF_SILU_ADD>(a, mrep, grid, block, st); break;
-      default: launch_gemv_xf<XF_NONE>(a, mrep, grid, block, st); break;
+      case XF_NORM: launch_gemv_xf<XF_NORM>(a, mrep, p.u, grid, block, st); break;
+      case XF_SILU_ADD: launch_gemv_xf<XF_SILU_ADD>(a, mrep, p.u, grid, block, st); break;
+      default: launch_gemv_xf<XF_NONE>(a, mrep, p.u, grid, block, st); break;
     }
   } else {
     if (a.epi.kind == EPI_CFG_DPM) return 1;
