@@ -164,10 +164,12 @@ int vv_gemv_tune(int nw, int ks, int handoff, int target_waves, int u);
  * stamps per workgroup (start, A staged, weights streamed, epilogue stored) to
  * buf (uint64[grid * 4]); NULL turns it off. */
 int vv_gemv_stamps(void* buf);
-/* Test switch: 1 (default) folds each codec Block1D's mixer (norm, depthwise
- * conv, gamma residual, FFN norm) into its fc1 GEMV when <= 16 rows fit; 0
- * runs the separate k_mix launch everywhere.  Results are bit-identical. */
-int vv_codec_mix_fusion(int on);
+/* Test switch (bit mask, default 3): bit 0 folds each codec Block1D's mixer
+ * (norm, depthwise conv, gamma residual, FFN norm) into its fc1 GEMV where
+ * <= 16 rows fit (XF_MIX); bit 1 runs whole narrow-stage blocks (C <= 128) as
+ * one k_block launch.  0 = separate k_mix + GEMM launches everywhere.  Every
+ * mask gives the same bits. */
+int vv_codec_mix_fusion(int mask);
 int vv_rmsnorm_bf16(int M, int C, const void* x, int64_t ldx, const void* w, float eps, void* y, int64_t ldy,
                     vv_stream st);
 

@@ -74,13 +74,14 @@ def test_codec_stream_real_shapes():
             st_s.zero(torch.tensor([0]))
 
 
-@pytest.mark.parametrize("n", [1, 2, 3])
-def test_mix_fusion_bit_exact(n):
+@pytest.mark.parametrize("n,mask", [(1, 1), (1, 2), (1, 3), (2, 3), (3, 3)])
+def test_mix_fusion_bit_exact(n, mask):
     """The codec Block1D mixer folded into fc1's prologue (XF_MIX, rows <= 16)
     must give the separate k_mix + fc1 path's bits, state included: three
     streamed frames per mode, then audio / semantic features / embeddings and
     the next frame compared exactly.  n = 3 exceeds the fused form's LDS and
-    runs unfused in both modes (the control)."""
+    runs XF_MIX unfused in both modes.  mask: which fusions are on (bit 0
+    XF_MIX, bit 1 k_block)."""
     from vibevoice_amd import _lib
     cfg = tiny_config(ratios=(8, 5, 5, 4, 2, 2), depths="3-3-3-3-3-3-8", nf=32)
     sd = synthetic_state_dict(cfg, seed=3, device="cpu", mode="test", with_acoustic_encoder=False)
@@ -91,7 +92,7 @@ def test_mix_fusion_bit_exact(n):
     slots = torch.arange(n, dtype=torch.int32, device=dev)
     outs = {}
     try:
-        for fuse in (0, 1):
+        for fuse in (0, mask):
             _lib.lib().vv_codec_mix_fusion(fuse)
             eng.codec_reset(slots)
             res = []
@@ -104,6 +105,6 @@ def test_mix_fusion_bit_exact(n):
             torch.cuda.synchronize()
             outs[fuse] = res
     finally:
-        _lib.lib().vv_codec_mix_fusion(1)
-    for i, (a, b) in enumerate(zip(outs[0], outs[1])):
+        _lib.lib().vv_codec_mix_fusion(3)
+    for i, (a, b) in enumerate(zip(outs[0], outs[mask])):
         assert torch.equal(a, b), (n, i, (a.float() - b.float()).abs().max().item())

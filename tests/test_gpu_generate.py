@@ -94,3 +94,42 @@ def test_graph_replay_matches_eager():
         assert torch.equal(o.sequences, outs[0].sequences)
         for b in range(2):
             assert torch.equal(o.speech_outputs[b].cpu(), outs[0].speech_outputs[b].cpu())
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_speculative_diffusion_is_exact(graphs):
+    """The diffusion queued before the token readback (GenerateSession._speculate)
+    changes nothing: sequences and audio equal the non-speculative loop bit for
+    bit, through mispredictions (speech_end / speech_start / eos after a
+    diffusion step: the CPU generator is restored and the right rows redone) and
+    in an unforced greedy run."""
+    cfg = tiny_config(hidden=256, layers=2, heads=2, kv_heads=1, inter=512)
+    sd = synthetic_state_dict(cfg, seed=5, device="cpu", mode="test", with_acoustic_encoder=False)
+    model = VibeVoiceForConditionalGenerationInference(cfg, sd, dev, max_batch=2, max_ctx=128)
+    model.set_ddpm_inference_steps(5)
+    g = torch.Generator().manual_seed(3)
+    ids = torch.randint(0, 151000, (2, 12), generator=g)
+    mask = torch.ones(2, 12, dtype=torch.long)
+    sched = [[D] * 4 + [E, S] + [D] * 3 + [X], [S] + [D] * 2 + [E] + [D] * 5 + [X]]
+    for forced in (sched, None):
+        outs, misses, rng = [], [], []
+        for spec in (False, True):
+            torch.manual_seed(77)
+            kw = dict(forced_tokens=forced) if forced else dict(max_new_tokens=12)
+            sess = model.generate_session(input_ids=ids, attention_mask=mask, tokenizer=TOK, cfg_scale=1.3,
+                                          use_graphs=graphs, speculate=spec, show_progress_bar=False, **kw)
+            while sess.step():
+                pass
+            outs.append(sess.result())
+            misses.append(sess.spec_miss)
+            rng.append(torch.get_rng_state())      # same CPU-generator consumption
+        assert torch.equal(rng[0], rng[1])
+        a, b = outs
+        assert torch.equal(a.sequences, b.sequences)
+        for i in range(2):
+            if a.speech_outputs[i] is None:
+                assert b.speech_outputs[i] is None
+            else:
+                assert torch.equal(a.speech_outputs[i].cpu(), b.speech_outputs[i].cpu())
+        if forced:
+            assert misses[1] > 0      # the mispredict path ran

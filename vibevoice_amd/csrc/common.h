@@ -18,7 +18,21 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 DEV float bf(bf16 x) { return (float)x; }
 DEV bf16 tobf(float x) { return (bf16)x; }
-DEV float rb(float x) { return (float)(bf16)x; }
+// Round to bf16 and back (a rounding point of the reference's bf16 torch ops).
+// The conversion is inline asm so the optimizer cannot see through it: written
+// as (float)(bf16)x, LLVM narrows e.g. y + rb(g * v) into bf16 arithmetic and
+// then contracts it into one FMA, dropping the product's rounding.
+DEV float rb(float x) {
+  unsigned r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, 0" : "=v"(r) : "v"(x));
+  return __uint_as_float(r << 16);
+}
+
+// MFMA 16x16x32 bf16 -> fp32: a = 16 rows x 32 k (lane l: row l & 15, k 8(l >> 4)..+7),
+// b likewise for the 16 columns; d lane l: column l & 15, rows 4(l >> 4) + i
+DEV f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
 
 DEV float silu_f(float x) { return x / (1.0f + __expf(-x)); }
 // GELU, exact erf form (transformers ACT2FN["gelu"]; modular_vibevoice_tokenizer.py:589)

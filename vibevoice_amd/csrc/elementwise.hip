@@ -75,145 +75,6 @@ __global__ void __launch_bounds__(256) k_dwconv(DwArgs a) {
   *(bf16x8*)xp = o;
 }
 
-// ---------------------------------------------------------------- Block1D front half, fused
-// One launch per Block1D for everything between the FFN GEMMs
-// (modular_vibevoice_tokenizer.py:667-684, streaming conv :327-382):
-//   n_t = ConvRMSNorm(x_t)                        -> conv buffer (next steps' history)
-//   y_t = x_t + bf16(bf16(dwconv_k7(n)_t + b) * gamma)
-//   a_t = ConvRMSNorm_ffn(y_t)                    -> fc1's input
-// A workgroup owns rows [t0, t0 + R) of one sample and all C channels; it
-// recomputes the normalised rows of its 6-row halo itself (history rows t < 0
-// come from the buffer), so no other workgroup's output is read: the residual
-// stream ping-pongs x -> y and fc2's epilogue writes the next block's x.
-// Rows are handled by groups of LPR = min(64, C/8) lanes, 8 channels per lane
-// per chunk; row sums reduce with shuffles inside the group.
-__global__ void __launch_bounds__(256) k_mix(MixArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int t0 = blockIdx.x * a.R, smp = blockIdx.y;
-  const int C = a.C, n8 = C >> 3;
-  const int rows = a.R + a.ctx;
-  bf16* nrm = (bf16*)smem;                       // [rows][C] normalised inputs of the conv
-  bf16* ybuf = nrm + (size_t)rows * C;           // [R][C]
-  float* ssp = (float*)(ybuf + (size_t)a.R * C); // [rows][n8] partial sums of squares
-  float* inv = ssp + (size_t)rows * n8;          // [rows] inverse RMS (x rows, then y rows)
-  const bf16* X = a.x + (long long)smp * a.T * C;
-  bf16* buf = a.buf + (long long)a.slots[smp] * a.buf_sB;
-  const int LPR = n8 < 64 ? n8 : 64;
-  const int gi = threadIdx.x / LPR, gl = threadIdx.x - gi * LPR, ng = blockDim.x / LPR;
-  // ---- this thread's conv item (row i, chunk c): the launch sizes R so that
-  // R * n8 == blockDim (one item per thread).  Its per-channel operands go out
-  // first, in one batch with the row loads below (vmcnt waits are in order).
-  const int e2 = threadIdx.x;
-  const int i2 = e2 / n8, c2 = e2 - i2 * n8;
-  const bool own = e2 < a.R * n8 && t0 + i2 < a.T;
-  bf16x8 wk[7], bb, gv, wf;
-  if (own) {
-#pragma unroll
-    for (int k = 0; k < 7; ++k) wk[k] = *(const bf16x8*)(a.dw_w + (size_t)c2 * 56 + k * 8);
-    bb = *(const bf16x8*)(a.dw_b + c2 * 8);
-    gv = *(const bf16x8*)(a.gamma + c2 * 8);
-    wf = *(const bf16x8*)(a.ffn_norm_w + c2 * 8);
-  }
-  // ---- phase 1: rows t0 - ctx .. t0 + R - 1 (history rows t < 0 are already
-  // normalised in the buffer; halo rows t >= 0 are recomputed from x)
-  // 8 items per thread per batch: all loads first, then the LDS stores
-  const bf16x8 z8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-  for (int e0 = threadIdx.x; e0 < rows * n8; e0 += 8 * blockDim.x) {
-    bf16x8 v[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int e = e0 + q * blockDim.x;
-      v[q] = z8;
-      if (e < rows * n8) {
-        const int i = e / n8, c = e - i * n8;
-        const int t = t0 - a.ctx + i;
-        if (t < 0) v[q] = *(const bf16x8*)(buf + (long long)(a.ctx + t) * C + c * 8);
-        else if (t < a.T) v[q] = *(const bf16x8*)(X + (long long)t * C + c * 8);
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int e = e0 + q * blockDim.x;
-      if (e < rows * n8) {
-        const int i = e / n8, c = e - i * n8;
-        const int t = t0 - a.ctx + i;
-        *(bf16x8*)(nrm + i * C + c * 8) = v[q];   // history: normalised; else raw, normalised below
-        float ss = 0.f;
-        if (t >= 0) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) ss += bf(v[q][j]) * bf(v[q][j]);
-        }
-        ssp[e] = ss;
-      }
-    }
-  }
-  __syncthreads();
-  for (int i = gi; i < rows && gi < ng; i += ng) {   // row sums in a fixed order
-    float ss = 0.f;
-    for (int c = gl; c < n8; c += LPR) ss += ssp[i * n8 + c];
-    for (int o = LPR >> 1; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
-    if (gl == 0) inv[i] = rsqrtf(ss / (float)C + a.eps);
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < rows * n8; e += blockDim.x) {
-    const int i = e / n8, c = e - i * n8;
-    const int t = t0 - a.ctx + i;
-    if (t < 0 || t >= a.T) continue;
-    const bf16x8 v = *(const bf16x8*)(nrm + i * C + c * 8);
-    const bf16x8 w = *(const bf16x8*)(a.norm_w + c * 8);
-    const float r = inv[i];
-    bf16x8 o8;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o8[j] = tobf(rb(rb(bf(v[j]) * r) * bf(w[j])));
-    *(bf16x8*)(nrm + i * C + c * 8) = o8;
-    if (i >= a.ctx) *(bf16x8*)(buf + (long long)(a.ctx + t) * C + c * 8) = o8;
-  }
-  __syncthreads();
-  // ---- phase 2: depthwise conv + gamma residual for the thread's item
-  if (own) {
-    const int t = t0 + i2;
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      const bf16x8 v = *(const bf16x8*)(nrm + (i2 + k) * C + c2 * 8);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int f = j * 7 + k;                 // tap k of channel 8 c2 + j
-        acc[j] += bf(wk[f >> 3][f & 7]) * bf(v[j]);
-      }
-    }
-    const bf16x8 xv = *(const bf16x8*)(X + (long long)t * C + c2 * 8);
-    bf16x8 y8;
-    float ss = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      y8[j] = tobf(bf(xv[j]) + rb(rb(acc[j] + bf(bb[j])) * bf(gv[j])));
-      ss += bf(y8[j]) * bf(y8[j]);
-    }
-    *(bf16x8*)(a.y + ((long long)smp * a.T + t) * C + c2 * 8) = y8;
-    *(bf16x8*)(ybuf + i2 * C + c2 * 8) = y8;
-    ssp[e2] = ss;
-  }
-  __syncthreads();
-  for (int i = gi; i < a.R && gi < ng; i += ng) {
-    float ss = 0.f;
-    for (int c = gl; c < n8; c += LPR) ss += ssp[i * n8 + c];
-    for (int o = LPR >> 1; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
-    if (gl == 0) inv[i] = rsqrtf(ss / (float)C + a.eps);
-  }
-  __syncthreads();
-  // ---- FFN pre-norm -> fc1's input row
-  if (own) {
-    const int t = t0 + i2;
-    const bf16x8 y8 = *(const bf16x8*)(ybuf + i2 * C + c2 * 8);
-    const float r = inv[i2];
-    bf16x8 o8;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o8[j] = tobf(rb(rb(bf(y8[j]) * r) * bf(wf[j])));
-    *(bf16x8*)(a.a + ((long long)smp * a.T + t) * C + c2 * 8) = o8;
-  }
-}
-
 // ---------------------------------------------------------------- conv C_out = 1 (decoder head)
 // TokenizerDecoder.head (:912): SConv1d(C -> 1, k=7).  Writes the audio chunk to
 // `out` and, when out2.base != nullptr, also into the semantic encoder's stem
@@ -393,17 +254,6 @@ int launch_dwconv(DwArgs a, hipStream_t st) {
   hipLaunchKernelGGL(k_dwconv, dim3(nblk((long long)a.M * (a.C / 8), 256)), dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
-int launch_mix(MixArgs a, hipStream_t st) {
-  if (a.n <= 0 || a.T <= 0) return 0;
-  if (a.C % 8 || a.C > 2048 || (256 % (a.C / 8 < 64 ? a.C / 8 : 64)) || a.ctx != 6) return 1;
-  if (a.R * (a.C / 8) != 256 && !(a.R == a.T && a.R * (a.C / 8) < 256)) return 1;   // one conv item per thread
-  const size_t lds = (size_t)(2 * a.R + a.ctx) * a.C * sizeof(bf16) +
-                     (size_t)(a.R + a.ctx) * (a.C / 8 + 1) * sizeof(float);
-  if (lds > 65536) return 1;
-  hipLaunchKernelGGL(k_mix, dim3((a.T + a.R - 1) / a.R, a.n), dim3(256), lds, st, a);
-  return hipGetLastError() == hipSuccess ? 0 : 2;
-}
-
 int launch_conv_cout1(Conv1Args a, hipStream_t st) {
   if (a.M <= 0) return 0;
   if (a.C % 8) return 1;

@@ -365,9 +365,9 @@ static RowMap buf_in_rows(const ConvBuf& b, int T, const int* slots) {
 
 // Codec Block1D front half folded into fc1's prologue where it fits (XF_MIX);
 // off only for the bit-exactness test against the k_mix path.
-static bool g_mix_fusion = true;
-extern "C" int vv_codec_mix_fusion(int on) {
-  g_mix_fusion = on != 0;
+static int g_mix_fusion = 3;   // bit 0: XF_MIX, bit 1: k_block
+extern "C" int vv_codec_mix_fusion(int mask) {
+  g_mix_fusion = mask & 3;
   return 0;
 }
 
@@ -418,12 +418,52 @@ static int convnet_run(vv_ctx* c, ConvNet& net, int n, const int* slots, RowMap 
         CHK(gemm(c, g, st));
       }
     }
+    const int Rb = std::max(1, std::min(T, 2048 / C));
+    if ((g_mix_fusion & 2) && block_lds(Rb, C)) {
+      // narrow stage: each Block1D is one k_block launch; the residual
+      // ping-pongs X -> Y -> X (a workgroup reads halo rows other workgroups own)
+      for (int j = 0; j < net.depth[i]; ++j) {
+        const std::string b = p + ".s" + std::to_string(i) + ".b" + std::to_string(j);
+        const ConvBuf& mb = net.mix[i][j];
+        BlockArgs ba;
+        memset(&ba, 0, sizeof(ba));
+        MixArgs& mx = ba.mix;
+        mx.n = n;
+        mx.T = T;
+        mx.C = C;
+        mx.R = Rb;
+        mx.eps = eps;
+        mx.ctx = mb.ctx;
+        mx.x = (j & 1) ? net.Y[i] : net.X[i];
+        mx.buf = mb.base;
+        mx.buf_sB = mb.sB;
+        mx.slots = slots;
+        mx.norm_w = W(c, b + ".norm");
+        mx.dw_w = W(c, b + ".dw_w");
+        mx.dw_b = W(c, b + ".dw_b");
+        mx.gamma = W(c, b + ".gamma");
+        mx.ffn_norm_w = W(c, b + ".ffn_norm");
+        ba.w1 = W(c, b + ".fc1_w");
+        ba.b1 = W(c, b + ".fc1_b");
+        ba.w2 = W(c, b + ".fc2_w");
+        ba.b2 = W(c, b + ".fc2_b");
+        ba.g2 = W(c, b + ".ffn_gamma");
+        if (j == net.depth[i] - 1) {
+          const ConvBuf& nb = (i + 1 < net.nst) ? net.tr[i + 1] : net.head;
+          ba.out = buf_in_rows(nb, T, slots);
+        } else {
+          ba.out = rowmap((j & 1) ? net.X[i] : net.Y[i], C, T, (long long)T * C);
+        }
+        KCHK(launch_block(ba, st));
+      }
+      continue;
+    }
     for (int j = 0; j < net.depth[i]; ++j) {
       const std::string b = p + ".s" + std::to_string(i) + ".b" + std::to_string(j);
       const ConvBuf& mb = net.mix[i][j];
       RowMap Y = rowmap(net.Y[i], C, T, (long long)T * C);
       RowMap Fm = rowmap(net.F, 4LL * C);
-      if (g_mix_fusion && gemv_mix_lds(n * T, T, C)) {
+      if ((g_mix_fusion & 1) && gemv_mix_lds(n * T, T, C)) {
         // few rows (T = 1, 8 stages at small batch): the mix runs in fc1's prologue
         GemmArgs g = gemm_args(c, n * T, 4 * C, C, X, W(c, b + ".fc1_w"), EPI_GELU, Fm, W(c, b + ".fc1_b"));
         g.xf.kind = XF_MIX;

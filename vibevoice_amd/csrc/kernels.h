@@ -110,6 +110,16 @@ struct MixArgs {
   const bf16* ffn_norm_w;  // [C]
 };
 
+// a whole codec Block1D in one launch (codec_block.hip, C <= 128)
+struct BlockArgs {
+  MixArgs mix;             // front half; mix.y / mix.a unused
+  const bf16 *w1, *b1;     // fc1 [4C][C] MFMA-packed, bias [4C]
+  const bf16 *w2, *b2;     // fc2 [C][4C] MFMA-packed, bias [C]
+  const bf16* g2;          // ffn_gamma [C]
+  RowMap out;              // block output rows (row = sample * T + t)
+  bf16 *dbg_a, *dbg_h;     // diagnostics (tools/block_check.hip): fc1 input / hidden rows, or nullptr
+};
+
 struct Conv1Args {
   int M, C, K;
   RowMap buf;
@@ -161,6 +171,8 @@ int launch_sum_rows(SumRows s, long long count, hipStream_t st);
 int launch_rmsnorm(NormArgs a, hipStream_t st);
 int launch_dwconv(DwArgs a, hipStream_t st);
 int launch_mix(MixArgs a, hipStream_t st);
+size_t block_lds(int R, int C);   // 0: k_block does not apply
+int launch_block(BlockArgs b, hipStream_t st);
 int launch_conv_cout1(Conv1Args a, hipStream_t st);
 int launch_conv_cin1(ConvIn1Args a, hipStream_t st);
 int launch_roll(const RollDesc* d, int nd, const int* slots, int ns, int mode, hipStream_t st);

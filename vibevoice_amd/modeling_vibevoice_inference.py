@@ -119,8 +119,11 @@ class VibeVoiceForConditionalGenerationInference:
                 audio_dev=torch.zeros(B, eng.hop, device=dev, dtype=dt),
                 pos_pin=torch.zeros(2 * B, dtype=torch.int32, pin_memory=True),
                 ids_pin=torch.zeros(B, dtype=torch.int32, pin_memory=True),
-                didx_pin=torch.zeros(B, dtype=torch.int32, pin_memory=True),
-                noise_pin=torch.zeros(B, D, dtype=dt, pin_memory=True))
+                # two sets: the speculative diffusion of step k writes one while
+                # step k-1's copy from the other may still be queued
+                didx_pins=[torch.zeros(B, dtype=torch.int32, pin_memory=True) for _ in range(2)],
+                noise_pins=[torch.zeros(B, D, dtype=dt, pin_memory=True) for _ in range(2)],
+                logits_pin=torch.zeros(B, 4, dtype=torch.float32, pin_memory=True))
         return self._bufs[B]
 
     # ------------------------------------------------------------ loading
@@ -308,6 +311,9 @@ class GenerateSession:
         for k, v in sb.items():
             setattr(self, k, v)
         self.use_graphs = kwargs.get("use_graphs", model.use_graphs)
+        self.speculate = kwargs.get("speculate", True)
+        self.spec_miss = 0
+        self.logits_ready = torch.cuda.Event()
         self.graphs = model._graph_cache
         self.seen = model._graph_seen
 
@@ -354,26 +360,63 @@ class GenerateSession:
                            logits_out=self.logits, max_pos=eng.max_ctx - 1, ntok=2 * B)
         self._replay(("lm",), body)
 
-    def _token_phase(self, n):
-        """next_embeds = embed(next tokens) (:584); for the n diffusion rows:
-        CFG diffusion sampling (:644, 712-725), streaming decode / encode and the
-        connectors (:651-687), overwriting those rows' embeddings."""
+    def _diff_phase(self, n):
+        """CFG diffusion sampling for the n rows in didx_dev (:644, 712-725):
+        noise_dev[:n] is replaced by the latents."""
         B, eng = self.B, self.eng
 
         def body():
-            eng.embed(self.ids_dev, out=self.x_in2)
-            if n == 0:
-                return
             d = self.didx_dev[:n]
             if n == B:
                 pos_h, neg_h = self.hid[:B], self.hid[B:]
             else:   # one gather keeps [pos | neg] adjacent (used in place by the engine)
                 both = self.hid.index_select(0, torch.cat([d, d + B]))
                 pos_h, neg_h = both[:n], both[n:]
-            x = self.noise_dev[:n]
-            eng.diffusion_sample(pos_h, neg_h, x, self.cfg_scale)
-            eng.codec_step(d, x, self.audio_dev[:n], embeds_out=self.x_in2, embed_rows=d)
-        self._replay(("token", n), body)
+            eng.diffusion_sample(pos_h, neg_h, self.noise_dev[:n], self.cfg_scale)
+        self._replay(("diff", n), body)
+
+    def _post_phase(self, n):
+        """next_embeds = embed(next tokens) (:584); for the n diffusion rows the
+        streaming decode / encode and the connectors (:651-687), overwriting
+        those rows' embeddings."""
+        eng = self.eng
+
+        def body():
+            eng.embed(self.ids_dev, out=self.x_in2)
+            if n:
+                d = self.didx_dev[:n]
+                eng.codec_step(d, self.noise_dev[:n], self.audio_dev[:n], embeds_out=self.x_in2, embed_rows=d)
+        self._replay(("post", n), body)
+
+    def _stage_diffusion(self, didx, buf):
+        """Draw the diffusion noise from the CPU generator (:716) and queue the
+        H2D copies of the row list and the noise (pinned set `buf`)."""
+        n = didx.numel()
+        dp, npin = self.didx_pins[buf], self.noise_pins[buf]
+        dp[:n].copy_(didx)
+        noise = torch.randn(2 * n, self.m.config.acoustic_vae_dim)
+        npin[:n].copy_(noise[:n])
+        self.didx_dev[:n].copy_(dp[:n], non_blocking=True)
+        self.noise_dev[:n].copy_(npin[:n], non_blocking=True)
+
+    def _speculate(self):
+        """Queue the diffusion for the rows whose last token was speech_start or
+        speech_diffusion BEFORE the token choice is read back, so the GPU runs it
+        while the host reads the logits and does the bookkeeping.  The choice
+        itself is unchanged: step() keeps the result only if exactly these rows
+        chose speech_diffusion, else it restores the CPU generator and redoes the
+        diffusion for the right rows.  Greedy decoding only (sampling draws from
+        the same generator before the noise, :505)."""
+        if self.do_sample or not self.speculate:
+            return None
+        last = self.seq[-1][:, -1]
+        rows = torch.nonzero(~self.finished & ((last == self.diff_id) | (last == self.start_id))).reshape(-1)
+        if rows.numel() == 0:
+            return None
+        state = torch.get_rng_state()
+        self._stage_diffusion(rows, self.step_idx & 1)
+        self._diff_phase(rows.numel())
+        return rows, state
 
     # ---------------------------------------------------------------- one iteration
     def step(self):
@@ -406,7 +449,11 @@ class GenerateSession:
             self._lm_phase()
             self.pos_len += 1
         # ---- token choice (:494-509); the argmax is always read back, as in the reference
-        lg = self.logits[:B].float().cpu()
+        self.logits_pin.copy_(self.logits[:B], non_blocking=True)
+        self.logits_ready.record()
+        spec = self._speculate()
+        self.logits_ready.synchronize()
+        lg = self.logits_pin.clone()
         if self.do_sample:
             pick = torch.multinomial(torch.softmax(lg, -1), 1).squeeze(1)
         else:
@@ -460,19 +507,24 @@ class GenerateSession:
                 q = torch.tensor(quirk)
                 eng.kv_copy(self.ints.put(q + B), self.ints.put(torch.ones_like(q)),
                             self.ints.put(torch.zeros_like(q)))
-            self.didx_pin[:n].copy_(didx)
-            self.didx_dev.copy_(self.didx_pin, non_blocking=True)
-            noise = torch.randn(2 * n, self.m.config.acoustic_vae_dim)    # CPU generator (:716)
-            self.noise_pin[:n].copy_(noise[:n])
-            self.noise_dev.copy_(self.noise_pin, non_blocking=True)
-            self._token_phase(n)
+            if spec is None or not torch.equal(spec[0], didx):
+                if spec is not None:   # mispredicted: the speculative copies may still be queued
+                    torch.cuda.current_stream().synchronize()
+                    torch.set_rng_state(spec[1])
+                    self.spec_miss += 1
+                self._stage_diffusion(didx, self.step_idx & 1)
+                self._diff_phase(n)
+            self._post_phase(n)
             audio = self.audio_dev[:n].clone()
             for i, b in enumerate(didx.tolist()):
                 self.audio_chunks[b].append(audio[i:i + 1])
             if st is not None:
                 st.put(audio[:, None, :], didx)
         else:
-            self._token_phase(0)
+            if spec is not None:
+                torch.set_rng_state(spec[1])
+                self.spec_miss += 1
+            self._post_phase(0)
         self.step_idx += 1
         return True
 
