@@ -74,11 +74,19 @@ def bytes_per_token(wb, cfg, B, S, ctx_pos, ctx_neg):
 
 
 # ------------------------------------------------------------------ dominant kernel, live
+ROOF_KERNEL = "k_gemv1<4, 1>"      # U = 4 chunks in flight, XF_NORM; 2-wave groups (gemm.hip gemv_plan)
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+
+
 def measure_gemv(model, B, iters=6):
-    """The LM MLP gate|up weight-streaming GEMV (k_gemv1<8, XF_NORM>, EPI_SILU_MUL): the
-    largest single launch of the loop (2I x H bf16 = 55 MB at 1.5B, 28 per LM
-    pass).  Timed with HIP events on the stream it is launched on, rotating
-    over the 28 layers' weights so the Infinity Cache cannot serve it."""
+    """The LM MLP gate|up weight-streaming GEMV (k_gemv1, XF_NORM prologue,
+    EPI_SILU_MUL): the largest single launch of the loop (2I x H bf16 = 55 MB at
+    1.5B, 28 per LM pass).  The 28 layers' launches are captured into a hipGraph
+    (as the loop runs them) and replayed; HIP events on the replay stream time
+    `iters` replays.  Rotating over the 28 layers' weights (1.5 GB) keeps the
+    Infinity Cache from serving them.  `traffic`: HBM bytes per launch from the
+    rocprofv3 PMC passes of tools/pmc_traffic.py (FETCH_SIZE x 2 on gfx950 +
+    WRITE_SIZE, MI355X_MICROARCH.md "HBM"), committed in profiles/."""
     from vibevoice_amd import _lib
     eng = model.engine
     lmc = model.config.decoder_config
@@ -87,30 +95,42 @@ def measure_gemv(model, B, iters=6):
     A = torch.randn(M, H, device=model.device).bfloat16()
     norm_w = [eng.w[f"lm.{l}.post_norm"] for l in range(nl)]
     Y = torch.empty(M, I, device=model.device, dtype=torch.bfloat16)
-    stream = torch.cuda.current_stream()
-    sp = ctypes.c_void_p(stream.cuda_stream)
     L = _lib.lib()
     Ws = [eng.w[f"lm.{l}.gu_w"] for l in range(nl)]
 
     def run():
+        sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
         for Wt, nw_ in zip(Ws, norm_w):   # the in-loop variant: post_attention_layernorm fused on load
             _lib.check(L.vv_gemm_bf16_norm(M, 2 * I, H, ctypes.c_void_p(A.data_ptr()), H,
                                            ctypes.c_void_p(nw_.data_ptr()), float(lmc.rms_norm_eps),
                                            ctypes.c_void_p(Wt.data_ptr()), _lib.EPI["silu_mul"],
                                            ctypes.c_void_p(Y.data_ptr()), I, eng.h, sp), "gemv")
     run()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        run()
+    g.replay()
+    stream = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(iters):
-        run()
+        g.replay()
     e1.record(stream)
     e1.synchronize()
     avg_s = e0.elapsed_time(e1) / 1e3 / (iters * nl)
     alg = 2 * I * H * 2 + M * H * 2 + M * I * 2
     ach = alg / avg_s / 1e9
-    return dict(kernel="k_gemv1<8, 1> (LM post-norm + gate|up + SiLU*up)", shape=f"M={M} N={2 * I} K={H}", bound="hbm",
-                achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
-                traffic=None, avg_us=round(avg_s * 1e6, 2), alg_bytes_per_launch=alg)
+    shape = f"M={M} N={2 * I} K={H}"
+    traffic = None
+    if os.path.exists(PMC_FILE):
+        with open(PMC_FILE) as f:
+            pmc = json.load(f)
+        if pmc.get("kernel") == ROOF_KERNEL and pmc.get("shape") == shape:
+            traffic = pmc["hbm_bytes_per_launch"]
+    return dict(kernel=f"{ROOF_KERNEL} (LM post-norm + gate|up + SiLU*up, graph-replayed)", shape=shape,
+                bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
+                traffic=traffic, traffic_unit="bytes per launch" if traffic else None,
+                avg_us=round(avg_s * 1e6, 2), alg_bytes_per_launch=alg)
 
 
 # ------------------------------------------------------------------ CPU baseline (oracle)

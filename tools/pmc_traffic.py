@@ -1,0 +1,89 @@
+"""HBM traffic of bench.py's roofline kernel (the LM gate|up GEMV, k_gemv1<4, 1>,
+M=2 N=17920 K=1536 at 1.5B, B=1) from rocprofv3 PMC counters, collected the way
+MI355X_MICROARCH.md "HBM" / "rocprofv3 PMC slots" prescribe: FETCH_SIZE and
+WRITE_SIZE in separate passes (they do not fit one TCC pass), FETCH_SIZE
+doubled on gfx950 (it tallies 128-B streaming requests at 64 B), per dispatch.
+
+usage (GPU box):
+  python tools/pmc_traffic.py run             # the workload alone (what rocprofv3 wraps)
+  python tools/pmc_traffic.py collect         # both rocprofv3 passes + summary ->
+                                              # profiles/r01_pmc_traffic.json
+"""
+import csv
+import ctypes
+import glob
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+KERNEL = "k_gemv1<4, 1>"
+M, N, K, NL = 2, 17920, 1536, 28
+
+
+def run():
+    import torch
+    from vibevoice_amd import _lib
+    from vibevoice_amd.weights import mfma_pack
+    L = _lib.lib()
+    torch.manual_seed(0)
+    Ws = [mfma_pack((torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()) for _ in range(NL)]
+    nws = [(1 + 0.1 * torch.randn(K, device="cuda")).bfloat16() for _ in range(NL)]
+    A = torch.randn(M, K, device="cuda").bfloat16()
+    Y = torch.empty(M, N // 2, device="cuda", dtype=torch.bfloat16)
+    sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for _ in range(4):
+        for W, nw in zip(Ws, nws):
+            _lib.check(L.vv_gemm_bf16_norm(M, N, K, ctypes.c_void_p(A.data_ptr()), K, ctypes.c_void_p(nw.data_ptr()),
+                                           1e-6, ctypes.c_void_p(W.data_ptr()), _lib.EPI["silu_mul"],
+                                           ctypes.c_void_p(Y.data_ptr()), N // 2, None, sp), "gemv")
+    torch.cuda.synchronize()
+
+
+def per_dispatch(path, counter):
+    vals = []
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            name = row.get("Kernel_Name", "")
+            if KERNEL + "(" in name:
+                if row.get("Counter_Name") == counter:
+                    vals.append(float(row["Counter_Value"]))
+    return vals
+
+
+def collect():
+    out = os.path.join(ROOT, "gpurun_out", "pmc")
+    res = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(out, counter.lower())
+        cmd = ["rocprofv3", "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
+               sys.executable, os.path.abspath(__file__), "run"]
+        subprocess.run(cmd, check=True, timeout=600)
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        with open(files[0]) as f:
+            print(counter, "header:", f.readline().strip()[:300])
+        vals = per_dispatch(files[0], counter)
+        print(counter, "dispatches", len(vals), "first values", vals[:3])
+        vals = vals[NL:]                      # drop the first sweep (cold code / TLB)
+        res[counter] = sum(vals) / len(vals)
+        res[counter + "_dispatches"] = len(vals)
+    # rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB
+    fetch = res["FETCH_SIZE"] * 1024 * 2       # gfx950: 128-B requests tallied at 64 B
+    write = res["WRITE_SIZE"] * 1024
+    alg = N * K * 2 + M * K * 2 + M * (N // 2) * 2
+    summary = dict(kernel=KERNEL, shape=f"M={M} N={N} K={K}", fetch_size_kib_raw=round(res["FETCH_SIZE"], 1),
+                   write_size_kib=round(res["WRITE_SIZE"], 1), dispatches=res["FETCH_SIZE_dispatches"],
+                   hbm_read_bytes=int(fetch), hbm_write_bytes=int(write), hbm_bytes_per_launch=int(fetch + write),
+                   alg_bytes_per_launch=alg, traffic_over_alg=round((fetch + write) / alg, 4),
+                   method="rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, tools/pmc_traffic.py run; "
+                          "FETCH_SIZE x 2 (gfx950), KiB -> bytes")
+    for path in (os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"), os.path.join(out, "pmc_traffic.json")):
+        with open(path, "w") as f:
+            json.dump(summary, f, indent=1)
+    print(json.dumps(summary))
+
+
+if __name__ == "__main__":
+    {"run": run, "collect": collect}[sys.argv[1]]()
