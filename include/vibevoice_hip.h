@@ -164,6 +164,9 @@ int vv_gemv_tune(int nw, int ks, int handoff, int target_waves, int u);
  * stamps per workgroup (start, A staged, weights streamed, epilogue stored) to
  * buf (uint64[grid * 4]); NULL turns it off. */
 int vv_gemv_stamps(void* buf);
+/* Diagnostic (benchmarks only): vv_attention_bf16 launches write 4 stamps per
+ * workgroup (start, K/V/Q landed, keys done, output stored); NULL: off. */
+int vv_attn_stamps(void* buf);
 /* Test switch (bit mask, default 3): bit 0 folds each codec Block1D's mixer
  * (norm, depthwise conv, gamma residual, FFN norm) into its fc1 GEMV where
  * <= 16 rows fit (XF_MIX); bit 1 runs whole narrow-stage blocks (C <= 128) as

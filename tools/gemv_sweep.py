@@ -25,6 +25,9 @@ SHAPES = [  # name, M, N, K, epi
     ("head.down", 2, 1536, 4608, "res"), ("head.final", 2, 64, 1536, "store"),
     ("codec.fc1", 1, 8192, 2048, "gelu"), ("codec.fc2", 1, 2048, 8192, "res"),
     ("lm.gu.b8", 16, 17920, 1536, "silu_mul"), ("lm.down.b8", 16, 1536, 8960, "res"),
+    ("head.ada.s10", 20, 21504, 1536, "store"), ("head.ada.s10.b8", 160, 21504, 1536, "store"),
+    ("codec.t40.fc1", 40, 2048, 512, "gelu"), ("codec.t40.fc2", 40, 512, 2048, "res"),
+    ("codec.t8.fc2", 8, 1024, 4096, "res"),
 ]
 
 
@@ -41,6 +44,9 @@ def main():
         return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     results = []
     shapes = SHAPES_NORM + SHAPES if "--norm" not in sys.argv else SHAPES_NORM
+    if "--only" in sys.argv:
+        only = sys.argv[sys.argv.index("--only") + 1].split(",")
+        shapes = [sh for sh in shapes if sh[0] in only]
     for name, M, N, K, epi in shapes:
         ncopy = max(2, (512 << 20) // (N * K * 2) + 1)
         Ws = [(torch.randn(N, K, device=dev) / K ** 0.5).bfloat16() for _ in range(ncopy)]

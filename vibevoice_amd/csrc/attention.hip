@@ -33,6 +33,11 @@ constexpr int ATT_KC = 64;          // per-row split granularity
 
 DEV f32x4 amfma(bf16x8 a, bf16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
 
+DEV void astamp(const AttnArgs& a, int which) {
+  if (a.stamps && threadIdx.x == 0)
+    a.stamps[((long long)blockIdx.y * gridDim.x + blockIdx.x) * 4 + which] = __builtin_amdgcn_s_memrealtime();
+}
+
 template <int G>
 __global__ void __launch_bounds__(64 * ATT_NW) k_attn(AttnArgs a) {
   __shared__ float wm[ATT_NW][G], wl[ATT_NW][G];
@@ -43,6 +48,7 @@ __global__ void __launch_bounds__(64 * ATT_NW) k_attn(AttnArgs a) {
   constexpr int d = 128;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int r = lane & 15, g = lane >> 4;
+  astamp(a, 0);
   const int qi = blockIdx.x / a.nkv, kh = blockIdx.x - qi * a.nkv, split = blockIdx.y;
   const int len = a.pos[qi] + 1;
   // this row's split size: >= a.chunk, all nsplit splits cover len; splits past
@@ -107,6 +113,10 @@ __global__ void __launch_bounds__(64 * ATT_NW) k_attn(AttnArgs a) {
     }
   };
   if (w0 < w1) load(w0);
+  if (a.stamps) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    astamp(a, 1);
+  }
   for (int c0 = w0; c0 < w1; c0 += 32) {
     bf16x8 kc[2][4], vc[8];
 #pragma unroll
@@ -173,6 +183,7 @@ __global__ void __launch_bounds__(64 * ATT_NW) k_attn(AttnArgs a) {
     }
   }
   __syncthreads();
+  astamp(a, 2);
   // merge the waves: waves with no keys carry m = -inf, l = 0
   if (t < G) {
     float M = -INFINITY;
@@ -204,6 +215,10 @@ __global__ void __launch_bounds__(64 * ATT_NW) k_attn(AttnArgs a) {
         const int h = e / d, j = e - h * d;
         a.out[(long long)qi * a.nh * d + (kh * G + h) * d + j] = tobf(res[q] / fl[h]);
       }
+    }
+    if (a.stamps) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      astamp(a, 3);
     }
     return;
   }

@@ -157,6 +157,7 @@ struct AttnArgs {
   float* part_o;        // [nq][nh][nsplit][d]
   float* part_ml;       // [nq][nh][nsplit][2]
   unsigned* counters;   // [nq * nkv] split tickets (zero between launches)
+  unsigned long long* stamps;   // diagnostics only (tools/attn_stamps.py): 4 stamps per workgroup
 };
 
 // out_r = sum_r in_r for every r (single-process tensor-parallel group)
@@ -179,7 +180,7 @@ int launch_roll(const RollDesc* d, int nd, const int* slots, int ns, int mode, h
 int launch_latent_to_dec(int n, int D, const bf16* lat, const bf16* s, const bf16* b, RowMap out, hipStream_t st);
 int launch_vae_features(int rows, int D, int frames, const bf16* mean, const bf16* stdv, const bf16* noise,
                         const bf16* s, const bf16* b, bf16* out, hipStream_t st);
-int launch_head_cond(int rows, int H, const bf16* condp, const bf16* temb, bf16* out, hipStream_t st);
+int launch_head_cond(int steps, int R, int H, const bf16* condp, const bf16* temb, bf16* out, hipStream_t st);
 int launch_silu(int n, const bf16* x, bf16* y, hipStream_t st);
 int launch_cfg_dpm(int n, int D, DpmCoef k, const bf16* eps, bf16* x, bf16* m1, hipStream_t st);
 int launch_gather_rows(int n, int C, const bf16* src, long long lds, const int* idx, RowMap dst, hipStream_t st);
