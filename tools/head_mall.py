@@ -15,8 +15,10 @@ sys.path.insert(0, ROOT)
 from vibevoice_amd import _lib  # noqa: E402
 from vibevoice_amd.weights import mfma_pack  # noqa: E402
 
-if len(sys.argv) > 1:
-    _lib.LIB_PATH = os.path.abspath(sys.argv[1])
+ARGS = [a for a in sys.argv[1:] if not a.startswith("--")]
+if ARGS:
+    _lib.LIB_PATH = os.path.abspath(ARGS[0])
+WITH_ADA = "--no-ada" not in sys.argv   # the loop now computes all steps' adaLN rows once per token
 
 
 def main():
@@ -40,8 +42,9 @@ def main():
 
     def step():
         sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-        _lib.check(L.vv_gemm_bf16(M, ada.shape[0], H, P(x), H, P(ada), None, _lib.EPI["store"], P(mod), mod.shape[1],
-                                  None, None, None, sp))
+        if WITH_ADA:
+            _lib.check(L.vv_gemm_bf16(M, ada.shape[0], H, P(x), H, P(ada), None, _lib.EPI["store"], P(mod),
+                                      mod.shape[1], None, None, None, sp))
         for l in range(NLY):
             _lib.check(L.vv_gemm_bf16_norm(M, 2 * I, H, P(x), H, P(nw), 1e-5, P(gus[l]), _lib.EPI["silu_mul"], P(hbuf),
                                            I, None, sp))
@@ -62,7 +65,7 @@ def main():
         e1.record()
         e1.synchronize()
         print(f"{os.path.basename(_lib.LIB_PATH)}: {e0.elapsed_time(e1) * 1e3 / S:8.2f} us per diffusion step "
-              f"(9 launches, 236 MB of weights)", flush=True)
+              f"({'9 launches, 236' if WITH_ADA else '8 launches, 170'} MB of weights)", flush=True)
 
 
 if __name__ == "__main__":

@@ -971,6 +971,13 @@ int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, 
     HIPCHK(hipMemcpyAsync(cat + (size_t)n * H, neg_h, (size_t)n * H * sizeof(bf16), hipMemcpyDeviceToDevice, st));
     cond = cat;
   }
+  // the per-step head weights (noisy, gate|up, down, final: 170 MB at 1.5B) are
+  // re-read by every diffusion step: default cache policy keeps them in the
+  // Infinity Cache across the S steps
+  auto hgemm = [&](GemmArgs g) {
+    g.keep = 1;
+    return gemm(c, g, st);
+  };
   // cond_proj is step-invariant: computed once per token (bit-identical to per step)
   CHK(gemm(c, gemm_args(c, R, H, H, rowmap(cond, H), W(c, "head.cond_w"), EPI_STORE, rowmap(condp, H)), st));
   RowMap xh_m = rowmap(xh, H), a_m = rowmap(a, H);
@@ -987,18 +994,18 @@ int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, 
     }
     const bf16* mod = mods + (size_t)(s % HEAD_SC) * R * MODW;
     // x = noisy_images_proj(cat[x, x])  -- both halves read the same n latent rows
-    CHK(gemm(c, gemm_args(c, R, H, D, rowmap(x_io, D, n, 0), W(c, "head.noisy_w"), EPI_STORE, xh_m), st));
+    CHK(hgemm(gemm_args(c, R, H, D, rowmap(x_io, D, n, 0), W(c, "head.noisy_w"), EPI_STORE, xh_m)));
     for (int l = 0; l < L; ++l) {
       const std::string p = "head." + std::to_string(l);
       const int o = 3 * H * l;
       // modulate(norm(x), shift, scale) fused into gate|up's A load
       GemmArgs g = gemm_args(c, R, 2 * F, H, xh_m, W(c, p + ".gu_w"), EPI_SILU_MUL, rowmap(act, F));
       g.xf = xf_norm(W(c, p + ".norm"), k.head_eps, mod, MODW, o, o + H);
-      CHK(gemm(c, g, st));
+      CHK(hgemm(g));
       g = gemm_args(c, R, H, F, rowmap(act, F), W(c, p + ".down_w"), EPI_RES, xh_m);
       g.epi.res = xh_m;
       g.epi.gate = rowmap(mod + o + 2 * H, MODW);
-      CHK(gemm(c, g, st));
+      CHK(hgemm(g));
     }
     // final layer: modulate(norm_final(x)) -> linear -> CFG + DPM-Solver++ step on x
     DpmCoef e = c->coef[s];
@@ -1011,9 +1018,9 @@ int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, 
       g.dpm.k = e;
       g.dpm.x = (bf16*)x_io;
       g.dpm.m1 = m1;
-      CHK(gemm(c, g, st));
+      CHK(hgemm(g));
     } else {
-      CHK(gemm(c, g, st));
+      CHK(hgemm(g));
       KCHK(launch_cfg_dpm(n, D, e, v, (bf16*)x_io, m1, st));
     }
   }

@@ -51,15 +51,18 @@ DEV void stamp(const GemmArgs& a, int which) {
 // Weight-stream load.  Decode weights are read once per step (GBs against a
 // 256 MB Infinity Cache), so they go out non-temporal (MI355X_MICROARCH.md
 // "nt-weights"); VV_W_NT=0 builds the default-policy variant for A/B runs.
+// KEEP (GemmArgs::keep): weights re-read soon — the diffusion head's 170 MB per
+// step is read S times per token and stays in the Infinity Cache with the
+// default policy (tools/head_mall.py: -7 % per head step).
 #ifndef VV_W_NT
 #define VV_W_NT 1
 #endif
+template <bool KEEP = false>
 DEV bf16x8 ldw(const bf16* p) {
 #if VV_W_NT
-  return __builtin_nontemporal_load((const bf16x8*)p);
-#else
-  return *(const bf16x8*)p;
+  if (!KEEP) return __builtin_nontemporal_load((const bf16x8*)p);
 #endif
+  return *(const bf16x8*)p;
 }
 
 DEV f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
@@ -330,7 +333,7 @@ DEV bool splitk_handoff(const GemmArgs& a, float* red, int TILE, unsigned* last_
 // M <= 16: the workgroup's A rows (its K range, transformed) are staged once in
 // LDS; each wave streams its weight chunks with a two-deep register ping-pong
 // (U chunks = U KB per wave in flight while the previous U are multiplied).
-template <int U, int XF>
+template <int U, int XF, bool KEEP = false>
 __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ float inv_s[16];
@@ -404,7 +407,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
       }
       if (first) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) wa[u] = ldw(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
+        for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
       }
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -512,7 +515,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
       }
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) wa[u] = ldw(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
+    for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
     if (XF == XF_NORM) {
       // per-item sums of squares -> LDS, rows reduced in a fixed order
 #pragma unroll
@@ -563,7 +566,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   } else {
     // many rows (B >= 8 batches): weights first, then the A rows in batches
 #pragma unroll
-    for (int u = 0; u < U; ++u) wa[u] = ldw(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
+    for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
     for (int e0 = threadIdx.x; e0 < a.M * n8; e0 += 4 * blockDim.x) {
       bf16x8 xv[4];
 #pragma unroll
@@ -626,7 +629,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   };
   auto load = [&](bf16x8 (&wf)[U], int c) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) wf[u] = ldw(wrow + min(c + u, max(c1 - 1, 0)) * 512);
+    for (int u = 0; u < U; ++u) wf[u] = ldw<KEEP>(wrow + min(c + u, max(c1 - 1, 0)) * 512);
   };
   for (int c = c0; c < c1; c += 2 * U) {
     load(wb, c + U);
@@ -909,9 +912,15 @@ static void launch_gemv_xf(const GemmArgs& a, int mrep, int u, dim3 grid, dim3 b
     const int kw = ((nchunk + a.ksplit - 1) / a.ksplit) * 32;
     const size_t xs_bytes = ((size_t)a.M * (kw + 8) * sizeof(bf16) + 15) & ~(size_t)15;
     const size_t lds = xs_bytes + (size_t)a.M * (kw / 8) * sizeof(float);
-    if (u == 4) hipLaunchKernelGGL((k_gemv1<4, XF>), grid, block, lds, st, a);
-    else if (u == 2) hipLaunchKernelGGL((k_gemv1<2, XF>), grid, block, lds, st, a);
-    else hipLaunchKernelGGL((k_gemv1<8, XF>), grid, block, lds, st, a);
+    if (a.keep) {
+      if (u == 4) hipLaunchKernelGGL((k_gemv1<4, XF, true>), grid, block, lds, st, a);
+      else if (u == 2) hipLaunchKernelGGL((k_gemv1<2, XF, true>), grid, block, lds, st, a);
+      else hipLaunchKernelGGL((k_gemv1<8, XF, true>), grid, block, lds, st, a);
+    } else {
+      if (u == 4) hipLaunchKernelGGL((k_gemv1<4, XF>), grid, block, lds, st, a);
+      else if (u == 2) hipLaunchKernelGGL((k_gemv1<2, XF>), grid, block, lds, st, a);
+      else hipLaunchKernelGGL((k_gemv1<8, XF>), grid, block, lds, st, a);
+    }
     return;
   }
   switch (mrep) {

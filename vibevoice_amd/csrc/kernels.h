@@ -70,6 +70,8 @@ struct GemmArgs {
   float* ws;
   unsigned* counters;
   unsigned long long* stamps;  // diagnostic builds only: 4 s_memrealtime stamps per workgroup
+  int keep;               // weights re-read soon (diffusion head): default cache policy, not nt
+  int pad2_;
 };
 
 struct NormArgs {
