@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--ddpm-steps", type=int, default=10)
     ap.add_argument("--model", default="1.5B", choices=["1.5B", "Large"])
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel ranks per model replica (RCCL)")
+    ap.add_argument("--context", type=int, default=0,
+                    help="grow the positive context to this many positions with synthetic K/V before timing "
+                         "(SURVEY.md §8d config 5: 64K-position decode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-tokens", type=int, default=8, help="timed tokens of the CPU oracle sample")
     return ap.parse_args()
@@ -233,8 +236,13 @@ def main():
     inp = synthetic_inputs(batch=B, speakers=args.speakers, voice_seconds=3.0, text_tokens=64, seed=100 + rank // T)
     L = inp["input_ids"].shape[1]
     total = W + K + 4
+    if args.context:   # the timed steps end at most at max_position_embeddings (65,536 for the 1.5B LM)
+        from vibevoice_amd.config import VibeVoiceConfig
+        mpe = VibeVoiceConfig.builtin(args.model).decoder_config.max_position_embeddings
+        args.context = min(args.context, mpe - total - 8)
     model = VibeVoiceForConditionalGenerationInference.from_pretrained(
-        f"synthetic:{args.model}", device_map=str(dev), synthetic_seed=0, max_batch=B, max_ctx=L + total + 8,
+        f"synthetic:{args.model}", device_map=str(dev), synthetic_seed=0, max_batch=B,
+        max_ctx=max(L, args.context) + total + 8,
         tp_group=tp_group)
     model.set_ddpm_inference_steps(S)
     tk = tokenizer_ids()
@@ -242,6 +250,8 @@ def main():
     torch.manual_seed(1234)
     sess = model.generate_session(**inp, tokenizer=tk, cfg_scale=1.3, generation_config={"do_sample": False},
                                   forced_tokens=forced, max_length_times=total / L + 1, max_new_tokens=total + 2)
+    if args.context:
+        sess.extend_context(args.context)
     for _ in range(W):
         assert sess.step()
     ctx0 = int(sess.pos_len.float().mean())
@@ -283,7 +293,9 @@ def main():
                     "prompt (3 s/speaker), random script ids in the processor's prompt layout, forced "
                     "speech_diffusion schedule (constrained argmax still computed and read back each step)",
             "config": {"workload": f"VibeVoice-{args.model} bf16, {B} dialogue(s)/replica x {args.speakers} "
-                                   f"speaker(s), {S} diffusion steps, TP={T}, prompt {L} tokens",
+                                   f"speaker(s), {S} diffusion steps, TP={T}, prompt {L} tokens"
+                                   + (f", positive context grown to {args.context} positions (synthetic K/V)"
+                                      if args.context else ""),
                        "model": f"VibeVoice-{args.model}", "global_batch": B * replicas, "seq_len": L,
                        "diffusion_steps": S, "parallelism": f"dp{replicas} (independent replicas), tp{T}"},
             "roofline": roof,

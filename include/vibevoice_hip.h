@@ -106,14 +106,20 @@ int vv_lm_forward_group(int n, vv_ctx* const* ctxs, int ntok, const void* embeds
 
 /* Copy the K/V cache entry src[i] -> dst[i] of slot slots[i] (all layers). */
 int vv_kv_copy(vv_ctx* ctx, int n, const int* slots, const int* src, const int* dst, vv_stream st);
+/* Benchmarks only: fill the KV cache of `slots` at
+ * positions [p0, p1) with deterministic pseudo-random values, so decode can be
+ * timed at a long context without a long prefill.  Not a reference operation. */
+int vv_kv_synthetic(vv_ctx* c, int n, const int* slots, int p0, int p1, unsigned seed, vv_stream stream);
 
 /* embeds_out[i] = embed_tokens[ids[i]] */
 int vv_embed(vv_ctx* ctx, int n, const int* ids, void* embeds_out, vv_stream st);
 
 /* n samples: pos_h, neg_h [n, H] conditions; x_io [n, latent] holds the first n
- * rows of the noise draw on entry and the denoised latent on return. */
+ * rows of the noise draw on entry and the denoised latent on return.
+ * sde_noise: NULL for the model's dpmsolver++; for sde-dpmsolver++ the fp32
+ * per-step draws [steps][2n][latent] (step()'s randn, dpm_solver.py:985-987). */
 int vv_diffusion_sample(vv_ctx* ctx, int n, const void* pos_h, const void* neg_h, void* x_io, float cfg_scale,
-                        vv_stream st);
+                        const float* sde_noise, vv_stream st);
 
 /* One streaming codec step for n samples in codec slots slots[n]:
  * latent [n, latent] -> audio_out [n, hop]; semantic features -> sem_out

@@ -49,7 +49,7 @@ def head_forward(sd, noisy, t, cond, n_layers, eps=1e-5):
 
 
 def sample_speech_tokens(sd, cond, neg_cond, noise, steps, cfg_scale, n_layers, eps=1e-5,
-                         return_trace=False):
+                         return_trace=False, sde_noise=None):
     """sample_speech_tokens (:712-725).
 
     `noise` is the [2n, latent] draw the reference makes with the CPU generator
@@ -57,19 +57,22 @@ def sample_speech_tokens(sd, cond, neg_cond, noise, steps, cfg_scale, n_layers, 
     Only rows [:n] influence the result; all 2n rows are stepped as in the
     reference so the trace matches.
     """
-    sched = DPMSolverPP()
+    # sde_noise: [steps, 2n, latent] fp32, the per-step draws step() makes for
+    # sde-dpmsolver++ (dpm_solver.py:985-987)
+    sched = DPMSolverPP(algorithm_type="sde-dpmsolver++" if sde_noise is not None else "dpmsolver++")
     sched.set_timesteps(steps)
     condition = torch.cat([cond, neg_cond], dim=0)
     speech = noise.clone()
     n = cond.shape[0]
     trace = []
-    for t in sched.timesteps:
+    for si, t in enumerate(sched.timesteps):
         half = speech[:n]
         combined = torch.cat([half, half], dim=0)
         eps_ = head_forward(sd, combined, t.repeat(2 * n).to(combined.dtype), condition, n_layers, eps)
         c_eps, u_eps = torch.split(eps_, n, dim=0)
         half_eps = u_eps + cfg_scale * (c_eps - u_eps)
-        speech = sched.step(torch.cat([half_eps, half_eps], dim=0), speech)
+        speech = sched.step(torch.cat([half_eps, half_eps], dim=0), speech,
+                            None if sde_noise is None else sde_noise[si])
         if return_trace:
             trace.append(speech[:n].clone())
     return (speech[:n], trace) if return_trace else speech[:n]

@@ -22,9 +22,17 @@ def cosine_alphas_cumprod(num_train_timesteps=1000, max_beta=0.999):
 
 
 class DPMSolverPP:
-    """Stateful restatement of DPMSolverMultistepScheduler for this config."""
+    """Stateful restatement of DPMSolverMultistepScheduler for this config.
 
-    def __init__(self, num_train_timesteps=1000):
+    algorithm_type "dpmsolver++" (the model's, modeling_vibevoice.py:138-142) or
+    "sde-dpmsolver++" (gradio_demo.py:114-118; "squaredcos_cap_v2" is the same
+    cosine betas, dpm_solver.py:239-241).  The SDE variant takes the step's
+    fp32 noise explicitly (step()'s variance_noise, :985-989)."""
+
+    def __init__(self, num_train_timesteps=1000, algorithm_type="dpmsolver++"):
+        if algorithm_type not in ("dpmsolver++", "sde-dpmsolver++"):
+            raise NotImplementedError(algorithm_type)
+        self.algorithm_type = algorithm_type
         self.T = num_train_timesteps
         self.alphas_cumprod = cosine_alphas_cumprod(num_train_timesteps)
         ac = self.alphas_cumprod
@@ -50,7 +58,7 @@ class DPMSolverPP:
         a = 1 / ((sigma ** 2 + 1) ** 0.5)                                # :483-487
         return a, sigma * a
 
-    def step(self, v, sample):
+    def step(self, v, sample, noise=None):
         """step() dpm_solver.py:935-1022; `v` and `sample` share a dtype.
 
         The dtype flow is the reference's: x0 = alpha*sample - sigma*v runs in
@@ -70,16 +78,29 @@ class DPMSolverPP:
         lam_t = torch.log(a_t) - torch.log(s_t)
         lam_0 = torch.log(a_0) - torch.log(s_0)
         h = lam_t - lam_0
+        sde = self.algorithm_type == "sde-dpmsolver++"
+        if sde:
+            assert noise is not None
+            noise = noise.to(torch.float32)
         if self.lower_order_nums < 1 or lower_final:                     # :1003-1004, :669-677
-            out = (s_t / s_0) * x - (a_t * (torch.exp(-h) - 1.0)) * x0
+            if sde:                                                      # :680-686
+                out = ((s_t / s_0 * torch.exp(-h)) * x + (a_t * (1 - torch.exp(-2.0 * h))) * x0
+                       + s_t * torch.sqrt(1.0 - torch.exp(-2 * h)) * noise)
+            else:
+                out = (s_t / s_0) * x - (a_t * (torch.exp(-h) - 1.0)) * x0
         else:                                                            # :738-764
             a_1, s_1 = self._alpha_sigma(self.sigmas[i - 1])
             lam_1 = torch.log(a_1) - torch.log(s_1)
             r0 = (lam_0 - lam_1) / h
             m0, m1 = self.model_outputs[1], self.model_outputs[0]
             d1 = (1.0 / r0) * (m0 - m1)
-            out = ((s_t / s_0) * x - (a_t * (torch.exp(-h) - 1.0)) * m0
-                   - 0.5 * (a_t * (torch.exp(-h) - 1.0)) * d1)
+            if sde:                                                      # :785-793 (midpoint)
+                out = ((s_t / s_0 * torch.exp(-h)) * x + (a_t * (1 - torch.exp(-2.0 * h))) * m0
+                       + 0.5 * (a_t * (1 - torch.exp(-2.0 * h))) * d1
+                       + s_t * torch.sqrt(1.0 - torch.exp(-2 * h)) * noise)
+            else:
+                out = ((s_t / s_0) * x - (a_t * (torch.exp(-h) - 1.0)) * m0
+                       - 0.5 * (a_t * (torch.exp(-h) - 1.0)) * d1)
         if self.lower_order_nums < 2:
             self.lower_order_nums += 1
         self.step_index += 1

@@ -51,6 +51,38 @@ def randomize(module, seed, std=0.05):
             p.copy_(p.to(torch.bfloat16).float())
 
 
+# ---------------------------------------------------------------- G1-SDE scheduler
+def g1_sde_scheduler():
+    """sde-dpmsolver++ as gradio_demo.py:114-118 configures it (from_config with
+    algorithm_type="sde-dpmsolver++", beta_schedule="squaredcos_cap_v2"); the
+    per-step noise is passed as variance_noise so the trace is deterministic."""
+    Sch = R["dpm"].DPMSolverMultistepScheduler
+    out = {}
+    for S in (1, 2, 5, 10, 20):
+        # from_config(base.config, **overrides) == the constructor with the base
+        # arguments plus the overrides (ConfigMixin; stubbed in the harness)
+        s = Sch(num_train_timesteps=1000, beta_schedule="squaredcos_cap_v2", prediction_type="v_prediction",
+                algorithm_type="sde-dpmsolver++")
+        s.set_timesteps(S)
+        out[f"sigmas_{S}"] = s.sigmas.numpy()
+        for dt, tag in ((torch.float32, "f32"), (torch.bfloat16, "bf16")):
+            g = torch.Generator().manual_seed(200 + S)
+            x = torch.randn(3, 64, generator=g).to(dt)
+            vs = torch.randn(S, 3, 64, generator=g).to(dt)
+            zs = torch.randn(S, 3, 64, generator=g)                     # fp32 (step() draws fp32 noise)
+            s.set_timesteps(S)
+            xs = []
+            cur = x
+            for i, t in enumerate(s.timesteps):
+                cur = s.step(vs[i], t, cur, variance_noise=zs[i]).prev_sample
+                xs.append(cur)
+            out[f"x_{tag}_{S}"] = f32(x)
+            out[f"v_{tag}_{S}"] = f32(vs)
+            out[f"z_{tag}_{S}"] = f32(zs)
+            out[f"trace_{tag}_{S}"] = f32(torch.stack(xs))
+    save("g1_sde_scheduler.npz", **out)
+
+
 # ---------------------------------------------------------------- G1 scheduler
 def g1_scheduler():
     Sch = R["dpm"].DPMSolverMultistepScheduler
@@ -260,7 +292,12 @@ def g7_qwen2():
 
 if __name__ == "__main__":
     torch.set_num_threads(8)
+    if len(sys.argv) > 1:                        # regenerate selected fixtures: make_golden.py g1_sde_scheduler
+        for name in sys.argv[1:]:
+            globals()[name]()
+        sys.exit(0)
     g1_scheduler()
+    g1_sde_scheduler()
     g2_g3_head()
     g4_g5_codec()
     g6_connector()

@@ -120,3 +120,33 @@ def test_streamer_and_stop_check():
     assert out2.sequences.shape[1] == 12 + 4
     assert sorted(st2.ended) == [0, 1]
     assert out2.speech_outputs[0].shape[-1] == 4 * m.engine.hop
+
+
+def test_noise_scheduler_swap_sde():
+    """gradio_demo.py:114-119: model.model.noise_scheduler replaced through
+    from_config(config, algorithm_type="sde-dpmsolver++",
+    beta_schedule="squaredcos_cap_v2"), then set_ddpm_inference_steps.  The SDE
+    noise comes from the device generator, so a seeded run is reproducible and
+    graph replay equals the eager loop; the result differs from the ODE solver's."""
+    cfg = tiny_config(hidden=256, layers=2, heads=2, kv_heads=1, inter=512)
+    m = _model(synthetic_state_dict(cfg, seed=9, device="cpu", mode="test", with_acoustic_encoder=False), cfg)
+    ids, mask = _inputs()
+    sched = [[D] * 5 + [X]] * 2
+
+    def run(graphs):
+        torch.manual_seed(5)
+        return m.generate(input_ids=ids, attention_mask=mask, tokenizer=TOK, cfg_scale=1.3, forced_tokens=sched,
+                          use_graphs=graphs, show_progress_bar=False)
+    ode = run(True)
+    ns = m.model.noise_scheduler
+    m.model.noise_scheduler = ns.from_config(ns.config, algorithm_type="sde-dpmsolver++",
+                                             beta_schedule="squaredcos_cap_v2")
+    m.set_ddpm_inference_steps(num_steps=5)
+    assert m.model.noise_scheduler.config.algorithm_type == "sde-dpmsolver++"
+    outs = [run(False), run(True), run(True)]
+    for o in outs[1:]:
+        for b in range(2):
+            assert torch.equal(o.speech_outputs[b].cpu(), outs[0].speech_outputs[b].cpu())
+    assert not torch.equal(outs[0].speech_outputs[0].cpu(), ode.speech_outputs[0].cpu())
+    with pytest.raises(NotImplementedError):
+        ns.from_config(ns.config, algorithm_type="dpmsolver")

@@ -48,6 +48,58 @@ def test_head_vs_reference_golden(S):
     assert err < 2e-2 and c > 0.999
 
 
+def real_head_sd(g):
+    from vibevoice_amd.config import VibeVoiceConfig
+    cfg = VibeVoiceConfig.builtin("1.5B")
+    hc = cfg.diffusion_head_config
+    H, F = hc.hidden_size, int(hc.hidden_size * hc.head_ffn_ratio)
+    sd = {}
+
+    def r(*s, std):
+        return (torch.randn(*s, generator=g) * std).bfloat16()
+    sd["noisy_images_proj.weight"] = r(H, 64, std=0.125)
+    sd["cond_proj.weight"] = r(H, H, std=H ** -0.5)
+    sd["t_embedder.mlp.0.weight"] = r(H, 256, std=0.0625)
+    sd["t_embedder.mlp.2.weight"] = r(H, H, std=H ** -0.5)
+    for i in range(hc.head_layers):
+        p = f"layers.{i}."
+        sd[p + "ffn.gate_proj.weight"] = r(F, H, std=H ** -0.5)
+        sd[p + "ffn.up_proj.weight"] = r(F, H, std=H ** -0.5)
+        sd[p + "ffn.down_proj.weight"] = r(H, F, std=F ** -0.5)
+        sd[p + "norm.weight"] = (1 + 0.1 * torch.randn(H, generator=g)).bfloat16()
+        sd[p + "adaLN_modulation.1.weight"] = r(3 * H, H, std=0.5 * H ** -0.5)
+    sd["final_layer.linear.weight"] = r(64, H, std=H ** -0.5)
+    sd["final_layer.adaLN_modulation.1.weight"] = r(2 * H, H, std=0.5 * H ** -0.5)
+    return sd, hc, H
+
+
+@pytest.mark.parametrize("n", [1, 3])
+def test_head_sde_vs_oracle(n):
+    """sde-dpmsolver++ (gradio_demo.py:114-118) at the real head shapes: the
+    per-step fp32 noise is given to both; the oracle's SDE scheduler is pinned
+    bit-exact to the reference (tests/golden/g1_sde_scheduler.npz)."""
+    from vibevoice_amd.schedule import Schedule
+    g = torch.Generator().manual_seed(12)
+    sd, hc, H = real_head_sd(g)
+    tiny = tiny_config(hidden=H, layers=1, heads=12, kv_heads=2, inter=256)
+    eng, _ = engine_with_head(tiny, sd)
+    eng.set_schedule(Schedule.from_config(eng.schedule.config, algorithm_type="sde-dpmsolver++",
+                                          beta_schedule="squaredcos_cap_v2"))
+    S = 10
+    eng.set_steps(S)
+    pos = (torch.randn(n, H, generator=g)).bfloat16()
+    neg = (torch.randn(n, H, generator=g)).bfloat16()
+    noise = torch.randn(2 * n, 64, generator=g).bfloat16()
+    z = torch.randn(S, 2 * n, 64, generator=g)
+    x = noise[:n].to(dev).contiguous()
+    eng.diffusion_sample(pos.to(dev), neg.to(dev), x, 1.3, sde_noise=z.to(dev))
+    torch.cuda.synchronize()
+    ref = ohead.sample_speech_tokens(sd, pos, neg, noise, S, 1.3, hc.head_layers, sde_noise=z)
+    err, c = rel_err(x, ref), cos(x, ref)
+    print(f"SDE n={n} rel_err={err:.3e} cos={c:.6f}")
+    assert err < 2e-2 and c > 0.999
+
+
 @pytest.mark.parametrize("n", [1, 3])
 def test_head_real_shape_vs_oracle(n):
     from vibevoice_amd.config import VibeVoiceConfig

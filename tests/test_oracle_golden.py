@@ -46,6 +46,24 @@ def test_scheduler_step_trace_bitexact(S, tag):
         assert torch.equal(x.float(), ref[i]), f"step {i}"
 
 
+@pytest.mark.parametrize("S", [1, 2, 5, 10, 20])
+@pytest.mark.parametrize("tag", ["f32", "bf16"])
+def test_sde_scheduler_step_trace_bitexact(S, tag):
+    """sde-dpmsolver++ (gradio_demo.py:114-118) with the reference's own per-step
+    fp32 noise (variance_noise): bit-exact vs the reference."""
+    z = load("g1_sde_scheduler.npz")
+    s = scheduler.DPMSolverPP(algorithm_type="sde-dpmsolver++")
+    s.set_timesteps(S)
+    assert (s.sigmas.numpy() == z[f"sigmas_{S}"]).all()
+    x = t(z, f"x_{tag}_{S}", DT[tag])
+    vs = t(z, f"v_{tag}_{S}", DT[tag])
+    zs = t(z, f"z_{tag}_{S}")
+    ref = t(z, f"trace_{tag}_{S}")
+    for i in range(S):
+        x = s.step(vs[i], x, zs[i])
+        assert torch.equal(x.float(), ref[i]), f"step {i}"
+
+
 @pytest.mark.parametrize("tag", ["f32", "bf16"])
 def test_head_forward(tag):
     z = load("g2_head.npz")

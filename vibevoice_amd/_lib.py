@@ -40,11 +40,12 @@ EXPORTS = [
     ("vv_set_schedule", I, [P, I, ctypes.POINTER(F), P, P]),
     ("vv_lm_forward", I, [P, I, P, I, P, P, I, I, P, P, P, P]),
     ("vv_kv_copy", I, [P, I, P, P, P, P]),
+    ("vv_kv_synthetic", I, [P, I, P, I, I, ctypes.c_uint, P]),
     ("vv_tp_unique_id", I, [P, I]),
     ("vv_tp_init", I, [P, I, I, P]),
     ("vv_lm_forward_group", I, [I, ctypes.POINTER(P), I, P, I, P, P, I, I, P, P, P, P]),
     ("vv_embed", I, [P, I, P, P, P]),
-    ("vv_diffusion_sample", I, [P, I, P, P, P, F, P]),
+    ("vv_diffusion_sample", I, [P, I, P, P, P, F, P, P]),
     ("vv_codec_step", I, [P, I, P, P, P, P, P, P, P]),
     ("vv_codec_reset", I, [P, I, P, P]),
     ("vv_acoustic_encode", I, [P, I, I, P, P, P]),

@@ -424,6 +424,36 @@ __global__ void __launch_bounds__(256) k_kv_copy(KVLayout kv, int n_layers, int 
   }
 }
 
+// Synthetic context (benchmarks only): K and V of every
+// layer / kv head at positions [p0, p1) of the given slots get deterministic
+// pseudo-random bf16 values in [-0.5, 0.5) (a hash of the element index), so a
+// decode step can be timed attending ~64K keys without a 64K-token prefill.
+__global__ void __launch_bounds__(256) k_kv_fill(KVLayout kv, int n_layers, int nkv, const int* slots, int p0, int p1,
+                                                 unsigned seed) {
+  const int span = p1 - p0;
+  const long long per_head = (long long)span * kv.d;
+  const long long total = per_head * n_layers * nkv;
+  const int slot = slots[blockIdx.y];
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const long long lh = e / per_head, r = e - lh * per_head;
+    const int layer = (int)(lh / nkv), h = (int)(lh - (long long)layer * nkv);
+    const int pos = p0 + (int)(r / kv.d), j = (int)(r % kv.d);
+    const long long base = (long long)layer * kv.s_layer + (long long)slot * kv.s_slot + (long long)h * kv.s_head;
+    unsigned x = (unsigned)(e * 2654435761ull) ^ (seed + 0x9e3779b9u * (unsigned)slot);
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    kv.k[base + (long long)pos * kv.d + j] = tobf((float)(x & 0xffff) / 65536.f - 0.5f);
+    kv.v[base + (long long)j * kv.max_ctx + pos] = tobf((float)(x >> 16) / 65536.f - 0.5f);   // V^T [dim][ctx]
+  }
+}
+
+int launch_kv_fill(KVLayout kv, int n_layers, int nkv, int n, const int* slots, int p0, int p1, unsigned seed,
+                   hipStream_t st) {
+  if (n <= 0 || p1 <= p0) return 0;
+  if (p0 < 0 || p1 > kv.max_ctx) return 1;
+  hipLaunchKernelGGL(k_kv_fill, dim3(2048, n), dim3(256), 0, st, kv, n_layers, nkv, slots, p0, p1, seed);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
 int launch_kv_copy(KVLayout kv, int n_layers, int nkv, int n, const int* slots, const int* src, const int* dst,
                    hipStream_t st) {
   if (n <= 0) return 0;

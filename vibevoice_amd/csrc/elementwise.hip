@@ -199,7 +199,7 @@ __global__ void k_silu(int n, const bf16* x, bf16* y) {
 // :717-724; DPMSolverMultistepScheduler.step dpm_solver.py:935-1022).  eps rows
 // [0, n) are the conditional and [n, 2n) the unconditional predictions.
 
-__global__ void k_cfg_dpm(int n, int D, DpmCoef k, const bf16* eps, bf16* x, bf16* m1) {
+__global__ void k_cfg_dpm(int n, int D, DpmCoef k, const bf16* eps, bf16* x, bf16* m1, const float* noise) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n * D) return;
   const float c = bf(eps[i]), u = bf(eps[i + n * D]);
@@ -211,6 +211,7 @@ __global__ void k_cfg_dpm(int n, int D, DpmCoef k, const bf16* eps, bf16* x, bf1
     const float d1 = rb(k.inv_r0 * rb(x0 - bf(m1[i])));
     out = out - rb(k.c_d1 * d1);
   }
+  if (noise) out = out + k.c_n * noise[i];
   x[i] = tobf(out);
   m1[i] = tobf(x0);
 }
@@ -302,8 +303,8 @@ int launch_silu(int n, const bf16* x, bf16* y, hipStream_t st) {
   hipLaunchKernelGGL(k_silu, dim3(nblk(n, 256)), dim3(256), 0, st, n, x, y);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
-int launch_cfg_dpm(int n, int D, DpmCoef k, const bf16* eps, bf16* x, bf16* m1, hipStream_t st) {
-  hipLaunchKernelGGL(k_cfg_dpm, dim3(nblk(n * D, 256)), dim3(256), 0, st, n, D, k, eps, x, m1);
+int launch_cfg_dpm(int n, int D, DpmCoef k, const bf16* eps, bf16* x, bf16* m1, const float* noise, hipStream_t st) {
+  hipLaunchKernelGGL(k_cfg_dpm, dim3(nblk(n * D, 256)), dim3(256), 0, st, n, D, k, eps, x, m1, noise);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 int launch_gather_rows(int n, int C, const bf16* src, long long lds, const int* idx, RowMap dst, hipStream_t st) {

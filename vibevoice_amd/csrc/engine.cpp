@@ -719,6 +719,7 @@ int vv_set_schedule(vv_ctx* c, int steps, const float* coef, const void* tfreq, 
     e.c_d1 = q[4];
     e.inv_r0 = q[5];
     e.order = (int)q[6];
+    e.c_n = q[7];
     e.cfg = 0.f;
   }
   // sized for the largest schedule once, so captured graphs keep valid pointers
@@ -736,6 +737,13 @@ int vv_set_schedule(vv_ctx* c, int steps, const float* coef, const void* tfreq, 
 int vv_kv_copy(vv_ctx* c, int n, const int* slots, const int* src, const int* dst, vv_stream vst) {
   if (!c->finalized) FAIL("vv_kv_copy before vv_finalize");
   KCHK(launch_kv_copy(c->kv, c->cfg.n_layers, c->cfg.n_kv_heads, n, slots, src, dst, (hipStream_t)vst));
+  return 0;
+}
+
+int vv_kv_synthetic(vv_ctx* c, int n, const int* slots, int p0, int p1, unsigned seed, vv_stream vst) {
+  if (!c->finalized) FAIL("vv_kv_synthetic before vv_finalize");
+  if (p0 < 0 || p1 > c->kv.max_ctx || p0 > p1) FAIL("vv_kv_synthetic: positions outside [0, max_ctx)");
+  KCHK(launch_kv_fill(c->kv, c->cfg.n_layers, c->cfg.n_kv_heads, n, slots, p0, p1, seed, (hipStream_t)vst));
   return 0;
 }
 
@@ -945,7 +953,7 @@ int vv_tp_init(vv_ctx* c, int rank, int size, const void* unique_id) {
 }
 
 int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, void* x_io, float cfg_scale,
-                        vv_stream vst) {
+                        const float* sde_noise, vv_stream vst) {
   hipStream_t st = (hipStream_t)vst;
   if (!c->finalized || c->steps == 0) FAIL("vv_diffusion_sample: engine not finalized or no schedule");
   if (n <= 0) return 0;
@@ -1010,6 +1018,8 @@ int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, 
     // final layer: modulate(norm_final(x)) -> linear -> CFG + DPM-Solver++ step on x
     DpmCoef e = c->coef[s];
     e.cfg = cfg_scale;
+    // sde-dpmsolver++: this step's [2n, D] fp32 draw; rows [0, n) update the live latents
+    const float* zs = sde_noise ? sde_noise + (size_t)s * R * D : nullptr;
     GemmArgs g = gemm_args(c, R, D, H, xh_m, W(c, "head.final_w"), EPI_STORE, rowmap(v, D));
     g.xf = xf_norm(nullptr, k.head_eps, mod, MODW, 3 * H * L, 3 * H * L + H);
     if (R <= 16) {
@@ -1018,10 +1028,11 @@ int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, 
       g.dpm.k = e;
       g.dpm.x = (bf16*)x_io;
       g.dpm.m1 = m1;
+      g.dpm.noise = zs;
       CHK(hgemm(g));
     } else {
       CHK(hgemm(g));
-      KCHK(launch_cfg_dpm(n, D, e, v, (bf16*)x_io, m1, st));
+      KCHK(launch_cfg_dpm(n, D, e, v, (bf16*)x_io, m1, zs, st));
     }
   }
   return 0;

@@ -200,6 +200,7 @@ DEV void epi_dpm(const GemmArgs& a, int n0, int lane, const float v[4]) {
       const float d1 = rb(k.inv_r0 * rb(x0 - bf(mv[i])));
       out = out - rb(k.c_d1 * d1);
     }
+    if (P.noise) out = out + k.c_n * P.noise[off + i];
     xo[i] = tobf(out);
     mo[i] = tobf(x0);
   }

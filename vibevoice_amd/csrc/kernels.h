@@ -9,6 +9,7 @@ struct DpmCoef {
   float c_x, c_d0, c_d1, inv_r0;
   int order;               // 1: x' = c_x x - bf16(c_d0 x0)
                            // 2: x' = c_x x - bf16(c_d0 x0) - bf16(c_d1 bf16(inv_r0 bf16(x0 - m1)))
+  float c_n;               // sde-dpmsolver++: + c_n * noise (fp32), added last (dpm_solver.py:680-686, 785-793)
 };
 
 struct KVLayout {
@@ -53,6 +54,7 @@ struct DpmEpi {          // EPI_CFG_DPM
   DpmCoef k;
   bf16* x;               // [n][N] latent, updated in place
   bf16* m1;              // [n][N] previous x0 (2nd-order history)
+  const float* noise;    // [n][N] this step's SDE noise rows, or nullptr (ODE)
 };
 
 struct GemmArgs {
@@ -184,10 +186,12 @@ int launch_vae_features(int rows, int D, int frames, const bf16* mean, const bf1
                         const bf16* s, const bf16* b, bf16* out, hipStream_t st);
 int launch_head_cond(int steps, int R, int H, const bf16* condp, const bf16* temb, bf16* out, hipStream_t st);
 int launch_silu(int n, const bf16* x, bf16* y, hipStream_t st);
-int launch_cfg_dpm(int n, int D, DpmCoef k, const bf16* eps, bf16* x, bf16* m1, hipStream_t st);
+int launch_cfg_dpm(int n, int D, DpmCoef k, const bf16* eps, bf16* x, bf16* m1, const float* noise, hipStream_t st);
 int launch_gather_rows(int n, int C, const bf16* src, long long lds, const int* idx, RowMap dst, hipStream_t st);
 int attn_plan(int nq, int nkv, int max_len, int* chunk);
 int launch_attn(AttnArgs a, hipStream_t st);
+int launch_kv_fill(KVLayout kv, int n_layers, int nkv, int n, const int* slots, int p0, int p1, unsigned seed,
+                   hipStream_t st);
 int launch_kv_copy(KVLayout kv, int n_layers, int nkv, int n, const int* slots, const int* src, const int* dst,
                    hipStream_t st);
 int launch_final_head(int R, int H, const bf16* h, const int* idx, const bf16* norm_w, float eps, bf16* hidden_out,

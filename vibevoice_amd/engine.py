@@ -115,6 +115,12 @@ class Engine:
         _lib.check(_lib.lib().vv_set_valid_ids(self.h, len(ids), arr), "set_valid_ids")
         self.n_valid = len(ids)
 
+    def set_schedule(self, schedule):
+        """Replace the solver (model.model.noise_scheduler = ...); coefficients are
+        rebuilt at the next set_steps."""
+        self.schedule = schedule
+        self.steps = None
+
     def set_steps(self, steps, stream=None):
         if steps == self.steps:
             return
@@ -176,15 +182,24 @@ class Engine:
         _lib.check(_lib.lib().vv_kv_copy(self.h, slots.shape[0], _ptr(slots), _ptr(src), _ptr(dst), _stream(stream)),
                    "kv_copy")
 
+    def kv_synthetic(self, slots, p0, p1, seed=0, stream=None):
+        """Benchmarks only: deterministic pseudo-random K/V at positions [p0, p1)."""
+        _lib.check(_lib.lib().vv_kv_synthetic(self.h, slots.shape[0], _ptr(slots), int(p0), int(p1), int(seed) & 0xffffffff,
+                                              _stream(stream)), "kv_synthetic")
+
     def embed(self, ids, out=None, stream=None):
         if out is None:
             out = torch.empty(ids.shape[0], self.hidden, dtype=torch.bfloat16, device=self.device)
         _lib.check(_lib.lib().vv_embed(self.h, ids.shape[0], _ptr(ids), _ptr(out), _stream(stream)), "embed")
         return out
 
-    def diffusion_sample(self, pos_h, neg_h, x_io, cfg_scale, stream=None):
+    def diffusion_sample(self, pos_h, neg_h, x_io, cfg_scale, sde_noise=None, stream=None):
+        """sde_noise: [steps, 2n, latent] fp32 per-step draws (sde-dpmsolver++ only)."""
+        if self.schedule.sde != (sde_noise is not None):
+            raise ValueError("sde_noise must be given exactly when the schedule is sde-dpmsolver++")
         _lib.check(_lib.lib().vv_diffusion_sample(self.h, pos_h.shape[0], _ptr(pos_h), _ptr(neg_h), _ptr(x_io),
-                                                  float(cfg_scale), _stream(stream)), "diffusion_sample")
+                                                  float(cfg_scale), _ptr(sde_noise), _stream(stream)),
+                   "diffusion_sample")
         return x_io
 
     def codec_step(self, slots, latent, audio_out, sem_out=None, embeds_out=None, embed_rows=None, stream=None):

@@ -57,6 +57,18 @@ class _ModelView:
     def noise_scheduler(self):
         return self._o.engine.schedule
 
+    @noise_scheduler.setter
+    def noise_scheduler(self, sched):
+        """gradio_demo.py:114-119 swaps in sde-dpmsolver++ via from_config, then calls
+        set_ddpm_inference_steps; captured graphs of the old solver are dropped."""
+        from .schedule import Schedule
+        if not isinstance(sched, Schedule):
+            raise TypeError("noise_scheduler must be built with noise_scheduler.from_config(...)")
+        torch.cuda.synchronize(self._o.device)    # graphs may still be executing: drain before freeing them
+        self._o.engine.set_schedule(sched)
+        self._o._graph_cache.clear()
+        self._o._graph_seen.clear()
+
 
 def load_state_dict(path):
     """Safetensors shards of a HF checkpoint dir (loaded with the safe loader only)."""
@@ -311,7 +323,13 @@ class GenerateSession:
         for k, v in sb.items():
             setattr(self, k, v)
         self.use_graphs = kwargs.get("use_graphs", model.use_graphs)
-        self.speculate = kwargs.get("speculate", True)
+        # sde-dpmsolver++ draws its per-step noise from the device generator
+        # (dpm_solver.py:985-987), which a missed speculation could not rewind
+        self.sde = eng.schedule.sde
+        self.speculate = kwargs.get("speculate", True) and not self.sde
+        if self.sde:
+            self.sde_buf = torch.empty(eng.steps * 2 * B * model.config.acoustic_vae_dim, device=dev,
+                                       dtype=torch.float32)
         self.spec_miss = 0
         self.logits_ready = torch.cuda.Event()
         self.graphs = model._graph_cache
@@ -332,6 +350,22 @@ class GenerateSession:
         eng.lm_forward(step_in, tok_slot.to(**i32), tok_pos.to(**i32), out_idx.to(**i32), hidden_out=self.hid,
                        logits_out=self.logits, max_pos=int(tok_pos.max()))
 
+    def extend_context(self, n_pos, seed=0):
+        """Benchmarks only: grow every positive row's
+        context to n_pos positions with synthetic K/V (vv_kv_synthetic) instead of
+        a long prefill, so decode is timed attending n_pos keys.  Positions stay
+        consistent (cache index == RoPE position); the values are not a
+        reference computation."""
+        i32 = dict(device=self.dev, dtype=torch.int32)
+        for b in range(self.B):
+            p0 = int(self.pos_len[b])
+            if n_pos <= p0:
+                continue
+            if n_pos + self.max_steps + 2 > self.eng.max_ctx:
+                raise RuntimeError(f"extend_context({n_pos}) needs max_ctx >= {n_pos + self.max_steps + 2}")
+            self.eng.kv_synthetic(torch.tensor([b], **i32), p0, n_pos, seed=seed + b)
+            self.pos_len[b] = n_pos
+
     # ---------------------------------------------------------------- device phases
     def _replay(self, key, fn):
         """Run `fn` (device work only, on static buffers).  With graphs on, the
@@ -339,7 +373,7 @@ class GenerateSession:
         eagerly so every kernel is loaded) and later ones replay it."""
         if not self.use_graphs:
             return fn()
-        full = (self.B, self.m.engine.steps, float(self.cfg_scale)) + key
+        full = (self.B, self.m.engine.steps, float(self.cfg_scale), self.sde) + key
         g = self.graphs.get(full)
         if g is None:
             if full not in self.seen:
@@ -372,7 +406,13 @@ class GenerateSession:
             else:   # one gather keeps [pos | neg] adjacent (used in place by the engine)
                 both = self.hid.index_select(0, torch.cat([d, d + B]))
                 pos_h, neg_h = both[:n], both[n:]
-            eng.diffusion_sample(pos_h, neg_h, self.noise_dev[:n], self.cfg_scale)
+            z = None
+            if self.sde:   # one [2n, latent] fp32 draw per step, in step order (randn_tensor, :985-987)
+                S, D = eng.steps, self.m.config.acoustic_vae_dim
+                z = self.sde_buf[:S * 2 * n * D].view(S, 2 * n, D)
+                for s in range(S):
+                    torch.randn(2 * n, D, device=self.dev, dtype=torch.float32, out=z[s])
+            eng.diffusion_sample(pos_h, neg_h, self.noise_dev[:n], self.cfg_scale, sde_noise=z)
         self._replay(("diff", n), body)
 
     def _post_phase(self, n):
