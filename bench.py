@@ -77,7 +77,7 @@ def bytes_per_token(wb, cfg, B, S, ctx_pos, ctx_neg):
 
 
 # ------------------------------------------------------------------ dominant kernel, live
-ROOF_KERNEL = "k_gemv1<4, 1>"      # U = 4 chunks in flight, XF_NORM; 2-wave groups (gemm.hip gemv_plan)
+ROOF_KERNEL = "k_gemv1<4, 1, false>"   # U = 4 chunks in flight, XF_NORM, non-temporal weights; 2-wave groups (gemm.hip gemv_plan)
 PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
 
 

@@ -1,4 +1,4 @@
-"""HBM traffic of bench.py's roofline kernel (the LM gate|up GEMV, k_gemv1<4, 1>,
+"""HBM traffic of bench.py's roofline kernel (the LM gate|up GEMV, k_gemv1<4, 1, false>,
 M=2 N=17920 K=1536 at 1.5B, B=1) from rocprofv3 PMC counters, collected the way
 MI355X_MICROARCH.md "HBM" / "rocprofv3 PMC slots" prescribe: FETCH_SIZE and
 WRITE_SIZE in separate passes (they do not fit one TCC pass), FETCH_SIZE
@@ -19,7 +19,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-KERNEL = "k_gemv1<4, 1>"
+KERNEL = "k_gemv1<4, 1, false>"
 M, N, K, NL = 2, 17920, 1536, 28
 
 
