@@ -166,6 +166,10 @@ int vv_attention_bf16(int nq, int nh, int nkv, const void* q, const void* k_cach
  * target waves per launch, weight chunks in flight per wave (2/4/8).
  * 0 / -1 restore the built-in plan. */
 int vv_gemv_tune(int nw, int ks, int handoff, int target_waves, int u);
+/* Tuning hook (benchmarks only): 16-row weight tiles per workgroup of the
+ * M <= 16 GEMV (the waves split into tpw groups that share one staging of the
+ * A rows); 0 restores the built-in plan. */
+int vv_gemv_tune_tpw(int tpw);
 /* Diagnostic (benchmarks only): M <= 16 GEMV launches write 4 s_memrealtime
  * stamps per workgroup (start, A staged, weights streamed, epilogue stored) to
  * buf (uint64[grid * 4]); NULL turns it off. */

@@ -105,3 +105,21 @@ def test_fused_rmsnorm_producer(M, N, K, weighted):
     e = rel_err(Y, ref)
     print(M, N, K, e)
     assert e < 4e-3
+
+
+@pytest.mark.parametrize("tpw", [0, 1, 2, 4, 8])
+@pytest.mark.parametrize("M,N,epi", [(16, 8208, "store"), (8, 8192, "res"), (12, 17920, "silu_mul"),
+                                     (2, 2064, "store")])
+def test_gemv_tiles_per_workgroup(tpw, M, N, epi):
+    """k_gemv1 with several 16-row weight tiles per workgroup sharing one A
+    staging (vv_gemv_tune_tpw; 0 = built-in plan), incl. a ragged last group
+    (N = 8208: 513 tiles) and waves that own no tile."""
+    L = _lib.lib()
+    L.vv_gemv_tune(8, 0, -1, 0, 0)
+    L.vv_gemv_tune_tpw(tpw)
+    try:
+        Y, ref = run(M, N, 1536, epi, bias=epi == "store", res=epi == "res")
+    finally:
+        L.vv_gemv_tune(0, 0, -1, 0, 0)
+        L.vv_gemv_tune_tpw(0)
+    assert rel_err(Y, ref) < 5e-3 and max_rel(Y, ref) < 3e-2

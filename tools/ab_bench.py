@@ -11,7 +11,10 @@ from vibevoice_amd import _lib  # noqa: E402
 
 name, val = sys.argv[1], sys.argv[2]
 if name == "lib":
+    import ctypes
     _lib.LIB_PATH = os.path.abspath(val)
+    probe = ctypes.CDLL(_lib.LIB_PATH)     # an older build may lack newer (diagnostic) exports
+    _lib.EXPORTS = [e for e in _lib.EXPORTS if hasattr(probe, e[0])]
     _lib.lib()
 else:
     getattr(_lib.lib(), "vv_" + name)(int(val))

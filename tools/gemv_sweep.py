@@ -18,7 +18,9 @@ from vibevoice_amd import _lib  # noqa: E402
 from vibevoice_amd.weights import mfma_pack, mfma_unpack  # noqa: E402
 
 SHAPES_NORM = [("lm.qkv+norm", 2, 2048, 1536, "store"), ("lm.gu+norm", 2, 17920, 1536, "silu_mul"),
-               ("head.gu+norm", 2, 9216, 1536, "silu_mul"), ("codec.fc1+norm", 1, 8192, 2048, "gelu")]
+               ("head.gu+norm", 2, 9216, 1536, "silu_mul"), ("codec.fc1+norm", 1, 8192, 2048, "gelu"),
+               ("lm.gu.b8+norm", 16, 17920, 1536, "silu_mul"), ("head.gu.b8+norm", 16, 9216, 1536, "silu_mul"),
+               ("lm.qkv.b8+norm", 16, 2048, 1536, "store"), ("lm.gu.b4+norm", 8, 17920, 1536, "silu_mul")]
 SHAPES = [  # name, M, N, K, epi
     ("lm.qkv", 2, 2048, 1536, "store"), ("lm.o", 2, 1536, 1536, "res"), ("lm.gu", 2, 17920, 1536, "silu_mul"),
     ("lm.down", 2, 1536, 8960, "res"), ("head.ada", 2, 21504, 1536, "store"), ("head.gu", 2, 9216, 1536, "silu_mul"),
@@ -112,30 +114,35 @@ def main():
             torch.cuda.synchronize()
             return ((Y.float() - ref).norm() / ref.norm()).item()
 
-        configs = [(0, 0, -1, 0, 0)]
-        if not quick:
-            configs += [(nw, 1, 1, 0, u) for nw, u in itertools.product((1, 2, 4, 8), (2, 4, 8))]
+        configs = [(0, 0, -1, 0, 0, 0)]
+        if "--tpw" in sys.argv:   # tiles per workgroup x waves x chunks in flight
+            configs += [(nw, 1, 1, 0, u, t) for nw, u, t in itertools.product((2, 4, 8), (2, 4, 8), (1, 2, 4, 8))
+                        if nw % t == 0]
+        elif not quick:
+            configs += [(nw, 1, 1, 0, u, 0) for nw, u in itertools.product((1, 2, 4, 8), (2, 4, 8))]
         best = None
         # two passes, min per config: the first launches of a shape run on a cold clock
         times = {}
         for _ in range(2):
             for cf in configs:
-                L.vv_gemv_tune(*cf)
+                L.vv_gemv_tune(*cf[:5])
+                L.vv_gemv_tune_tpw(cf[5])
                 try:
                     t = measure()
                 except RuntimeError:
                     continue
                 times[cf] = min(times.get(cf, 1e9), t)
-        for nw, ks, h, tw, u in configs:
+        for nw, ks, h, tw, u, tp in configs:
             L.vv_gemv_tune(nw, ks, h, tw, u)
+            L.vv_gemv_tune_tpw(tp)
             try:
                 err = check()
-                us = times[(nw, ks, h, tw, u)]
+                us = times[(nw, ks, h, tw, u, tp)]
             except (RuntimeError, KeyError) as e:
                 print(name, (nw, ks, h, tw), "error", e)
                 continue
             gbs = (N * K * 2 + M * K * 2 + M * outN * 2) / us / 1e3
-            rec = dict(shape=name, M=M, N=N, K=K, nw=nw, ks=ks, handoff=h, target=tw, u=u, us=round(us, 2),
+            rec = dict(shape=name, M=M, N=N, K=K, nw=nw, ks=ks, handoff=h, target=tw, u=u, tpw=tp, us=round(us, 2),
                        gbs=round(gbs, 1), err=err)
             results.append(rec)
             ok = err < 1e-2
@@ -144,6 +151,7 @@ def main():
             if not ok:
                 print("BAD", json.dumps(rec), flush=True)
         L.vv_gemv_tune(0, 0, -1, 0, 0)
+        L.vv_gemv_tune_tpw(0)
         if best is None:
             print(name, "no valid configuration")
             continue
@@ -151,7 +159,7 @@ def main():
                 and r["handoff"] == -1][0]
         print(f"{name:12s} M={M:2d} N={N:6d} K={K:5d} default {dflt['us']:7.2f} us {dflt['gbs']:7.1f} GB/s | "
               f"best {best['us']:7.2f} us {best['gbs']:7.1f} GB/s nw={best['nw']} ks={best['ks']} "
-              f"u={best['u']}", flush=True)
+              f"u={best['u']} tpw={best['tpw']}", flush=True)
         del Ws
         torch.cuda.empty_cache()
     os.makedirs("gpurun_out", exist_ok=True)

@@ -57,6 +57,7 @@ EXPORTS = [
     ("vv_gemm_bf16_norm", I, [I, I, I, P, I64, P, F, P, I, P, I64, P, P]),
     ("vv_attention_bf16", I, [I, I, I, P, P, P, I64, I64, P, P, I, P, P, P]),
     ("vv_gemv_tune", I, [I, I, I, I, I]),
+    ("vv_gemv_tune_tpw", I, [I]),
     ("vv_gemv_stamps", I, [P]),
     ("vv_attn_stamps", I, [P]),
     ("vv_codec_mix_fusion", I, [I]),

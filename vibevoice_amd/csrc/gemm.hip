@@ -334,7 +334,7 @@ DEV bool splitk_handoff(const GemmArgs& a, float* red, int TILE, unsigned* last_
 // M <= 16: the workgroup's A rows (its K range, transformed) are staged once in
 // LDS; each wave streams its weight chunks with a two-deep register ping-pong
 // (U chunks = U KB per wave in flight while the previous U are multiplied).
-template <int U, int XF, bool KEEP = false>
+template <int U, int XF, bool KEEP = false, int TPW = 1>
 __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ float inv_s[16];
@@ -343,14 +343,25 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   stamp(a, 0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, NW = blockDim.x >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int n0 = blockIdx.x * 16;
+  // The workgroup owns TPW consecutive 16-row weight tiles and stages the A
+  // rows once for all of them (at M = 16 one tile per workgroup re-read the
+  // whole A block per 16 weight rows: as many L2 bytes as weight bytes, and the
+  // LDS it needed capped residency at 2 workgroups per CU).  Waves are
+  // tile-major: wave = tile_in_group * KW + k-slice.
+  const int KW = TPW == 1 ? NW : NW / TPW;
+  const int tw = TPW == 1 ? 0 : wave / KW, kwv = TPW == 1 ? wave : wave - tw * KW;
+  const int ntile = a.N >> 4;
+  const int tile = blockIdx.x * TPW + tw;
+  const bool tile_ok = TPW == 1 || tile < ntile;
   const int nchunk = a.K >> 5;
   // this workgroup's chunk range, then each wave's
   const int b0 = (int)((long long)nchunk * blockIdx.y / a.ksplit);
   const int b1 = (int)((long long)nchunk * (blockIdx.y + 1) / a.ksplit);
-  const int c0 = b0 + (int)((long long)(b1 - b0) * wave / NW);
-  const int c1 = b0 + (int)((long long)(b1 - b0) * (wave + 1) / NW);
-  const bf16* wrow = a.w + (long long)(n0 >> 4) * a.K * 16 + lane * 8;  // MFMA-packed W
+  const int c0 = b0 + (int)((long long)(b1 - b0) * kwv / KW);
+  const int c1 = tile_ok ? b0 + (int)((long long)(b1 - b0) * (kwv + 1) / KW) : c0;
+  // MFMA-packed W (a wave past the last tile streams nothing; its clamped
+  // prologue loads read tile 0)
+  const bf16* wrow = a.w + (long long)(tile_ok ? tile : 0) * a.K * 16 + lane * 8;
   const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
 
   // ---- A staging into LDS (rows [0, M) x chunks [b0, b1), row stride padded
@@ -640,24 +651,25 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   }
   stamp(a, 2);
 
-  // ---- reduce the waves of this workgroup
+  // ---- reduce each tile's K-slice waves (tile t's sum lands in slab t * KW)
 #pragma unroll
   for (int i = 0; i < 4; ++i) red[(wave * 4 + i) * 64 + lane] = acc[i];
   __syncthreads();
-  if (NW > 1) {
-    for (int e = threadIdx.x; e < 256; e += blockDim.x) {
+  if (KW > 1) {
+    for (int e = threadIdx.x; e < TPW * 256; e += blockDim.x) {
+      const int base = (e >> 8) * KW * 256 + (e & 255);
       float s = 0.f;
-      for (int w = 1; w < NW; ++w) s += red[w * 256 + e];
-      red[e] += s;
+      for (int w = 1; w < KW; ++w) s += red[base + w * 256];
+      red[base] += s;
     }
     __syncthreads();
   }
-  if (a.ksplit > 1 && !splitk_handoff(a, red, 256, &last_flag)) return;
-  if (wave == 0) {
+  if (a.ksplit > 1 && !splitk_handoff(a, red, 256, &last_flag)) return;   // host: ksplit > 1 => TPW == 1
+  if (wave < TPW && (TPW == 1 || blockIdx.x * TPW + wave < ntile)) {
     float v[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = red[i * 64 + lane];
-    epi_tile(a, r, n0, lane, v);
+    for (int i = 0; i < 4; ++i) v[i] = red[wave * KW * 256 + i * 64 + lane];
+    epi_tile(a, r, (blockIdx.x * TPW + wave) * 16, lane, v);
     if (a.stamps) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       stamp(a, 3);
@@ -828,7 +840,7 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
 }
 
 // ------------------------------------------------------------------ host launch
-static int g_tune_nw = 0, g_tune_ks = 0, g_tune_handoff = -1, g_tune_waves = 0, g_tune_u = 0;
+static int g_tune_nw = 0, g_tune_ks = 0, g_tune_handoff = -1, g_tune_waves = 0, g_tune_u = 0, g_tune_tpw = 0;
 static unsigned long long* g_stamps = nullptr;
 static const bool g_shape_log = getenv("VV_GEMM_LOG") != nullptr;
 
@@ -847,7 +859,13 @@ extern "C" int vv_gemv_tune(int nw, int ks, int handoff, int target_waves, int u
   return 0;
 }
 
-struct GemmPlan { int nw, ksplit, u; };
+// diagnostic: force k_gemv1's tiles per workgroup (0: plan)
+extern "C" int vv_gemv_tune_tpw(int tpw) {
+  g_tune_tpw = tpw;
+  return 0;
+}
+
+struct GemmPlan { int nw, ksplit, u, tpw; };
 
 // Measured on MI355X (tools/gemv_sweep.py two-pass min, profiles/r01_gemv_sweep*.txt).
 // NO cross-workgroup split-K (a hand-off costs >= 2 us in the sc1 form, up to
@@ -860,10 +878,13 @@ struct GemmPlan { int nw, ksplit, u; };
 //   * 16 < M <= 64 (k_gemv): 4 waves, 1 for >= 1024 tiles (the batched head
 //     adaLN, M = 2 x 10 steps: 35 -> 20.5 us)
 //   * few tiles, short rows (qkv, o_proj): 4 x 8, all chunks in flight at once
-//   * 8 <= M <= 16 otherwise: 8 x 2
+//   * 8 <= M <= 16 otherwise: 8 x 2; with many tiles the workgroup owns tpw
+//     tiles that share one staging of the A rows (tools/gemv_sweep.py --tpw,
+//     profiles/r01_gemv_sweep_tpw.txt: B = 8 LM gate|up 30.5 -> 20.0 us, head
+//     gate|up 4 tiles per group 15.6 us)
 static GemmPlan gemv_plan(int N, int K, int M) {
   const int chunks = K / 32, tiles = N / 16;
-  int nw = 4, ks = 1, u = 4;
+  int nw = 4, ks = 1, u = 4, tpw = 1;
   if (tiles <= 128 && chunks >= 128) {
     if (M >= 8) nw = 4;
     else if (tiles == 128 && chunks >= 256) u = 8;
@@ -873,6 +894,13 @@ static GemmPlan gemv_plan(int N, int K, int M) {
   } else if (M >= 8) {
     nw = 8;
     u = 2;
+    if (tiles >= 1024) {  // many tiles: 8 tiles per workgroup (one wave each) share one A staging
+      tpw = 8;
+      u = M > 8 ? 4 : 8;
+    } else if (tiles >= 512) {
+      tpw = 4;
+      u = 4;
+    }
   } else if (tiles >= 1024) {
     nw = 2;
   } else if (tiles <= 128) {
@@ -889,8 +917,9 @@ static GemmPlan gemv_plan(int N, int K, int M) {
   if (g_tune_nw > 0) nw = g_tune_nw;
   if (g_tune_ks > 0) ks = g_tune_ks;
   if (g_tune_u > 0) u = g_tune_u;
+  if (g_tune_tpw > 0) tpw = g_tune_tpw;
   if (ks > chunks) ks = chunks;
-  return {nw, ks, u};
+  return {nw, ks, u, tpw};
 }
 
 static int max_waves(int) { return 8; }
@@ -900,6 +929,21 @@ static bool gemv1_fits(const GemmArgs& a) {
   const int nchunk = a.K >> 5;
   const size_t kw = ((nchunk + a.ksplit - 1) / a.ksplit) * 32;
   return (((size_t)a.M * (kw + 8) * 2 + 15) & ~(size_t)15) + (size_t)a.M * (kw / 8) * 4 <= 65536;
+}
+
+// TPW is a template argument so the one-tile form (every M < 8 launch) keeps
+// its straight-line index math (a runtime tiles-per-group cost 1 us per launch)
+template <int XF, int TPW>
+static void launch_gemv1(const GemmArgs& a, int u, dim3 grid, dim3 block, size_t lds, hipStream_t st) {
+  if (a.keep) {
+    if (u == 4) hipLaunchKernelGGL((k_gemv1<4, XF, true, TPW>), grid, block, lds, st, a);
+    else if (u == 2) hipLaunchKernelGGL((k_gemv1<2, XF, true, TPW>), grid, block, lds, st, a);
+    else hipLaunchKernelGGL((k_gemv1<8, XF, true, TPW>), grid, block, lds, st, a);
+  } else {
+    if (u == 4) hipLaunchKernelGGL((k_gemv1<4, XF, false, TPW>), grid, block, lds, st, a);
+    else if (u == 2) hipLaunchKernelGGL((k_gemv1<2, XF, false, TPW>), grid, block, lds, st, a);
+    else hipLaunchKernelGGL((k_gemv1<8, XF, false, TPW>), grid, block, lds, st, a);
+  }
 }
 
 template <int XF>
@@ -913,15 +957,10 @@ static void launch_gemv_xf(const GemmArgs& a, int mrep, int u, dim3 grid, dim3 b
     const int kw = ((nchunk + a.ksplit - 1) / a.ksplit) * 32;
     const size_t xs_bytes = ((size_t)a.M * (kw + 8) * sizeof(bf16) + 15) & ~(size_t)15;
     const size_t lds = xs_bytes + (size_t)a.M * (kw / 8) * sizeof(float);
-    if (a.keep) {
-      if (u == 4) hipLaunchKernelGGL((k_gemv1<4, XF, true>), grid, block, lds, st, a);
-      else if (u == 2) hipLaunchKernelGGL((k_gemv1<2, XF, true>), grid, block, lds, st, a);
-      else hipLaunchKernelGGL((k_gemv1<8, XF, true>), grid, block, lds, st, a);
-    } else {
-      if (u == 4) hipLaunchKernelGGL((k_gemv1<4, XF>), grid, block, lds, st, a);
-      else if (u == 2) hipLaunchKernelGGL((k_gemv1<2, XF>), grid, block, lds, st, a);
-      else hipLaunchKernelGGL((k_gemv1<8, XF>), grid, block, lds, st, a);
-    }
+    if (a.tpw == 1) launch_gemv1<XF, 1>(a, u, grid, block, lds, st);
+    else if (a.tpw == 2) launch_gemv1<XF, 2>(a, u, grid, block, lds, st);
+    else if (a.tpw == 4) launch_gemv1<XF, 4>(a, u, grid, block, lds, st);
+    else launch_gemv1<XF, 8>(a, u, grid, block, lds, st);
     return;
   }
   switch (mrep) {
@@ -974,7 +1013,10 @@ int launch_gemm(GemmArgs a, hipStream_t st) {
     a.ksplit = p.ksplit;
     if (a.ksplit > 1 && (!a.ws || !a.counters || a.N / 16 > 65536)) a.ksplit = 1;
     a.handoff = g_tune_handoff >= 0 ? g_tune_handoff : 1;
-    dim3 grid(a.N / 16, a.ksplit), block(64 * p.nw);
+    a.tpw = 1;
+    if (mrep == 1 && a.ksplit == 1 && a.xf.kind != XF_MIX && (p.tpw == 2 || p.tpw == 4 || p.tpw == 8) && p.nw % p.tpw == 0 && gemv1_fits(a))
+      a.tpw = p.tpw;
+    dim3 grid((a.N / 16 + a.tpw - 1) / a.tpw, a.ksplit), block(64 * p.nw);
     if (a.xf.kind == XF_MIX) {
       const size_t lds = gemv_mix_lds(a.M, a.xf.T, a.K);
       if (mrep != 1 || a.ksplit != 1 || !lds || (64 * p.nw) % (a.K / 8) || a.xf.ctx != 6) return 1;

@@ -61,7 +61,7 @@ struct GemmArgs {
   int M, N, K;
   int ksplit;
   int handoff;            // split-K hand-off form (gemm.hip: splitk_handoff)
-  int pad_;
+  int tpw;                // k_gemv1: 16-row weight tiles per workgroup (set by launch_gemm)
   RowMap a;
   const bf16* w;
   long long ldw;
