@@ -290,6 +290,69 @@ def g7_qwen2():
     save("g7_qwen2.npz", **out)
 
 
+# ---------------------------------------------------------------- G9 processor
+PROC_SCRIPTS = [
+    "Speaker 1: Hello there, welcome to the show.\nSpeaker 2: It's great to be here!\n\nSpeaker 1:   Fine, thanks.",
+    "Speaker 0: Today we talk about podcasts.\nnot a speaker line\nSpeaker 0: How are you doing?",
+]
+PROC_JSON = '[{"speaker": "1", "text": " Hello there. "}, {"speaker": "x", "text": "skip"}, {"speaker": 2, "text": "Hi"}]'
+PROC_TXT = "Speaker 2: first\nplain line here\n\nspeaker 3 :  third  \nSpeaker 4:\n"
+
+
+def g9_processor():
+    """VibeVoiceProcessor (vibevoice/processor/vibevoice_processor.py) with the
+    reference's own VibeVoiceTextTokenizerFast over the tiny Qwen2-style
+    vocabulary (tiny_tokenizer.py; the real Qwen2.5 files are not available
+    offline): batches with ragged voice prompts (dBFS normalisation, frame
+    counts, left padding), a single script, no voices, no padding, and the
+    .json / .txt script converters."""
+    import json
+    import tempfile
+    import tiny_tokenizer
+    from vibevoice.processor.vibevoice_processor import VibeVoiceProcessor
+    from vibevoice.processor.vibevoice_tokenizer_processor import VibeVoiceTokenizerProcessor
+    from vibevoice.modular.modular_vibevoice_text_tokenizer import VibeVoiceTextTokenizerFast
+    tok = VibeVoiceTextTokenizerFast.from_pretrained(tiny_tokenizer.DIR)
+    proc = VibeVoiceProcessor(tokenizer=tok, audio_processor=VibeVoiceTokenizerProcessor())
+    rng = np.random.default_rng(9)
+    voices = [(0.3 * rng.standard_normal(n)).astype(np.float32) for n in (7000, 12345, 3200, 640)]
+    voices[2][:10] = 4.0                                   # clips after normalisation: avoid_clipping path
+    out = {f"voice{i}": v for i, v in enumerate(voices)}
+    out["scripts"] = np.array(PROC_SCRIPTS)
+    out["ids"] = np.array([tok.speech_start_id, tok.speech_end_id, tok.speech_diffusion_id, tok.eos_token_id,
+                           tok.pad_id])
+    cases = {
+        "a": dict(text=PROC_SCRIPTS, voice_samples=[[voices[0], voices[1]], [voices[2]]], padding=True,
+                  return_tensors="pt"),
+        "b": dict(text=PROC_SCRIPTS[0], voice_samples=[voices[3], voices[1], voices[0]], return_tensors="pt"),
+        "c": dict(text=PROC_SCRIPTS, padding=True, return_tensors="pt"),
+    }
+    for tag, kw in cases.items():
+        be = proc(**kw)
+        for k in ("input_ids", "attention_mask", "speech_input_mask", "speech_tensors", "speech_masks"):
+            v = be.get(k)
+            if v is not None:
+                out[f"{tag}_{k}"] = v.numpy()
+        out[f"{tag}_parsed"] = np.array(json.dumps(be["parsed_scripts"]))
+        out[f"{tag}_speakers"] = np.array(json.dumps(be["all_speakers_list"]))
+    be = proc(text=PROC_SCRIPTS, padding=False, return_tensors=None)            # ragged python lists
+    out["d_lengths"] = np.array([len(x) for x in be["input_ids"]])
+    out["d_input_ids"] = np.concatenate([np.array(x) for x in be["input_ids"]])
+    out["d_attention_mask"] = np.concatenate([np.array(x) for x in be["attention_mask"]])
+    with tempfile.TemporaryDirectory() as d:
+        pj, pt = os.path.join(d, "s.json"), os.path.join(d, "s.txt")
+        with open(pj, "w") as f:
+            f.write(PROC_JSON)
+        with open(pt, "w") as f:
+            f.write(PROC_TXT)
+        out["json_src"], out["txt_src"] = np.array(PROC_JSON), np.array(PROC_TXT)
+        out["json_script"] = np.array(proc._convert_json_to_script(pj))
+        out["txt_script"] = np.array(proc._convert_text_to_script(pt))
+        be = proc(text=[pj, pt], padding=True, return_tensors="pt")
+        out["e_input_ids"] = be["input_ids"].numpy()
+    save("g9_processor.npz", **out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     if len(sys.argv) > 1:                        # regenerate selected fixtures: make_golden.py g1_sde_scheduler

@@ -150,3 +150,47 @@ def test_noise_scheduler_swap_sde():
     assert not torch.equal(outs[0].speech_outputs[0].cpu(), ode.speech_outputs[0].cpu())
     with pytest.raises(NotImplementedError):
         ns.from_config(ns.config, algorithm_type="dpmsolver")
+
+
+def test_processor_to_generate_with_audio_streamer():
+    """demo/inference_from_file.py's path end to end on a tiny model: the
+    product VibeVoiceProcessor (tiny Qwen2-style vocabulary, voice prompts of
+    ragged lengths; speech_tok_compress_ratio = the tiny codec's hop) -> the
+    engine's generate() with the product AudioStreamer.  Every streamed chunk
+    equals speech_outputs, sequences extend input_ids, and the voice latents
+    change the result (the prefill splice is live)."""
+    import numpy as np
+    from vibevoice_amd.processor import VibeVoiceProcessor, VibeVoiceTextTokenizerFast
+    from vibevoice_amd.streamer import AudioStreamer
+    tok_dir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "tiny_qwen_tokenizer")
+    tk = VibeVoiceTextTokenizerFast.from_pretrained(tok_dir)
+    cfg = tiny_config(hidden=256, layers=2, heads=2, kv_heads=1, inter=512)
+    sd = synthetic_state_dict(cfg, seed=12, device="cpu", mode="test", with_acoustic_encoder=True)
+    m = VibeVoiceForConditionalGenerationInference(cfg, sd, dev, max_batch=2, max_ctx=512)
+    m.set_ddpm_inference_steps(3)
+    proc = VibeVoiceProcessor(tokenizer=tk, speech_tok_compress_ratio=m.engine.hop)
+    rng = np.random.default_rng(5)
+    v = [(0.2 * rng.standard_normal(n)).astype(np.float32) for n in (37, 20)]
+    scripts = ["Speaker 1: Hello there.\nSpeaker 2: Hi!", "Speaker 1: Fine, thanks."]
+    inputs = proc(text=scripts, voice_samples=[[v[0], v[1]], [v[1]]], padding=True, return_tensors="pt")
+    d = tk.speech_diffusion_id
+    sched = [[d] * 4 + [tk.eos_token_id], [d] * 2 + [tk.speech_end_id, tk.eos_token_id]]
+
+    def run(streamer, voices=True):
+        kw = dict(inputs)
+        if not voices:
+            kw["speech_tensors"] = torch.zeros_like(kw["speech_tensors"])
+        torch.manual_seed(7)
+        return m.generate(**kw, tokenizer=tk, cfg_scale=1.3, forced_tokens=sched, audio_streamer=streamer,
+                          generation_config={"do_sample": False}, show_progress_bar=False)
+    st = AudioStreamer(batch_size=2)
+    out = run(st)
+    L = inputs["input_ids"].shape[1]
+    assert torch.equal(out.sequences[:, :L], inputs["input_ids"])
+    assert st.finished_flags == [True, True]
+    for b, n in enumerate((4, 2)):
+        chunks = list(st.get_stream(b))
+        assert len(chunks) == n
+        assert torch.equal(torch.cat(chunks, dim=-1).reshape(-1), out.speech_outputs[b].cpu().reshape(-1))
+    silent = run(None, voices=False)
+    assert not torch.equal(silent.speech_outputs[0].cpu(), out.speech_outputs[0].cpu())
