@@ -177,6 +177,10 @@ int vv_gemv_stamps(void* buf);
 /* Diagnostic (benchmarks only): vv_attention_bf16 launches write 4 stamps per
  * workgroup (start, K/V/Q landed, keys done, output stored); NULL: off. */
 int vv_attn_stamps(void* buf);
+/* Tuning hook (benchmarks only): attention keys per split (multiple of 32;
+ * 0 = built-in) and the largest split count merged inside the attention
+ * kernel (more splits go to the separate merge pass; -1 = built-in). */
+int vv_attn_tune(int chunk, int merge_in);
 /* Test switch (bit mask, default 3): bit 0 folds each codec Block1D's mixer
  * (norm, depthwise conv, gamma residual, FFN norm) into its fc1 GEMV where
  * <= 16 rows fit (XF_MIX); bit 1 runs whole narrow-stage blocks (C <= 128) as

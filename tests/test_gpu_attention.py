@@ -2,7 +2,8 @@
 PyTorch fp32 reference (softmax(q k^T / sqrt(128)) v, GQA), at the 1.5B head
 layout (12 q / 2 kv heads) and the Large layout (28 / 4), cache in the engine's
 layout (K [slot][kv_head][ctx][128], V transposed [slot][kv_head][128][ctx]): single-workgroup
-contexts, the in-launch split merge (> 1024 keys), ragged rows sharing a
+contexts, the in-launch split merge (<= 8 splits of 64 keys), the k_attn_merge pass
+(longer), splits of 128 and 192 keys (4 and 8 waves), ragged rows sharing a
 launch, and length-1 rows.  Tolerance: rel L2 < 1e-2 (bf16 output)."""
 import ctypes
 
@@ -49,7 +50,10 @@ def reference(q, K, V, slots, pos):
 
 
 @pytest.mark.parametrize("nh,nkv,lens", [(12, 2, [1, 37, 170, 1024]), (12, 2, [1025, 3000, 64]),
-                                         (28, 4, [300, 5000]), (12, 2, [65536 // 8])])
+                                         (28, 4, [300, 5000]), (12, 2, [65536 // 8]),
+                                         (12, 2, [1, 63, 65, 200, 512]),      # <= 8 splits: in-kernel merge
+                                         (12, 2, [20000, 5]),                 # 128-key splits, 4 waves
+                                         (12, 2, [40000, 700])])              # 192-key splits, 8 waves
 def test_attention_vs_torch(nh, nkv, lens):
     eng = tiny_engine()
     g = torch.Generator(device=dev).manual_seed(sum(lens) + nh)

@@ -16,8 +16,8 @@ if name == "lib":
     probe = ctypes.CDLL(_lib.LIB_PATH)     # an older build may lack newer (diagnostic) exports
     _lib.EXPORTS = [e for e in _lib.EXPORTS if hasattr(probe, e[0])]
     _lib.lib()
-else:
-    getattr(_lib.lib(), "vv_" + name)(int(val))
+else:   # e.g. attn_tune 128,8
+    getattr(_lib.lib(), "vv_" + name)(*[int(v) for v in val.split(",")])
 sys.argv = ["bench.py"] + sys.argv[3:]
 import bench  # noqa: E402
 

@@ -17,9 +17,9 @@ from vibevoice_amd import _lib  # noqa: E402
 def main():
     eng = tiny_engine()
     L = _lib.lib()
-    for ctx in (250, 1000):
+    for ctx, stride in ((250, 250), (250, 256), (1000, 1000), (1000, 1024)):
         nq, nh, nkv, NL = 2, 12, 2, 28
-        Ks = [torch.randn(nq, nkv, ctx, 128, device="cuda").bfloat16() for _ in range(NL)]
+        Ks = [torch.randn(nq, nkv, stride, 128, device="cuda").bfloat16() for _ in range(NL)]
         Vs = [torch.randn_like(k) for k in Ks]
         q = torch.randn(nq, nh * 128, device="cuda").bfloat16()
         out = torch.empty_like(q)
@@ -30,7 +30,7 @@ def main():
         def run(i):
             L.vv_attn_stamps(ctypes.c_void_p(st[i].data_ptr()))
             _lib.check(L.vv_attention_bf16(nq, nh, nkv, ctypes.c_void_p(q.data_ptr()), ctypes.c_void_p(Ks[i].data_ptr()),
-                                           ctypes.c_void_p(Vs[i].data_ptr()), nkv * ctx * 128, ctx * 128,
+                                           ctypes.c_void_p(Vs[i].data_ptr()), nkv * stride * 128, stride * 128,
                                            ctypes.c_void_p(slots.data_ptr()), ctypes.c_void_p(pos.data_ptr()), ctx,
                                            ctypes.c_void_p(out.data_ptr()), eng.h,
                                            ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
@@ -46,10 +46,13 @@ def main():
         nwg = int((s[0, :, 0] > 0).sum())
         s = s[:, :nwg]
         first = s[:, :, 0].min(1).values
-        last = s[:, :, 3].max(1).values
-        print(f"ctx {ctx}: {nwg} workgroups/launch | span {(last - first)[1:].mean():.2f} us, gap to next "
+        done = s[:, :, 3] > 0                       # workgroups that stored output (others hand off partials)
+        s3 = torch.where(done, s[:, :, 3], s[:, :, 2])
+        last = s3.max(1).values
+        print(f"ctx {ctx} stride {stride}: {nwg} workgroups/launch | span {(last - first)[1:].mean():.2f} us, gap to next "
               f"{(first[1:] - last[:-1]).mean():.2f} us | per WG: loads {(s[:, :, 1] - s[:, :, 0]).mean():.2f} "
-              f"all waves done {(s[:, :, 2] - s[:, :, 1]).mean():.2f} merge+store {(s[:, :, 3] - s[:, :, 2]).mean():.2f} | "
+              f"all waves done {(s[:, :, 2] - s[:, :, 1]).mean():.2f} merge+store "
+              f"{(s[:, :, 3] - s[:, :, 2])[done].mean():.2f} ({int(done[0].sum())} storing WGs) | "
               f"start spread {(s[:, :, 0].max(1).values - first).mean():.2f}", flush=True)
 
 

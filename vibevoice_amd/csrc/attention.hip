@@ -14,22 +14,39 @@
 
 
 // ---------------------------------------------------------------- attention
-// Grid (query row x kv head, split); a workgroup of ATT_NW waves owns keys
-// [k0, k1) of its split and hands each wave a contiguous sub-range, merged in
-// LDS — short contexts need no cross-workgroup merge.  Per wave, 32 keys per
-// step on the matrix cores (mfma 16x16x32 bf16):
+// Grid (query row x kv head, split); a workgroup of NW waves owns keys [k0, k1)
+// of its split and hands each wave a contiguous sub-range, merged in LDS.  Per
+// wave, 32 keys per step on the matrix cores (mfma 16x16x32 bf16):
 //   S[16 heads x 16 keys] = Q[heads x 128] . K^T   (2 tiles, 4 MFMAs each; the
 //       G <= 8 query heads of the kv head are the rows, padded to 16)
 //   online softmax on S in registers (row = head spread over 16 lanes)
 //   P (bf16, as the reference's eager path rounds it) -> per-wave LDS tile ->
 //   O[heads x 128] += P[heads x 32 keys] . V[32 keys x 128] (8 MFMAs, V^T cache)
-// K / V of the next step are prefetched while the current one computes.  With
-// nsplit > 1 the splits' (m, l, O) merge in the last-arriving workgroup (agent
-// release / ticket / acquire, cdna_hip_programming.md Guideline 16).
-constexpr int ATT_NW = 8;           // waves per workgroup
-constexpr int ATT_KEYS = 1024;      // keys per workgroup before the launch splits
+// K / V of the next step are prefetched while the current one computes.
+//
+// Splits: one CU takes in K/V at only ~20-30 GB/s (tools/attn_stamps.py: 4
+// workgroups of 1,024 keys took 19 us), so long contexts are spread over up to
+// ATT_SPLITS_MAX splits of >= ATT_CHUNK keys, 8 waves x 32 keys per step.  The
+// splits' (m, l, O) merge in the last-arriving workgroup (write-through
+// partials + one ticket, no fences) for <= ATT_MERGE_IN splits, else in
+// k_attn_merge (one workgroup per query head and 64 dims: the partials of 256
+// splits are 128 KB per head, too much for one CU).  Thinner splits at short
+// contexts do not pay: the in-kernel merge costs ~6 us of dependent round
+// trips (ticket, partial loads, store) and a merge launch ~4 us, against the
+// 2-4 us the extra CUs save (plan sweep over 64-1024 keys per split x merge
+// form, tools/ab_bench.py attn_tune: all within 1.5 % at B = 1 and 8).
 constexpr int ATT_GMAX = 8;
-constexpr int ATT_KC = 64;          // per-row split granularity
+constexpr int ATT_KC = 32;            // per-row split granularity (one wave step)
+constexpr int ATT_CHUNK = 256;        // keys per split (8 waves x one 32-key step)
+constexpr int ATT_SPLITS_MAX = 256;
+constexpr int ATT_MERGE_IN = 8;       // splits merged inside k_attn
+
+// keys per split of a row with `len` keys: >= a.chunk, and all a.nsplit splits
+// cover len (k_attn and k_attn_merge must agree)
+DEV int row_chunk(const AttnArgs& a, int len) {
+  const int c = (len + a.nsplit - 1) / a.nsplit;
+  return max(a.chunk, (c + ATT_KC - 1) / ATT_KC * ATT_KC);
+}
 
 DEV f32x4 amfma(bf16x8 a, bf16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
 
@@ -38,11 +55,11 @@ DEV void astamp(const AttnArgs& a, int which) {
     a.stamps[((long long)blockIdx.y * gridDim.x + blockIdx.x) * 4 + which] = __builtin_amdgcn_s_memrealtime();
 }
 
-template <int G>
-__global__ void __launch_bounds__(64 * ATT_NW) k_attn(AttnArgs a) {
-  __shared__ float wm[ATT_NW][G], wl[ATT_NW][G];
-  __shared__ float wo[ATT_NW][G][128];
-  __shared__ __attribute__((aligned(16))) bf16 pt[ATT_NW][16][32];
+template <int G, int NW>
+__global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
+  __shared__ float wm[NW][G], wl[NW][G];
+  __shared__ float wo[NW][G][128];
+  __shared__ __attribute__((aligned(16))) bf16 pt[NW][16][32];
   __shared__ float fm[G], fl[G];
   __shared__ unsigned last_flag;
   constexpr int d = 128;
@@ -53,14 +70,13 @@ __global__ void __launch_bounds__(64 * ATT_NW) k_attn(AttnArgs a) {
   const int len = a.pos[qi] + 1;
   // this row's split size: >= a.chunk, all nsplit splits cover len; splits past
   // the row's last key exit at once
-  int chunk = (len + a.nsplit - 1) / a.nsplit;
-  chunk = max(a.chunk, (chunk + ATT_KC - 1) / ATT_KC * ATT_KC);
+  const int chunk = row_chunk(a, len);
   const int nact = (len + chunk - 1) / chunk;
   if (split >= nact) return;
   const int k0 = split * chunk;
   const int k1 = min(len, k0 + chunk);
   // this wave's keys, in 32-key steps
-  const int per = ((k1 - k0 + ATT_NW - 1) / ATT_NW + 31) / 32 * 32;
+  const int per = ((k1 - k0 + NW - 1) / NW + 31) / 32 * 32;
   const int w0 = k0 + wave * per;
   const int w1 = min(k1, w0 + per);
   const long long cbase = (long long)a.layer * a.kv.s_layer + (long long)a.slots[qi] * a.kv.s_slot +
@@ -187,22 +203,22 @@ __global__ void __launch_bounds__(64 * ATT_NW) k_attn(AttnArgs a) {
   // merge the waves: waves with no keys carry m = -inf, l = 0
   if (t < G) {
     float M = -INFINITY;
-    for (int w = 0; w < ATT_NW; ++w) M = fmaxf(M, wm[w][t]);
+    for (int w = 0; w < NW; ++w) M = fmaxf(M, wm[w][t]);
     float L = 0.f;
-    for (int w = 0; w < ATT_NW; ++w) L += wm[w][t] == -INFINITY ? 0.f : __expf(wm[w][t] - M) * wl[w][t];
+    for (int w = 0; w < NW; ++w) L += wm[w][t] == -INFINITY ? 0.f : __expf(wm[w][t] - M) * wl[w][t];
     fm[t] = M;
     fl[t] = L;
   }
   __syncthreads();
-  constexpr int NE = (G * 128 + 64 * ATT_NW - 1) / (64 * ATT_NW);
+  constexpr int NE = (G * 128 + 64 * NW - 1) / (64 * NW);
   float res[NE];
 #pragma unroll
   for (int q = 0; q < NE; ++q) {
-    const int e = t + q * 64 * ATT_NW;
+    const int e = t + q * 64 * NW;
     float sum = 0.f;
     if (e < G * d) {
       const int h = e / d, j = e - h * d;
-      for (int w = 0; w < ATT_NW; ++w)
+      for (int w = 0; w < NW; ++w)
         if (wm[w][h] != -INFINITY) sum += __expf(wm[w][h] - fm[h]) * wo[w][h][j];
     }
     res[q] = sum;
@@ -210,7 +226,7 @@ __global__ void __launch_bounds__(64 * ATT_NW) k_attn(AttnArgs a) {
   if (nact == 1) {
 #pragma unroll
     for (int q = 0; q < NE; ++q) {
-      const int e = t + q * 64 * ATT_NW;
+      const int e = t + q * 64 * NW;
       if (e < G * d) {
         const int h = e / d, j = e - h * d;
         a.out[(long long)qi * a.nh * d + (kh * G + h) * d + j] = tobf(res[q] / fl[h]);
@@ -222,49 +238,104 @@ __global__ void __launch_bounds__(64 * ATT_NW) k_attn(AttnArgs a) {
     }
     return;
   }
+  // partials: plain stores when k_attn_merge follows (the kernel boundary
+  // publishes them); else write-through (sc1, agent-scope relaxed) stores, each
+  // wave's vmcnt(0), a workgroup barrier and one ticket add; the last arriver
+  // reads them with sc1 loads.  No release / acquire fence: an agent fence
+  // writes back the XCD's whole L2 (MI355X_MICROARCH.md "publish-large", the
+  // hand-off table's first row).
+  const bool wt = !a.merge;
 #pragma unroll
   for (int q = 0; q < NE; ++q) {
-    const int e = t + q * 64 * ATT_NW;
+    const int e = t + q * 64 * NW;
     if (e < G * d) {
       const int h = e / d, j = e - h * d;
       const long long pidx = ((long long)qi * a.nh + kh * G + h) * a.nsplit + split;
-      a.part_o[pidx * d + j] = res[q];
-      if (j == 0) {
-        a.part_ml[pidx * 2] = fm[h];
-        a.part_ml[pidx * 2 + 1] = fl[h];
+      if (wt) {
+        __hip_atomic_store(a.part_o + pidx * d + j, res[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (j == 0) {
+          __hip_atomic_store(a.part_ml + pidx * 2, fm[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(a.part_ml + pidx * 2 + 1, fl[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else {
+        a.part_o[pidx * d + j] = res[q];
+        if (j == 0) {
+          a.part_ml[pidx * 2] = fm[h];
+          a.part_ml[pidx * 2 + 1] = fl[h];
+        }
       }
     }
   }
+  if (!wt) return;    // k_attn_merge runs next
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     unsigned* ctr = a.counters + blockIdx.x;
     const unsigned tk = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last_flag = tk == (unsigned)(nact - 1);
-    if (last_flag) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (last_flag) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   if (!last_flag) return;
   // merge the splits: out = sum_s e^{m_s - M} o_s / sum_s e^{m_s - M} l_s
-  for (int e = t; e < G * d; e += 64 * ATT_NW) {
+  auto ld = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  for (int e = t; e < G * d; e += 64 * NW) {
     const int h = e / d, j = e - h * d;
     const long long p0 = ((long long)qi * a.nh + kh * G + h) * a.nsplit;
+    float mv[ATT_MERGE_IN], lv[ATT_MERGE_IN], ov[ATT_MERGE_IN];
+#pragma unroll
+    for (int s2 = 0; s2 < ATT_MERGE_IN; ++s2) {
+      if (s2 < nact) {
+        mv[s2] = ld(a.part_ml + (p0 + s2) * 2);
+        lv[s2] = ld(a.part_ml + (p0 + s2) * 2 + 1);
+        ov[s2] = ld(a.part_o + (p0 + s2) * d + j);
+      }
+    }
     float M = -INFINITY;
-    for (int s2 = 0; s2 < nact; ++s2) M = fmaxf(M, a.part_ml[(p0 + s2) * 2]);
+#pragma unroll
+    for (int s2 = 0; s2 < ATT_MERGE_IN; ++s2)
+      if (s2 < nact) M = fmaxf(M, mv[s2]);
     float num = 0.f, den = 0.f;
-    for (int s2 = 0; s2 < nact; ++s2) {
-      const float w = __expf(a.part_ml[(p0 + s2) * 2] - M);
-      num += w * a.part_o[(p0 + s2) * d + j];
-      den += w * a.part_ml[(p0 + s2) * 2 + 1];
+#pragma unroll
+    for (int s2 = 0; s2 < ATT_MERGE_IN; ++s2) {
+      if (s2 < nact) {
+        const float w = __expf(mv[s2] - M);
+        num += w * ov[s2];
+        den += w * lv[s2];
+      }
     }
     a.out[(long long)qi * a.nh * d + (kh * G + h) * d + j] = tobf(num / den);
   }
+  if (a.stamps) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    astamp(a, 3);
+  }
+}
+
+// Split merge for long contexts: out = sum_s e^{m_s - M} o_s / sum_s e^{m_s - M} l_s
+// (the same order and arithmetic as k_attn's in-kernel merge).  Grid (row x
+// query head, 2), one thread per dim.
+__global__ void __launch_bounds__(64) k_attn_merge(AttnArgs a) {
+  constexpr int d = 128;
+  const int qi = blockIdx.x / a.nh, h = blockIdx.x - qi * a.nh;
+  const int len = a.pos[qi] + 1;
+  const int chunk = row_chunk(a, len);
+  const int nact = (len + chunk - 1) / chunk;
+  if (nact <= 1) return;                     // k_attn stored this row itself
+  const int j = blockIdx.y * 64 + threadIdx.x;
+  const long long p0 = ((long long)qi * a.nh + h) * a.nsplit;
+  const float* ml = a.part_ml + p0 * 2;
+  const float* o = a.part_o + p0 * d + j;
+  float M = -INFINITY;
+  for (int s2 = 0; s2 < nact; ++s2) M = fmaxf(M, ml[s2 * 2]);
+  float num = 0.f, den = 0.f;
+#pragma unroll 8
+  for (int s2 = 0; s2 < nact; ++s2) {
+    const float w = __expf(ml[s2 * 2] - M);
+    num += w * o[(long long)s2 * d];
+    den += w * ml[s2 * 2 + 1];
+  }
+  a.out[(long long)qi * a.nh * d + h * d + j] = tobf(num / den);
 }
 
 // ---------------------------------------------------------------- restricted lm_head
@@ -358,40 +429,59 @@ int launch_final_head(int R, int H, const bf16* h, const int* idx, const bf16* n
 }
 
 
-// Launch plan for keys up to max_len: aim for ~1024 workgroups over
-// (rows x kv heads x splits), never below 64 keys per split, at most 64
-// splits (merge cost).  Each row then sizes its own splits from its length
-// (k_attn), so a plan made for max_ctx serves every step of a captured graph.
-// Launch plan for keys up to max_len: one workgroup per (row, kv head) takes up
-// to ATT_KEYS keys (split over its 8 waves); longer contexts split the keys
-// over workgroups (<= 64).  Each row sizes its own splits from its length
-// (k_attn), so a plan made for max_ctx serves every step of a captured graph.
+// Launch plan for keys up to max_len: splits of ATT_CHUNK keys (at most
+// ATT_SPLITS_MAX; beyond that the splits grow in ATT_CHUNK steps).  Each row
+// sizes its own splits from its length (row_chunk), so a plan made for
+// max_ctx serves every step of a captured graph.
+static int g_att_chunk = 0, g_att_merge_in = -1;   // diagnostic overrides (vv_attn_tune)
+extern "C" int vv_attn_tune(int chunk, int merge_in) {
+  if (chunk % ATT_KC) return 1;
+  g_att_chunk = chunk;
+  g_att_merge_in = merge_in;
+  return 0;
+}
+
 int attn_plan(int nq, int nkv, int max_len, int* chunk) {
   (void)nq;
   (void)nkv;
-  int ns = (max_len + ATT_KEYS - 1) / ATT_KEYS;
-  if (ns > 64) ns = 64;
+  int c = g_att_chunk > 0 ? g_att_chunk : ATT_CHUNK;
+  int ns = (max_len + c - 1) / c;
+  if (ns > ATT_SPLITS_MAX) {
+    c = ((max_len + ATT_SPLITS_MAX - 1) / ATT_SPLITS_MAX + ATT_CHUNK - 1) / ATT_CHUNK * ATT_CHUNK;
+    ns = (max_len + c - 1) / c;
+  }
   if (ns < 1) ns = 1;
-  *chunk = ATT_KC;
+  *chunk = c;
   return ns;
+}
+
+template <int NW>
+static void launch_attn_nw(const AttnArgs& a, dim3 grid, hipStream_t st) {
+  const dim3 blk(64 * NW);
+  switch (a.nh / a.nkv) {
+    case 1: hipLaunchKernelGGL((k_attn<1, NW>), grid, blk, 0, st, a); break;
+    case 2: hipLaunchKernelGGL((k_attn<2, NW>), grid, blk, 0, st, a); break;
+    case 3: hipLaunchKernelGGL((k_attn<3, NW>), grid, blk, 0, st, a); break;
+    case 4: hipLaunchKernelGGL((k_attn<4, NW>), grid, blk, 0, st, a); break;
+    case 5: hipLaunchKernelGGL((k_attn<5, NW>), grid, blk, 0, st, a); break;
+    case 6: hipLaunchKernelGGL((k_attn<6, NW>), grid, blk, 0, st, a); break;
+    case 7: hipLaunchKernelGGL((k_attn<7, NW>), grid, blk, 0, st, a); break;
+    default: hipLaunchKernelGGL((k_attn<8, NW>), grid, blk, 0, st, a); break;
+  }
 }
 
 int launch_attn(AttnArgs a, hipStream_t st) {
   if (a.nq <= 0) return 0;
-  if (a.kv.d != 128 || a.nh % a.nkv || a.nh / a.nkv > ATT_GMAX || a.chunk % ATT_KC) return 1;
+  if (a.kv.d != 128 || a.nh % a.nkv || a.nh / a.nkv > ATT_GMAX || a.chunk % ATT_KC || a.nsplit > ATT_SPLITS_MAX)
+    return 1;
   if (a.nsplit > 1 && (!a.part_o || !a.part_ml || !a.counters)) return 1;
+  a.merge = a.nsplit > (g_att_merge_in >= 0 ? g_att_merge_in : ATT_MERGE_IN) ? 1 : 0;
   dim3 grid(a.nq * a.nkv, a.nsplit);
-  const dim3 blk(64 * ATT_NW);
-  switch (a.nh / a.nkv) {
-    case 1: hipLaunchKernelGGL(k_attn<1>, grid, blk, 0, st, a); break;
-    case 2: hipLaunchKernelGGL(k_attn<2>, grid, blk, 0, st, a); break;
-    case 3: hipLaunchKernelGGL(k_attn<3>, grid, blk, 0, st, a); break;
-    case 4: hipLaunchKernelGGL(k_attn<4>, grid, blk, 0, st, a); break;
-    case 5: hipLaunchKernelGGL(k_attn<5>, grid, blk, 0, st, a); break;
-    case 6: hipLaunchKernelGGL(k_attn<6>, grid, blk, 0, st, a); break;
-    case 7: hipLaunchKernelGGL(k_attn<7>, grid, blk, 0, st, a); break;
-    default: hipLaunchKernelGGL(k_attn<8>, grid, blk, 0, st, a); break;
-  }
+  const int nw = a.chunk >= 256 ? 8 : a.chunk >= 128 ? 4 : 2;   // 32 keys per wave step
+  if (nw == 8) launch_attn_nw<8>(a, grid, st);
+  else if (nw == 4) launch_attn_nw<4>(a, grid, st);
+  else launch_attn_nw<2>(a, grid, st);
+  if (a.merge) hipLaunchKernelGGL(k_attn_merge, dim3(a.nq * a.nh, 2), dim3(64), 0, st, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

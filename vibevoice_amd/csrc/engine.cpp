@@ -672,8 +672,11 @@ int vv_finalize(vv_ctx* c) {
   // ---- LM KV cache: [layer][slot][kv_head][ctx][d]
   c->lm_slots = 2 * k.max_batch;
   c->kv.d = d;
-  c->kv.max_ctx = k.max_ctx;
-  c->kv.s_head = (long long)k.max_ctx * d;
+  // position stride of the cache rounded up to 64 (128 B): V^T rows [dim][ctx]
+  // are read 16 B at a time by the attention kernel, and an odd stride left
+  // every other row misaligned
+  c->kv.max_ctx = (k.max_ctx + 63) / 64 * 64;
+  c->kv.s_head = (long long)c->kv.max_ctx * d;
   c->kv.s_slot = c->kv.s_head * k.n_kv_heads;
   c->kv.s_layer = c->kv.s_slot * c->lm_slots;
   const size_t kvb = (size_t)c->kv.s_layer * k.n_layers * sizeof(bf16);
@@ -682,7 +685,7 @@ int vv_finalize(vv_ctx* c) {
   c->kv.k = (bf16*)c->kv_k.p;
   c->kv.v = (bf16*)c->kv_v.p;
   // ---- attention split partials for decode (2 * max_batch rows, <= 64 splits) + tickets
-  CHK(c->attn_part.ensure((size_t)2 * k.max_batch * k.n_heads * 64 * (d + 2) * sizeof(float)));
+  CHK(c->attn_part.ensure((size_t)2 * k.max_batch * k.n_heads * 256 * (d + 2) * sizeof(float)));
   CHK(c->attn_cnt.ensure(65536 * sizeof(unsigned)));
   HIPCHK(hipMemset(c->attn_cnt.p, 0, 65536 * sizeof(unsigned)));
   // ---- split-K slabs + tickets
@@ -742,7 +745,7 @@ int vv_kv_copy(vv_ctx* c, int n, const int* slots, const int* src, const int* ds
 
 int vv_kv_synthetic(vv_ctx* c, int n, const int* slots, int p0, int p1, unsigned seed, vv_stream vst) {
   if (!c->finalized) FAIL("vv_kv_synthetic before vv_finalize");
-  if (p0 < 0 || p1 > c->kv.max_ctx || p0 > p1) FAIL("vv_kv_synthetic: positions outside [0, max_ctx)");
+  if (p0 < 0 || p1 > c->cfg.max_ctx || p0 > p1) FAIL("vv_kv_synthetic: positions outside [0, max_ctx)");
   KCHK(launch_kv_fill(c->kv, c->cfg.n_layers, c->cfg.n_kv_heads, n, slots, p0, p1, seed, (hipStream_t)vst));
   return 0;
 }

@@ -151,7 +151,8 @@ struct RollDesc {
 
 struct AttnArgs {
   int nq, nh, nkv, layer, nsplit;
-  int chunk;            // keys per split (multiple of 64)
+  int chunk;            // keys per split (multiple of 32)
+  int merge;            // set by launch_attn: 1 = splits merged by k_attn_merge
   float scale;
   const bf16* q;        // [nq][nh*d]
   bf16* out;            // [nq][nh*d]
