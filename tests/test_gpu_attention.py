@@ -70,3 +70,27 @@ def test_attention_vs_torch(nh, nkv, lens):
     e = rel_err(out, ref)
     print(lens, e)
     assert e < 1e-2
+
+
+@pytest.mark.parametrize("chunk,merge_in", [(64, 8), (64, 0), (128, 8), (128, 0), (1024, 8)])
+def test_attention_plan_variants(chunk, merge_in):
+    """Every split plan the tuning hook can select (keys per split -> 2 / 4 / 8
+    waves; in-kernel ticket merge or the separate merge pass) gives the same
+    attention within bf16 tolerance."""
+    eng = tiny_engine()
+    L = _lib.lib()
+    lens = [1, 40, 300, 700]
+    g = torch.Generator(device=dev).manual_seed(chunk + merge_in)
+    K = torch.randn(4, 2, 700, 128, device=dev, generator=g).bfloat16()
+    V = torch.randn(4, 2, 700, 128, device=dev, generator=g).bfloat16()
+    q = torch.randn(4, 12 * 128, device=dev, generator=g).bfloat16()
+    slots = torch.arange(4, device=dev, dtype=torch.int32)
+    pos = torch.tensor([n - 1 for n in lens], device=dev, dtype=torch.int32)
+    _lib.check(L.vv_attn_tune(chunk, merge_in), "attn_tune")
+    try:
+        out = run_attention(eng, q, K, V, slots, pos, 700)
+        torch.cuda.synchronize()
+    finally:
+        L.vv_attn_tune(0, -1)
+    ref = reference(q.cpu(), K.cpu(), V.cpu(), slots.cpu(), pos.cpu())
+    assert rel_err(out, ref) < 1e-2
