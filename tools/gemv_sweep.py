@@ -30,6 +30,8 @@ SHAPES = [  # name, M, N, K, epi
     ("head.ada.s10", 20, 21504, 1536, "store"), ("head.ada.s10.b8", 160, 21504, 1536, "store"),
     ("codec.t40.fc1", 40, 2048, 512, "gelu"), ("codec.t40.fc2", 40, 512, 2048, "res"),
     ("codec.t8.fc2", 8, 1024, 4096, "res"),
+    ("head.down.b8", 16, 1536, 4608, "res"), ("codec.fc2.b8", 8, 2048, 8192, "res"), ("lm.o.b8", 16, 1536, 1536, "res"),
+    ("head.down.b4", 8, 1536, 4608, "res"), ("lm.down.b4", 8, 1536, 8960, "res"),
 ]
 
 
@@ -115,7 +117,10 @@ def main():
             return ((Y.float() - ref).norm() / ref.norm()).item()
 
         configs = [(0, 0, -1, 0, 0, 0)]
-        if "--tpw" in sys.argv:   # tiles per workgroup x waves x chunks in flight
+        if "--ks" in sys.argv:    # cross-workgroup split-K x hand-off form x waves x chunks in flight
+            configs += [(nw, ks, h, 0, u, 0) for nw, ks, h, u in itertools.product((4, 8), (1, 2, 3), (0, 1), (4, 8))
+                        if ks > 1 or h == 1]
+        elif "--tpw" in sys.argv:   # tiles per workgroup x waves x chunks in flight
             configs += [(nw, 1, 1, 0, u, t) for nw, u, t in itertools.product((2, 4, 8), (2, 4, 8), (1, 2, 4, 8))
                         if nw % t == 0]
         elif not quick:

@@ -873,8 +873,10 @@ struct GemmPlan { int nw, ksplit, u, tpw; };
 // and weight chunks in flight per wave (u):
 //   * >= 1024 tiles (LM gate|up, head adaLN): 2 waves — every workgroup resident
 //     in the first round (4-wave groups left a second-round tail: 16.7 -> 14.0 us)
-//   * few tiles, long rows (LM / head down): 8 waves x 4; at M >= 8, 4 waves
-//     (B = 8 LM down 22.5 -> 18.7 us); 128 tiles x K >= 8192 (codec fc2): 4 x 8
+//   * few tiles, long rows (LM / head down): 8 waves x 4; 128 tiles x K >= 8192
+//     (codec fc2): 4 x 8; at M >= 8 two workgroups split K (the only shapes
+//     where the hand-off pays, profiles/r01_gemv_sweep_ks.txt: B = 8 LM down
+//     18.7 -> 15.5 us, head down 13.0 -> 12.3, B = 8 codec fc2 13.1 -> 12.0)
 //   * 16 < M <= 64 (k_gemv): 4 waves, 1 for >= 1024 tiles (the batched head
 //     adaLN, M = 2 x 10 steps: 35 -> 20.5 us)
 //   * few tiles, short rows (qkv, o_proj): 4 x 8, all chunks in flight at once
@@ -886,9 +888,15 @@ static GemmPlan gemv_plan(int N, int K, int M) {
   const int chunks = K / 32, tiles = N / 16;
   int nw = 4, ks = 1, u = 4, tpw = 1;
   if (tiles <= 128 && chunks >= 128) {
-    if (M >= 8) nw = 4;
-    else if (tiles == 128 && chunks >= 256) u = 8;
-    else nw = 8;
+    if (M >= 8) {   // batched rows: 2-way split-K (sc1 hand-off) reaches 2x the CUs
+      ks = 2;
+      if (chunks >= 256) u = 8;
+      else nw = 8;
+    } else if (tiles == 128 && chunks >= 256) {
+      u = 8;
+    } else {
+      nw = 8;
+    }
   } else if (M > 16) {
     nw = tiles >= 1024 ? 1 : 4;   // k_gemv (A from L2 per chunk): batched head adaLN 35 -> 20.5 us
   } else if (M >= 8) {
