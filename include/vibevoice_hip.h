@@ -59,6 +59,11 @@ typedef struct vv_config {
 } vv_config;
 
 const char* vv_last_error(void);
+/* Counter of workspace reallocations (any ctx of the process).  A workspace
+ * grows when a call needs more than any earlier one (e.g. a longer prefill);
+ * device pointers captured into a hipGraph before that are stale, so a host
+ * that replays graphs re-captures them when this value changes. */
+int vv_ws_epoch(void);
 int vv_create(const vv_config* cfg, int device, vv_ctx** out);
 void vv_destroy(vv_ctx* ctx);
 

@@ -133,3 +133,29 @@ def test_speculative_diffusion_is_exact(graphs):
                 assert torch.equal(a.speech_outputs[i].cpu(), b.speech_outputs[i].cpu())
         if forced:
             assert misses[1] > 0      # the mispredict path ran
+
+
+def test_graphs_recaptured_after_workspace_growth():
+    """A second generate() with a longer prompt grows the LM workspace (its
+    prefill has more rows); hipGraphs captured by the first call hold the old
+    pointers and must be re-captured (vv_ws_epoch), not replayed: the second
+    call equals the same call on the eager path."""
+    cfg = tiny_config(hidden=256, layers=2, heads=2, kv_heads=1, inter=512)
+    sd = synthetic_state_dict(cfg, seed=8, device="cpu", mode="test", with_acoustic_encoder=False)
+    model = VibeVoiceForConditionalGenerationInference(cfg, sd, dev, max_batch=2, max_ctx=256)
+    model.set_ddpm_inference_steps(3)
+    sched = [[D] * 6 + [X], [D] * 5 + [X]]
+
+    def run(L, graphs):
+        ids = torch.randint(0, 151000, (2, L), generator=torch.Generator().manual_seed(L))
+        torch.manual_seed(77)
+        return model.generate(input_ids=ids, attention_mask=torch.ones(2, L, dtype=torch.long), tokenizer=TOK,
+                              cfg_scale=1.3, forced_tokens=sched, use_graphs=graphs, max_new_tokens=10,
+                              show_progress_bar=False)
+    run(6, True)                      # captures the loop-body graphs at a small workspace
+    e0 = model._graph_epoch
+    long_graph = run(120, True)       # 240 prefill rows: the workspace grows
+    assert model._graph_epoch != e0
+    long_eager = run(120, False)
+    for b in range(2):
+        assert torch.equal(long_graph.speech_outputs[b].cpu(), long_eager.speech_outputs[b].cpu())

@@ -56,6 +56,7 @@ EXPORTS = [
     ("vv_rmsnorm_bf16", I, [I, I, P, I64, P, F, P, I64, P]),
     ("vv_gemm_bf16_norm", I, [I, I, I, P, I64, P, F, P, I, P, I64, P, P]),
     ("vv_attention_bf16", I, [I, I, I, P, P, P, I64, I64, P, P, I, P, P, P]),
+    ("vv_ws_epoch", I, []),
     ("vv_gemv_tune", I, [I, I, I, I, I]),
     ("vv_gemv_tune_tpw", I, [I]),
     ("vv_gemv_stamps", I, [P]),

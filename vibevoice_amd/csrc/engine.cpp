@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <atomic>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -60,11 +61,16 @@ struct ConvBuf {
   int ctx = 0, T = 0, C = 0, rows = 0;
 };
 
+// Bumped whenever a workspace moves: a hipGraph captured earlier bakes the old
+// pointers in, so the host drops its graphs when this changes (vv_ws_epoch).
+static std::atomic<int> g_ws_epoch{0};
+
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
   int ensure(size_t b) {
     if (b <= bytes) return 0;
+    if (p) g_ws_epoch.fetch_add(1);
     if (p) (void)hipFree(p);
     p = nullptr;
     bytes = 0;
@@ -125,6 +131,7 @@ struct vv_ctx {
   DevBuf lm_ws;  // h, a, qkv, q, att, act
   size_t lm_ws_tokens = 0;
   DevBuf attn_part, attn_cnt;
+  DevBuf norm_ws;   // pre-normalised A rows of XF_NORM GEMMs with > 16 rows
   DevBuf valid_ids;
   int n_valid = 0;
   // split-K
@@ -198,14 +205,27 @@ static ATransform xf_norm(const bf16* w, float eps, const bf16* mod = nullptr, l
   return x;
 }
 
+static int rmsnorm(int M, int C, RowMap in, RowMap out, const bf16* w, float eps, hipStream_t st,
+                   const bf16* mod = nullptr, long long mod_ld = 0, int shift_off = 0, int scale_off = 0);
+
 static int gemm(vv_ctx* c, GemmArgs g, hipStream_t st) {
   if (!g.w) FAIL("gemm: null weight");
+  if (g.xf.kind == XF_NORM && g.M > 16) {
+    // more rows than one MFMA tile: the GEMV / GEMM kernels would re-normalise
+    // the A block in every workgroup (B = 32: LM gate|up 334 us); normalise it
+    // once (k_rmsnorm: the same arithmetic and summation order, bit-identical)
+    CHK(c->norm_ws.ensure((size_t)g.M * g.K * sizeof(bf16)));
+    CHK(rmsnorm(g.M, g.K, g.a, rowmap(c->norm_ws.p, g.K), g.xf.w, g.xf.eps, st, g.xf.mod, g.xf.mod_ld,
+                g.xf.shift_off, g.xf.scale_off));
+    g.a = rowmap(c->norm_ws.p, g.K);
+    g.xf.kind = XF_NONE;
+  }
   KCHK(launch_gemm(g, st));
   return 0;
 }
 
 static int rmsnorm(int M, int C, RowMap in, RowMap out, const bf16* w, float eps, hipStream_t st,
-                   const bf16* mod = nullptr, long long mod_ld = 0, int shift_off = 0, int scale_off = 0) {
+                   const bf16* mod, long long mod_ld, int shift_off, int scale_off) {
   NormArgs a;
   memset(&a, 0, sizeof(a));
   a.M = M;
@@ -557,6 +577,7 @@ static int convnet_roll(ConvNet& net, int n, const int* slots, int mode, hipStre
 extern "C" {
 
 const char* vv_last_error(void) { return g_err.c_str(); }
+int vv_ws_epoch(void) { return g_ws_epoch.load(); }
 
 int vv_create(const vv_config* cfg, int device, vv_ctx** out) {
   if (!cfg || !out) FAIL("vv_create: null argument");
@@ -576,7 +597,7 @@ void vv_destroy(vv_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
-  DevBuf* bufs[] = {&c->kv_k, &c->kv_v, &c->lm_ws, &c->attn_part, &c->attn_cnt, &c->valid_ids, &c->splitk_ws, &c->splitk_cnt,
+  DevBuf* bufs[] = {&c->norm_ws, &c->kv_k, &c->kv_v, &c->lm_ws, &c->attn_part, &c->attn_cnt, &c->valid_ids, &c->splitk_ws, &c->splitk_cnt,
                     &c->temb, &c->tfreq_tmp, &c->head_ws, &c->codec_ws, &c->slot_scratch};
   for (DevBuf* b : bufs) b->release();
   ConvNet* nets[] = {&c->dec, &c->sem, &c->aenc};

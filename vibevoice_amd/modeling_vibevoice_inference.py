@@ -27,6 +27,7 @@ from typing import List, Optional
 
 import torch
 
+from . import _lib
 from .config import VibeVoiceConfig
 from .engine import Engine
 from .weights import synthetic_state_dict
@@ -113,6 +114,7 @@ class VibeVoiceForConditionalGenerationInference:
         self.use_graphs = True          # capture the steady-state loop body into hipGraphs
         self._bufs = {}
         self._graph_cache, self._graph_seen = {}, set()
+        self._graph_epoch = None        # engine workspace epoch the cached graphs were captured at
 
     def _step_buffers(self, B):
         """Static device operands of the loop body for batch B (shared by every
@@ -373,6 +375,12 @@ class GenerateSession:
         eagerly so every kernel is loaded) and later ones replay it."""
         if not self.use_graphs:
             return fn()
+        ep = _lib.lib().vv_ws_epoch()
+        if ep != self.m._graph_epoch:    # a workspace moved (e.g. a longer prefill): captured pointers are stale
+            torch.cuda.current_stream().synchronize()
+            self.graphs.clear()
+            self.seen.clear()
+            self.m._graph_epoch = ep
         full = (self.B, self.m.engine.steps, float(self.cfg_scale), self.sde) + key
         g = self.graphs.get(full)
         if g is None:
