@@ -175,6 +175,9 @@ int vv_gemv_tune(int nw, int ks, int handoff, int target_waves, int u);
  * M <= 16 GEMV (the waves split into tpw groups that share one staging of the
  * A rows); 0 restores the built-in plan. */
 int vv_gemv_tune_tpw(int tpw);
+/* Tuning hook (benchmarks only): GEMMs with more than m rows (m >= 16) use the
+ * tiled MFMA kernel instead of the GEMV family; 0 restores the built-in 64. */
+int vv_gemv_tune_maxm(int m);
 /* Diagnostic (benchmarks only): M <= 16 GEMV launches write 4 s_memrealtime
  * stamps per workgroup (start, A staged, weights streamed, epilogue stored) to
  * buf (uint64[grid * 4]); NULL turns it off. */

@@ -1,7 +1,7 @@
 """Decode / prefill attention kernel (k_attn via vv_attention_bf16) vs a plain
 PyTorch fp32 reference (softmax(q k^T / sqrt(128)) v, GQA), at the 1.5B head
 layout (12 q / 2 kv heads) and the Large layout (28 / 4), cache in the engine's
-layout (K [slot][kv_head][ctx][128], V transposed [slot][kv_head][128][ctx]): single-workgroup
+layout (K [slot][kv_head][ctx][128], V [slot][kv_head][ctx/32][128][32]): single-workgroup
 contexts, the in-launch split merge (<= 8 splits of 64 keys), the k_attn_merge pass
 (longer), splits of 128 and 192 keys (4 and 8 waves), ragged rows sharing a
 launch, and length-1 rows.  Tolerance: rel L2 < 1e-2 (bf16 output)."""
@@ -26,8 +26,9 @@ def run_attention(eng, q, K, V, slots, pos, max_pos_p1):
     nq, nh = q.shape[0], q.shape[1] // 128
     nslot, nkv, ctx, _ = K.shape
     out = torch.empty_like(q)
-    VT = V.transpose(2, 3).contiguous()          # engine layout: V transposed per head, [dim][ctx]
-    rc = _lib.lib().vv_attention_bf16(nq, nh, nkv, P(q), P(K), P(VT), nkv * ctx * 128, ctx * 128, P(slots), P(pos),
+    # engine layout: V in blocks of 32 positions, each [128 dims][32 positions]
+    VB = V.view(nslot, nkv, ctx // 32, 32, 128).transpose(3, 4).contiguous()
+    rc = _lib.lib().vv_attention_bf16(nq, nh, nkv, P(q), P(K), P(VB), nkv * ctx * 128, ctx * 128, P(slots), P(pos),
                                       max_pos_p1, P(out), eng.h,
                                       ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
     _lib.check(rc, "attention")
@@ -58,7 +59,7 @@ def test_attention_vs_torch(nh, nkv, lens):
     eng = tiny_engine()
     g = torch.Generator(device=dev).manual_seed(sum(lens) + nh)
     nslot = len(lens)
-    ctx = max(lens)
+    ctx = (max(lens) + 31) // 32 * 32                  # cache capacity: whole 32-position V blocks
     K = torch.randn(nslot, nkv, ctx, 128, device=dev, generator=g).bfloat16()
     V = torch.randn(nslot, nkv, ctx, 128, device=dev, generator=g).bfloat16()
     q = torch.randn(len(lens), nh * 128, device=dev, generator=g).bfloat16()
@@ -81,8 +82,8 @@ def test_attention_plan_variants(chunk, merge_in):
     L = _lib.lib()
     lens = [1, 40, 300, 700]
     g = torch.Generator(device=dev).manual_seed(chunk + merge_in)
-    K = torch.randn(4, 2, 700, 128, device=dev, generator=g).bfloat16()
-    V = torch.randn(4, 2, 700, 128, device=dev, generator=g).bfloat16()
+    K = torch.randn(4, 2, 704, 128, device=dev, generator=g).bfloat16()
+    V = torch.randn(4, 2, 704, 128, device=dev, generator=g).bfloat16()
     q = torch.randn(4, 12 * 128, device=dev, generator=g).bfloat16()
     slots = torch.arange(4, device=dev, dtype=torch.int32)
     pos = torch.tensor([n - 1 for n in lens], device=dev, dtype=torch.int32)

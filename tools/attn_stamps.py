@@ -17,7 +17,7 @@ from vibevoice_amd import _lib  # noqa: E402
 def main():
     eng = tiny_engine()
     L = _lib.lib()
-    for ctx, stride in ((250, 250), (250, 256), (1000, 1000), (1000, 1024)):
+    for ctx, stride in ((250, 256), (1000, 1024), (16000, 16000)):   # strides: whole 32-position V blocks
         nq, nh, nkv, NL = 2, 12, 2, 28
         Ks = [torch.randn(nq, nkv, stride, 128, device="cuda").bfloat16() for _ in range(NL)]
         Vs = [torch.randn_like(k) for k in Ks]
@@ -25,7 +25,7 @@ def main():
         out = torch.empty_like(q)
         slots = torch.arange(nq, device="cuda", dtype=torch.int32)
         pos = torch.full((nq,), ctx - 1, device="cuda", dtype=torch.int32)
-        st = torch.zeros(NL, 64, 4, dtype=torch.int64, device="cuda")
+        st = torch.zeros(NL, 1024, 4, dtype=torch.int64, device="cuda")   # >= workgroups per launch
 
         def run(i):
             L.vv_attn_stamps(ctypes.c_void_p(st[i].data_ptr()))

@@ -59,6 +59,7 @@ EXPORTS = [
     ("vv_ws_epoch", I, []),
     ("vv_gemv_tune", I, [I, I, I, I, I]),
     ("vv_gemv_tune_tpw", I, [I]),
+    ("vv_gemv_tune_maxm", I, [I]),
     ("vv_gemv_stamps", I, [P]),
     ("vv_attn_stamps", I, [P]),
     ("vv_attn_tune", I, [I, I]),

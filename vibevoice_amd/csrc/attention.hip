@@ -4,10 +4,11 @@
 // (modeling_qwen2.py:99-134, 150-173, 195-247) as called by VibeVoiceModel.forward
 // (vibevoice/modular/modeling_vibevoice.py:169-209).
 //
-// KV cache layout: K [layer][slot][kv_head][ctx][d]; V transposed per head,
-// [layer][slot][kv_head][d][ctx], so both MFMA operands of the kernel below
-// (K as the key-column operand of Q.K^T, V as the key-row operand of P.V) are
-// contiguous 16-byte loads.  A row's cache holds only the entries its
+// KV cache layout: K [layer][slot][kv_head][ctx][d]; V [layer][slot][kv_head]
+// in blocks of 32 positions, each [d][32] (common.h v_off), so both MFMA
+// operands of the kernel below (K as the key-column operand of Q.K^T, V as the
+// key-row operand of P.V) are contiguous 16-byte loads, and a wave's V loads
+// for one 32-key step are one 8 KB contiguous block.  A row's cache holds only the entries its
 // attention mask keeps, in order, so cache index == RoPE position (SURVEY.md
 // §8a rows a3, a7).
 #include "kernels.h"
@@ -34,10 +35,12 @@
 // contexts do not pay: the in-kernel merge costs ~6 us of dependent round
 // trips (ticket, partial loads, store) and a merge launch ~4 us, against the
 // 2-4 us the extra CUs save (plan sweep over 64-1024 keys per split x merge
-// form, tools/ab_bench.py attn_tune: all within 1.5 % at B = 1 and 8).
+// form, tools/ab_bench.py attn_tune: all within 1.5 % at B = 1 and 8).  At a
+// 64K context 1,024-key splits (64 per row) beat 256-key splits (255): 4.47 vs
+// 4.86 ms per step -- fewer partials to merge, each CU still streaming.
 constexpr int ATT_GMAX = 8;
 constexpr int ATT_KC = 32;            // per-row split granularity (one wave step)
-constexpr int ATT_CHUNK = 256;        // keys per split (8 waves x one 32-key step)
+constexpr int ATT_CHUNK = 1024;       // keys per split (8 waves x 4 steps of 32 keys)
 constexpr int ATT_SPLITS_MAX = 256;
 constexpr int ATT_MERGE_IN = 8;       // splits merged inside k_attn
 
@@ -82,8 +85,7 @@ __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
   const long long cbase = (long long)a.layer * a.kv.s_layer + (long long)a.slots[qi] * a.kv.s_slot +
                           (long long)kh * a.kv.s_head;
   const bf16* K = a.kv.k + cbase;             // [ctx][128]
-  const bf16* VT = a.kv.v + cbase;            // [128][max_ctx]
-  const int ldv = a.kv.max_ctx;
+  const bf16* VB = a.kv.v + cbase;            // 32-position blocks of [128][32] (v_off)
   const bf16x8 z8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
 
   // Q fragments (A operand): row = head r (zero past G), k = dims 32c + 8g .. +7;
@@ -119,7 +121,7 @@ __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
     const int kb = c0 + 8 * g;                 // B operand of O: k = keys kb .. kb+7, col = dim
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      bf16x8 v = kb < w1 ? *(const bf16x8*)(VT + (long long)(16 * j + r) * ldv + kb) : z8;
+      bf16x8 v = kb < w1 ? *(const bf16x8*)(VB + v_off(16 * j + r, kb)) : z8;
       if (kb + 8 > w1) {
 #pragma unroll
         for (int e = 0; e < 8; ++e)
@@ -312,30 +314,56 @@ __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
   }
 }
 
-// Split merge for long contexts: out = sum_s e^{m_s - M} o_s / sum_s e^{m_s - M} l_s
-// (the same order and arithmetic as k_attn's in-kernel merge).  Grid (row x
-// query head, 2), one thread per dim.
-__global__ void __launch_bounds__(64) k_attn_merge(AttnArgs a) {
-  constexpr int d = 128;
+// Split merge for long contexts: out = sum_s e^{m_s - M} o_s / sum_s e^{m_s - M} l_s.
+// Grid (row x query head, 2 halves of the 128 dims), 8 waves: wave w folds
+// splits w, w + 8, ... (lane = dim), then the 8
+// partial (M_w, num_w, den_w) combine in LDS in wave order.  (One thread per
+// dim walking all 255 splits of a 64K context took 33 us: a chain of loads.)
+__global__ void __launch_bounds__(512) k_attn_merge(AttnArgs a) {
+  constexpr int d = 128, NWM = 8;
+  __shared__ float sm[NWM], snum[NWM][64], sden[NWM];
   const int qi = blockIdx.x / a.nh, h = blockIdx.x - qi * a.nh;
   const int len = a.pos[qi] + 1;
   const int chunk = row_chunk(a, len);
   const int nact = (len + chunk - 1) / chunk;
   if (nact <= 1) return;                     // k_attn stored this row itself
-  const int j = blockIdx.y * 64 + threadIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int j = blockIdx.y * 64 + lane;
   const long long p0 = ((long long)qi * a.nh + h) * a.nsplit;
   const float* ml = a.part_ml + p0 * 2;
   const float* o = a.part_o + p0 * d + j;
-  float M = -INFINITY;
-  for (int s2 = 0; s2 < nact; ++s2) M = fmaxf(M, ml[s2 * 2]);
-  float num = 0.f, den = 0.f;
-#pragma unroll 8
-  for (int s2 = 0; s2 < nact; ++s2) {
-    const float w = __expf(ml[s2 * 2] - M);
-    num += w * o[(long long)s2 * d];
-    den += w * ml[s2 * 2 + 1];
+  // one online pass (running max, rescaled sums): the unrolled body's loads
+  // do not depend on the accumulators, so 16 splits' loads are in flight at once
+  float M = -INFINITY, num = 0.f, den = 0.f;
+#pragma unroll 16
+  for (int s2 = w; s2 < nact; s2 += NWM) {
+    const float m = ml[s2 * 2], l = ml[s2 * 2 + 1], ov = o[(long long)s2 * d];
+    const float Mn = fmaxf(M, m);
+    const float sc = __expf(M - Mn), e = __expf(m - Mn);
+    num = num * sc + e * ov;
+    den = den * sc + e * l;
+    M = Mn;
   }
-  a.out[(long long)qi * a.nh * d + h * d + j] = tobf(num / den);
+  snum[w][lane] = num;
+  if (lane == 0) {
+    sm[w] = M;
+    sden[w] = den;
+  }
+  __syncthreads();
+  if (w == 0) {
+    float Mt = -INFINITY;
+#pragma unroll
+    for (int v = 0; v < NWM; ++v) Mt = fmaxf(Mt, sm[v]);
+    float nt = 0.f, dt = 0.f;
+#pragma unroll
+    for (int v = 0; v < NWM; ++v) {
+      if (sm[v] == -INFINITY) continue;       // a wave with no split
+      const float e = __expf(sm[v] - Mt);
+      nt += e * snum[v][lane];
+      dt += e * sden[v];
+    }
+    a.out[(long long)qi * a.nh * d + h * d + j] = tobf(nt / dt);
+  }
 }
 
 // ---------------------------------------------------------------- restricted lm_head
@@ -481,7 +509,7 @@ int launch_attn(AttnArgs a, hipStream_t st) {
   if (nw == 8) launch_attn_nw<8>(a, grid, st);
   else if (nw == 4) launch_attn_nw<4>(a, grid, st);
   else launch_attn_nw<2>(a, grid, st);
-  if (a.merge) hipLaunchKernelGGL(k_attn_merge, dim3(a.nq * a.nh, 2), dim3(64), 0, st, a);
+  if (a.merge) hipLaunchKernelGGL(k_attn_merge, dim3(a.nq * a.nh, 2), dim3(512), 0, st, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
@@ -508,9 +536,8 @@ __global__ void __launch_bounds__(256) k_kv_copy(KVLayout kv, int n_layers, int 
     const int l = e / (nkv * d), r = e - l * nkv * d, h = r / d, j = r - h * d;
     const long long b = (long long)l * kv.s_layer + (long long)slots[i] * kv.s_slot + (long long)h * kv.s_head + j;
     kv.k[b + (long long)dst[i] * d] = kv.k[b + (long long)src[i] * d];
-    // V^T: element (dim j, position p) at head base + j * max_ctx + p
-    const long long bv = b - j + (long long)j * kv.max_ctx;
-    kv.v[bv + dst[i]] = kv.v[bv + src[i]];
+    const long long hb = b - j;                 // V: common.h v_off
+    kv.v[hb + v_off(j, dst[i])] = kv.v[hb + v_off(j, src[i])];
   }
 }
 
@@ -532,7 +559,7 @@ __global__ void __launch_bounds__(256) k_kv_fill(KVLayout kv, int n_layers, int 
     unsigned x = (unsigned)(e * 2654435761ull) ^ (seed + 0x9e3779b9u * (unsigned)slot);
     x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
     kv.k[base + (long long)pos * kv.d + j] = tobf((float)(x & 0xffff) / 65536.f - 0.5f);
-    kv.v[base + (long long)j * kv.max_ctx + pos] = tobf((float)(x >> 16) / 65536.f - 0.5f);   // V^T [dim][ctx]
+    kv.v[base + v_off(j, pos)] = tobf((float)(x >> 16) / 65536.f - 0.5f);
   }
 }
 

@@ -34,6 +34,13 @@ DEV f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// V cache of one (layer, slot, kv head): positions in blocks of 32, each block
+// [128 dims][32 positions] (8 KB contiguous) -- attention's P.V operand loads
+// (8 positions of one dim per lane) then read whole 1 KB pieces instead of
+// 64 B slices of rows max_ctx apart (64K context: 37 -> see DESIGN.md).
+// Element (dim i, position p):
+DEV long long v_off(int i, int p) { return (long long)(p >> 5) * (128 * 32) + i * 32 + (p & 31); }
+
 DEV float silu_f(float x) { return x / (1.0f + __expf(-x)); }
 // GELU, exact erf form (transformers ACT2FN["gelu"]; modular_vibevoice_tokenizer.py:589)
 DEV float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }

@@ -702,7 +702,7 @@ int vv_finalize(vv_ctx* c) {
   c->kv.s_layer = c->kv.s_slot * c->lm_slots;
   const size_t kvb = (size_t)c->kv.s_layer * k.n_layers * sizeof(bf16);
   CHK(c->kv_k.ensure(kvb));
-  CHK(c->kv_v.ensure(kvb + 256));   // V^T rows are read 16 B at a time: pad the tail
+  CHK(c->kv_v.ensure(kvb + 256));
   c->kv.k = (bf16*)c->kv_k.p;
   c->kv.v = (bf16*)c->kv_v.p;
   // ---- attention split partials for decode (2 * max_batch rows, <= 64 splits) + tickets
@@ -1242,6 +1242,7 @@ int vv_attention_bf16(int nq, int nh, int nkv, const void* q, const void* k_cach
   kv.s_head = s_head;
   kv.d = 128;
   kv.max_ctx = (int)(s_head / 128);
+  if (s_head % (128 * 32)) FAIL("vv_attention_bf16: the V cache is blocked by 32 positions (s_head % 4096 != 0)");
   AttnArgs at;
   memset(&at, 0, sizeof(at));
   int chunk = 0;

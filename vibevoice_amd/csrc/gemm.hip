@@ -161,12 +161,13 @@ DEV void epi_rope(const GemmArgs& a, int m, int n0, int lane, float v[4]) {
     *(bf16x4*)(dst + j + 64) = o2;
   } else {
     if (m >= a.M) return;
-    // V cache is transposed per head ([dim][ctx], attention.hip)
+    // V cache in 32-position blocks of [dim][position] (common.h v_off)
     const int hv = h - R.nh - R.nkv;
-    bf16* dst = R.kv.v + (long long)R.layer * R.kv.s_layer + (long long)R.slots[m] * R.kv.s_slot +
-                (long long)hv * R.kv.s_head + (long long)((n0 % d) + 4 * g) * R.kv.max_ctx + R.pos[m];
+    bf16* hb = R.kv.v + (long long)R.layer * R.kv.s_layer + (long long)R.slots[m] * R.kv.s_slot +
+               (long long)hv * R.kv.s_head;
+    const int dim0 = (n0 % d) + 4 * g, p = R.pos[m];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dst[(long long)i * R.kv.max_ctx] = tobf(v[i]);
+    for (int i = 0; i < 4; ++i) hb[v_off(dim0 + i, p)] = tobf(v[i]);
   }
 }
 
@@ -841,6 +842,11 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
 
 // ------------------------------------------------------------------ host launch
 static int g_tune_nw = 0, g_tune_ks = 0, g_tune_handoff = -1, g_tune_waves = 0, g_tune_u = 0, g_tune_tpw = 0;
+static int g_gemv_max_m = 64;   // more rows than this: the tiled k_gemm (vv_gemv_tune_maxm)
+extern "C" int vv_gemv_tune_maxm(int m) {
+  g_gemv_max_m = m > 0 ? m : 64;
+  return 0;
+}
 static unsigned long long* g_stamps = nullptr;
 static const bool g_shape_log = getenv("VV_GEMM_LOG") != nullptr;
 
@@ -1014,7 +1020,7 @@ int launch_gemm(GemmArgs a, hipStream_t st) {
   if (g_shape_log) {   // VV_GEMM_LOG=1: one line per launch (shape census for profiles/)
     fprintf(stderr, "vv_gemm M=%d N=%d K=%d xf=%d epi=%d\n", a.M, a.N, a.K, a.xf.kind, a.epi.kind);
   }
-  if (a.M <= 64) {
+  if (a.M <= 64 && (a.M <= 16 || a.M <= g_gemv_max_m || a.epi.kind == EPI_CFG_DPM)) {
     const int mrep = (a.M + 15) / 16;
     GemmPlan p = gemv_plan(a.N, a.K, a.M);
     if (p.nw > max_waves(mrep)) p.nw = max_waves(mrep);
