@@ -629,15 +629,19 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   stamp(a, 1);
 
   f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const bool xok = r < a.M;
-  const bf16* xrow = xs + r * lds_ld + 8 * g - b0 * 32;
+  // A fragment reads are unconditional (a guarded LDS read compiled to an
+  // exec-masked ds_read + lgkmcnt(0) per chunk): lanes of rows >= M read row
+  // M - 1 -- they only feed output columns the epilogue drops -- and chunks past
+  // the wave's range re-read its last chunk against a zeroed weight fragment
+  const bf16* xrow = xs + min(r, a.M - 1) * lds_ld + 8 * g - b0 * 32;
   auto compute = [&](bf16x8 (&wf)[U], int c) {
+    bf16x8 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = *(const bf16x8*)(xrow + min(c + u, c1 - 1) * 32);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const bool ok = c + u < c1;
-      const bf16x8 w = ok ? wf[u] : zero8;
-      const bf16x8 x = (xok && ok) ? *(const bf16x8*)(xrow + (c + u) * 32) : zero8;
-      acc = mfma(w, x, acc);
+      const bf16x8 w = c + u < c1 ? wf[u] : zero8;
+      acc = mfma(w, x[u], acc);
     }
   };
   auto load = [&](bf16x8 (&wf)[U], int c) {
@@ -706,7 +710,7 @@ __global__ void __launch_bounds__(512) k_gemv(GemmArgs a) {
   for (int mr = 0; mr < MREP; ++mr) {
     const int m = r + 16 * mr;
     xok[mr] = m < a.M;
-    xrow[mr] = xok[mr] ? rm_bf(a.a, m) + 8 * g : nullptr;
+    xrow[mr] = rm_bf(a.a, min(m, a.M - 1)) + 8 * g;   // rows >= M: a valid row, results dropped
     inv[mr] = XF == XF_NORM ? inv_s[m] : 0.f;
   }
   f32x4 acc[MREP];
@@ -720,7 +724,7 @@ __global__ void __launch_bounds__(512) k_gemv(GemmArgs a) {
     for (int u = 0; u < U; ++u) {
       const int cc = min(c + u, max(c1 - 1, 0));
 #pragma unroll
-      for (int mr = 0; mr < MREP; ++mr) xf[u][mr] = xok[mr] ? *(const bf16x8*)(xrow[mr] + cc * 32) : zero8;
+      for (int mr = 0; mr < MREP; ++mr) xf[u][mr] = *(const bf16x8*)(xrow[mr] + cc * 32);
       wf[u] = ldw(wrow + cc * 512);
     }
   };
