@@ -178,6 +178,10 @@ int vv_gemv_tune_tpw(int tpw);
 /* Tuning hook (benchmarks only): GEMMs with more than m rows (m >= 16) use the
  * tiled MFMA kernel instead of the GEMV family; 0 restores the built-in 64. */
 int vv_gemv_tune_maxm(int m);
+/* Tuning hook (benchmarks only): 0 = the 16 < M <= 64 GEMVs with >= 256 tiles
+ * use k_gemv (A fragments per tile) instead of k_gemvw (A held per K slice
+ * across several tiles); 1 = built-in. */
+int vv_gemv_tune_wide(int on);
 /* Diagnostic (benchmarks only): M <= 16 GEMV launches write 4 s_memrealtime
  * stamps per workgroup (start, A staged, weights streamed, epilogue stored) to
  * buf (uint64[grid * 4]); NULL turns it off. */

@@ -123,3 +123,21 @@ def test_gemv_tiles_per_workgroup(tpw, M, N, epi):
         L.vv_gemv_tune(0, 0, -1, 0, 0)
         L.vv_gemv_tune_tpw(0)
     assert rel_err(Y, ref) < 5e-3 and max_rel(Y, ref) < 3e-2
+
+
+@pytest.mark.parametrize("wide", [1, 0])
+@pytest.mark.parametrize("M,N,K,epi", [(17, 4096, 1024, "gelu"), (33, 9216, 1536, "silu_mul"),
+                                       (64, 17920, 1536, "silu_mul"), (48, 8192, 4608, "res"),
+                                       (40, 21504, 1536, "store"), (64, 16400, 1024, "store")])
+def test_gemv_wide_rows(wide, M, N, K, epi):
+    """16 < M <= 64 with >= 256 weight tiles: k_gemvw (A per K slice held in
+    registers across 1-4 tiles, slices reduced in LDS) and, for comparison,
+    k_gemv; K blocks that end inside a wave's slice (K = 1024, 4608) and a
+    ragged last tile group (N = 16400: 1025 tiles in groups of 4)."""
+    L = _lib.lib()
+    L.vv_gemv_tune_wide(wide)
+    try:
+        Y, ref = run(M, N, K, epi, bias=epi != "silu_mul", res=epi == "res")
+    finally:
+        L.vv_gemv_tune_wide(1)
+    assert rel_err(Y, ref) < 5e-3 and max_rel(Y, ref) < 3e-2

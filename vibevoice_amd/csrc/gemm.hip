@@ -772,6 +772,128 @@ __global__ void __launch_bounds__(512) k_gemv(GemmArgs a) {
   }
 }
 
+// 16 < M <= 64 with many weight tiles (B >= 9 decode rows, the batched head
+// adaLN, 64-row codec stages).  k_gemv re-reads the A fragments from L2 for
+// every 16 weight rows -- at M = 64 four times the weight bytes (B = 32: LM
+// gate|up 51 us for 55 MB).  Here each of the 8 waves holds the A fragments of
+// its K slice (GW_NCH chunks per K block) in registers and applies them to the
+// workgroup's TPW weight tiles, streaming those tiles' chunks of the slice with
+// a ping-pong over tiles; the 8 slices reduce in LDS per tile, in wave order,
+// before the epilogue.  A crosses L2 once per workgroup.
+constexpr int GW_NCH = 6;   // 32-column chunks per wave per K block (8 waves: 1,536 columns)
+
+template <int MREP, int TPW, bool KEEP>
+__global__ void __launch_bounds__(512) k_gemvw(GemmArgs a) {
+  __shared__ float red[8][MREP * 256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int ntile = a.N >> 4, nchunk = a.K >> 5;
+  const int t0 = blockIdx.x * TPW;
+  const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+  f32x4 acc[TPW][MREP];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i)
+#pragma unroll
+    for (int mr = 0; mr < MREP; ++mr) acc[i][mr] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // rows >= M read row M - 1 (their output columns are dropped): no guarded loads
+  const bf16* arow[MREP];
+#pragma unroll
+  for (int mr = 0; mr < MREP; ++mr) arow[mr] = rm_bf(a.a, min(16 * mr + r, a.M - 1)) + 8 * g;
+  for (int kb = 0; kb < nchunk; kb += 8 * GW_NCH) {
+    const int cw = kb + wave * GW_NCH;        // this wave's first chunk of the block (wave-uniform)
+    if (cw >= nchunk) continue;
+    bf16x8 xf[GW_NCH][MREP];
+#pragma unroll
+    for (int c = 0; c < GW_NCH; ++c)
+#pragma unroll
+      for (int mr = 0; mr < MREP; ++mr) xf[c][mr] = *(const bf16x8*)(arow[mr] + min(cw + c, nchunk - 1) * 32);
+    bf16x8 wa[GW_NCH], wb[GW_NCH];
+    auto wload = [&](bf16x8 (&w)[GW_NCH], int i) {
+      const int t = min(t0 + i, ntile - 1);
+      const bf16* wr = a.w + (long long)t * a.K * 16 + lane * 8;
+#pragma unroll
+      for (int c = 0; c < GW_NCH; ++c) w[c] = ldw<KEEP>(wr + min(cw + c, nchunk - 1) * 512);
+    };
+    auto mac = [&](bf16x8 (&w)[GW_NCH], int i) {
+#pragma unroll
+      for (int c = 0; c < GW_NCH; ++c) {
+        const bf16x8 wc = cw + c < nchunk ? w[c] : zero8;   // chunks past K: zero weights
+#pragma unroll
+        for (int mr = 0; mr < MREP; ++mr) acc[i][mr] = mfma(wc, xf[c][mr], acc[i][mr]);
+      }
+    };
+    wload(wa, 0);
+#pragma unroll
+    for (int i = 0; i < TPW; i += 2) {
+      if (i + 1 < TPW) wload(wb, i + 1);
+      mac(wa, i);
+      if (i + 2 < TPW) wload(wa, i + 2);
+      if (i + 1 < TPW) mac(wb, i + 1);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+#pragma unroll
+    for (int mr = 0; mr < MREP; ++mr)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[wave][mr * 256 + j * 64 + lane] = acc[i][mr][j];
+    __syncthreads();
+    for (int e = threadIdx.x; e < MREP * 256; e += 512) {
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) sum += red[w][e];
+      red[0][e] = sum;
+    }
+    __syncthreads();
+    const int t = t0 + i;
+    if (t < ntile) {
+      for (int mr = wave; mr < MREP; mr += 8) {
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = red[0][mr * 256 + j * 64 + lane];
+        epi_tile(a, 16 * mr + r, t * 16, lane, v);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int MREP, int TPW>
+static void launch_gemvw_t(const GemmArgs& a, hipStream_t st) {
+  const dim3 grid((a.N / 16 + TPW - 1) / TPW);
+  if (a.keep) hipLaunchKernelGGL((k_gemvw<MREP, TPW, true>), grid, dim3(512), 0, st, a);
+  else hipLaunchKernelGGL((k_gemvw<MREP, TPW, false>), grid, dim3(512), 0, st, a);
+}
+
+static int g_gemvw = 1;   // diagnostic: 0 = k_gemv for every 16 < M <= 64 (vv_gemv_tune_wide)
+extern "C" int vv_gemv_tune_wide(int on) {
+  g_gemvw = on;
+  return 0;
+}
+
+// 16 < M <= 64, >= 256 tiles, plain A (no transform), one K split
+static bool launch_gemvw(const GemmArgs& a, hipStream_t st) {
+  const int tiles = a.N / 16;
+  if (!g_gemvw || a.M <= 16 || a.M > 64 || tiles < 256 || a.xf.kind != XF_NONE || a.epi.kind == EPI_CFG_DPM)
+    return false;
+  const int mrep = (a.M + 15) / 16;
+  const int tpw = tiles >= 1024 ? 4 : tiles >= 512 ? 2 : 1;   // ~256-340 workgroups
+  if (mrep == 2) {
+    if (tpw == 4) launch_gemvw_t<2, 4>(a, st);
+    else if (tpw == 2) launch_gemvw_t<2, 2>(a, st);
+    else launch_gemvw_t<2, 1>(a, st);
+  } else if (mrep == 3) {
+    if (tpw == 4) launch_gemvw_t<3, 4>(a, st);
+    else if (tpw == 2) launch_gemvw_t<3, 2>(a, st);
+    else launch_gemvw_t<3, 1>(a, st);
+  } else {
+    if (tpw == 4) launch_gemvw_t<4, 4>(a, st);
+    else if (tpw == 2) launch_gemvw_t<4, 2>(a, st);
+    else launch_gemvw_t<4, 1>(a, st);
+  }
+  return true;
+}
+
 // ------------------------------------------------------------------ tiled GEMM (M > 64)
 template <int BN, int XF>
 __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
@@ -1025,6 +1147,7 @@ int launch_gemm(GemmArgs a, hipStream_t st) {
     fprintf(stderr, "vv_gemm M=%d N=%d K=%d xf=%d epi=%d\n", a.M, a.N, a.K, a.xf.kind, a.epi.kind);
   }
   if (a.M <= 64 && (a.M <= 16 || a.M <= g_gemv_max_m || a.epi.kind == EPI_CFG_DPM)) {
+    if (launch_gemvw(a, st)) return hipGetLastError() == hipSuccess ? 0 : 2;
     const int mrep = (a.M + 15) / 16;
     GemmPlan p = gemv_plan(a.N, a.K, a.M);
     if (p.nw > max_waves(mrep)) p.nw = max_waves(mrep);
