@@ -182,6 +182,10 @@ int vv_gemv_tune_maxm(int m);
  * use k_gemv (A fragments per tile) instead of k_gemvw (A held per K slice
  * across several tiles); 1 = built-in. */
 int vv_gemv_tune_wide(int on);
+/* Tuning hook (benchmarks only): the largest dynamic LDS (bytes) the M <= 16
+ * GEMV may stage its A slice in before it falls back to per-wave A fragment
+ * loads, up to 148 KiB (per-kernel opt-in above 64 KB); 0 = built-in (64 KB). */
+int vv_gemv_tune_lds(int bytes);
 /* Diagnostic (benchmarks only): M <= 16 GEMV launches write 4 s_memrealtime
  * stamps per workgroup (start, A staged, weights streamed, epilogue stored) to
  * buf (uint64[grid * 4]); NULL turns it off. */

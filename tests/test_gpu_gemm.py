@@ -141,3 +141,20 @@ def test_gemv_wide_rows(wide, M, N, K, epi):
     finally:
         L.vv_gemv_tune_wide(1)
     assert rel_err(Y, ref) < 5e-3 and max_rel(Y, ref) < 3e-2
+
+
+@pytest.mark.parametrize("lds", [0, 151552])
+@pytest.mark.parametrize("M,N,K,epi", [(16, 1536, 8960, "res"), (16, 1536, 4608, "res"), (8, 2048, 8192, "res"),
+                                       (12, 1536, 8960, "store"), (16, 1024, 16384, "gelu")])
+def test_gemv_large_lds_staging(lds, M, N, K, epi):
+    """M <= 16 long-row GEMVs (B = 8 down projections, split over two
+    workgroups): the A slice staged in > 64 KB of LDS (per-kernel opt-in,
+    tuning hook) vs the built-in per-wave fragment form; K = 16384 still
+    exceeds the LDS limit and takes the fragment form either way."""
+    L = _lib.lib()
+    L.vv_gemv_tune_lds(lds)
+    try:
+        Y, ref = run(M, N, K, epi, bias=True, res=epi == "res")
+    finally:
+        L.vv_gemv_tune_lds(0)
+    assert rel_err(Y, ref) < 5e-3 and max_rel(Y, ref) < 3e-2

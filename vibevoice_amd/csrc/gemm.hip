@@ -1064,11 +1064,36 @@ static GemmPlan gemv_plan(int N, int K, int M) {
 
 static int max_waves(int) { return 8; }
 
-// k_gemv1 stages the A slice in LDS (<= 64 KB)
-static bool gemv1_fits(const GemmArgs& a) {
+// k_gemv1's dynamic LDS: the staged A slice (+ per-item sums of squares for
+// the fused RMSNorm).  Built-in limit 64 KB.  Up to GEMV1_LDS_MAX is possible
+// with the per-kernel opt-in (one workgroup may hold 160 KiB; k_gemv1's static
+// arrays take ~8.3 KB) so the B = 8 down projections (M = 16 rows of 4,480 /
+// 2,304 columns per K split) stage A once per workgroup instead of k_gemv's
+// per-wave fragment loads -- measured slower (B = 8 step 5.51 -> 5.83 ms: one
+// workgroup per CU leaves too few weight loads in flight), so it stays a hook.
+constexpr size_t GEMV1_LDS_MAX = 151552, GEMV1_LDS_DEFAULT = 65536;
+static size_t g_gemv1_lds_max = GEMV1_LDS_DEFAULT;   // diagnostic (vv_gemv_tune_lds)
+extern "C" int vv_gemv_tune_lds(int bytes) {
+  g_gemv1_lds_max = bytes > 0 && (size_t)bytes <= GEMV1_LDS_MAX ? (size_t)bytes : GEMV1_LDS_DEFAULT;
+  return 0;
+}
+static size_t gemv1_lds(const GemmArgs& a) {
   const int nchunk = a.K >> 5;
   const size_t kw = ((nchunk + a.ksplit - 1) / a.ksplit) * 32;
-  return (((size_t)a.M * (kw + 8) * 2 + 15) & ~(size_t)15) + (size_t)a.M * (kw / 8) * 4 <= 65536;
+  const size_t xs = ((size_t)a.M * (kw + 8) * sizeof(bf16) + 15) & ~(size_t)15;
+  return xs + (a.xf.kind == XF_NORM ? (size_t)a.M * (kw / 8) * sizeof(float) : 0);
+}
+static bool gemv1_fits(const GemmArgs& a) { return gemv1_lds(a) <= g_gemv1_lds_max; }
+
+template <int U, int XF, bool KEEP, int TPW>
+static void go_gemv1(const GemmArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t st) {
+  if (lds > 65536) {   // > 64 KB of dynamic LDS needs the opt-in, once per instantiation
+    static const bool attr = hipFuncSetAttribute((const void*)k_gemv1<U, XF, KEEP, TPW>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)GEMV1_LDS_MAX) == hipSuccess;
+    (void)attr;   // a refused opt-in surfaces as the launch error
+  }
+  hipLaunchKernelGGL((k_gemv1<U, XF, KEEP, TPW>), grid, block, lds, st, a);
 }
 
 // TPW is a template argument so the one-tile form (every M < 8 launch) keeps
@@ -1076,13 +1101,13 @@ static bool gemv1_fits(const GemmArgs& a) {
 template <int XF, int TPW>
 static void launch_gemv1(const GemmArgs& a, int u, dim3 grid, dim3 block, size_t lds, hipStream_t st) {
   if (a.keep) {
-    if (u == 4) hipLaunchKernelGGL((k_gemv1<4, XF, true, TPW>), grid, block, lds, st, a);
-    else if (u == 2) hipLaunchKernelGGL((k_gemv1<2, XF, true, TPW>), grid, block, lds, st, a);
-    else hipLaunchKernelGGL((k_gemv1<8, XF, true, TPW>), grid, block, lds, st, a);
+    if (u == 4) go_gemv1<4, XF, true, TPW>(a, grid, block, lds, st);
+    else if (u == 2) go_gemv1<2, XF, true, TPW>(a, grid, block, lds, st);
+    else go_gemv1<8, XF, true, TPW>(a, grid, block, lds, st);
   } else {
-    if (u == 4) hipLaunchKernelGGL((k_gemv1<4, XF, false, TPW>), grid, block, lds, st, a);
-    else if (u == 2) hipLaunchKernelGGL((k_gemv1<2, XF, false, TPW>), grid, block, lds, st, a);
-    else hipLaunchKernelGGL((k_gemv1<8, XF, false, TPW>), grid, block, lds, st, a);
+    if (u == 4) go_gemv1<4, XF, false, TPW>(a, grid, block, lds, st);
+    else if (u == 2) go_gemv1<2, XF, false, TPW>(a, grid, block, lds, st);
+    else go_gemv1<8, XF, false, TPW>(a, grid, block, lds, st);
   }
 }
 
@@ -1093,10 +1118,7 @@ static void launch_gemv_xf(const GemmArgs& a, int mrep, int u, dim3 grid, dim3 b
     return;
   }
   if (mrep == 1) {
-    const int nchunk = a.K >> 5;
-    const int kw = ((nchunk + a.ksplit - 1) / a.ksplit) * 32;
-    const size_t xs_bytes = ((size_t)a.M * (kw + 8) * sizeof(bf16) + 15) & ~(size_t)15;
-    const size_t lds = xs_bytes + (size_t)a.M * (kw / 8) * sizeof(float);
+    const size_t lds = gemv1_lds(a);
     if (a.tpw == 1) launch_gemv1<XF, 1>(a, u, grid, block, lds, st);
     else if (a.tpw == 2) launch_gemv1<XF, 2>(a, u, grid, block, lds, st);
     else if (a.tpw == 4) launch_gemv1<XF, 4>(a, u, grid, block, lds, st);
