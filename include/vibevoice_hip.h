@@ -197,6 +197,11 @@ int vv_attn_stamps(void* buf);
  * 0 = built-in) and the largest split count merged inside the attention
  * kernel (more splits go to the separate merge pass; -1 = built-in). */
 int vv_attn_tune(int chunk, int merge_in);
+/* Tuning hook (benchmarks / tests): the attention kernel for many query rows
+ * per slot (prompt prefill): -1 = built-in choice (>= 256 rows and >= 32 rows
+ * per slot of the engine -> the 32-row-tile prefill kernel), 0 = always the
+ * per-row decode kernel, 1 = always the prefill kernel. */
+int vv_attn_prefill(int mode);
 /* Test switch (bit mask, default 3): bit 0 folds each codec Block1D's mixer
  * (norm, depthwise conv, gamma residual, FFN norm) into its fc1 GEMV where
  * <= 16 rows fit (XF_MIX); bit 1 runs whole narrow-stage blocks (C <= 128) as

@@ -95,3 +95,67 @@ def test_attention_plan_variants(chunk, merge_in):
         L.vv_attn_tune(0, -1)
     ref = reference(q.cpu(), K.cpu(), V.cpu(), slots.cpu(), pos.cpu())
     assert rel_err(out, ref) < 1e-2
+
+
+def _prefill_case(nh, nkv, runs, g):
+    """runs: [(slot, first_pos, count)] -> query rows in that order (consecutive
+    positions per run), cache filled for every slot up to its last position."""
+    nslot = max(s for s, _, _ in runs) + 1
+    ctx = (max(p + n for _, p, n in runs) + 63) // 64 * 64
+    K = torch.randn(nslot, nkv, ctx, 128, device=dev, generator=g).bfloat16()
+    V = torch.randn(nslot, nkv, ctx, 128, device=dev, generator=g).bfloat16()
+    slots = torch.tensor([s for s, p, n in runs for _ in range(n)], device=dev, dtype=torch.int32)
+    pos = torch.tensor([p + i for s, p, n in runs for i in range(n)], device=dev, dtype=torch.int32)
+    q = torch.randn(slots.numel(), nh * 128, device=dev, generator=g).bfloat16()
+    return q, K, V, slots, pos, ctx
+
+
+@pytest.mark.parametrize("nh,nkv,runs", [
+    (12, 2, [(0, 0, 700)]),                               # one prompt's causal prefill
+    (12, 2, [(0, 0, 137), (1, 0, 300), (2, 0, 45)]),      # B = 3 ragged prompts in one launch (tiles span slots)
+    (12, 2, [(1, 500, 70), (0, 0, 33)]),                  # a continuation chunk (keys before the first row)
+    (28, 4, [(0, 0, 260), (1, 0, 5)]),                    # Large head layout (G = 7)
+    (8, 8, [(0, 0, 100)]),                                # G = 1
+])
+def test_prefill_attention_vs_torch(nh, nkv, runs):
+    """k_attn_pf (32-row tiles x the G heads of a kv head, transposed MFMA
+    softmax) vs the fp32 torch reference, causal per row, rows of several
+    slots in one launch.  Tolerance as above (bf16 P and output)."""
+    g = torch.Generator(device=dev).manual_seed(len(runs) * 1000 + nh)
+    q, K, V, slots, pos, ctx = _prefill_case(nh, nkv, runs, g)
+    eng = tiny_engine()
+    L = _lib.lib()
+    L.vv_attn_prefill(1)
+    try:
+        out = run_attention(eng, q, K, V, slots, pos, ctx)
+        torch.cuda.synchronize()
+    finally:
+        L.vv_attn_prefill(-1)
+    ref = reference(q.cpu(), K.cpu(), V.cpu(), slots.cpu(), pos.cpu())
+    assert torch.isfinite(out).all()
+    assert rel_err(out, ref) < 1e-2
+
+
+def test_prefill_attention_scattered_rows():
+    """Rows in arbitrary (slot, position) order -- every tile needs several
+    slot passes; the prefill kernel and the per-row decode kernel agree."""
+    g = torch.Generator(device=dev).manual_seed(77)
+    nslot, ctx, n = 5, 512, 150
+    K = torch.randn(nslot, 2, ctx, 128, device=dev, generator=g).bfloat16()
+    V = torch.randn(nslot, 2, ctx, 128, device=dev, generator=g).bfloat16()
+    slots = torch.randint(0, nslot, (n,), device=dev, generator=g, dtype=torch.int32)
+    pos = torch.randint(0, ctx, (n,), device=dev, generator=g, dtype=torch.int32)
+    q = torch.randn(n, 12 * 128, device=dev, generator=g).bfloat16()
+    eng = tiny_engine()
+    L = _lib.lib()
+    outs = []
+    for mode in (1, 0):
+        L.vv_attn_prefill(mode)
+        try:
+            outs.append(run_attention(eng, q, K, V, slots, pos, ctx))
+            torch.cuda.synchronize()
+        finally:
+            L.vv_attn_prefill(-1)
+    ref = reference(q.cpu(), K.cpu(), V.cpu(), slots.cpu(), pos.cpu())
+    assert rel_err(outs[0], ref) < 1e-2 and rel_err(outs[1], ref) < 1e-2
+    assert rel_err(outs[0], outs[1]) < 1e-2

@@ -66,10 +66,22 @@ def oracle_sd(sd):
     return {k[len("model.language_model."):]: v for k, v in sd.items() if k.startswith("model.language_model.")}
 
 
-@pytest.mark.parametrize("ctx", [40, 600, 2500])
-def test_lm_real_shapes_vs_oracle(ctx):
+@pytest.mark.parametrize("ctx,pf", [(40, -1), (600, -1), (2500, -1), (600, 0)])
+def test_lm_real_shapes_vs_oracle(ctx, pf):
+    """pf = -1: the engine's own attention choice (the 801- and 3,334-row
+    prefills take the 32-row-tile prefill kernel); 0: the per-row decode
+    kernel forced for the prefill too."""
+    from vibevoice_amd import _lib
     cfg = tiny_config(hidden=1536, layers=2, heads=12, kv_heads=2, inter=8960)
     eng, sd = make_engine(cfg, seed=1, max_batch=2, max_ctx=4096)
+    _lib.lib().vv_attn_prefill(pf)
+    try:
+        _lm_real_shapes(eng, sd, cfg, ctx)
+    finally:
+        _lib.lib().vv_attn_prefill(-1)
+
+
+def _lm_real_shapes(eng, sd, cfg, ctx):
     lcfg = dict(cfg.decoder_config)
     osd = oracle_sd(sd)
     g = torch.Generator().manual_seed(ctx)

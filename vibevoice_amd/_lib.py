@@ -65,6 +65,7 @@ EXPORTS = [
     ("vv_gemv_stamps", I, [P]),
     ("vv_attn_stamps", I, [P]),
     ("vv_attn_tune", I, [I, I]),
+    ("vv_attn_prefill", I, [I]),
     ("vv_codec_mix_fusion", I, [I]),
 ]
 

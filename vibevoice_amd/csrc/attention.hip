@@ -457,6 +457,200 @@ int launch_final_head(int R, int H, const bf16* h, const int* idx, const bf16* n
 }
 
 
+// ---------------------------------------------------------------- prefill attention
+// The causal prefill of a prompt (the reference runs the
+// whole prompt through Qwen2Model once, modeling_vibevoice_inference.py:484 at
+// step 0): thousands of query rows over the same slot.  k_attn gives every row
+// its own pass over its keys (K/V re-read per row, 6 of 16 MFMA rows used), so
+// here a workgroup takes PF_Q = 32 consecutive query rows x the G query heads of
+// one kv head (wave = head), and the G waves stream the same K/V (L1/L2 hits
+// after the first wave).  Per wave and 32-key step, on the matrix cores
+// (mfma 16x16x32 bf16), transposed so P never leaves registers:
+//   S^T[32 keys x 32 queries] = K . Q^T   (A = K rows from the cache, B = the
+//       wave's Q fragments held for the whole kernel): lane holds keys
+//       16kt + 4g + i of query column r
+//   online softmax per query column (the 4 lanes r, r+16, r+32, r+48 hold its
+//       keys: two xor-shuffles for the max; the sum stays per lane until the end)
+//   O^T[128 dims x 32 queries] += V^T . P^T, with the MFMA's k slots 8g..8g+7
+//       mapped to keys {4g..4g+3, 16+4g..16+4g+3}: exactly the lane's own P
+//       values (bf16, as the reference's eager path rounds them), so V^T's A
+//       fragment is two 8-byte loads from the [dim][32 pos] V blocks.
+// Rows of a tile may belong to different slots (sample boundaries, ragged
+// prompts): the tile loops over its distinct slots, each pass masking the rows
+// of other slots, so any (slot, pos) list is exact; runs of one slot cost one
+// pass.  Keys > the row's position are masked (causal); the pass spans keys
+// [0, max position of its rows].
+constexpr int PF_Q = 32;
+
+template <int G>
+__global__ void __launch_bounds__(64 * G) k_attn_pf(AttnArgs a) {
+  constexpr int d = 128;
+  __shared__ int s_slot[PF_Q], s_pos[PF_Q];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int ntile = (a.nq + PF_Q - 1) / PF_Q;
+  const int q0 = (ntile - 1 - (int)blockIdx.x) * PF_Q;   // late (long) tiles first
+  const int kh = blockIdx.y, h = kh * G + wave;
+  if (threadIdx.x < PF_Q) {
+    const int qi = q0 + threadIdx.x;
+    s_slot[threadIdx.x] = qi < a.nq ? a.slots[qi] : -1;
+    s_pos[threadIdx.x] = qi < a.nq ? a.pos[qi] : -1;
+  }
+  __syncthreads();
+  const bf16x8 z8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+  int qslot[2], qpos[2];
+  bf16x8 qf[2][4];   // B operand of S^T: column = query 16qt + r, k = dims 32c + 8g .. +7
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int j = 16 * qt + r, qi = q0 + j;
+    qslot[qt] = s_slot[j];
+    qpos[qt] = s_pos[j];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      qf[qt][c] = qi < a.nq ? *(const bf16x8*)(a.q + (long long)qi * a.nh * d + h * d + 32 * c + 8 * g) : z8;
+  }
+  f32x4 o[8][2];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) o[dt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  const float sl2 = a.scale * 1.4426950408889634f;   // scores in log2 units
+  unsigned valid = 0;
+  for (int j = 0; j < PF_Q; ++j)
+    if (s_slot[j] >= 0) valid |= 1u << j;
+  unsigned done = 0;
+  while (done != valid) {
+    // one pass per distinct slot of the tile
+    const int slot = s_slot[__builtin_ctz(valid & ~done)];
+    int kmax = 0;
+    for (int j = 0; j < PF_Q; ++j)
+      if (s_slot[j] == slot) {
+        done |= 1u << j;
+        kmax = max(kmax, s_pos[j]);
+      }
+    const int nk = kmax + 1;
+    const bool in0 = qslot[0] == slot, in1 = qslot[1] == slot;
+    const long long cbase = (long long)a.layer * a.kv.s_layer + (long long)slot * a.kv.s_slot +
+                            (long long)kh * a.kv.s_head;
+    const bf16* K = a.kv.k + cbase;    // [ctx][128]
+    const bf16* VB = a.kv.v + cbase;   // 32-position blocks of [128][32] (v_off)
+    for (int k0 = 0; k0 < nk; k0 += 32) {
+      // K rows k0 .. k0+31 (the cache's 32-position granule is allocated; rows
+      // past nk are masked below)
+      bf16x8 kf[2][4], vf[8];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) kf[kt][c] = *(const bf16x8*)(K + (long long)(k0 + 16 * kt + r) * d + 32 * c + 8 * g);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        const bf16* vp = VB + v_off(16 * dt + r, k0 + 4 * g);
+        const bf16x4 lo = *(const bf16x4*)vp, hi = *(const bf16x4*)(vp + 16);
+        vf[dt] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      if (k0 + 32 > nk) {   // unwritten V past the last key would meet P = 0: zero it (0 * NaN)
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (k0 + (e < 4 ? 4 * g + e : 16 + 4 * g + e - 4) >= nk) vf[dt][e] = (bf16)0.f;
+      }
+      f32x4 s[2][2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          s[kt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int c = 0; c < 4; ++c) s[kt][qt] = amfma(kf[kt][c], qf[qt][c], s[kt][qt]);
+        }
+      bf16x8 pf[2];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const bool in = qt == 0 ? in0 : in1;
+        float x[2][4], mx = -INFINITY;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int key = k0 + 16 * kt + 4 * g + i;
+            x[kt][i] = in && key <= qpos[qt] ? s[kt][qt][i] * sl2 : -INFINITY;
+            mx = fmaxf(mx, x[kt][i]);
+          }
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float mnew = fmaxf(m[qt], mx);
+        const bool live = mnew != -INFINITY;
+        const float al = live ? exp2f(m[qt] - mnew) : 1.f;
+        float ps = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float p = live ? exp2f(x[kt][i] - mnew) : 0.f;
+            ps += p;
+            pf[qt][4 * kt + i] = (bf16)p;
+          }
+        l[qt] = l[qt] * al + ps;
+        m[qt] = mnew;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) o[dt][qt] *= al;
+      }
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) o[dt][qt] = amfma(vf[dt], pf[qt], o[dt][qt]);
+    }
+  }
+  // lane holds O^T[dim 16dt + 4g + i][query 16qt + r]; l summed over the 4 lanes of the column
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    float L = l[qt] + __shfl_xor(l[qt], 16);
+    L += __shfl_xor(L, 32);
+    const int qi = q0 + 16 * qt + r;
+    if (qi < a.nq) {
+      const float inv = 1.f / L;
+      bf16* op = a.out + (long long)qi * a.nh * d + h * d + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        bf16x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = tobf(o[dt][qt][i] * inv);
+        *(bf16x4*)(op + 16 * dt) = v;
+      }
+    }
+  }
+}
+
+static int g_att_prefill = -1;   // diagnostic override (vv_attn_prefill): -1 auto, 0 never, 1 always
+extern "C" int vv_attn_prefill(int mode) {
+  g_att_prefill = mode < 0 ? -1 : mode > 0 ? 1 : 0;
+  return 0;
+}
+
+// Tiles of 32 rows over at most nslots slots average <= 2 passes once
+// nq >= 32 * nslots; decode steps (one row per slot) stay on k_attn.
+bool attn_use_prefill(int nq, int nslots) {
+  if (g_att_prefill >= 0) return g_att_prefill == 1;
+  return nq >= 256 && nq >= PF_Q * nslots;
+}
+
+static int launch_attn_pf(const AttnArgs& a, hipStream_t st) {
+  const dim3 grid((a.nq + PF_Q - 1) / PF_Q, a.nkv);
+  switch (a.nh / a.nkv) {
+    case 1: hipLaunchKernelGGL((k_attn_pf<1>), grid, dim3(64), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((k_attn_pf<2>), grid, dim3(128), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((k_attn_pf<3>), grid, dim3(192), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((k_attn_pf<4>), grid, dim3(256), 0, st, a); break;
+    case 5: hipLaunchKernelGGL((k_attn_pf<5>), grid, dim3(320), 0, st, a); break;
+    case 6: hipLaunchKernelGGL((k_attn_pf<6>), grid, dim3(384), 0, st, a); break;
+    case 7: hipLaunchKernelGGL((k_attn_pf<7>), grid, dim3(448), 0, st, a); break;
+    default: hipLaunchKernelGGL((k_attn_pf<8>), grid, dim3(512), 0, st, a); break;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
 // Launch plan for keys up to max_len: splits of ATT_CHUNK keys (at most
 // ATT_SPLITS_MAX; beyond that the splits grow in ATT_CHUNK steps).  Each row
 // sizes its own splits from its length (row_chunk), so a plan made for
@@ -500,8 +694,9 @@ static void launch_attn_nw(const AttnArgs& a, dim3 grid, hipStream_t st) {
 
 int launch_attn(AttnArgs a, hipStream_t st) {
   if (a.nq <= 0) return 0;
-  if (a.kv.d != 128 || a.nh % a.nkv || a.nh / a.nkv > ATT_GMAX || a.chunk % ATT_KC || a.nsplit > ATT_SPLITS_MAX)
-    return 1;
+  if (a.kv.d != 128 || a.nh % a.nkv || a.nh / a.nkv > ATT_GMAX) return 1;
+  if (a.prefill) return launch_attn_pf(a, st);
+  if (a.chunk % ATT_KC || a.nsplit > ATT_SPLITS_MAX) return 1;
   if (a.nsplit > 1 && (!a.part_o || !a.part_ml || !a.counters)) return 1;
   a.merge = a.nsplit > (g_att_merge_in >= 0 ? g_att_merge_in : ATT_MERGE_IN) ? 1 : 0;
   dim3 grid(a.nq * a.nkv, a.nsplit);

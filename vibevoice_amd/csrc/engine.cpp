@@ -782,7 +782,7 @@ int vv_embed(vv_ctx* c, int n, const int* ids, void* out, vv_stream vst) {
 // interleave its ranks layer by layer (vv_lm_forward_group) or all-reduce over
 // RCCL between the halves (vv_lm_forward).
 struct LmPass {
-  int ntok = 0, nsplit = 1, chunk = 64;
+  int ntok = 0, nsplit = 1, chunk = 64, prefill = 0;
   bf16 *h = nullptr, *q = nullptr, *att = nullptr, *act = nullptr;
   RowMap in_m, hm;
   const int *slot = nullptr, *pos = nullptr;
@@ -807,7 +807,8 @@ static int lm_begin(vv_ctx* c, LmPass& P, int ntok, const void* embeds, int embe
   P.q = qkv + (size_t)ntok * c->qkv_n;
   P.att = P.q + (size_t)ntok * nhd;
   P.act = P.att + (size_t)ntok * nhd;
-  P.nsplit = attn_plan(ntok, k.n_kv_heads, max_pos_p1, &P.chunk);
+  P.prefill = attn_use_prefill(ntok, c->lm_slots) ? 1 : 0;
+  P.nsplit = P.prefill ? 1 : attn_plan(ntok, k.n_kv_heads, max_pos_p1, &P.chunk);
   if (P.nsplit > 1) {
     if ((size_t)ntok * k.n_kv_heads > 65536) FAIL("attention split tickets exhausted");
     CHK(c->attn_part.ensure((size_t)ntok * k.n_heads * P.nsplit * (d + 2) * sizeof(float)));
@@ -863,6 +864,7 @@ static int lm_attn_half(vv_ctx* c, LmPass& P, int l, hipStream_t st) {
   at.layer = l;
   at.nsplit = P.nsplit;
   at.chunk = P.chunk;
+  at.prefill = P.prefill;
   at.counters = (unsigned*)c->attn_cnt.p;
   at.scale = 1.0f / sqrtf((float)d);
   at.q = P.q;
@@ -1246,7 +1248,9 @@ int vv_attention_bf16(int nq, int nh, int nkv, const void* q, const void* k_cach
   AttnArgs at;
   memset(&at, 0, sizeof(at));
   int chunk = 0;
-  at.nsplit = attn_plan(nq, nkv, max_pos_p1, &chunk);
+  // the slot count is unknown here: auto keeps k_attn (vv_attn_prefill(1) forces k_attn_pf)
+  at.prefill = attn_use_prefill(nq, nq) ? 1 : 0;
+  at.nsplit = at.prefill ? 1 : attn_plan(nq, nkv, max_pos_p1, &chunk);
   if (at.nsplit > 1) {
     if ((size_t)nq * nkv > 65536) FAIL("attention split tickets exhausted");
     CHK(c->attn_part.ensure((size_t)nq * nh * at.nsplit * (128 + 2) * sizeof(float)));

@@ -163,6 +163,7 @@ struct AttnArgs {
   float* part_ml;       // [nq][nh][nsplit][2]
   unsigned* counters;   // [nq * nkv] split tickets (zero between launches)
   unsigned long long* stamps;   // diagnostics only (tools/attn_stamps.py): 4 stamps per workgroup
+  int prefill;          // 1: k_attn_pf (query rows in runs sharing a slot; no splits), see attn_use_prefill
 };
 
 // out_r = sum_r in_r for every r (single-process tensor-parallel group)
@@ -190,6 +191,9 @@ int launch_silu(int n, const bf16* x, bf16* y, hipStream_t st);
 int launch_cfg_dpm(int n, int D, DpmCoef k, const bf16* eps, bf16* x, bf16* m1, const float* noise, hipStream_t st);
 int launch_gather_rows(int n, int C, const bf16* src, long long lds, const int* idx, RowMap dst, hipStream_t st);
 int attn_plan(int nq, int nkv, int max_len, int* chunk);
+// true: nq query rows over at most nslots distinct slots take the prefill
+// kernel (k_attn_pf: 32-row tiles share K/V; no split workspace)
+bool attn_use_prefill(int nq, int nslots);
 int launch_attn(AttnArgs a, hipStream_t st);
 int launch_kv_fill(KVLayout kv, int n_layers, int nkv, int n, const int* slots, int p0, int p1, unsigned seed,
                    hipStream_t st);
