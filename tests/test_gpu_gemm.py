@@ -158,3 +158,21 @@ def test_gemv_large_lds_staging(lds, M, N, K, epi):
     finally:
         L.vv_gemv_tune_lds(0)
     assert rel_err(Y, ref) < 5e-3 and max_rel(Y, ref) < 3e-2
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(256, 2048, 1536, "store"), (257, 1536, 1536, "res"), (1000, 1536, 8960, "res"),
+                                       (1000, 17920, 1536, "silu_mul"), (4100, 2048, 1536, "store"),
+                                       (300, 1024, 512, "gelu"), (640, 512, 128, "f32")])
+def test_gemm_big_tile(M, N, K, epi):
+    """Prefill-sized GEMMs on the LDS-staged 128 x 128 tile (k_gemm_big) vs
+    torch fp32, and vs k_gemm (same K order of MFMA accumulation) -- ragged
+    last row tile, every epilogue kind the prefill uses."""
+    L = _lib.lib()
+    Y, ref = run(M, N, K, epi, bias=epi != "silu_mul", res=epi == "res")
+    L.vv_gemm_tune_big(0)
+    try:
+        Y0, _ = run(M, N, K, epi, bias=epi != "silu_mul", res=epi == "res")
+    finally:
+        L.vv_gemm_tune_big(1)
+    assert rel_err(Y, ref) < 5e-3
+    assert torch.equal(Y, Y0)

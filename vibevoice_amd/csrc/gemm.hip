@@ -966,6 +966,90 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ LDS-staged GEMM (prefill-sized M)
+// M >= GEMM_BIG_M rows (a prompt's prefill: thousands of tokens through every
+// projection).  k_gemm's operands come straight from L2
+// per wave (4 fragments per 4 MFMAs); here a 128 x 128 tile of 4 waves (each
+// 64 x 64: 4 weight tiles x 4 row tiles, 16 accumulators) stages each 64-deep
+// K step in LDS with 16-byte global_load_lds: the packed weight blocks are
+// already 1 KB MFMA fragments (one wave instruction each), and the A rows are
+// gathered per lane into the same fragment order (lane l <- row l & 15,
+// k 8(l >> 4)), so every LDS read is a conflict-free lane-linear ds_read_b128.
+// One __shared__ array (a second LDS object makes hipcc wait vmcnt(0) early,
+// cdna_hip_programming.md §5 trap 4a), two barriers per K step, ~3 workgroups
+// per CU overlap each other's staging.  Workgroups are remapped XCD-major so
+// each XCD's L2 holds a compact block of (row tile, weight tile) pairs.
+constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
+constexpr int GEMM_BIG_M = 256;
+
+__global__ void __launch_bounds__(256) k_gemm_big(GemmArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 sm[2 * 16 * 512];   // [W blocks 16][A blocks 16] x 1 KB
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ntm = (a.M + GB_M - 1) / GB_M, ntn = a.N / GB_N, total = ntm * ntn;
+  // XCD-major remap: consecutive ids go round-robin over the 8 XCDs; give XCD x
+  // the contiguous range [x * per, (x + 1) * per) of tiles
+  const int per = (total + 7) >> 3;
+  const int t = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (t >= total) return;
+  // grouped order inside the range: 4 row tiles sweep the weight tiles together
+  constexpr int GM = 4;
+  const int grp = t / (GM * ntn), gm = min(GM, ntm - grp * GM), tin = t - grp * GM * ntn;
+  const int tm = grp * GM + tin % gm, tn = tin / gm;
+  const int nchunk = a.K >> 5;
+  // staging: wave w fills W blocks 4w..4w+3 and A blocks 4w..4w+3 (block j = (tile j >> 1, chunk j & 1))
+  const bf16* wsrc[4];
+  const bf16* asrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = 4 * wave + i;
+    wsrc[i] = a.w + ((long long)(tn * 8 + (j >> 1)) * nchunk + (j & 1)) * 512 + lane * 8;
+    const int m = min(tm * GB_M + (j >> 1) * 16 + r, a.M - 1);
+    asrc[i] = rm_bf(a.a, m) + (j & 1) * 32 + 8 * g;
+  }
+  bf16* wl = sm;
+  bf16* al = sm + 16 * 512;
+  f32x4 acc[4][4];   // [weight tile nt][row tile mt]
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) acc[nt][mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int ks = 0; ks < (a.K >> 6); ++ks) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = 4 * wave + i;
+      __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + (long long)ks * 1024), (__attribute__((address_space(3))) void*)(wl + j * 512), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + ks * GB_K), (__attribute__((address_space(3))) void*)(al + j * 512), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      bf16x8 wf[4], xf[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) wf[nt] = *(const bf16x8*)(wl + ((wn * 4 + nt) * 2 + c) * 512 + lane * 8);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) xf[mt] = *(const bf16x8*)(al + ((wm * 4 + mt) * 2 + c) * 512 + lane * 8);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc[nt][mt] = mfma(wf[nt], xf[mt], acc[nt][mt]);
+    }
+    __syncthreads();
+  }
+  // epilogue: one epi_tile body in a rolled loop, the accumulators rotated
+  // through acc[0][0] (16 unrolled copies of epi_tile's RoPE / DPM forms
+  // spilled the accumulators to scratch)
+#pragma unroll 1
+  for (int i = 0; i < 16; ++i) {
+    float v[4] = {acc[0][0][0], acc[0][0][1], acc[0][0][2], acc[0][0][3]};
+    epi_tile(a, tm * GB_M + (wm * 4 + (i & 3)) * 16 + r, tn * GB_N + (wn * 4 + (i >> 2)) * 16, lane, v);
+#pragma unroll
+    for (int k = 0; k < 15; ++k) acc[k >> 2][k & 3] = acc[(k + 1) >> 2][(k + 1) & 3];
+  }
+}
+
 // ------------------------------------------------------------------ host launch
 static int g_tune_nw = 0, g_tune_ks = 0, g_tune_handoff = -1, g_tune_waves = 0, g_tune_u = 0, g_tune_tpw = 0;
 static int g_gemv_max_m = 64;   // more rows than this: the tiled k_gemm (vv_gemv_tune_maxm)
@@ -1132,8 +1216,19 @@ static void launch_gemv_xf(const GemmArgs& a, int mrep, int u, dim3 grid, dim3 b
   }
 }
 
+static int g_gemm_big = 1;   // diagnostic (vv_gemm_tune_big): 0 keeps every M > 64 GEMM on k_gemm
+extern "C" int vv_gemm_tune_big(int on) {
+  g_gemm_big = on ? 1 : 0;
+  return 0;
+}
+
 template <int XF>
 static int launch_gemm_xf(const GemmArgs& a, hipStream_t st) {
+  if (XF == XF_NONE && g_gemm_big && a.M >= GEMM_BIG_M && a.N % GB_N == 0 && a.K % GB_K == 0) {
+    const int total = ((a.M + GB_M - 1) / GB_M) * (a.N / GB_N);
+    hipLaunchKernelGGL(k_gemm_big, dim3(((total + 7) >> 3) * 8), dim3(256), 0, st, a);
+    return 0;
+  }
   if (a.N % 64 == 0) {
     dim3 grid((a.M + 63) / 64, a.N / 64);
     hipLaunchKernelGGL((k_gemm<64, XF>), grid, dim3(256), 0, st, a);
