@@ -164,15 +164,18 @@ def test_gemv_large_lds_staging(lds, M, N, K, epi):
                                        (1000, 17920, 1536, "silu_mul"), (4100, 2048, 1536, "store"),
                                        (300, 1024, 512, "gelu"), (640, 512, 128, "f32")])
 def test_gemm_big_tile(M, N, K, epi):
-    """Prefill-sized GEMMs on the LDS-staged 128 x 128 tile (k_gemm_big) vs
-    torch fp32, and vs k_gemm (same K order of MFMA accumulation) -- ragged
+    """Prefill-sized GEMMs on the LDS-staged 128 x 128 tile (k_gemm_big, two
+    stages; and its single-stage form) vs torch fp32, and vs k_gemm (same K
+    order of MFMA accumulation: bit-identical) -- ragged
     last row tile, every epilogue kind the prefill uses."""
     L = _lib.lib()
     Y, ref = run(M, N, K, epi, bias=epi != "silu_mul", res=epi == "res")
-    L.vv_gemm_tune_big(0)
+    outs = {}
     try:
-        Y0, _ = run(M, N, K, epi, bias=epi != "silu_mul", res=epi == "res")
+        for mode in (0, 1):   # k_gemm; the single-stage k_gemm_big
+            L.vv_gemm_tune_big(mode)
+            outs[mode], _ = run(M, N, K, epi, bias=epi != "silu_mul", res=epi == "res")
     finally:
-        L.vv_gemm_tune_big(1)
+        L.vv_gemm_tune_big(-1)
     assert rel_err(Y, ref) < 5e-3
-    assert torch.equal(Y, Y0)
+    assert torch.equal(Y, outs[0]) and torch.equal(Y, outs[1])

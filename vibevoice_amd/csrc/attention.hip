@@ -463,29 +463,60 @@ int launch_final_head(int R, int H, const bf16* h, const int* idx, const bf16* n
 // step 0): thousands of query rows over the same slot.  k_attn gives every row
 // its own pass over its keys (K/V re-read per row, 6 of 16 MFMA rows used), so
 // here a workgroup takes PF_Q = 32 consecutive query rows x the G query heads of
-// one kv head (wave = head), and the G waves stream the same K/V (L1/L2 hits
-// after the first wave).  Per wave and 32-key step, on the matrix cores
-// (mfma 16x16x32 bf16), transposed so P never leaves registers:
-//   S^T[32 keys x 32 queries] = K . Q^T   (A = K rows from the cache, B = the
-//       wave's Q fragments held for the whole kernel): lane holds keys
-//       16kt + 4g + i of query column r
+// one kv head (wave = head).  Per 32-key step the workgroup stages K and V once
+// in LDS (16 one-KB blocks of 16-byte global_load_lds, already in MFMA fragment
+// order, so every LDS read is a conflict-free lane-linear ds_read_b128), in a
+// ring of PF_NS stages: later steps are in flight while the G waves compute s.  Per wave
+// and step, on the matrix cores (mfma 16x16x32 bf16), transposed so P never
+// leaves registers:
+//   S^T[32 keys x 32 queries] = K . Q^T   (A = K rows, B = the wave's Q
+//       fragments held for the whole kernel).  Row 4g+i of key tile kt is key
+//       8g + 4kt + i (the K fragment gathers its rows in that order), so a lane
+//       holds keys 8g .. 8g+7 of query column r
 //   online softmax per query column (the 4 lanes r, r+16, r+32, r+48 hold its
 //       keys: two xor-shuffles for the max; the sum stays per lane until the end)
-//   O^T[128 dims x 32 queries] += V^T . P^T, with the MFMA's k slots 8g..8g+7
-//       mapped to keys {4g..4g+3, 16+4g..16+4g+3}: exactly the lane's own P
-//       values (bf16, as the reference's eager path rounds them), so V^T's A
-//       fragment is two 8-byte loads from the [dim][32 pos] V blocks.
+//   O^T[128 dims x 32 queries] += V^T . P^T: the MFMA's k slots 8g .. 8g+7 are
+//       the lane's own P values (bf16, as the reference's eager path rounds
+//       them) and V^T's fragment is 16 contiguous bytes of a [dim][32 pos] V block.
 // Rows of a tile may belong to different slots (sample boundaries, ragged
 // prompts): the tile loops over its distinct slots, each pass masking the rows
 // of other slots, so any (slot, pos) list is exact; runs of one slot cost one
 // pass.  Keys > the row's position are masked (causal); the pass spans keys
 // [0, max position of its rows].
 constexpr int PF_Q = 32;
+constexpr float PF_LAZY = 8.f;       // running-max slack (log2 units) before O is rescaled
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int PF_STAGE = 16 * 512;   // bf16 elements per staged step: 8 K + 8 V fragment blocks
+constexpr int PF_NS = 2;             // LDS stages: step s+1 in flight while step s computes (4 measured no faster)
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate must be constant)
+DEV void wait_vm(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;   // conservative
+  }
+}
 
 template <int G>
-__global__ void __launch_bounds__(64 * G) k_attn_pf(AttnArgs a) {
+__global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >= 4 ? 3 : 1))) k_attn_pf(AttnArgs a) {
   constexpr int d = 128;
-  __shared__ int s_slot[PF_Q], s_pos[PF_Q];
+  constexpr int NI_MAX = (16 + G - 1) / G;   // staging instructions per wave and step
+  // one LDS array (a second __shared__ object can make hipcc drain the
+  // prefetch early, cdna_hip_programming.md §5 trap 4a): 2 stages + row table
+  __shared__ __attribute__((aligned(16))) bf16 sm[PF_NS * PF_STAGE + 4 * PF_Q];
+  int* s_slot = (int*)(sm + PF_NS * PF_STAGE);
+  int* s_pos = s_slot + PF_Q;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int ntile = (a.nq + PF_Q - 1) / PF_Q;
@@ -496,18 +527,38 @@ __global__ void __launch_bounds__(64 * G) k_attn_pf(AttnArgs a) {
     s_slot[threadIdx.x] = qi < a.nq ? a.slots[qi] : -1;
     s_pos[threadIdx.x] = qi < a.nq ? a.pos[qi] : -1;
   }
-  __syncthreads();
   const bf16x8 z8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-  int qslot[2], qpos[2];
   bf16x8 qf[2][4];   // B operand of S^T: column = query 16qt + r, k = dims 32c + 8g .. +7
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
-    const int j = 16 * qt + r, qi = q0 + j;
-    qslot[qt] = s_slot[j];
-    qpos[qt] = s_pos[j];
+    const int qi = q0 + 16 * qt + r;
 #pragma unroll
     for (int c = 0; c < 4; ++c)
       qf[qt][c] = qi < a.nq ? *(const bf16x8*)(a.q + (long long)qi * a.nh * d + h * d + 32 * c + 8 * g) : z8;
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // no plain loads in flight beside the staging
+  __syncthreads();
+  int qslot[2], qpos[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    qslot[qt] = s_slot[16 * qt + r];
+    qpos[qt] = s_pos[16 * qt + r];
+  }
+  // this wave's staging blocks j = wave + G * i: j < 8 K fragment (kt = j >> 2,
+  // c = j & 3; lane row r' -> key 8(r' >> 2) + 4kt + (r' & 3)), j >= 8 V^T
+  // fragment dt = j - 8 (dims 16dt + r', keys 8g' .. 8g'+7); both advance by
+  // 128 elements per key
+  const int ni = (16 - wave + G - 1) / G;
+  int soff[NI_MAX];   // element offset in the step's 32-key K block / V block (< 4096)
+#pragma unroll
+  for (int i = 0; i < NI_MAX; ++i) {
+    const int j = wave + G * i;
+    if (j < 8) {
+      const int kt = j >> 2, c = j & 3;
+      soff[i] = (8 * (r >> 2) + 4 * kt + (r & 3)) * d + 32 * c + 8 * g;
+    } else {
+      soff[i] = (int)v_off(16 * (j - 8) + r, 8 * g);
+    }
   }
   f32x4 o[8][2];
 #pragma unroll
@@ -523,84 +574,119 @@ __global__ void __launch_bounds__(64 * G) k_attn_pf(AttnArgs a) {
   while (done != valid) {
     // one pass per distinct slot of the tile
     const int slot = s_slot[__builtin_ctz(valid & ~done)];
-    int kmax = 0;
+    int kmax = 0, kmin = 1 << 30;
+    unsigned seg = 0;
     for (int j = 0; j < PF_Q; ++j)
       if (s_slot[j] == slot) {
-        done |= 1u << j;
+        seg |= 1u << j;
         kmax = max(kmax, s_pos[j]);
+        kmin = min(kmin, s_pos[j]);
       }
-    const int nk = kmax + 1;
+    done |= seg;
+    // steps whose keys every valid row of the tile attends need no mask (rows
+    // past nq are never stored)
+    const int kfull = seg == valid ? kmin + 1 : 0;
+    const int nk = kmax + 1, nsteps = (nk + 31) >> 5;
     const bool in0 = qslot[0] == slot, in1 = qslot[1] == slot;
     const long long cbase = (long long)a.layer * a.kv.s_layer + (long long)slot * a.kv.s_slot +
                             (long long)kh * a.kv.s_head;
     const bf16* K = a.kv.k + cbase;    // [ctx][128]
     const bf16* VB = a.kv.v + cbase;   // 32-position blocks of [128][32] (v_off)
-    for (int k0 = 0; k0 < nk; k0 += 32) {
-      // K rows k0 .. k0+31 (the cache's 32-position granule is allocated; rows
-      // past nk are masked below)
-      bf16x8 kf[2][4], vf[8];
+    auto issue = [&](int step) {
+      bf16* st = sm + (step & (PF_NS - 1)) * PF_STAGE;
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) kf[kt][c] = *(const bf16x8*)(K + (long long)(k0 + 16 * kt + r) * d + 32 * c + 8 * g);
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) {
-        const bf16* vp = VB + v_off(16 * dt + r, k0 + 4 * g);
-        const bf16x4 lo = *(const bf16x4*)vp, hi = *(const bf16x4*)(vp + 16);
-        vf[dt] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-      if (k0 + 32 > nk) {   // unwritten V past the last key would meet P = 0: zero it (0 * NaN)
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            if (k0 + (e < 4 ? 4 * g + e : 16 + 4 * g + e - 4) >= nk) vf[dt][e] = (bf16)0.f;
-      }
+      for (int i = 0; i < NI_MAX; ++i)
+        if (i < ni) {
+          const bf16* src = (wave + G * i >= 8 ? VB : K) + (long long)step * 32 * d + soff[i];
+          __builtin_amdgcn_global_load_lds((const void*)src,
+                                           (__attribute__((address_space(3))) void*)(st + (wave + G * i) * 512),
+                                           16, 0, 0);
+        }
+    };
+    for (int p = 0; p < PF_NS - 1 && p < nsteps; ++p) issue(p);
+    for (int step = 0; step < nsteps; ++step) {
+      // the buffer of step + NS - 1 was released by the previous step's closing barrier
+      if (step + PF_NS - 1 < nsteps) issue(step + PF_NS - 1);
+      wait_vm(ni * min(PF_NS - 1, nsteps - 1 - step));   // this wave's loads of `step` have landed
+      asm volatile("s_barrier" ::: "memory");
+      const int k0 = step * 32;
+      const bf16* st = sm + (step & (PF_NS - 1)) * PF_STAGE;
       f32x4 s[2][2];
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+      for (int kt = 0; kt < 2; ++kt) {
+        bf16x8 kf[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) kf[c] = *(const bf16x8*)(st + (kt * 4 + c) * 512 + lane * 8);
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) {
           s[kt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int c = 0; c < 4; ++c) s[kt][qt] = amfma(kf[kt][c], qf[qt][c], s[kt][qt]);
+          for (int c = 0; c < 4; ++c) s[kt][qt] = amfma(kf[c], qf[qt][c], s[kt][qt]);
         }
-      bf16x8 pf[2];
+      }
+      // online softmax with a lazy running max: a column's m (log2 units) moves
+      // only when a score exceeds it by > PF_LAZY, so P <= 2^PF_LAZY and the
+      // O / l rescale (64 multiplies per column pair) runs only on the steps
+      // where some column of the wave moved (a wave-uniform branch)
+      const bool full = k0 + 32 <= kfull;
+      float x[2][2][4], al[2];
+      bool move[2];
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
         const bool in = qt == 0 ? in0 : in1;
-        float x[2][4], mx = -INFINITY;
+        float mx = -INFINITY;
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const int key = k0 + 16 * kt + 4 * g + i;
-            x[kt][i] = in && key <= qpos[qt] ? s[kt][qt][i] * sl2 : -INFINITY;
-            mx = fmaxf(mx, x[kt][i]);
+            const int key = k0 + 8 * g + 4 * kt + i;
+            x[qt][kt][i] = full || (in && key <= qpos[qt]) ? s[kt][qt][i] * sl2 : -INFINITY;
+            mx = fmaxf(mx, x[qt][kt][i]);
           }
         mx = fmaxf(mx, __shfl_xor(mx, 16));
         mx = fmaxf(mx, __shfl_xor(mx, 32));
-        const float mnew = fmaxf(m[qt], mx);
-        const bool live = mnew != -INFINITY;
-        const float al = live ? exp2f(m[qt] - mnew) : 1.f;
+        move[qt] = mx > m[qt] + PF_LAZY;   // also the first live step (m = -inf); lanes of a column agree
+        al[qt] = move[qt] ? exp2f(m[qt] - mx) : 1.f;
+        if (move[qt]) m[qt] = mx;
+      }
+      if (__builtin_amdgcn_ballot_w64(move[0] || move[1])) {
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          l[qt] *= al[qt];
+#pragma unroll
+          for (int dt = 0; dt < 8; ++dt) o[dt][qt] *= al[qt];
+        }
+      }
+      bf16x8 pf[2];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const bool live = m[qt] != -INFINITY;
         float ps = 0.f;
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float p = live ? exp2f(x[kt][i] - mnew) : 0.f;
+            const float p = live ? exp2f(x[qt][kt][i] - m[qt]) : 0.f;
             ps += p;
             pf[qt][4 * kt + i] = (bf16)p;
           }
-        l[qt] = l[qt] * al + ps;
-        m[qt] = mnew;
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) o[dt][qt] *= al;
+        l[qt] += ps;
       }
+      // unwritten V past the last key would meet P = 0: zero it (0 * NaN) with a
+      // bit mask over the lane's keys 8g .. 8g+7 (branch-free: a uniform branch
+      // per fragment serialised the LDS reads)
+      const int lim = nk - k0 - 8 * g;
+      u32x4 vm;
 #pragma unroll
-      for (int dt = 0; dt < 8; ++dt)
+      for (int p2 = 0; p2 < 4; ++p2) vm[p2] = (2 * p2 < lim ? 0xFFFFu : 0u) | (2 * p2 + 1 < lim ? 0xFFFF0000u : 0u);
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) o[dt][qt] = amfma(vf[dt], pf[qt], o[dt][qt]);
+      for (int dt = 0; dt < 8; ++dt) {
+        const u32x4 raw = *(const u32x4*)(st + (8 + dt) * 512 + lane * 8);
+        const bf16x8 vf = __builtin_bit_cast(bf16x8, raw & vm);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) o[dt][qt] = amfma(vf, pf[qt], o[dt][qt]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // this stage is free for step + NS
     }
   }
   // lane holds O^T[dim 16dt + 4g + i][query 16qt + r]; l summed over the 4 lanes of the column

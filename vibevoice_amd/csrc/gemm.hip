@@ -982,8 +982,10 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
 constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 constexpr int GEMM_BIG_M = 256;
 
+template <int NS>
 __global__ void __launch_bounds__(256) k_gemm_big(GemmArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16 sm[2 * 16 * 512];   // [W blocks 16][A blocks 16] x 1 KB
+  constexpr int STAGE = 2 * 16 * 512;   // [W blocks 16][A blocks 16] x 1 KB
+  __shared__ __attribute__((aligned(16))) bf16 sm[NS * STAGE];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int wm = wave >> 1, wn = wave & 1;
@@ -997,7 +999,7 @@ __global__ void __launch_bounds__(256) k_gemm_big(GemmArgs a) {
   constexpr int GM = 4;
   const int grp = t / (GM * ntn), gm = min(GM, ntm - grp * GM), tin = t - grp * GM * ntn;
   const int tm = grp * GM + tin % gm, tn = tin / gm;
-  const int nchunk = a.K >> 5;
+  const int nchunk = a.K >> 5, nks = a.K >> 6;
   // staging: wave w fills W blocks 4w..4w+3 and A blocks 4w..4w+3 (block j = (tile j >> 1, chunk j & 1))
   const bf16* wsrc[4];
   const bf16* asrc[4];
@@ -1008,22 +1010,38 @@ __global__ void __launch_bounds__(256) k_gemm_big(GemmArgs a) {
     const int m = min(tm * GB_M + (j >> 1) * 16 + r, a.M - 1);
     asrc[i] = rm_bf(a.a, m) + (j & 1) * 32 + 8 * g;
   }
-  bf16* wl = sm;
-  bf16* al = sm + 16 * 512;
+  auto issue = [&](int ks) {
+    bf16* st = sm + (ks % NS) * STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = 4 * wave + i;
+      __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + (long long)ks * 1024),
+                                       (__attribute__((address_space(3))) void*)(st + j * 512), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + ks * GB_K),
+                                       (__attribute__((address_space(3))) void*)(st + 16 * 512 + j * 512), 16, 0, 0);
+    }
+  };
   f32x4 acc[4][4];   // [weight tile nt][row tile mt]
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) acc[nt][mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  for (int ks = 0; ks < (a.K >> 6); ++ks) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j = 4 * wave + i;
-      __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + (long long)ks * 1024), (__attribute__((address_space(3))) void*)(wl + j * 512), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + ks * GB_K), (__attribute__((address_space(3))) void*)(al + j * 512), 16, 0, 0);
+  if (NS > 1) issue(0);
+  for (int ks = 0; ks < nks; ++ks) {
+    if (NS == 1) {
+      issue(ks);
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    } else if (ks + 1 < nks) {
+      // step ks + 1 streams into the other stage (released by the previous
+      // step's closing barrier) while this one computes; raw barriers so the
+      // prefetch stays in flight (cdna_hip_programming.md "Pipelining across barriers")
+      issue(ks + 1);
+      asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    const bf16* wl = sm + (ks % NS) * STAGE;
+    const bf16* al = wl + 16 * 512;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       bf16x8 wf[4], xf[4];
@@ -1036,7 +1054,7 @@ __global__ void __launch_bounds__(256) k_gemm_big(GemmArgs a) {
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) acc[nt][mt] = mfma(wf[nt], xf[mt], acc[nt][mt]);
     }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
   // epilogue: one epi_tile body in a rolled loop, the accumulators rotated
   // through acc[0][0] (16 unrolled copies of epi_tile's RoPE / DPM forms
@@ -1216,9 +1234,9 @@ static void launch_gemv_xf(const GemmArgs& a, int mrep, int u, dim3 grid, dim3 b
   }
 }
 
-static int g_gemm_big = 1;   // diagnostic (vv_gemm_tune_big): 0 keeps every M > 64 GEMM on k_gemm
+static int g_gemm_big = 2;   // diagnostic (vv_gemm_tune_big): 0 keeps every M > 64 GEMM on k_gemm; 1 / 2 LDS stages
 extern "C" int vv_gemm_tune_big(int on) {
-  g_gemm_big = on ? 1 : 0;
+  g_gemm_big = on < 0 ? 2 : on > 2 ? 2 : on;
   return 0;
 }
 
@@ -1226,7 +1244,8 @@ template <int XF>
 static int launch_gemm_xf(const GemmArgs& a, hipStream_t st) {
   if (XF == XF_NONE && g_gemm_big && a.M >= GEMM_BIG_M && a.N % GB_N == 0 && a.K % GB_K == 0) {
     const int total = ((a.M + GB_M - 1) / GB_M) * (a.N / GB_N);
-    hipLaunchKernelGGL(k_gemm_big, dim3(((total + 7) >> 3) * 8), dim3(256), 0, st, a);
+    if (g_gemm_big == 1) hipLaunchKernelGGL(k_gemm_big<1>, dim3(((total + 7) >> 3) * 8), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k_gemm_big<2>, dim3(((total + 7) >> 3) * 8), dim3(256), 0, st, a);
     return 0;
   }
   if (a.N % 64 == 0) {
