@@ -487,7 +487,25 @@ constexpr int PF_Q = 32;
 constexpr float PF_LAZY = 8.f;       // running-max slack (log2 units) before O is rescaled
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int PF_STAGE = 16 * 512;   // bf16 elements per staged step: 8 K + 8 V fragment blocks
-constexpr int PF_NS = 2;             // LDS stages: step s+1 in flight while step s computes (4 measured no faster)
+constexpr int PF_NS = 2;             // LDS stages: step s+1 in flight while step s computes (4, and a software
+                                     // pipeline issuing S of step s+1 before the softmax of s, measured no faster)
+
+// max / sum over lanes {l, l^16, l^32, l^48} (one query column of an MFMA
+// tile): gfx950's v_permlane16_swap / v_permlane32_swap (VALU, a few cycles)
+// instead of two ds_bpermute round trips.  With the value in both operands,
+// the 16-swap yields rows (0,0,2,2) and (1,1,3,3), the 32-swap (0,1,0,1) and (2,3,2,3).
+DEV float col_max(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+DEV float col_sum(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
 
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate must be constant)
 DEV void wait_vm(int n) {
@@ -643,8 +661,7 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
             x[qt][kt][i] = full || (in && key <= qpos[qt]) ? s[kt][qt][i] * sl2 : -INFINITY;
             mx = fmaxf(mx, x[qt][kt][i]);
           }
-        mx = fmaxf(mx, __shfl_xor(mx, 16));
-        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        mx = col_max(mx);
         move[qt] = mx > m[qt] + PF_LAZY;   // also the first live step (m = -inf); lanes of a column agree
         al[qt] = move[qt] ? exp2f(m[qt] - mx) : 1.f;
         if (move[qt]) m[qt] = mx;
@@ -692,8 +709,7 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
   // lane holds O^T[dim 16dt + 4g + i][query 16qt + r]; l summed over the 4 lanes of the column
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
-    float L = l[qt] + __shfl_xor(l[qt], 16);
-    L += __shfl_xor(L, 32);
+    const float L = col_sum(l[qt]);
     const int qi = q0 + 16 * qt + r;
     if (qi < a.nq) {
       const float inv = 1.f / L;
