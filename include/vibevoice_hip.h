@@ -187,10 +187,11 @@ int vv_gemv_tune_wide(int on);
  * loads, up to 148 KiB (per-kernel opt-in above 64 KB); 0 = built-in (64 KB). */
 int vv_gemv_tune_lds(int bytes);
 /* Tuning hook (benchmarks / tests): XF-free GEMMs with >= 256 rows,
- * N % 128 == 0 and K % 64 == 0 take the LDS-staged 128 x 128 tile (k_gemm_big,
- * the prefill projections) with 2 LDS stages (-1 / 2 = built-in) or 1 stage
- * (1); 0 = they stay on k_gemm. */
-int vv_gemm_tune_big(int on);
+ * N % 128 == 0, K % 64 == 0 and >= 256 such tiles (or >= 2^30 MACs) take the
+ * LDS-staged 128 x 128 tile (k_gemm_big, the prefill projections) with 2 LDS
+ * stages (-1 / 2 = built-in) or 1 stage (1); 0 = they stay on k_gemm;
+ * + 4 = any tile count (tests). */
+int vv_gemm_tune_big(int mode);
 /* Diagnostic (benchmarks only): M <= 16 GEMV launches write 4 s_memrealtime
  * stamps per workgroup (start, A staged, weights streamed, epilogue stored) to
  * buf (uint64[grid * 4]); NULL turns it off. */

@@ -169,13 +169,12 @@ def test_gemm_big_tile(M, N, K, epi):
     order of MFMA accumulation: bit-identical) -- ragged
     last row tile, every epilogue kind the prefill uses."""
     L = _lib.lib()
-    Y, ref = run(M, N, K, epi, bias=epi != "silu_mul", res=epi == "res")
     outs = {}
     try:
-        for mode in (0, 1):   # k_gemm; the single-stage k_gemm_big
+        for mode in (6, 5, 0):   # k_gemm_big 2 / 1 stages at any tile count; k_gemm
             L.vv_gemm_tune_big(mode)
-            outs[mode], _ = run(M, N, K, epi, bias=epi != "silu_mul", res=epi == "res")
+            outs[mode], ref = run(M, N, K, epi, bias=epi != "silu_mul", res=epi == "res")
     finally:
         L.vv_gemm_tune_big(-1)
-    assert rel_err(Y, ref) < 5e-3
-    assert torch.equal(Y, outs[0]) and torch.equal(Y, outs[1])
+    assert rel_err(outs[6], ref) < 5e-3
+    assert torch.equal(outs[6], outs[0]) and torch.equal(outs[5], outs[0])

@@ -981,6 +981,7 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
 // each XCD's L2 holds a compact block of (row tile, weight tile) pairs.
 constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 constexpr int GEMM_BIG_M = 256;
+constexpr int GEMM_BIG_TILES = 256;
 
 template <int NS>
 __global__ void __launch_bounds__(256) k_gemm_big(GemmArgs a) {
@@ -1234,16 +1235,26 @@ static void launch_gemv_xf(const GemmArgs& a, int mrep, int u, dim3 grid, dim3 b
   }
 }
 
-static int g_gemm_big = 2;   // diagnostic (vv_gemm_tune_big): 0 keeps every M > 64 GEMM on k_gemm; 1 / 2 LDS stages
-extern "C" int vv_gemm_tune_big(int on) {
-  g_gemm_big = on < 0 ? 2 : on > 2 ? 2 : on;
+// diagnostic (vv_gemm_tune_big): 0 keeps every M > 64 GEMM on k_gemm; 1 / 2 LDS
+// stages; + 4 ignores the tile-count threshold (tests of small shapes)
+static int g_gemm_big = 2, g_gemm_big_any = 0;
+extern "C" int vv_gemm_tune_big(int mode) {
+  g_gemm_big_any = mode >= 0 && (mode & 4) ? 1 : 0;
+  mode = mode < 0 ? 2 : mode & 3;
+  g_gemm_big = mode > 2 ? 2 : mode;
   return 0;
 }
 
 template <int XF>
 static int launch_gemm_xf(const GemmArgs& a, hipStream_t st) {
-  if (XF == XF_NONE && g_gemm_big && a.M >= GEMM_BIG_M && a.N % GB_N == 0 && a.K % GB_K == 0) {
-    const int total = ((a.M + GB_M - 1) / GB_M) * (a.N / GB_N);
+  // k_gemm_big only with >= one 128 x 128 tile per CU or >= 2^30 MACs: the
+  // decode loop's codec GEMMs (B = 8: 320 - 1,600 rows x 256 - 1,024 columns
+  // x K <= 1,024: 24 - 104 such tiles) are faster as k_gemm's 4x more 64 x 64
+  // workgroups (B = 8 step 5.53 ms vs 5.83), a 1K-token prompt's o / down /
+  // q|k|v projections (108 - 144 tiles, K >= 1,536) on k_gemm_big (14.5 -> 13.4 ms)
+  const int total = ((a.M + GB_M - 1) / GB_M) * (a.N / GB_N);
+  if (XF == XF_NONE && g_gemm_big && a.M >= GEMM_BIG_M && a.N % GB_N == 0 && a.K % GB_K == 0 &&
+      (total >= GEMM_BIG_TILES || (long long)a.M * a.N * a.K >= (1LL << 30) || g_gemm_big_any)) {
     if (g_gemm_big == 1) hipLaunchKernelGGL(k_gemm_big<1>, dim3(((total + 7) >> 3) * 8), dim3(256), 0, st, a);
     else hipLaunchKernelGGL(k_gemm_big<2>, dim3(((total + 7) >> 3) * 8), dim3(256), 0, st, a);
     return 0;
