@@ -36,15 +36,17 @@ SCHEDULES = [
 ]
 
 
-@pytest.mark.parametrize("refresh_negative", [True, False])
-def test_generate_matches_reference_loop(refresh_negative):
+@pytest.mark.parametrize("refresh_negative,prompt", [(True, 10), (False, 10), (True, 300)])
+def test_generate_matches_reference_loop(refresh_negative, prompt):
+    """prompt = 300: the 597-row prefill takes the prefill attention kernel
+    (k_attn_pf, rows of two slots per launch) inside generate()."""
     cfg = tiny_config(hidden=256, layers=2, heads=2, kv_heads=1, inter=512)
     sd = synthetic_state_dict(cfg, seed=21, device="cpu", mode="test", with_acoustic_encoder=False)
-    model = VibeVoiceForConditionalGenerationInference(cfg, sd, dev, max_batch=2, max_ctx=128)
+    model = VibeVoiceForConditionalGenerationInference(cfg, sd, dev, max_batch=2, max_ctx=max(128, 3 * prompt + 8))
     model.set_ddpm_inference_steps(5)
     g = torch.Generator().manual_seed(2)
-    ids = torch.randint(0, 151000, (2, 10), generator=g)
-    mask = torch.ones(2, 10, dtype=torch.long)
+    ids = torch.randint(0, 151000, (2, prompt), generator=g)
+    mask = torch.ones(2, prompt, dtype=torch.long)
     mask[1, :3] = 0
     ids[1, :3] = TOK.pad_token_id
     torch.manual_seed(1234)
