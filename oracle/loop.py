@@ -8,6 +8,9 @@ cache plus an attention mask that is reset (:563-580) and shifted
 (:628 vs :618) — so a test comparing the two checks the product's compacted
 bookkeeping against the reference's literal semantics.
 
+Pinned by golden G8 (tests/golden/make_golden.py:g8_loop): the reference's
+own generate() run end to end in fp32; tests/test_oracle_golden.py.
+
 Supported: text prompts (no voice prompt), refresh_negative True/False,
 greedy choice among the valid ids, or a forced token schedule.
 """

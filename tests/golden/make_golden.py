@@ -290,6 +290,88 @@ def g7_qwen2():
     save("g7_qwen2.npz", **out)
 
 
+# ------------------------------------------------------- G8 generate() loop trace
+G8_IDS = dict(eos=151643, start=151652, end=151653, diffusion=151654, pad=151655)
+G8_SCHEDULES = [
+    [151654, 151654, 151654, 151654, 151654, 151653, 151652, 151654, 151643],
+    [151654, 151653, 151654, 151654, 151652, 151654, 151654, 151643],   # step 1: skip at the KV-shift boundary
+]
+
+
+def g8_loop():
+    """The reference's own generate() (modeling_vibevoice_inference.py:327-710)
+    run end to end on CPU in fp32 with the tiny config of tests/tiny.py and the
+    seeded synthetic weights (vibevoice_amd.weights.synthetic_state_dict, seed
+    21, mode "test"; the test regenerates them), B = 2 left-padded text prompts,
+    forced token schedules (diffusion x k, speech_end, speech_start while the
+    other sample diffuses, the skip correction incl. its KV-shift boundary case,
+    eos), both refresh_negative modes, S = 5, cfg 1.3, torch.manual_seed(1234).
+    HF-4.51.3 plumbing shims: ref_harness.install_generate_shims.  The prompt
+    has no voice: the prefill's voice-encoder call (which generate() always
+    makes, :470-476) gets a dummy one-frame clip (hop 4) masked out of every position, and
+    the global RNG is restored around it so the diffusion noise stream is the
+    one a voice-free prompt would draw."""
+    import types
+    sys.path.insert(0, os.path.dirname(HERE))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from tiny import tiny_config, tiny_dict
+    from vibevoice_amd.weights import synthetic_state_dict
+    forced = []
+    ref_harness.install_generate_shims(R["mvi"], forced)
+    d = tiny_dict(hidden=256, layers=2, heads=2, kv_heads=1, inter=512)
+    d["torch_dtype"] = "float32"
+    d["decoder_config"]["attn_implementation"] = "eager"
+    rcfg = R["cfg"].VibeVoiceConfig(**d)
+    cls = R["mvi"].VibeVoiceForConditionalGenerationInference
+    torch.manual_seed(0)
+    model = cls(rcfg).float().eval()
+    sd = synthetic_state_dict(tiny_config(hidden=256, layers=2, heads=2, kv_heads=1, inter=512), seed=21,
+                              device="cpu", dtype=torch.float32, mode="test")
+    missing, unexpected = model.load_state_dict(sd, strict=False)
+    assert not unexpected, unexpected
+    missing = [k for k in missing if not k.startswith("model.acoustic_tokenizer.encoder.") and k != "lm_head.weight"]
+    assert not missing, missing
+    assert torch.equal(model.lm_head.weight, sd["model.language_model.embed_tokens.weight"])
+    model.set_ddpm_inference_steps(5)
+    orig = cls._process_speech_inputs
+
+    def voice_free(self, *a, **k):
+        st = torch.get_rng_state()
+        try:
+            return orig(self, *a, **k)
+        finally:
+            torch.set_rng_state(st)
+    cls._process_speech_inputs = voice_free
+    tok = types.SimpleNamespace(speech_start_id=G8_IDS["start"], speech_end_id=G8_IDS["end"],
+                                speech_diffusion_id=G8_IDS["diffusion"], eos_token_id=G8_IDS["eos"],
+                                bos_token_id=None, pad_token_id=G8_IDS["pad"])
+    g = torch.Generator().manual_seed(2)
+    P = 10
+    ids = torch.randint(0, 151000, (2, P), generator=g)
+    mask = torch.ones(2, P, dtype=torch.long)
+    mask[1, :3] = 0
+    ids[1, :3] = G8_IDS["pad"]
+    forced[:] = G8_SCHEDULES
+    out = {"input_ids": ids.numpy(), "attention_mask": mask.numpy(),
+           "schedules": np.array([s + [G8_IDS["eos"]] * (9 - len(s)) for s in G8_SCHEDULES]),
+           "schedule_lens": np.array([len(s) for s in G8_SCHEDULES]),
+           "sd_checksum": np.array([float(v.double().sum()) for v in sd.values()])}
+    for refresh in (True, False):
+        torch.manual_seed(1234)
+        with torch.no_grad():
+            o = model.generate(input_ids=ids, attention_mask=mask, tokenizer=tok, cfg_scale=1.3,
+                               speech_tensors=torch.zeros(1, 4), speech_masks=torch.zeros(1, 1, dtype=torch.bool),
+                               speech_input_mask=torch.zeros(2, P, dtype=torch.bool), refresh_negative=refresh,
+                               show_progress_bar=False)
+        tag = "refresh" if refresh else "norefresh"
+        out[f"{tag}/sequences"] = o.sequences.numpy()
+        out[f"{tag}/reach"] = o.reach_max_step_sample.numpy()
+        for b, a in enumerate(o.speech_outputs):
+            out[f"{tag}/audio{b}"] = f32(a)
+    cls._process_speech_inputs = orig
+    save("g8_loop.npz", **out)
+
+
 # ---------------------------------------------------------------- G9 processor
 PROC_SCRIPTS = [
     "Speaker 1: Hello there, welcome to the show.\nSpeaker 2: It's great to be here!\n\nSpeaker 1:   Fine, thanks.",
@@ -365,3 +447,4 @@ if __name__ == "__main__":
     g4_g5_codec()
     g6_connector()
     g7_qwen2()
+    g8_loop()

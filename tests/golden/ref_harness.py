@@ -136,3 +136,84 @@ def load():
     mvi.VibeVoiceForConditionalGenerationInference.tie_weights = tie_weights
     _loaded.update(dpm=dpm, cfg=cfg, head=head, tok=tok, mv=mv, mvi=mvi)
     return _loaded
+
+
+def install_generate_shims(mvi, forced):
+    """Let the reference's own generate() (modeling_vibevoice_inference.py:327-710)
+    run under transformers 5.15 on CPU, for the G8 loop trace.
+
+    Harness-side only.  The loop body (negative-stream reset / skip, diffusion,
+    streaming codec, connectors) is the reference's code unchanged; the shims
+    replace only the transformers-4.51.3 plumbing it calls, which 5.15 changed:
+      * `_build_generate_config_model_kwargs` (:255-325): GenerationConfig with
+        the tokenizer ids, max_length = L + max_new_tokens (4.51.3
+        `_prepare_generated_length`), a fresh DynamicCache, cache_position =
+        arange(L); the logits processors are the list returned to the loop,
+        which here holds one `forced` schedule processor (the loop appends its
+        own VibeVoiceTokenConstraintProcessor after it, :415-418);
+      * GenerationMixin 4.51.3 `prepare_inputs_for_generation` /
+        `_update_model_kwargs_for_generation` (position_ids =
+        cumsum(mask) - 1 with masked -> 1, mask gets a column of ones,
+        cache_position += 1);
+      * `DynamicCache.key_cache / value_cache` (:572-576, 624-631): lists of the
+        per-layer K/V tensors (5.15 keeps them in `layers[i].keys/values`);
+    `forced[b][step]` (eos after the list ends) wins the argmax: its logit is
+    raised to 1e30 before the reference's constraint processor runs.
+    """
+    from transformers import GenerationConfig, LogitsProcessor, LogitsProcessorList
+    from transformers.cache_utils import DynamicCache
+
+    DynamicCache.key_cache = property(lambda self: [layer.keys for layer in self.layers])
+    DynamicCache.value_cache = property(lambda self: [layer.values for layer in self.layers])
+
+    class Forced(LogitsProcessor):
+        def __init__(self, L0, eos):
+            self.L0, self.eos = L0, eos
+
+        def __call__(self, input_ids, scores):
+            step = input_ids.shape[1] - self.L0
+            scores = scores.clone()
+            for b in range(scores.shape[0]):
+                tok = forced[b][step] if step < len(forced[b]) else self.eos
+                scores[b, tok] = 1e30
+            return scores
+
+    def build(self, generation_config, inputs, tokenizer, return_processors=False, **kwargs):
+        gc = GenerationConfig(**(generation_config or {}), bos_token_id=tokenizer.bos_token_id,
+                              eos_token_id=tokenizer.eos_token_id, pad_token_id=tokenizer.pad_token_id)
+        gc.speech_start_id = tokenizer.speech_start_id
+        gc.speech_end_id = tokenizer.speech_end_id
+        gc.speech_diffusion_id = tokenizer.speech_diffusion_id
+        input_ids = kwargs["input_ids"]
+        L = input_ids.shape[-1]
+        gc.max_length = L + kwargs["max_new_tokens"]
+        gc.use_cache = True
+        model_kwargs = dict(attention_mask=kwargs["attention_mask"], use_cache=True,
+                            past_key_values=DynamicCache(), cache_position=torch.arange(L, dtype=torch.long))
+        if return_processors:
+            return gc, model_kwargs, input_ids, LogitsProcessorList([Forced(L, gc.eos_token_id)]), None
+        return gc, model_kwargs, input_ids
+
+    def prepare_inputs_for_generation(self, input_ids, past_key_values=None, attention_mask=None,
+                                      inputs_embeds=None, cache_position=None, use_cache=True, **kw):
+        if inputs_embeds is not None or cache_position[-1] >= input_ids.shape[1]:
+            input_ids = input_ids[:, -cache_position.shape[0]:]
+        elif input_ids.shape[1] != cache_position.shape[0]:
+            input_ids = input_ids[:, cache_position]
+        pos = attention_mask.long().cumsum(-1) - 1
+        pos.masked_fill_(attention_mask == 0, 1)
+        return dict(input_ids=input_ids.clone(), inputs_embeds=None, cache_position=cache_position,
+                    past_key_values=past_key_values, use_cache=use_cache, attention_mask=attention_mask,
+                    position_ids=pos[:, -input_ids.shape[1]:].clone())
+
+    def update_model_kwargs(self, outputs, model_kwargs, is_encoder_decoder=False, num_new_tokens=1):
+        model_kwargs["past_key_values"] = outputs.past_key_values
+        m = model_kwargs["attention_mask"]
+        model_kwargs["attention_mask"] = torch.cat([m, m.new_ones((m.shape[0], 1))], dim=-1)
+        model_kwargs["cache_position"] = model_kwargs["cache_position"][-1:] + num_new_tokens
+        return model_kwargs
+
+    cls = mvi.VibeVoiceForConditionalGenerationInference
+    cls._build_generate_config_model_kwargs = build
+    cls.prepare_inputs_for_generation = prepare_inputs_for_generation
+    cls._update_model_kwargs_for_generation = update_model_kwargs

@@ -174,3 +174,36 @@ def test_qwen2_compacted_kv(tag):
     for s in range(steps.shape[0]):
         h = lm.forward_rows(sd, LMCFG, steps[s], kvs)
         close(h[:, -1], ref[s + 1], *TOL[tag])
+
+
+@pytest.mark.parametrize("refresh", [True, False])
+def test_loop_trace_g8(refresh):
+    """oracle/loop.py (the literal restatement of generate(),
+    modeling_vibevoice_inference.py:327-710) vs the reference's own generate()
+    run end to end in fp32 (G8, tests/golden/make_golden.py:g8_loop): same
+    synthetic weights, B = 2 left-padded prompts, forced schedules through
+    diffusion / speech_end / speech_start / the skip correction (incl. the
+    KV-shift boundary case) / eos.  Token sequences and reach flags equal; audio
+    within fp32 op-order noise (rel L2 < 1e-4)."""
+    from oracle import loop
+    from tiny import tiny_config
+    from vibevoice_amd.weights import synthetic_state_dict
+    z = load("g8_loop.npz")
+    cfg = tiny_config(hidden=256, layers=2, heads=2, kv_heads=1, inter=512)
+    sd = synthetic_state_dict(cfg, seed=21, device="cpu", dtype=torch.float32, mode="test")
+    chk = torch.tensor([float(v.double().sum()) for v in sd.values()], dtype=torch.float64)
+    assert torch.allclose(chk, torch.from_numpy(z["sd_checksum"]), rtol=1e-12, atol=1e-9), "weights drifted"
+    scheds = [list(map(int, s[:n])) for s, n in zip(z["schedules"], z["schedule_lens"])]
+    ids = dict(eos=151643, start=151652, end=151653, diffusion=151654)
+    torch.manual_seed(1234)
+    seqs, audio, reach = loop.generate(sd, cfg, torch.from_numpy(z["input_ids"]), torch.from_numpy(z["attention_mask"]),
+                                       ids, ddpm_steps=5, cfg_scale=1.3, forced=scheds, refresh_negative=refresh,
+                                       dtype=torch.float32)
+    tag = "refresh" if refresh else "norefresh"
+    assert torch.equal(seqs, torch.from_numpy(z[f"{tag}/sequences"]))
+    assert torch.equal(reach, torch.from_numpy(z[f"{tag}/reach"]))
+    for b in range(2):
+        ref = torch.from_numpy(z[f"{tag}/audio{b}"])
+        assert audio[b].shape == ref.shape, (audio[b].shape, ref.shape)
+        err = ((audio[b].float() - ref).norm() / ref.norm()).item()
+        assert err < 1e-4, f"sample {b} audio rel L2 {err:.3e}"
