@@ -11,7 +11,7 @@ bookkeeping against the reference's literal semantics.
 Pinned by golden G8 (tests/golden/make_golden.py:g8_loop): the reference's
 own generate() run end to end in fp32; tests/test_oracle_golden.py.
 
-Supported: text prompts (no voice prompt), refresh_negative True/False,
+Supported: text prompts with or without voice prompts, refresh_negative True/False,
 greedy choice among the valid ids, or a forced token schedule.
 """
 import torch
@@ -31,6 +31,30 @@ def connector(sd, p, x):
     return F.linear(y, sd[p + "fc2.weight"], sd[p + "fc2.bias"])
 
 
+def voice_embeds(sd, cfg, speech_tensors, speech_masks, dtype, voice_noise=None):
+    """Voice-prompt prefill, `_process_speech_inputs(..., "audio")`
+    (modeling_vibevoice_inference.py:150-163): non-streaming acoustic encode,
+    sample(dist_type="gaussian") on the global RNG (modular_vibevoice_tokenizer.py:
+    979-987: one randn per clip scaled by fix_std / 0.8, then randn_like(mean)),
+    (z + bias) * scale, acoustic connector, rows of the valid frames.
+    voice_noise = (per-clip draw [Nv], randn_like(mean)) replays the two draws
+    of another generator (the GPU run draws them on the device, as the
+    reference does there)."""
+    asd = _sub(sd, "model.acoustic_tokenizer.")
+    ed = codec.codec_dims(cfg.acoustic_tokenizer_config, "encoder")
+    mean = codec.encode(asd, ed, speech_tensors.to(dtype).unsqueeze(1), None, None, streaming=False)
+    value = cfg.acoustic_tokenizer_config.fix_std / 0.8
+    if voice_noise is None:
+        std = torch.randn(mean.shape[0], dtype=mean.dtype) * value
+        eps = torch.randn_like(mean)
+    else:
+        std = voice_noise[0].to(mean.dtype) * value
+        eps = voice_noise[1].to(mean.dtype).reshape(mean.shape)
+    z = mean + std[:, None, None] * eps
+    feats = (z + sd["model.speech_bias_factor"]) * sd["model.speech_scaling_factor"]
+    return connector(sd, "model.acoustic_connector.", feats)[speech_masks]
+
+
 class _NegRow:
     """Cache + mask of one sample's negative stream (reference representation)."""
 
@@ -41,7 +65,7 @@ class _NegRow:
 
 def generate(sd, cfg, input_ids, attention_mask, tokenizer_ids, ddpm_steps=10, cfg_scale=1.3,
              forced=None, refresh_negative=True, max_length_times=2, max_new_tokens=None, dtype=torch.bfloat16,
-             record=None):
+             record=None, speech_tensors=None, speech_masks=None, speech_input_mask=None, voice_noise=None):
     """Returns (sequences [B, L+steps], audio list per sample, reach_max [B]).
 
     sd: full state dict (reference names) in `dtype`.  cfg: VibeVoiceConfig.
@@ -90,10 +114,16 @@ def generate(sd, cfg, input_ids, attention_mask, tokenizer_ids, ddpm_steps=10, c
             break
         # ---- positive pass (:467-486)
         if step == 0:
+            emb0 = emb_w[input_ids]
+            if speech_tensors is not None and speech_masks is not None:       # forward :221-225
+                emb0 = emb0.clone()
+                v = voice_embeds(sd, cfg, speech_tensors, speech_masks, dtype, voice_noise)
+                if speech_input_mask is not None:
+                    emb0[speech_input_mask] = v.to(emb0.dtype)
             hs = []
             for b in range(B):
                 keep = attention_mask[b].bool()
-                x = emb_w[input_ids[b][keep]][None]
+                x = emb0[b][keep][None]
                 hs.append(lm.forward_rows(lsd, lmc, x, pos_kv[b:b + 1])[0, -1])
             hpos = torch.stack(hs)
         else:

@@ -310,7 +310,9 @@ def g8_loop():
     has no voice: the prefill's voice-encoder call (which generate() always
     makes, :470-476) gets a dummy one-frame clip (hop 4) masked out of every position, and
     the global RNG is restored around it so the diffusion noise stream is the
-    one a voice-free prompt would draw."""
+    one a voice-free prompt would draw.  A third run (refresh_negative) adds
+    voice prompts: two clips scattered at speech_input_mask, encoder + gaussian
+    sample on the global RNG + connector, all the reference's code."""
     import types
     sys.path.insert(0, os.path.dirname(HERE))
     sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
@@ -369,6 +371,28 @@ def g8_loop():
         for b, a in enumerate(o.speech_outputs):
             out[f"{tag}/audio{b}"] = f32(a)
     cls._process_speech_inputs = orig
+    # voice-prompt prefill (_process_speech_inputs, :150-163, gaussian sample on the
+    # global RNG): clip 0 (5 frames) in sample 0, clip 1 (13 samples -> 4 frames,
+    # zero-padded to 20) in sample 1 after its 3 pad positions
+    vt = torch.zeros(2, 20)
+    vt[0] = 0.3 * torch.randn(20, generator=g)
+    vt[1, :13] = 0.3 * torch.randn(13, generator=g)
+    vm = torch.zeros(2, 5, dtype=torch.bool)
+    vm[0, :5] = True
+    vm[1, :4] = True
+    sim = torch.zeros(2, P, dtype=torch.bool)
+    sim[0, 1:6] = True
+    sim[1, 4:8] = True
+    out.update({"voice/speech_tensors": f32(vt), "voice/speech_masks": vm.numpy(),
+                "voice/speech_input_mask": sim.numpy()})
+    torch.manual_seed(1234)
+    with torch.no_grad():
+        o = model.generate(input_ids=ids, attention_mask=mask, tokenizer=tok, cfg_scale=1.3, speech_tensors=vt,
+                           speech_masks=vm, speech_input_mask=sim, refresh_negative=True, show_progress_bar=False)
+    out["voice/sequences"] = o.sequences.numpy()
+    out["voice/reach"] = o.reach_max_step_sample.numpy()
+    for b, a in enumerate(o.speech_outputs):
+        out[f"voice/audio{b}"] = f32(a)
     save("g8_loop.npz", **out)
 
 

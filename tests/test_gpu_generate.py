@@ -76,6 +76,47 @@ def test_generate_matches_reference_loop(refresh_negative, prompt):
         assert e < max(5e-2, 2 * noise) and c > 0.995
 
 
+def test_generate_voice_prompt_matches_reference_loop():
+    """Voice-prompt prefill inside generate() (_process_speech_inputs,
+    modeling_vibevoice_inference.py:150-163, spliced at speech_input_mask,
+    :221-225): the golden G8 inputs (two ragged clips, one per sample) through
+    the HIP encoder / gaussian sample / connector / scatter vs oracle/loop.py,
+    which G8 pins to the reference's own generate() with voices.  The two
+    gaussian-sample draws are made on the device (as the reference does on a
+    GPU) and replayed into the oracle; tolerance as above."""
+    from golden_io import load
+    z = load("g8_loop.npz")
+    cfg = tiny_config(hidden=256, layers=2, heads=2, kv_heads=1, inter=512)
+    sd = synthetic_state_dict(cfg, seed=21, device="cpu", mode="test", with_acoustic_encoder=True)
+    model = VibeVoiceForConditionalGenerationInference(cfg, sd, dev, max_batch=2, max_ctx=128)
+    model.set_ddpm_inference_steps(5)
+    ids, mask = torch.from_numpy(z["input_ids"]), torch.from_numpy(z["attention_mask"])
+    voice = {k: torch.from_numpy(z[f"voice/{k}"]) for k in ("speech_tensors", "speech_masks", "speech_input_mask")}
+    torch.manual_seed(1234)                       # seeds the CPU and the device generators
+    out = model.generate(input_ids=ids, attention_mask=mask, tokenizer=TOK, cfg_scale=1.3, forced_tokens=SCHEDULES,
+                         show_progress_bar=False, **voice)
+    torch.cuda.synchronize()
+    nv, frames = voice["speech_masks"].shape
+    torch.cuda.manual_seed(1234)                  # replay the prefill's two device draws
+    draw = torch.randn(nv, device=dev, dtype=torch.bfloat16).cpu()
+    eps = torch.randn(nv, frames, cfg.acoustic_vae_dim, device=dev, dtype=torch.bfloat16).cpu()
+    res = []
+    for s32 in (False, True):
+        torch.manual_seed(1234)
+        sdx = {k: v.float() for k, v in sd.items()} if s32 else sd
+        res.append(oloop.generate(sdx, cfg, ids, mask, IDS, ddpm_steps=5, cfg_scale=1.3, forced=SCHEDULES,
+                                  dtype=torch.float32 if s32 else torch.bfloat16, voice_noise=(draw, eps), **voice))
+    (seqs, audio, reach), (_, audio32, _) = res
+    assert torch.equal(out.sequences, seqs)
+    assert torch.equal(out.reach_max_step_sample.cpu(), reach)
+    for b in range(2):
+        got, ref = out.speech_outputs[b], audio[b]
+        assert got.shape == ref.shape, (got.shape, ref.shape)
+        e, c, noise = rel_err(got, ref), cos(got, ref), rel_err(ref, audio32[b])
+        print(f"voice sample {b} audio rel_err {e:.3e} cos {c:.6f} (bf16 reference vs fp32: {noise:.3e})")
+        assert e < max(5e-2, 2 * noise) and c > 0.995
+
+
 def test_graph_replay_matches_eager():
     """The hipGraph-captured loop body replays exactly the eager kernel sequence."""
     cfg = tiny_config(hidden=256, layers=2, heads=2, kv_heads=1, inter=512)

@@ -176,14 +176,14 @@ def test_qwen2_compacted_kv(tag):
         close(h[:, -1], ref[s + 1], *TOL[tag])
 
 
-@pytest.mark.parametrize("refresh", [True, False])
-def test_loop_trace_g8(refresh):
+@pytest.mark.parametrize("refresh,voice", [(True, False), (False, False), (True, True)])
+def test_loop_trace_g8(refresh, voice):
     """oracle/loop.py (the literal restatement of generate(),
     modeling_vibevoice_inference.py:327-710) vs the reference's own generate()
     run end to end in fp32 (G8, tests/golden/make_golden.py:g8_loop): same
     synthetic weights, B = 2 left-padded prompts, forced schedules through
     diffusion / speech_end / speech_start / the skip correction (incl. the
-    KV-shift boundary case) / eos.  Token sequences and reach flags equal; audio
+    KV-shift boundary case) / eos, with and without voice prompts.  Token sequences and reach flags equal; audio
     within fp32 op-order noise (rel L2 < 1e-4)."""
     from oracle import loop
     from tiny import tiny_config
@@ -195,11 +195,14 @@ def test_loop_trace_g8(refresh):
     assert torch.allclose(chk, torch.from_numpy(z["sd_checksum"]), rtol=1e-12, atol=1e-9), "weights drifted"
     scheds = [list(map(int, s[:n])) for s, n in zip(z["schedules"], z["schedule_lens"])]
     ids = dict(eos=151643, start=151652, end=151653, diffusion=151654)
+    kw = {}
+    if voice:      # voice-prompt prefill (modeling_vibevoice_inference.py:150-163, 221-225)
+        kw = {k: torch.from_numpy(z[f"voice/{k}"]) for k in ("speech_tensors", "speech_masks", "speech_input_mask")}
     torch.manual_seed(1234)
     seqs, audio, reach = loop.generate(sd, cfg, torch.from_numpy(z["input_ids"]), torch.from_numpy(z["attention_mask"]),
                                        ids, ddpm_steps=5, cfg_scale=1.3, forced=scheds, refresh_negative=refresh,
-                                       dtype=torch.float32)
-    tag = "refresh" if refresh else "norefresh"
+                                       dtype=torch.float32, **kw)
+    tag = "voice" if voice else "refresh" if refresh else "norefresh"
     assert torch.equal(seqs, torch.from_numpy(z[f"{tag}/sequences"]))
     assert torch.equal(reach, torch.from_numpy(z[f"{tag}/reach"]))
     for b in range(2):
