@@ -145,7 +145,37 @@ __global__ void __launch_bounds__(256) k_roll(const RollDesc* d, const int* slot
     }
     if (r.T >= r.ctx || mode == 1) return;
   }
-  // narrow or overlapping buffers: one thread per channel, rows in order
+  // narrow or overlapping buffers (T < ctx: the source rows overlap the
+  // destination rows).  Up to ROLL_REGS rows: each thread loads all its rows
+  // into registers first, then stores them, so the ctx loads are in flight
+  // together (one memory round trip instead of ctx dependent ones).
+  constexpr int ROLL_REGS = 16;
+  if (r.ctx <= ROLL_REGS) {
+    if ((r.C & 7) == 0) {
+      const int n8 = r.C >> 3;
+      for (int c = threadIdx.x; c < n8; c += blockDim.x) {
+        bf16x8 v[ROLL_REGS];
+#pragma unroll
+        for (int i = 0; i < ROLL_REGS; ++i)
+          if (i < r.ctx) v[i] = *(const bf16x8*)(base + (long long)(r.T + i) * r.C + c * 8);
+#pragma unroll
+        for (int i = 0; i < ROLL_REGS; ++i)
+          if (i < r.ctx) *(bf16x8*)(base + (long long)i * r.C + c * 8) = v[i];
+      }
+    } else {
+      for (int c = threadIdx.x; c < r.C; c += blockDim.x) {
+        bf16 v[ROLL_REGS];
+#pragma unroll
+        for (int i = 0; i < ROLL_REGS; ++i)
+          if (i < r.ctx) v[i] = mode == 0 ? base[(long long)(r.T + i) * r.C + c] : tobf(0.f);
+#pragma unroll
+        for (int i = 0; i < ROLL_REGS; ++i)
+          if (i < r.ctx) base[(long long)i * r.C + c] = v[i];
+      }
+    }
+    return;
+  }
+  // longer contexts: one thread per channel, rows in order
   for (int c = threadIdx.x; c < r.C; c += blockDim.x)
     for (int i = 0; i < r.ctx; ++i)
       base[(long long)i * r.C + c] = mode == 0 ? base[(long long)(r.T + i) * r.C + c] : tobf(0.f);

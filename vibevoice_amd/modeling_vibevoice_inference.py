@@ -123,20 +123,27 @@ class VibeVoiceForConditionalGenerationInference:
             dev, eng, dt = self.device, self.engine, self.dtype
             H, D = eng.hidden, self.config.acoustic_vae_dim
             i32 = dict(device=dev, dtype=torch.int32)
+            # host -> device control data travels in two copies per step:
+            # [positions(2B) | next ids(B)] (int32) and [noise(B, D) bf16 | diffusion rows(B) int32]
+            # (noise first: its rows stay 128-byte aligned)
+            ctl_dev, ctl_pin = torch.zeros(3 * B, **i32), torch.zeros(3 * B, dtype=torch.int32, pin_memory=True)
+            nb = B * D * torch.finfo(dt).bits // 8
+            dn_dev = torch.zeros(nb + 4 * B, device=dev, dtype=torch.uint8)
+            # two sets: the speculative diffusion of step k writes one while
+            # step k-1's copy from the other may still be queued
+            dn_pins = [torch.zeros(nb + 4 * B, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
             self._bufs[B] = dict(
                 rows2=torch.arange(2 * B, **i32),
                 x_in2=torch.zeros(2 * B, H, device=dev, dtype=dt),
                 hid=torch.zeros(2 * B, H, device=dev, dtype=dt),
                 logits=torch.zeros(2 * B, 4, device=dev, dtype=torch.float32),
-                pos_dev=torch.zeros(2 * B, **i32), ids_dev=torch.zeros(B, **i32), didx_dev=torch.zeros(B, **i32),
-                noise_dev=torch.zeros(B, D, device=dev, dtype=dt),
+                ctl_dev=ctl_dev, ctl_pin=ctl_pin,
+                pos_dev=ctl_dev[:2 * B], ids_dev=ctl_dev[2 * B:], pos_pin=ctl_pin[:2 * B], ids_pin=ctl_pin[2 * B:],
+                dn_dev=dn_dev, dn_pins=dn_pins,
+                noise_dev=dn_dev[:nb].view(dt).view(B, D), didx_dev=dn_dev[nb:].view(torch.int32),
+                noise_pins=[p[:nb].view(dt).view(B, D) for p in dn_pins],
+                didx_pins=[p[nb:].view(torch.int32) for p in dn_pins],
                 audio_dev=torch.zeros(B, eng.hop, device=dev, dtype=dt),
-                pos_pin=torch.zeros(2 * B, dtype=torch.int32, pin_memory=True),
-                ids_pin=torch.zeros(B, dtype=torch.int32, pin_memory=True),
-                # two sets: the speculative diffusion of step k writes one while
-                # step k-1's copy from the other may still be queued
-                didx_pins=[torch.zeros(B, dtype=torch.int32, pin_memory=True) for _ in range(2)],
-                noise_pins=[torch.zeros(B, D, dtype=dt, pin_memory=True) for _ in range(2)],
                 logits_pin=torch.zeros(B, 4, dtype=torch.float32, pin_memory=True))
         return self._bufs[B]
 
@@ -333,6 +340,7 @@ class GenerateSession:
             self.sde_buf = torch.empty(eng.steps * 2 * B * model.config.acoustic_vae_dim, device=dev,
                                        dtype=torch.float32)
         self.spec_miss = 0
+        self.pos_pushed = False
         self.logits_ready = torch.cuda.Event()
         self.graphs = model._graph_cache
         self.seen = model._graph_seen
@@ -367,6 +375,7 @@ class GenerateSession:
                 raise RuntimeError(f"extend_context({n_pos}) needs max_ctx >= {n_pos + self.max_steps + 2}")
             self.eng.kv_synthetic(torch.tensor([b], **i32), p0, n_pos, seed=seed + b)
             self.pos_len[b] = n_pos
+        self.pos_pushed = False
 
     # ---------------------------------------------------------------- device phases
     def _replay(self, key, fn):
@@ -436,6 +445,18 @@ class GenerateSession:
                 eng.codec_step(d, self.noise_dev[:n], self.audio_dev[:n], embeds_out=self.x_in2, embed_rows=d)
         self._replay(("post", n), body)
 
+    def _push_controls(self, nxt):
+        """One H2D copy: this step's token ids (read by the post phase) and the
+        next step's positive / negative positions (its LM phase), which are final
+        once the bookkeeping of this step is done.  The previous copy from the
+        same pinned buffer finished before this step's logits were read back."""
+        B = self.B
+        self.ids_pin.copy_(nxt)
+        self.pos_pin[:B].copy_(self.pos_len)
+        self.pos_pin[B:].copy_(self.neg_len)
+        self.ctl_dev.copy_(self.ctl_pin, non_blocking=True)
+        self.pos_pushed = True
+
     def _stage_diffusion(self, didx, buf):
         """Draw the diffusion noise from the CPU generator (:716) and queue the
         H2D copies of the row list and the noise (pinned set `buf`)."""
@@ -444,8 +465,7 @@ class GenerateSession:
         dp[:n].copy_(didx)
         noise = torch.randn(2 * n, self.m.config.acoustic_vae_dim)
         npin[:n].copy_(noise[:n])
-        self.didx_dev[:n].copy_(dp[:n], non_blocking=True)
-        self.noise_dev[:n].copy_(npin[:n], non_blocking=True)
+        self.dn_dev.copy_(self.dn_pins[buf], non_blocking=True)      # rows + noise in one copy
 
     def _speculate(self):
         """Queue the diffusion for the rows whose last token was speech_start or
@@ -491,9 +511,11 @@ class GenerateSession:
             self.done = True
             return False
         if step > 0:
-            self.pos_pin[:B].copy_(self.pos_len)
-            self.pos_pin[B:].copy_(self.neg_len)
-            self.pos_dev.copy_(self.pos_pin, non_blocking=True)
+            if not self.pos_pushed:   # normally sent with the previous step's ids (_push_controls)
+                self.pos_pin[:B].copy_(self.pos_len)
+                self.pos_pin[B:].copy_(self.neg_len)
+                self.pos_dev.copy_(self.pos_pin, non_blocking=True)
+            self.pos_pushed = False
             self._lm_phase()
             self.pos_len += 1
         # ---- token choice (:494-509); the argmax is always read back, as in the reference
@@ -534,8 +556,6 @@ class GenerateSession:
         starts = ~finished & (nxt == self.start_id)                         # :563-580
         if self.refresh_negative:
             self.neg_len[starts] = 0     # mask reset: empty context, next position 0
-        self.ids_pin.copy_(nxt)
-        self.ids_dev.copy_(self.ids_pin, non_blocking=True)
         diff = ~finished & (nxt == self.diff_id)                            # :588
         if diff.any():
             didx = torch.nonzero(diff).reshape(-1)
@@ -555,6 +575,7 @@ class GenerateSession:
                 q = torch.tensor(quirk)
                 eng.kv_copy(self.ints.put(q + B), self.ints.put(torch.ones_like(q)),
                             self.ints.put(torch.zeros_like(q)))
+            self._push_controls(nxt)
             if spec is None or not torch.equal(spec[0], didx):
                 if spec is not None:   # mispredicted: the speculative copies may still be queued
                     torch.cuda.current_stream().synchronize()
@@ -572,6 +593,7 @@ class GenerateSession:
             if spec is not None:
                 torch.set_rng_state(spec[1])
                 self.spec_miss += 1
+            self._push_controls(nxt)
             self._post_phase(0)
         self.step_idx += 1
         return True
