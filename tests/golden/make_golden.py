@@ -370,6 +370,21 @@ def g8_loop():
         out[f"{tag}/reach"] = o.reach_max_step_sample.numpy()
         for b, a in enumerate(o.speech_outputs):
             out[f"{tag}/audio{b}"] = f32(a)
+    # per-sample length cap (:421-422, 543-553): max_length_times = 0.5 gives
+    # max_steps 5 and caps of 5 / 3 steps (the left-padded sample has 7 tokens),
+    # so sample 1 finishes with reach_max_step_sample while sample 0 diffuses on
+    forced[:] = [[G8_IDS["diffusion"]] * 9, [G8_IDS["diffusion"]] * 9]
+    torch.manual_seed(1234)
+    with torch.no_grad():
+        o = model.generate(input_ids=ids, attention_mask=mask, tokenizer=tok, cfg_scale=1.3,
+                           speech_tensors=torch.zeros(1, 4), speech_masks=torch.zeros(1, 1, dtype=torch.bool),
+                           speech_input_mask=torch.zeros(2, P, dtype=torch.bool), max_length_times=0.5,
+                           show_progress_bar=False)
+    out["cap/sequences"] = o.sequences.numpy()
+    out["cap/reach"] = o.reach_max_step_sample.numpy()
+    for b, a in enumerate(o.speech_outputs):
+        out[f"cap/audio{b}"] = f32(a)
+    forced[:] = G8_SCHEDULES
     cls._process_speech_inputs = orig
     # voice-prompt prefill (_process_speech_inputs, :150-163, gaussian sample on the
     # global RNG): clip 0 (5 frames) in sample 0, clip 1 (13 samples -> 4 frames,

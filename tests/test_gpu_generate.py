@@ -117,6 +117,42 @@ def test_generate_voice_prompt_matches_reference_loop():
         assert e < max(5e-2, 2 * noise) and c > 0.995
 
 
+def test_generate_length_cap_matches_reference_loop():
+    """Per-sample length caps (modeling_vibevoice_inference.py:421-422, 543-553):
+    max_length_times = 0.5 on G8's ragged prompts (10 / 7 tokens) caps the
+    loop at 5 steps and the left-padded sample at 3, which then finishes with
+    reach_max_step_sample while the other diffuses on.  Sequences and reach
+    flags equal the reference's own generate() (golden G8 "cap"); audio vs the
+    oracle as above."""
+    from golden_io import load
+    z = load("g8_loop.npz")
+    cfg = tiny_config(hidden=256, layers=2, heads=2, kv_heads=1, inter=512)
+    sd = synthetic_state_dict(cfg, seed=21, device="cpu", mode="test", with_acoustic_encoder=False)
+    model = VibeVoiceForConditionalGenerationInference(cfg, sd, dev, max_batch=2, max_ctx=128)
+    model.set_ddpm_inference_steps(5)
+    ids, mask = torch.from_numpy(z["input_ids"]), torch.from_numpy(z["attention_mask"])
+    sched = [[D] * 9, [D] * 9]
+    torch.manual_seed(1234)
+    out = model.generate(input_ids=ids, attention_mask=mask, tokenizer=TOK, cfg_scale=1.3, forced_tokens=sched,
+                         max_length_times=0.5, show_progress_bar=False)
+    torch.cuda.synchronize()
+    assert torch.equal(out.sequences, torch.from_numpy(z["cap/sequences"]))
+    assert torch.equal(out.reach_max_step_sample.cpu(), torch.from_numpy(z["cap/reach"]))
+    res = []
+    for s32 in (False, True):
+        torch.manual_seed(1234)
+        sdx = {k: v.float() for k, v in sd.items()} if s32 else sd
+        res.append(oloop.generate(sdx, cfg, ids, mask, IDS, ddpm_steps=5, cfg_scale=1.3, forced=sched,
+                                  max_length_times=0.5, dtype=torch.float32 if s32 else torch.bfloat16))
+    (_, audio, _), (_, audio32, _) = res
+    for b in range(2):
+        got, ref = out.speech_outputs[b], audio[b]
+        assert got.shape == ref.shape == z[f"cap/audio{b}"].shape, (got.shape, ref.shape)
+        e, c, noise = rel_err(got, ref), cos(got, ref), rel_err(ref, audio32[b])
+        print(f"cap sample {b} audio rel_err {e:.3e} cos {c:.6f} (bf16 reference vs fp32: {noise:.3e})")
+        assert e < max(5e-2, 2 * noise) and c > 0.995
+
+
 def test_graph_replay_matches_eager():
     """The hipGraph-captured loop body replays exactly the eager kernel sequence."""
     cfg = tiny_config(hidden=256, layers=2, heads=2, kv_heads=1, inter=512)

@@ -176,8 +176,9 @@ def test_qwen2_compacted_kv(tag):
         close(h[:, -1], ref[s + 1], *TOL[tag])
 
 
-@pytest.mark.parametrize("refresh,voice", [(True, False), (False, False), (True, True)])
-def test_loop_trace_g8(refresh, voice):
+@pytest.mark.parametrize("refresh,voice,cap", [(True, False, False), (False, False, False), (True, True, False),
+                                               (True, False, True)])
+def test_loop_trace_g8(refresh, voice, cap):
     """oracle/loop.py (the literal restatement of generate(),
     modeling_vibevoice_inference.py:327-710) vs the reference's own generate()
     run end to end in fp32 (G8, tests/golden/make_golden.py:g8_loop): same
@@ -198,11 +199,13 @@ def test_loop_trace_g8(refresh, voice):
     kw = {}
     if voice:      # voice-prompt prefill (modeling_vibevoice_inference.py:150-163, 221-225)
         kw = {k: torch.from_numpy(z[f"voice/{k}"]) for k in ("speech_tensors", "speech_masks", "speech_input_mask")}
+    if cap:        # per-sample length cap (:421-422, 543-553): all-diffusion, max_length_times 0.5
+        scheds, kw = [[ids["diffusion"]] * 9] * 2, dict(max_length_times=0.5)
     torch.manual_seed(1234)
     seqs, audio, reach = loop.generate(sd, cfg, torch.from_numpy(z["input_ids"]), torch.from_numpy(z["attention_mask"]),
                                        ids, ddpm_steps=5, cfg_scale=1.3, forced=scheds, refresh_negative=refresh,
                                        dtype=torch.float32, **kw)
-    tag = "voice" if voice else "refresh" if refresh else "norefresh"
+    tag = "cap" if cap else "voice" if voice else "refresh" if refresh else "norefresh"
     assert torch.equal(seqs, torch.from_numpy(z[f"{tag}/sequences"]))
     assert torch.equal(reach, torch.from_numpy(z[f"{tag}/reach"]))
     for b in range(2):
