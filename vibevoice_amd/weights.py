@@ -359,3 +359,41 @@ def pack(sd, cfg: VibeVoiceConfig, device, with_acoustic_encoder=True, tp_rank=0
         if is_gemm_weight(k):
             out[k] = mfma_pack(out[k])
     return out
+
+
+def write_synthetic_checkpoint(path, cfg: VibeVoiceConfig, seed=0, mode="bench", shard_bytes=2 << 30):
+    """An offline stand-in for a HF checkpoint directory:
+    config.json + `model-0000i-of-0000n.safetensors` shards with the reference's
+    state-dict names, the tied lm_head left out as the reference's checkpoints
+    do (modeling_vibevoice_inference.py:120-129), so
+    `from_pretrained(path)` and the demos' `--model_path` run without network.
+    Returns the shard file names."""
+    import json
+    import os
+    from safetensors.torch import save_file
+    os.makedirs(path, exist_ok=True)
+    sd = synthetic_state_dict(cfg, seed=seed, device="cpu", mode=mode)
+    tied = cfg.decoder_config.get("tie_word_embeddings", True)
+    names = sorted(k for k in sd if not (tied and k == "lm_head.weight"))
+    shards, cur, size = [], [], 0
+    for k in names:
+        nb = sd[k].numel() * sd[k].element_size()
+        if cur and size + nb > shard_bytes:
+            shards.append(cur)
+            cur, size = [], 0
+        cur.append(k)
+        size += nb
+    shards.append(cur)
+    files = [f"model-{i + 1:05d}-of-{len(shards):05d}.safetensors" for i in range(len(shards))]
+    for f, part in zip(files, shards):
+        save_file({k: sd[k].contiguous() for k in part}, os.path.join(path, f), metadata={"format": "pt"})
+    with open(os.path.join(path, "config.json"), "w") as fh:
+        json.dump(cfg.to_dict(), fh, indent=2)
+    return files
+
+
+if __name__ == "__main__":      # python -m vibevoice_amd.weights <dir> [1.5B|Large] [seed]
+    import sys
+    _dir, _name = sys.argv[1], (sys.argv[2] if len(sys.argv) > 2 else "1.5B")
+    _seed = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+    print("\n".join(write_synthetic_checkpoint(_dir, VibeVoiceConfig.builtin(_name), seed=_seed)))
