@@ -1109,9 +1109,12 @@ struct GemmPlan { int nw, ksplit, u, tpw; };
 //   * >= 1024 tiles (LM gate|up, head adaLN): 2 waves — every workgroup resident
 //     in the first round (4-wave groups left a second-round tail: 16.7 -> 14.0 us)
 //   * few tiles, long rows (LM / head down): 8 waves x 4; 128 tiles x K >= 8192
-//     (codec fc2): 4 x 8; at M >= 8 two workgroups split K (the only shapes
+//     (codec fc2): 4 x 8; at M >= 8 two workgroups split K (the shapes
 //     where the hand-off pays, profiles/r01_gemv_sweep_ks.txt: B = 8 LM down
-//     18.7 -> 15.5 us, head down 13.0 -> 12.3, B = 8 codec fc2 13.1 -> 12.0)
+//     18.7 -> 15.5 us, head down 13.0 -> 12.3, B = 8 codec fc2 13.1 -> 12.0),
+//     and at M < 8 for < 128 tiles x K >= 8192 (LM down: 96 tiles reach only 96
+//     CUs; same-box interleaved A/B, 5 pairs: B = 1 step 3.749 -> 3.725 ms,
+//     B = 2 4.41 -> 4.30 ms)
 //   * 16 < M <= 64 (k_gemv): 4 waves, 1 for >= 1024 tiles (the batched head
 //     adaLN, M = 2 x 10 steps: 35 -> 20.5 us)
 //   * few tiles, short rows (qkv, o_proj): 4 x 8, all chunks in flight at once
@@ -1127,6 +1130,9 @@ static GemmPlan gemv_plan(int N, int K, int M) {
       ks = 2;
       if (chunks >= 256) u = 8;
       else nw = 8;
+    } else if (tiles < 128 && chunks >= 256) {   // M < 8 LM down: 2-way split-K, 8 waves x 4
+      ks = 2;
+      nw = 8;
     } else if (tiles == 128 && chunks >= 256) {
       u = 8;
     } else {
