@@ -11,9 +11,13 @@ tokens), so every step emits one 3200-sample audio frame per sample.
 
 Default workload = BASELINE.json configs[1]: VibeVoice-1.5B bf16, 1 speaker
 (3 s voice prompt + 1-sentence script), 10 diffusion steps, TP=1, one MI355X.
-`--batch 8 --speakers 2` is configs[2].  With `--gpus N` (torchrun, one rank
-per GPU) every rank runs its own independent dialogues: DP replicas, no
-collective on the data path (DESIGN.md "Multi-GPU").
+`--batch 8 --speakers 2` is configs[2].  With `--gpus N` every rank (one
+process per GPU) runs its own independent dialogues: DP replicas, no
+collective on the data path (DESIGN.md "Multi-GPU").  `--tp T` groups T
+consecutive ranks into one tensor-parallel replica (RCCL all-reduce).
+`--gpus N` outside a torchrun environment starts the N ranks itself (a child
+`torch.distributed.run` on 127.0.0.1, before this process touches a GPU) and
+exits with its status; inside one, WORLD_SIZE must equal N.
 
 Prints ONE JSON line on rank 0 (metric contract: BASELINE.json / SURVEY.md §8d).
 """
@@ -49,7 +53,48 @@ def parse():
                          "(SURVEY.md §8d config 5: 64K-position decode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-tokens", type=int, default=8, help="timed tokens of the CPU oracle sample")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="tests only: run the launch / barrier / max-over-ranks / JSON path with an empty step "
+                         "(no engine; works on a CPU host over gloo)")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def maybe_launch(args, argv=None):
+    """`--gpus N` (N > 1) without a torchrun environment: run this script under
+    `torch.distributed.run` with N ranks on 127.0.0.1 as a CHILD process and
+    return its exit status (None: nothing launched, run in-process).  Called
+    before any GPU call, so this process never initialises the GPU."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import subprocess
+    argv = sys.argv[1:] if argv is None else argv
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def tp_groups(world, rank, T):
+    """Consecutive ranks form one TP group of T; the groups are DP replicas.
+    Every rank creates every group (torch.distributed.new_group is collective).
+    Returns (this rank's group or None for T == 1, replica index, replicas)."""
+    if world % T:
+        raise SystemExit(f"--tp {T} must divide the {world} ranks")
+    group = None
+    if T > 1:
+        groups = [torch.distributed.new_group(list(range(g * T, (g + 1) * T))) for g in range(world // T)]
+        group = groups[rank // T]
+    return group, rank // T, world // T
 
 
 # ------------------------------------------------------------------ algorithmic bytes
@@ -84,7 +129,9 @@ PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
 def measure_gemv(model, B, iters=6):
     """The LM MLP gate|up weight-streaming GEMV (k_gemv1, XF_NORM prologue,
     EPI_SILU_MUL): the largest single launch of the loop (2I x H bf16 = 55 MB at
-    1.5B, 28 per LM pass).  The 28 layers' launches are captured into a hipGraph
+    1.5B, 28 per LM pass).  vv_gemm_bf16_norm with the engine handle goes
+    through the engine's own GEMM dispatch, so at M = 2B > 16 this times what
+    the loop launches there (k_rmsnorm once + the GEMV on normalised rows).  The 28 layers' launches are captured into a hipGraph
     (as the loop runs them) and replayed; HIP events on the replay stream time
     `iters` replays.  Rotating over the 28 layers' weights (1.5 GB) keeps the
     Infinity Cache from serving them.  `traffic`: HBM bytes per launch from the
@@ -130,7 +177,10 @@ def measure_gemv(model, B, iters=6):
             pmc = json.load(f)
         if pmc.get("kernel") == ROOF_KERNEL and pmc.get("shape") == shape:
             traffic = pmc["hbm_bytes_per_launch"]
-    return dict(kernel=f"{ROOF_KERNEL} (LM post-norm + gate|up + SiLU*up, graph-replayed)", shape=shape,
+    kernel = (f"{ROOF_KERNEL} (LM post-norm + gate|up + SiLU*up, graph-replayed)" if M <= 16 else
+              "k_rmsnorm + k_gemv/k_gemvw (the engine's M > 16 dispatch: post-norm once, then gate|up + SiLU*up; "
+              "graph-replayed, both launches timed)")
+    return dict(kernel=kernel, shape=shape,
                 bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
                 traffic=traffic, traffic_unit="bytes per launch" if traffic else None,
                 avg_us=round(avg_s * 1e6, 2), alg_bytes_per_launch=alg)
@@ -219,21 +269,22 @@ def throughput(dt, batch, steps, world):
 # ------------------------------------------------------------------ main
 def main():
     args = parse()
+    rc = maybe_launch(args)
+    if rc is not None:
+        sys.exit(rc)
     world, rank, local, dev = dist_setup()
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch with --nproc-per-node {args.gpus}")
+    if args.plumbing:
+        return plumbing(args, world, rank, dev)
 
     from vibevoice_amd.modeling_vibevoice_inference import VibeVoiceForConditionalGenerationInference
     from vibevoice_amd.synthetic import synthetic_inputs, tokenizer_ids
 
     B, S, K, W = args.batch, args.ddpm_steps, args.steps, args.warmup
     T = args.tp
-    if world % T:
-        raise SystemExit(f"--tp {T} must divide the {world} ranks")
-    tp_group = None
-    if T > 1:   # consecutive ranks form one TP group; groups are DP replicas
-        groups = [torch.distributed.new_group(list(range(g * T, (g + 1) * T))) for g in range(world // T)]
-        tp_group = groups[rank // T]
-    replicas = world // T
-    inp = synthetic_inputs(batch=B, speakers=args.speakers, voice_seconds=3.0, text_tokens=64, seed=100 + rank // T)
+    tp_group, replica, replicas = tp_groups(world, rank, T)
+    inp = synthetic_inputs(batch=B, speakers=args.speakers, voice_seconds=3.0, text_tokens=64, seed=100 + replica)
     L = inp["input_ids"].shape[1]
     total = W + K + 4
     if args.context:   # the timed steps end at most at max_position_embeddings (65,536 for the 1.5B LM)
@@ -305,6 +356,28 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def plumbing(args, world, rank, dev):
+    """--plumbing: the multi-rank harness of main() (groups, barrier + sync on
+    both sides, max over ranks, whole-job value, one JSON line on rank 0)
+    around an empty step of known length (rank r sleeps 1 ms x (r + 1))."""
+    _, _, replicas = tp_groups(world, rank, args.tp)
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(1e-3 * (rank + 1))
+    barrier(world)
+    dt = max_over_ranks(time.perf_counter() - t0, world, dev)
+    tps, audio_per_s = throughput(dt, args.batch, args.steps, replicas)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(audio_per_s, 3), "unit": "audio-sec/wall-sec",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(dt / args.steps * 1e3, 4), "scaling": "weak",
+                          "data": "plumbing (empty step)", "config": {"parallelism": f"dp{replicas}, tp{args.tp}"},
+                          "backend": torch.distributed.get_backend() if world > 1 else None}), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 

@@ -65,11 +65,26 @@ class _NegRow:
 
 def generate(sd, cfg, input_ids, attention_mask, tokenizer_ids, ddpm_steps=10, cfg_scale=1.3,
              forced=None, refresh_negative=True, max_length_times=2, max_new_tokens=None, dtype=torch.bfloat16,
-             record=None, speech_tensors=None, speech_masks=None, speech_input_mask=None, voice_noise=None):
+             record=None, speech_tensors=None, speech_masks=None, speech_input_mask=None, voice_noise=None,
+             do_sample=False, sample_q=None, teacher=None):
     """Returns (sequences [B, L+steps], audio list per sample, reach_max [B]).
 
     sd: full state dict (reference names) in `dtype`.  cfg: VibeVoiceConfig.
     tokenizer_ids: dict(start, end, diffusion, eos).
+    record: dict filled per loop step (the teacher-forcing trace the GPU
+    parity tests replay): "prompt_embeds" (the un-padded prompt rows, voice
+    spliced in, row-major over samples), per step "logits" [B, 4 valid],
+    "hpos" [B, H], "hneg" [B, H] (None when no negative pass ran), "didx",
+    "noise", "latents" [n, D], "audio" [n, 1, hop], "next_embeds" [B, H]
+    (the next step's input).
+    do_sample: `torch.multinomial(softmax(scores), 1)` over the constrained
+    full-vocabulary fp32 scores (:496-505) on the global CPU generator, as the
+    reference's CPU run draws it.  sample_q(step) -> [B, 4] replays another
+    generator's Exp(1) draws at the 4 valid ids (sorted by id) instead: ATen's
+    one-sample multinomial is argmax(p / q) over a [B, vocab] Exp(1) draw.
+    teacher: another run's `record` — its prompt embeddings, per-step next
+    inputs and latents replace this run's own (teacher forcing), so each step
+    of this run sees exactly that run's inputs (per-step precision studies).
     """
     lmc = dict(cfg.decoder_config)
     lsd = _sub(sd, "model.language_model.")
@@ -102,6 +117,7 @@ def generate(sd, cfg, input_ids, attention_mask, tokenizer_ids, ddpm_steps=10, c
     neg = [_NegRow(nl) for _ in range(B)]
     neg_started = False
     inputs_embeds = None
+    dstep = 0                                                         # diffusion steps so far
 
     def logits_of(hrow):
         return (hrow @ lm_head.t()).float()                          # bf16 Linear then .float() (:494-498)
@@ -121,6 +137,11 @@ def generate(sd, cfg, input_ids, attention_mask, tokenizer_ids, ddpm_steps=10, c
                 if speech_input_mask is not None:
                     emb0[speech_input_mask] = v.to(emb0.dtype)
             hs = []
+            if teacher is not None:
+                emb0 = emb0.clone()
+                emb0[attention_mask.bool()] = teacher["prompt_embeds"].to(emb0.dtype)
+            if record is not None:
+                record["prompt_embeds"] = emb0[attention_mask.bool()].clone()
             for b in range(B):
                 keep = attention_mask[b].bool()
                 x = emb0[b][keep][None]
@@ -131,8 +152,17 @@ def generate(sd, cfg, input_ids, attention_mask, tokenizer_ids, ddpm_steps=10, c
         lg = logits_of(hpos)
         if record is not None:
             record.setdefault("logits", []).append(lg[:, valid].clone())
+            record.setdefault("hpos", []).append(hpos.clone())
         if forced is not None:
             nxt = torch.tensor([forced[b][step] if step < len(forced[b]) else eos for b in range(B)])
+        elif do_sample:
+            scores = torch.full_like(lg, float("-inf"))               # VibeVoiceTokenConstraintProcessor (:54-67)
+            scores[:, valid] = lg[:, valid]
+            if sample_q is None:
+                nxt = torch.multinomial(F.softmax(scores, dim=-1), num_samples=1).squeeze(1)
+            else:
+                p = F.softmax(scores[:, valid], dim=-1)
+                nxt = torch.tensor(valid)[(p / sample_q(step)).argmax(-1)]
         else:
             sub = lg[:, valid]
             nxt = torch.tensor(valid)[sub.argmax(-1)]
@@ -187,9 +217,15 @@ def generate(sd, cfg, input_ids, attention_mask, tokenizer_ids, ddpm_steps=10, c
             correct_cnt[nd] += 1
             n = didx.numel()
             noise = torch.randn(2 * n, cfg.acoustic_vae_dim).to(dtype)  # :716
+            if record is not None:
+                record.setdefault("noise", []).append(noise.clone())
             lat = head.sample_speech_tokens(hsd, hpos[didx], hneg[didx], noise, ddpm_steps, cfg_scale,
                                             cfg.diffusion_head_config.head_layers,
                                             cfg.diffusion_head_config.rms_norm_eps)
+            own_lat = lat
+            if teacher is not None:
+                lat = teacher["latents"][dstep].to(lat.dtype)
+            dstep += 1
             z = (lat / scale - bias).unsqueeze(-1)                    # :651
             a = codec.decode(asd, dd, z, a_state, didx)
             for i, b in enumerate(didx.tolist()):
@@ -198,7 +234,14 @@ def generate(sd, cfg, input_ids, attention_mask, tokenizer_ids, ddpm_steps=10, c
             next_embeds[didx] = connector(sd, "model.acoustic_connector.", lat) + \
                 connector(sd, "model.semantic_connector.", sem)
             if record is not None:
-                record.setdefault("latents", []).append(lat.clone())
+                record.setdefault("latents", []).append(own_lat.clone())
+                record.setdefault("audio", []).append(a.clone())
+        if record is not None:
+            record.setdefault("hneg", []).append(None if hneg is None else hneg.clone())
+            record.setdefault("didx", []).append(didx.clone())
+            record.setdefault("next_embeds", []).append(next_embeds.clone())
+        if teacher is not None:
+            next_embeds = teacher["next_embeds"][step].to(next_embeds.dtype)
         inputs_embeds = next_embeds
     outs = [torch.cat(c, dim=-1) if c else None for c in audio]
     return seqs, outs, reach

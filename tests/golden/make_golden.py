@@ -408,7 +408,39 @@ def g8_loop():
     out["voice/reach"] = o.reach_max_step_sample.numpy()
     for b, a in enumerate(o.speech_outputs):
         out[f"voice/audio{b}"] = f32(a)
+    # do_sample=True (:502-505): no forced schedule; the reference draws
+    # torch.multinomial over the constrained full-vocabulary probabilities and the
+    # diffusion noise from the same global CPU generator, interleaved
+    cls._process_speech_inputs = voice_free
+    forced[:] = []
+    # the tied embedding rows of the 4 control ids are scaled down so their logits
+    # are O(1) and the draw is not a foregone conclusion (test weights give logits ~16)
+    emb = model.model.language_model.embed_tokens.weight
+    rows = [G8_IDS[k] for k in ("eos", "start", "end", "diffusion")]
+    mats = [emb] if model.lm_head.weight is emb else [emb, model.lm_head.weight]   # tied: one tensor
+    saved = [w.data[rows].clone() for w in mats]
+    for w in mats:
+        w.data[rows] *= SAMPLE_ROW_SCALE
+    for seed in SAMPLE_SEEDS:
+        torch.manual_seed(seed)
+        with torch.no_grad():
+            o = model.generate(input_ids=ids, attention_mask=mask, tokenizer=tok, cfg_scale=1.3,
+                               speech_tensors=torch.zeros(1, 4), speech_masks=torch.zeros(1, 1, dtype=torch.bool),
+                               speech_input_mask=torch.zeros(2, P, dtype=torch.bool), refresh_negative=True,
+                               generation_config={"do_sample": True}, show_progress_bar=False)
+        out[f"sample{seed}/sequences"] = o.sequences.numpy()
+        out[f"sample{seed}/reach"] = o.reach_max_step_sample.numpy()
+        for b, a in enumerate(o.speech_outputs):
+            out[f"sample{seed}/audio{b}"] = f32(a) if a is not None else np.zeros(0, np.float32)
+    for w, v in zip(mats, saved):
+        w.data[rows] = v
+    forced[:] = G8_SCHEDULES
+    cls._process_speech_inputs = orig
     save("g8_loop.npz", **out)
+
+
+SAMPLE_SEEDS = (1234, 77)
+SAMPLE_ROW_SCALE = 0.05
 
 
 # ---------------------------------------------------------------- G9 processor

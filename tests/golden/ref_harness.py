@@ -121,8 +121,14 @@ def load():
         return _loaded
     _install_diffusers_stub()
     _patch_transformers()
-    if REF not in sys.path:
-        sys.path.insert(0, REF)
+    # the repository ships its own `vibevoice/` import-path package (drop-in
+    # names over vibevoice_amd): the reference's must win here
+    if REF in sys.path:
+        sys.path.remove(REF)
+    sys.path.insert(0, REF)
+    for name in [n for n in sys.modules if n == "vibevoice" or n.startswith("vibevoice.")]:
+        if not (getattr(sys.modules[name], "__file__", "") or "").startswith(REF):
+            del sys.modules[name]
     import vibevoice.schedule.dpm_solver as dpm
     import vibevoice.modular.configuration_vibevoice as cfg
     import vibevoice.modular.modular_vibevoice_diffusion_head as head
@@ -158,7 +164,8 @@ def install_generate_shims(mvi, forced):
       * `DynamicCache.key_cache / value_cache` (:572-576, 624-631): lists of the
         per-layer K/V tensors (5.15 keeps them in `layers[i].keys/values`);
     `forced[b][step]` (eos after the list ends) wins the argmax: its logit is
-    raised to 1e30 before the reference's constraint processor runs.
+    raised to 1e30 before the reference's constraint processor runs; an empty
+    `forced` leaves the scores alone (the do_sample fixture).
     """
     from transformers import GenerationConfig, LogitsProcessor, LogitsProcessorList
     from transformers.cache_utils import DynamicCache
@@ -171,6 +178,8 @@ def install_generate_shims(mvi, forced):
             self.L0, self.eos = L0, eos
 
         def __call__(self, input_ids, scores):
+            if not forced:          # an empty schedule list: the model's own choice (greedy or sampled)
+                return scores
             step = input_ids.shape[1] - self.L0
             scores = scores.clone()
             for b in range(scores.shape[0]):

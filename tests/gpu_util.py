@@ -4,6 +4,8 @@ import torch
 
 def rel_err(a, b):
     a, b = a.float().cpu(), b.float().cpu()
+    assert a.numel() == b.numel(), (a.shape, b.shape)   # no silent broadcasting
+    a = a.reshape(b.shape)
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 

@@ -108,3 +108,39 @@ def test_mix_fusion_bit_exact(n, mask):
         _lib.lib().vv_codec_mix_fusion(3)
     for i, (a, b) in enumerate(zip(outs[0], outs[mask])):
         assert torch.equal(a, b), (n, i, (a.float() - b.float()).abs().max().item())
+
+
+@pytest.mark.parametrize("n", [3, 4, 5, 6, 8])
+def test_codec_stream_batch_sizes(n):
+    """The streaming codec at the real shapes with n = 3..8 diffusing rows
+    (configs[2]: B = 8), slots scattered over a max_batch 8 engine: three
+    frames vs the oracle, per row."""
+    cfg = tiny_config(ratios=(8, 5, 5, 4, 2, 2), depths="3-3-3-3-3-3-8", nf=32)
+    sd = synthetic_state_dict(cfg, seed=3, device="cpu", mode="test", with_acoustic_encoder=False)
+    eng = Engine(cfg, sd, dev, max_batch=8, max_ctx=64)
+    hop = cfg.hop
+    dd = ocodec.codec_dims(cfg.acoustic_tokenizer_config, "decoder")
+    ed = ocodec.codec_dims(cfg.semantic_tokenizer_config, "encoder")
+    sd_a, sd_s = sub(sd, "model.acoustic_tokenizer."), sub(sd, "model.semantic_tokenizer.")
+    st_a, st_s = ocodec.StreamState(8), ocodec.StreamState(8)
+    s_f, b_f = sd["model.speech_scaling_factor"], sd["model.speech_bias_factor"]
+    g = torch.Generator().manual_seed(11)
+    slots = sorted(torch.randperm(8, generator=g)[:n].tolist())
+    eng.codec_reset(torch.arange(8, dtype=torch.int32, device=dev))
+    bad = []
+    for step in range(3):
+        lat = torch.randn(n, 64, generator=g).bfloat16()
+        d_slots = torch.tensor(slots, dtype=torch.int32, device=dev)
+        audio = torch.empty(n, hop, dtype=torch.bfloat16, device=dev)
+        sem = torch.empty(n, 128, dtype=torch.bfloat16, device=dev)
+        eng.codec_step(d_slots, lat.to(dev), audio, sem)
+        idx = torch.tensor(slots)
+        a_ref = ocodec.decode(sd_a, dd, (lat / s_f - b_f).unsqueeze(-1), st_a, idx)[:, 0]
+        s_ref = ocodec.encode(sd_s, ed, a_ref[:, None], st_s, idx)[:, 0]
+        torch.cuda.synchronize()
+        for r in range(n):
+            ea, es = rel_err(audio[r], a_ref[r]), rel_err(sem[r], s_ref[r])
+            print(f"n {n} step {step} row {r} (slot {slots[r]}): audio rel {ea:.3e} sem rel {es:.3e}")
+            if not (ea < 3e-2 and es < 3e-2):
+                bad.append((step, r, ea, es))
+    assert not bad, bad

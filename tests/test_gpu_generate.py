@@ -238,3 +238,69 @@ def test_graphs_recaptured_after_workspace_growth():
     long_eager = run(120, False)
     for b in range(2):
         assert torch.equal(long_graph.speech_outputs[b].cpu(), long_eager.speech_outputs[b].cpu())
+
+
+def test_device_multinomial_is_argmax_over_exponential_draw():
+    """On the ROCm device too, torch.multinomial(p, 1) (what the reference's GPU
+    run calls, modeling_vibevoice_inference.py:505) equals argmax(p / q) over a
+    [B, vocab] Exp(1) draw from the same device-generator state — the draw the
+    product makes when do_sample=True."""
+    V, idx = 151936, [151643, 151652, 151653, 151654]
+    for t in range(20):
+        s = torch.full((3, V), float("-inf"), device=dev)
+        s[:, idx] = torch.randn(3, 4, generator=torch.Generator().manual_seed(t)).to(dev) * 2
+        p = torch.softmax(s, -1)
+        torch.cuda.manual_seed(t)
+        a = torch.multinomial(p, 1).squeeze(1).cpu()
+        torch.cuda.manual_seed(t)
+        q = torch.empty(3, V, device=dev).exponential_(1)
+        c = torch.tensor(idx)[(torch.softmax(s[:, idx], -1) / q[:, idx]).argmax(-1).cpu()]
+        assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("seed", [1234, 77])
+def test_generate_do_sample_matches_reference_loop(seed):
+    """generate(generation_config={"do_sample": True}) on G8's sampling weights
+    (control rows scaled so the draws are live; oracle/loop.py is pinned to the
+    reference's own sampled generate() by G8 "sample<seed>").  The product
+    draws the multinomial's Exp(1) vector on the device generator, as the
+    reference's GPU run does; the test replays those device draws into the
+    oracle (sample_q) while the diffusion noise comes from the CPU generator in
+    both.  Sequences equal; audio as in the forced tests."""
+    from test_oracle_golden import g8_sample_weights
+    from golden_io import load
+    z = load("g8_loop.npz")
+    cfg, sd32 = g8_sample_weights()
+    sd = {k: v.to(torch.bfloat16) for k, v in sd32.items()}
+    model = VibeVoiceForConditionalGenerationInference(cfg, sd, dev, max_batch=2, max_ctx=128)
+    model.set_ddpm_inference_steps(5)
+    ids, mask = torch.from_numpy(z["input_ids"]), torch.from_numpy(z["attention_mask"])
+    torch.manual_seed(seed)
+    out = model.generate(input_ids=ids, attention_mask=mask, tokenizer=TOK, cfg_scale=1.3,
+                         generation_config={"do_sample": True}, show_progress_bar=False)
+    torch.cuda.synchronize()
+    valid = sorted(IDS[k] for k in ("start", "end", "diffusion", "eos"))
+    torch.cuda.manual_seed(seed)
+    qs = [torch.empty(2, cfg.decoder_config.vocab_size, device=dev).exponential_(1)[:, valid].cpu()
+          for _ in range(out.sequences.shape[1] - ids.shape[1])]
+    res = []
+    for s32 in (False, True):
+        torch.manual_seed(seed)
+        res.append(oloop.generate(sd32 if s32 else sd, cfg, ids, mask, IDS, ddpm_steps=5, cfg_scale=1.3,
+                                  do_sample=True, sample_q=lambda k: qs[k],
+                                  dtype=torch.float32 if s32 else torch.bfloat16))
+    (seqs, audio, reach), (_, audio32, _) = res
+    print("sampled", (out.sequences[:, ids.shape[1]:] - 151640).tolist())
+    assert torch.equal(out.sequences, seqs)
+    assert torch.equal(out.reach_max_step_sample.cpu(), reach)
+    for b in range(2):
+        got, ref = out.speech_outputs[b], audio[b]
+        if ref is None:
+            assert got is None
+            continue
+        assert got.shape == ref.shape, (got.shape, ref.shape)
+        a32 = audio32[b]
+        noise = rel_err(ref, a32) if a32 is not None and a32.shape == ref.shape else 0.0
+        e, c = rel_err(got, ref), cos(got, ref)
+        print(f"do_sample sample {b} audio rel_err {e:.3e} cos {c:.6f} (bf16 reference vs fp32: {noise:.3e})")
+        assert e < max(5e-2, 2 * noise) and c > 0.995

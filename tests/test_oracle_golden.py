@@ -213,3 +213,66 @@ def test_loop_trace_g8(refresh, voice, cap):
         assert audio[b].shape == ref.shape, (audio[b].shape, ref.shape)
         err = ((audio[b].float() - ref).norm() / ref.norm()).item()
         assert err < 1e-4, f"sample {b} audio rel L2 {err:.3e}"
+
+
+G8_SAMPLE_ROWS = [151643, 151652, 151653, 151654]
+G8_SAMPLE_ROW_SCALE = 0.05          # make_golden.py SAMPLE_ROW_SCALE
+
+
+def g8_sample_weights(dtype=torch.float32):
+    """G8's weights with the 4 control rows of the tied embedding / lm_head
+    scaled as make_golden.py's do_sample runs scale them."""
+    from tiny import tiny_config
+    from vibevoice_amd.weights import synthetic_state_dict
+    cfg = tiny_config(hidden=256, layers=2, heads=2, kv_heads=1, inter=512)
+    sd = synthetic_state_dict(cfg, seed=21, device="cpu", dtype=torch.float32, mode="test")
+    e = sd["model.language_model.embed_tokens.weight"].clone()
+    e[G8_SAMPLE_ROWS] *= G8_SAMPLE_ROW_SCALE
+    sd["model.language_model.embed_tokens.weight"] = sd["lm_head.weight"] = e
+    return cfg, {k: v.to(dtype) for k, v in sd.items()}
+
+
+@pytest.mark.parametrize("seed", [1234, 77])
+def test_loop_do_sample_g8(seed):
+    """do_sample=True (modeling_vibevoice_inference.py:502-505): the oracle's
+    literal torch.multinomial over the constrained full-vocabulary
+    probabilities on the global CPU generator, interleaved with the diffusion
+    noise draws, vs the reference's own generate() (G8 sample runs: sampled
+    speech_start / speech_end / diffusion / eos, a diffusion token at step 0).
+    Sequences equal, audio within fp32 op-order noise."""
+    from oracle import loop
+    z = load("g8_loop.npz")
+    cfg, sd = g8_sample_weights()
+    ids = dict(eos=151643, start=151652, end=151653, diffusion=151654)
+    torch.manual_seed(seed)
+    seqs, audio, reach = loop.generate(sd, cfg, torch.from_numpy(z["input_ids"]), torch.from_numpy(z["attention_mask"]),
+                                       ids, ddpm_steps=5, cfg_scale=1.3, do_sample=True, dtype=torch.float32)
+    tag = f"sample{seed}"
+    assert torch.equal(seqs, torch.from_numpy(z[f"{tag}/sequences"]))
+    assert torch.equal(reach, torch.from_numpy(z[f"{tag}/reach"]))
+    for b in range(2):
+        ref = torch.from_numpy(z[f"{tag}/audio{b}"])
+        if ref.numel() == 0:
+            assert audio[b] is None
+            continue
+        assert audio[b].shape == ref.shape, (audio[b].shape, ref.shape)
+        err = ((audio[b].float() - ref).norm() / ref.norm()).item()
+        assert err < 1e-4, f"sample {b} audio rel L2 {err:.3e}"
+
+
+def test_multinomial_is_argmax_over_exponential_draw():
+    """The identity the product's sampling rests on (ATen's one-sample
+    multinomial path): torch.multinomial(p, 1) == argmax(p / q) with q ~ Exp(1)
+    drawn over the whole row from the same generator state, and only the
+    nonzero-probability columns of q matter."""
+    V, idx = 151936, [151643, 151652, 151653, 151654]
+    for t in range(50):
+        s = torch.full((3, V), float("-inf"))
+        s[:, idx] = torch.randn(3, 4, generator=torch.Generator().manual_seed(t)) * 2
+        p = torch.softmax(s, -1)
+        torch.manual_seed(t)
+        a = torch.multinomial(p, 1).squeeze(1)
+        torch.manual_seed(t)
+        q = torch.empty(3, V).exponential_(1)
+        c = torch.tensor(idx)[(torch.softmax(s[:, idx], -1) / q[:, idx]).argmax(-1)]
+        assert torch.equal(a, c)

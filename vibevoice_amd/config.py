@@ -32,6 +32,9 @@ def _depths(d):
 class VibeVoiceConfig:
     """Attribute view over the JSON dict, with the derived codec layout."""
 
+    model_type = "vibevoice"     # configuration_vibevoice.py:165
+    sub_configs = {}             # read by AutoModelForCausalLM.from_config (no text_config sub-config)
+
     def __init__(self, d):
         self.raw = copy.deepcopy(d)
         self.decoder_config = _Attr(d["decoder_config"])

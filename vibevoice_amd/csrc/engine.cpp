@@ -1224,9 +1224,11 @@ int vv_gemm_bf16_norm(int M, int N, int K, const void* A, int64_t lda, const voi
   g.epi.kind = epi;
   g.epi.out = rowmap(Y, ldy);
   g.xf = xf_norm((const bf16*)norm_w, eps);
-  if (c) {
+  if (c) {   // the engine's own dispatch (M > 16: k_rmsnorm once, then the GEMV on normalised rows)
     g.ws = (float*)c->splitk_ws.p;
     g.counters = (unsigned*)c->splitk_cnt.p;
+    CHK(gemm(c, g, (hipStream_t)vst));
+    return 0;
   }
   KCHK(launch_gemm(g, (hipStream_t)vst));
   return 0;

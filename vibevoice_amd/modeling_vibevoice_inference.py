@@ -71,18 +71,87 @@ class _ModelView:
         self._o._graph_seen.clear()
 
 
-def load_state_dict(path):
-    """Safetensors shards of a HF checkpoint dir (loaded with the safe loader only)."""
+def load_state_dict(path, cfg=None):
+    """Safetensors shards of a HF checkpoint dir, loaded with the safe loader
+    only.  With `model.safetensors.index.json` present exactly the shards its
+    weight_map names are read (a HF loader's rule); otherwise every
+    *.safetensors file.  lm_head follows the reference's tie rule
+    (modeling_vibevoice_inference.py:120-129): tied to the embedding when the
+    config's top-level tie_word_embeddings is set (or the checkpoint has none)."""
+    import json
     from safetensors.torch import load_file
-    files = sorted(f for f in os.listdir(path) if f.endswith(".safetensors"))
+    index = os.path.join(path, "model.safetensors.index.json")
+    if os.path.exists(index):
+        with open(index) as f:
+            wmap = json.load(f)["weight_map"]
+        files = sorted(set(wmap.values()))
+    else:
+        files = sorted(f for f in os.listdir(path) if f.endswith(".safetensors"))
     if not files:
         raise FileNotFoundError(f"no .safetensors files under {path}")
     sd = {}
     for f in files:
         sd.update(load_file(os.path.join(path, f)))
-    if "lm_head.weight" not in sd and "model.language_model.embed_tokens.weight" in sd:
-        sd["lm_head.weight"] = sd["model.language_model.embed_tokens.weight"]
+    emb = sd.get("model.language_model.embed_tokens.weight")
+    tied = cfg.tie_word_embeddings if cfg is not None else "lm_head.weight" not in sd
+    if emb is not None and (tied or "lm_head.weight" not in sd):
+        sd["lm_head.weight"] = emb
     return sd
+
+
+def resolve_device(device_map):
+    """The one ROCm device a `device_map` (as HF / accelerate accept it) names.
+    Accepted: "cuda", "cuda:N", torch.device("cuda", N), N, "auto" (the current
+    device) and {"": <one of these>}.  Everything that asks for the CPU / MPS /
+    disk, or splits the model over devices, raises: this engine has no CPU
+    path, and tensor parallelism is requested with `tp_group=` instead."""
+    d = device_map
+    if isinstance(d, dict):
+        vals = set(map(str, d.values()))
+        if len(vals) != 1:
+            raise ValueError(f"device_map {device_map!r} splits the model; the HIP engine keeps it on one GPU "
+                             "(tensor parallelism: tp_group=)")
+        d = next(iter(d.values()))
+    if isinstance(d, int) and not isinstance(d, bool):
+        d = torch.device("cuda", d)
+    if d == "auto":
+        d = torch.device("cuda", torch.cuda.current_device() if torch.cuda.is_available() else 0)
+    if isinstance(d, str):
+        try:
+            d = torch.device(d)
+        except RuntimeError:
+            d = None
+    if not isinstance(d, torch.device) or d.type != "cuda":
+        raise ValueError(f"device_map={device_map!r}: the VibeVoice MI355X engine runs on a ROCm GPU only "
+                         "(use device_map=\"cuda\"); there is no CPU/MPS path — the reference's CPU eager run "
+                         "is the test oracle (oracle/), not part of this package")
+    if d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device() if torch.cuda.is_available() else 0)
+    return d
+
+
+def resolve_dtype(torch_dtype):
+    """bf16 is the compute type (the reference's GPU dtype,
+    demo/inference_from_file.py:265); anything else raises."""
+    if torch_dtype in (None, "auto", "bfloat16", torch.bfloat16):
+        return torch.bfloat16
+    raise ValueError(f"torch_dtype={torch_dtype!r}: the MI355X engine computes in bfloat16 "
+                     "(torch_dtype=torch.bfloat16)")
+
+
+class VibeVoiceTokenConstraintProcessor:
+    """LogitsProcessor that keeps only the valid speech-control ids
+    (modeling_vibevoice_inference.py:54-67).  generate() does not call it — the
+    engine computes only those 4 logits (k_final_head) — it is exported for
+    callers that apply it to their own scores."""
+
+    def __init__(self, valid_token_ids, device=None):
+        self.valid_token_ids = torch.tensor(valid_token_ids, dtype=torch.long, device=device)
+
+    def __call__(self, input_ids, scores):
+        mask = torch.full_like(scores, float("-inf"))
+        mask[:, self.valid_token_ids] = 0
+        return scores + mask
 
 
 class VibeVoiceForConditionalGenerationInference:
@@ -148,27 +217,50 @@ class VibeVoiceForConditionalGenerationInference:
         return self._bufs[B]
 
     # ------------------------------------------------------------ loading
+    config_class = VibeVoiceConfig          # AutoModelForCausalLM.register checks this name (vibevoice/ shim)
+
     @classmethod
     def from_pretrained(cls, path, torch_dtype=torch.bfloat16, device_map="cuda", attn_implementation="hip",
                         synthetic_seed=0, **kw):
         """`path`: a checkpoint dir (config.json + *.safetensors), or
         "synthetic:1.5B" / "synthetic:Large" for seeded random weights at the
-        real shapes (no checkpoints are reachable offline)."""
-        if torch_dtype not in (torch.bfloat16, None):
-            raise ValueError("the MI355X engine computes in bfloat16 (torch_dtype=torch.bfloat16)")
-        dev = device_map if isinstance(device_map, str) and device_map.startswith("cuda") else "cuda"
+        real shapes (no checkpoints are reachable offline).
+
+        `device_map` / `torch_dtype` as the demos pass them
+        (demo/inference_from_file.py:282-305): a CUDA (ROCm) device and bf16.
+        The CPU / MPS / fp32 branches of the demo are refused with an explicit
+        error — there is no CPU path behind this class."""
+        resolve_dtype(torch_dtype)
+        dev = resolve_device(device_map)
         if str(path).startswith("synthetic:"):
             cfg = VibeVoiceConfig.builtin(str(path).split(":", 1)[1])
             sd = synthetic_state_dict(cfg, seed=synthetic_seed, device=dev)
         else:
             cfg = VibeVoiceConfig.from_json_file(os.path.join(path, "config.json"))
-            sd = load_state_dict(path)
+            sd = load_state_dict(path, cfg)
         return cls(cfg, sd, dev, attn_implementation=attn_implementation, **kw)
+
+    @classmethod
+    def _from_config(cls, config, torch_dtype=None, device_map="cuda", attn_implementation="hip", seed=0, **kw):
+        """AutoModelForCausalLM.from_config(config): random-init weights, as
+        PreTrainedModel._from_config builds an untrained model (seeded here)."""
+        resolve_dtype(torch_dtype)
+        dev = resolve_device(device_map)
+        return cls(config, synthetic_state_dict(config, seed=seed, device=dev), dev,
+                   attn_implementation=attn_implementation, **kw)
 
     def eval(self):
         return self
 
-    def to(self, *a, **k):
+    def to(self, *args, **kwargs):
+        """Moving the engine is not possible: accept only the device it lives on
+        and bf16 (the reference's `.to("mps")` / fp32 branch raise here)."""
+        for a in list(args) + list(kwargs.values()):
+            if isinstance(a, torch.dtype):
+                resolve_dtype(a)
+            elif a is not None and not isinstance(a, bool):
+                if resolve_device(a) != self.device:
+                    raise ValueError(f"the engine lives on {self.device}; it cannot be moved to {a}")
         return self
 
     def set_ddpm_inference_steps(self, num_steps=None):
@@ -326,6 +418,15 @@ class GenerateSession:
         self.ints = _Staging(dev, torch.int32, 1 << 16)
         self.valid_t = torch.tensor(self.valid)
         self.order_t = torch.tensor(self.order)
+        if self.do_sample:
+            # torch.multinomial(softmax(scores), 1) (:502-505) over the full-vocabulary
+            # constrained scores is ATen's one-sample path: argmax(p / q), q ~ Exp(1)
+            # drawn for EVERY vocabulary entry on the logits' device generator.  The
+            # same [B, vocab] draw is made here (same generator, same offsets), and only
+            # its 4 legal columns are read back.
+            self.vocab = int(model.config.decoder_config.vocab_size)
+            self.q_cols = torch.tensor(self.valid, device=dev)
+            self.q_pin = torch.zeros(B, 4, dtype=torch.float32, pin_memory=True)
         # static device operands of the loop body (graph-capturable): LM rows are
         # [positive B | negative B]; the negative rows consume the same input (:594-596)
         sb = model._step_buffers(B)
@@ -473,9 +574,10 @@ class GenerateSession:
         while the host reads the logits and does the bookkeeping.  The choice
         itself is unchanged: step() keeps the result only if exactly these rows
         chose speech_diffusion, else it restores the CPU generator and redoes the
-        diffusion for the right rows.  Greedy decoding only (sampling draws from
-        the same generator before the noise, :505)."""
-        if self.do_sample or not self.speculate:
+        diffusion for the right rows.  Sampling (:505) draws on the device
+        generator, the noise on the CPU one (:716), so both modes speculate;
+        sde-dpmsolver++ (device-generator noise after the sampling draw) does not."""
+        if not self.speculate:
             return None
         last = self.seq[-1][:, -1]
         rows = torch.nonzero(~self.finished & ((last == self.diff_id) | (last == self.start_id))).reshape(-1)
@@ -520,12 +622,16 @@ class GenerateSession:
             self.pos_len += 1
         # ---- token choice (:494-509); the argmax is always read back, as in the reference
         self.logits_pin.copy_(self.logits[:B], non_blocking=True)
+        if self.do_sample:
+            q = torch.empty(B, self.vocab, device=dev, dtype=torch.float32).exponential_(1)
+            self.q_pin.copy_(q.index_select(1, self.q_cols), non_blocking=True)
         self.logits_ready.record()
         spec = self._speculate()
         self.logits_ready.synchronize()
         lg = self.logits_pin.clone()
         if self.do_sample:
-            pick = torch.multinomial(torch.softmax(lg, -1), 1).squeeze(1)
+            r = torch.softmax(lg, -1) / self.q_pin                            # ties -> lowest id, as over the vocab
+            pick = self.order_t[r[:, self.order].argmax(-1)]
         else:
             pick = self.order_t[lg[:, self.order].argmax(-1)]
         nxt = self.valid_t[pick]

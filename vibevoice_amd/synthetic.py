@@ -44,19 +44,24 @@ def _voice(g, seconds, sr=24000, dbfs=-25.0):
     return wav * (target / wav.pow(2).mean().sqrt())
 
 
-def synthetic_inputs(batch=1, speakers=1, voice_seconds=3.0, text_tokens=64, seed=0, hop=3200):
+def synthetic_inputs(batch=1, speakers=1, voice_seconds=3.0, text_tokens=64, seed=0, hop=3200, text_jitter=0):
     """Processor-shaped dict: input_ids, attention_mask, speech_input_mask,
-    speech_tensors, speech_masks (voice_seconds=0 -> no voice prompt)."""
+    speech_tensors, speech_masks (voice_seconds=0 -> no voice prompt).
+    voice_seconds may be a list (cycled over the voices: ragged clips, zero-
+    padded in speech_tensors as the processor pads them); text_jitter adds
+    0..text_jitter random tokens per script line (ragged, left-padded rows)."""
     g = torch.Generator().manual_seed(seed)
     rows, masks, voices = [], [], []
+    secs = list(voice_seconds) if isinstance(voice_seconds, (list, tuple)) else [voice_seconds]
+    has_voice = any(v > 0 for v in secs)
     for _ in range(batch):
         ids = _text(g, SYSTEM_TOKENS)
         sim = [False] * len(ids)
-        if voice_seconds > 0:
+        if has_voice:
             ids += _text(g, SECTION_TOKENS)
             sim += [False] * SECTION_TOKENS
             for _ in range(speakers):
-                wav = _voice(g, voice_seconds)
+                wav = _voice(g, secs[len(voices) % len(secs)])
                 frames = math.ceil(wav.numel() / hop)
                 piece = _text(g, SPEAKER_PREFIX) + [SPEECH_START] + [SPEECH_DIFFUSION] * frames + [SPEECH_END] + \
                     _text(g, 1)
@@ -67,7 +72,8 @@ def synthetic_inputs(batch=1, speakers=1, voice_seconds=3.0, text_tokens=64, see
         sim += [False] * SECTION_TOKENS
         per = max(1, text_tokens // speakers)
         for _ in range(speakers):
-            line = _text(g, SPEAKER_PREFIX + per + 1)
+            extra = int(torch.randint(0, text_jitter + 1, (1,), generator=g)) if text_jitter else 0
+            line = _text(g, SPEAKER_PREFIX + per + extra + 1)
             ids += line
             sim += [False] * len(line)
         ids += _text(g, SECTION_TOKENS) + [SPEECH_START]

@@ -361,20 +361,33 @@ def pack(sd, cfg: VibeVoiceConfig, device, with_acoustic_encoder=True, tp_rank=0
     return out
 
 
-def write_synthetic_checkpoint(path, cfg: VibeVoiceConfig, seed=0, mode="bench", shard_bytes=2 << 30):
+def write_synthetic_checkpoint(path, cfg: VibeVoiceConfig, seed=0, mode="bench", shard_bytes=2 << 30,
+                               tokenizer_dir=None, speech_tok_compress_ratio=None, state_dict=None):
     """An offline stand-in for a HF checkpoint directory:
     config.json + `model-0000i-of-0000n.safetensors` shards with the reference's
-    state-dict names, the tied lm_head left out as the reference's checkpoints
-    do (modeling_vibevoice_inference.py:120-129), so
+    state-dict names + `model.safetensors.index.json` (metadata.total_size and
+    the tensor -> shard weight_map a HF loader reads), so
     `from_pretrained(path)` and the demos' `--model_path` run without network.
+    The lm_head is left out when the top-level `tie_word_embeddings` ties it to
+    the embedding — the flag the reference's tie_weights reads
+    (modeling_vibevoice_inference.py:120-129) and synthetic_state_dict uses.
+    Stale shards / index of an earlier write are removed first (the loader
+    would otherwise mix them in).  `tokenizer_dir`: also write the
+    preprocessor_config.json VibeVoiceProcessor.from_pretrained(path) reads,
+    naming that local Qwen2-style tokenizer (vibevoice_processor.py:67-105).
+    `state_dict`: write these tensors instead of synthetic_state_dict(cfg, seed).
     Returns the shard file names."""
     import json
     import os
     from safetensors.torch import save_file
     os.makedirs(path, exist_ok=True)
-    sd = synthetic_state_dict(cfg, seed=seed, device="cpu", mode=mode)
-    tied = cfg.decoder_config.get("tie_word_embeddings", True)
-    names = sorted(k for k in sd if not (tied and k == "lm_head.weight"))
+    for f in os.listdir(path):
+        if f.endswith(".safetensors") or f == "model.safetensors.index.json":
+            os.remove(os.path.join(path, f))
+    sd = state_dict if state_dict is not None else synthetic_state_dict(cfg, seed=seed, device="cpu", mode=mode)
+    emb = sd[LM + "embed_tokens.weight"]
+    drop_head = cfg.tie_word_embeddings or sd.get("lm_head.weight") is emb
+    names = sorted(k for k in sd if not (drop_head and k == "lm_head.weight"))
     shards, cur, size = [], [], 0
     for k in names:
         nb = sd[k].numel() * sd[k].element_size()
@@ -385,10 +398,24 @@ def write_synthetic_checkpoint(path, cfg: VibeVoiceConfig, seed=0, mode="bench",
         size += nb
     shards.append(cur)
     files = [f"model-{i + 1:05d}-of-{len(shards):05d}.safetensors" for i in range(len(shards))]
+    weight_map, total = {}, 0
     for f, part in zip(files, shards):
         save_file({k: sd[k].contiguous() for k in part}, os.path.join(path, f), metadata={"format": "pt"})
+        for k in part:
+            weight_map[k] = f
+            total += sd[k].numel() * sd[k].element_size()
+    with open(os.path.join(path, "model.safetensors.index.json"), "w") as fh:
+        json.dump({"metadata": {"total_size": total}, "weight_map": weight_map}, fh, indent=2)
     with open(os.path.join(path, "config.json"), "w") as fh:
         json.dump(cfg.to_dict(), fh, indent=2)
+    if tokenizer_dir is not None:
+        pc = {"processor_class": "VibeVoiceProcessor",
+              "speech_tok_compress_ratio": int(speech_tok_compress_ratio or cfg.hop), "db_normalize": True,
+              "audio_processor": {"feature_extractor_type": "VibeVoiceTokenizerProcessor", "sampling_rate": 24000,
+                                  "normalize_audio": True, "target_dB_FS": -25, "eps": 1e-6},
+              "language_model_pretrained_name": os.path.abspath(tokenizer_dir)}
+        with open(os.path.join(path, "preprocessor_config.json"), "w") as fh:
+            json.dump(pc, fh, indent=2)
     return files
 
 
