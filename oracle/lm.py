@@ -23,7 +23,7 @@ def rms(x, w, eps):
 
 
 def rope_cos_sin(pos, head_dim, theta, dtype):
-    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float) / head_dim))
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float, device=pos.device) / head_dim))
     f = pos.float()[:, None] * inv[None, :]
     emb = torch.cat([f, f], dim=-1)
     return emb.cos().to(dtype), emb.sin().to(dtype)
@@ -75,7 +75,7 @@ def forward_rows(sd, cfg, x, kvs, commit=True):
         outs = []
         for r in range(R):
             L0 = kvs[r].length()
-            pos = torch.arange(L0, L0 + T)
+            pos = torch.arange(L0, L0 + T, device=x.device)
             cos, sin = rope_cos_sin(pos, d, theta, x.dtype)
             qr = q[r].view(T, nh, d).transpose(0, 1)
             kr = k[r].view(T, nkv, d).transpose(0, 1)
@@ -89,7 +89,7 @@ def forward_rows(sd, cfg, x, kvs, commit=True):
             kk = kc.repeat_interleave(rep, dim=0)
             vv = vc.repeat_interleave(rep, dim=0)
             s = torch.matmul(qr, kk.transpose(1, 2)) * d ** -0.5
-            mask = torch.full((T, kc.shape[1]), float("-inf"))
+            mask = torch.full((T, kc.shape[1]), float("-inf"), device=x.device)
             mask = torch.triu(mask, diagonal=L0 + 1)
             pw = F.softmax(s.float() + mask, dim=-1).to(x.dtype)
             outs.append(torch.matmul(pw, vv).transpose(0, 1).reshape(T, nh * d))
@@ -129,7 +129,7 @@ def forward_rows_masked(sd, cfg, x, kvs, masks):
         outs = []
         for r in range(R):
             m = masks[r]
-            pos = torch.tensor([int(m.long().sum()) - 1])
+            pos = torch.tensor([int(m.long().sum()) - 1], device=x.device)
             cos, sin = rope_cos_sin(pos, d, theta, x.dtype)
             qr = q[r].view(1, nh, d).transpose(0, 1)
             kr = k[r].view(1, nkv, d).transpose(0, 1)
@@ -143,8 +143,8 @@ def forward_rows_masked(sd, cfg, x, kvs, masks):
             kk = kc.repeat_interleave(rep, dim=0)
             vv = vc.repeat_interleave(rep, dim=0)
             s = torch.matmul(qr, kk.transpose(1, 2)) * d ** -0.5
-            bias = torch.zeros(kc.shape[1])
-            bias[~m] = float("-inf")
+            bias = torch.zeros(kc.shape[1], device=x.device)
+            bias[~m.to(x.device)] = float("-inf")
             pw = F.softmax(s.float() + bias, dim=-1).to(x.dtype)
             outs.append(torch.matmul(pw, vv).transpose(0, 1).reshape(1, nh * d))
         o = F.linear(torch.stack(outs), sd[p + "self_attn.o_proj.weight"])

@@ -54,7 +54,9 @@ def reference(q, K, V, slots, pos):
                                          (28, 4, [300, 5000]), (12, 2, [65536 // 8]),
                                          (12, 2, [1, 63, 65, 200, 512]),      # <= 8 splits: in-kernel merge
                                          (12, 2, [20000, 5]),                 # 128-key splits, 4 waves
-                                         (12, 2, [40000, 700])])              # 192-key splits, 8 waves
+                                         (12, 2, [40000, 700]),               # 192-key splits, 8 waves
+                                         (12, 2, [65000, 3]),                 # configs[4]: 64K context
+                                         (28, 4, [32768, 17])])               # Large at its 32K limit
 def test_attention_vs_torch(nh, nkv, lens):
     eng = tiny_engine()
     g = torch.Generator(device=dev).manual_seed(sum(lens) + nh)

@@ -1,0 +1,207 @@
+"""VibeVoice-Large shapes, tensor parallelism at real shapes, and the 64K
+context (BASELINE.json configs[3] and configs[4]) on the MI355X.
+
+* Large Qwen2 layers (qwen2.5_7b_32k.json: H 3584, I 18944, 28 q / 4 kv heads,
+  vocab 152,064) vs oracle/lm.py: ragged prefill + decode steps, and the
+  restricted lm_head (the 4 legal rows of the Large vocabulary).
+* The Large diffusion head (H 3584, FFN 10,752, 4 layers), S = 10, CFG 1.3,
+  vs oracle/head.py, for 1 and 4 diffusing rows (configs[3]: 4 speakers).
+* TP = 4 (and 2) of the Large layers — the Megatron split of
+  configuration_vibevoice.py:175-183, driven by vv_lm_forward_group (the
+  ranks' shards interleaved layer by layer on one GPU, on-device sum as the
+  all-reduce) — vs the TP = 1 engine.
+* configs[4]: a 65,000-token 1.5B-shape prefill followed by decode steps vs
+  oracle/lm.py run as the checker on the GPU (chunked causal prefill), and
+  TP = 2 at a 33,000-token context vs the TP = 1 engine.
+Tolerance: rel L2 < 2e-2 and cosine > 0.999 (bf16), as test_gpu_lm.py.
+"""
+import pytest
+import torch
+
+from gpu_util import cos, rel_err
+from oracle import head as ohead
+from oracle import lm as olm
+from tiny import tiny_config
+from vibevoice_amd.config import VibeVoiceConfig
+from vibevoice_amd.engine import Engine
+from vibevoice_amd.weights import synthetic_state_dict
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+I32 = dict(dtype=torch.int32, device=dev)
+VALID = [151643, 151652, 151653, 151654]
+LARGE = dict(hidden=3584, heads=28, kv_heads=4, inter=18944, vocab=152064)
+
+
+def large_cfg(layers=2):
+    return tiny_config(layers=layers, **LARGE)
+
+
+def oracle_sd(sd, device="cpu"):
+    p = "model.language_model."
+    return {k[len(p):]: v.to(device) for k, v in sd.items() if k.startswith(p)}
+
+
+def _rows(g, lens, H):
+    x = [torch.randn(n, H, generator=g).bfloat16() for n in lens]
+    slots = torch.cat([torch.full((n,), r) for r, n in enumerate(lens)]).to(**I32)
+    pos = torch.cat([torch.arange(n) for n in lens]).to(**I32)
+    out_idx = torch.tensor([sum(lens[:r + 1]) - 1 for r in range(len(lens))]).to(**I32)
+    return x, slots, pos, out_idx
+
+
+@pytest.mark.parametrize("ctx", [40, 700])
+def test_large_lm_layers_vs_oracle(ctx):
+    cfg = large_cfg()
+    sd = synthetic_state_dict(cfg, seed=21, device="cpu", mode="test", with_acoustic_encoder=False)
+    assert sd["lm_head.weight"].shape == (152064, 3584)
+    eng = Engine(cfg, sd, dev, max_batch=2, max_ctx=1024, valid_ids=VALID)
+    osd, lcfg = oracle_sd(sd), dict(cfg.decoder_config)
+    g = torch.Generator().manual_seed(ctx)
+    lens = [ctx, ctx // 3 + 1]
+    xs, slots, pos, out_idx = _rows(g, lens, 3584)
+    kvs = [olm.RowKV(2) for _ in lens]
+    ref = torch.stack([olm.forward_rows(osd, lcfg, xs[r][None], kvs[r:r + 1])[0, -1] for r in range(2)])
+    h, logits = eng.lm_forward(torch.cat(xs).to(dev), slots, pos, out_idx)
+    torch.cuda.synchronize()
+    print(f"Large prefill ctx {ctx}: rel {rel_err(h, ref):.3e} cos {cos(h, ref):.6f}")
+    assert rel_err(h, ref) < 2e-2 and cos(h, ref) > 0.999
+    # the final head: bf16(h . W[id]) over the 4 legal rows of the Large lm_head
+    lref = (h.float().cpu() @ sd["lm_head.weight"][VALID].float().t()).bfloat16().float()
+    assert torch.allclose(logits.cpu(), lref, rtol=1e-2, atol=1e-2 * lref.abs().max().item())
+    L = torch.tensor(lens)
+    for s in range(3):
+        step_x = torch.randn(2, 3584, generator=g).bfloat16()
+        ref = olm.forward_rows(osd, lcfg, step_x[:, None], kvs)[:, -1]
+        h, _ = eng.lm_forward(step_x.to(dev), torch.arange(2).to(**I32), L.to(**I32), torch.arange(2).to(**I32))
+        L += 1
+        torch.cuda.synchronize()
+        print(f"Large step {s}: rel {rel_err(h, ref):.3e} cos {cos(h, ref):.6f}")
+        assert rel_err(h, ref) < 2e-2 and cos(h, ref) > 0.999
+
+
+@pytest.mark.parametrize("n", [1, 4])
+def test_large_head_vs_oracle(n):
+    """modular_vibevoice_diffusion_head.py:254-280 + the CFG DPM-Solver++ loop
+    (modeling_vibevoice_inference.py:712-725) at H = 3584."""
+    cfg = VibeVoiceConfig.builtin("Large")
+    hc = cfg.diffusion_head_config
+    lm_cfg = tiny_config(layers=1, **LARGE)
+    sd = synthetic_state_dict(lm_cfg, seed=22, device="cpu", mode="test", with_acoustic_encoder=False)
+    hsd = {k[len("model.prediction_head."):]: v for k, v in sd.items() if k.startswith("model.prediction_head.")}
+    assert hsd["layers.0.ffn.gate_proj.weight"].shape == (int(3584 * hc.head_ffn_ratio), 3584)
+    eng = Engine(lm_cfg, sd, dev, max_batch=4, max_ctx=64)
+    S = 10
+    eng.set_steps(S)
+    g = torch.Generator().manual_seed(n)
+    pos = torch.randn(n, 3584, generator=g).bfloat16()
+    neg = torch.randn(n, 3584, generator=g).bfloat16()
+    noise = torch.randn(2 * n, 64, generator=g).bfloat16()
+    x = noise[:n].to(dev).contiguous()
+    eng.diffusion_sample(pos.to(dev), neg.to(dev), x, 1.3)
+    torch.cuda.synchronize()
+    ref = ohead.sample_speech_tokens(hsd, pos, neg, noise, S, 1.3, hc.head_layers)
+    ref32 = ohead.sample_speech_tokens({k: v.float() for k, v in hsd.items()}, pos.float(), neg.float(),
+                                       noise.float(), S, 1.3, hc.head_layers)
+    e, c, sdev = rel_err(x, ref), cos(x, ref), rel_err(ref32, ref)
+    print(f"Large head n={n}: rel {e:.3e} cos {c:.6f} (bf16 reference vs fp32 {sdev:.3e})")
+    assert e < max(2e-2, 2 * sdev) and c > 0.999
+
+
+@pytest.mark.parametrize("tp", [2, 4])
+def test_large_tp_group_matches_single_engine(tp):
+    """configs[3]: the Large backbone split over `tp` ranks (whole KV heads per
+    rank: 4 kv heads -> TP <= 4)."""
+    cfg = large_cfg()
+    sd = synthetic_state_dict(cfg, seed=23, device="cpu", mode="test", with_acoustic_encoder=False)
+    full = Engine(cfg, sd, dev, max_batch=2, max_ctx=512, valid_ids=VALID)
+    group = [Engine(cfg, sd, dev, max_batch=2, max_ctx=512, valid_ids=VALID, tp_rank=r, tp_size=tp)
+             for r in range(tp)]
+    g = torch.Generator().manual_seed(tp)
+    lens = [60, 23]
+    xs, slots, pos, out_idx = _rows(g, lens, 3584)
+    x = torch.cat(xs).to(dev)
+    h1, l1 = full.lm_forward(x, slots, pos, out_idx)
+    hg, lg = group[0].lm_forward_group(group[1:], x, slots, pos, out_idx)
+    torch.cuda.synchronize()
+    print(f"Large TP={tp} prefill: rel {rel_err(hg, h1):.3e} cos {cos(hg, h1):.6f}")
+    assert rel_err(hg, h1) < 2e-2 and cos(hg, h1) > 0.999
+    assert torch.allclose(lg, l1, rtol=2e-2, atol=2e-2 * l1.abs().max().item())
+    L = torch.tensor(lens)
+    rows = torch.arange(2).to(**I32)
+    for s in range(3):
+        step = torch.randn(2, 3584, generator=g).bfloat16().to(dev)
+        h1, _ = full.lm_forward(step, rows, L.to(**I32), rows)
+        hg, _ = group[0].lm_forward_group(group[1:], step, rows, L.to(**I32), rows)
+        L += 1
+        torch.cuda.synchronize()
+        print(f"Large TP={tp} step {s}: rel {rel_err(hg, h1):.3e} cos {cos(hg, h1):.6f}")
+        assert rel_err(hg, h1) < 2e-2 and cos(hg, h1) > 0.999
+
+
+def _oracle_prefill_gpu(osd, lcfg, x, kv, chunk=4096):
+    """oracle/lm.py on the GPU, causal prefill in chunks of `chunk` rows (the
+    [rows x keys] fp32 scores of one chunk fit; the whole 65K x 65K would not)."""
+    h = None
+    for i in range(0, x.shape[0], chunk):
+        h = olm.forward_rows(osd, lcfg, x[None, i:i + chunk], [kv])
+    return h[0, -1]
+
+
+def test_64k_context_prefill_and_decode_vs_oracle():
+    """configs[4]: a 65,000-position context (the 1.5B LM allows 65,536) built
+    by a real prefill (k_attn_pf + k_gemm_big), then 3 decode steps attending
+    all of it (k_attn splits + merge), 1.5B layer shapes, 2 layers."""
+    cfg = tiny_config(hidden=1536, layers=2, heads=12, kv_heads=2, inter=8960)
+    cfg.decoder_config["max_position_embeddings"] = 65536
+    sd = synthetic_state_dict(cfg, seed=24, device="cpu", mode="test", with_acoustic_encoder=False)
+    N = 65000
+    eng = Engine(cfg, sd, dev, max_batch=1, max_ctx=N + 8, valid_ids=VALID)
+    osd, lcfg = oracle_sd(sd, dev), dict(cfg.decoder_config)
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(N, 1536, device=dev, generator=g).bfloat16()
+    zero = torch.zeros(N, **I32)
+    h, _ = eng.lm_forward(x, zero, torch.arange(N).to(**I32), torch.tensor([N - 1]).to(**I32))
+    kv = olm.RowKV(2)
+    with torch.no_grad():
+        ref = _oracle_prefill_gpu(osd, lcfg, x, kv)
+    torch.cuda.synchronize()
+    print(f"64K prefill: rel {rel_err(h, ref):.3e} cos {cos(h, ref):.6f}")
+    assert rel_err(h, ref) < 2e-2 and cos(h, ref) > 0.999
+    for s in range(3):
+        step = torch.randn(1, 1536, device=dev, generator=g).bfloat16()
+        h, _ = eng.lm_forward(step, torch.zeros(1, **I32), torch.tensor([N + s]).to(**I32),
+                              torch.zeros(1, **I32))
+        with torch.no_grad():
+            ref = olm.forward_rows(osd, lcfg, step[None], [kv])[0, -1]
+        torch.cuda.synchronize()
+        print(f"64K decode step {s} (attends {N + s + 1} keys): rel {rel_err(h, ref):.3e} cos {cos(h, ref):.6f}")
+        assert rel_err(h, ref) < 2e-2 and cos(h, ref) > 0.999
+
+
+def test_tp2_long_context_matches_single_engine():
+    """configs[4] under TP = 2 (1.5B: 2 kv heads -> one per rank): a
+    33,000-token prefill and decode steps, group vs the TP = 1 engine."""
+    cfg = tiny_config(hidden=1536, layers=2, heads=12, kv_heads=2, inter=8960)
+    cfg.decoder_config["max_position_embeddings"] = 65536
+    sd = synthetic_state_dict(cfg, seed=25, device="cpu", mode="test", with_acoustic_encoder=False)
+    N = 33000
+    full = Engine(cfg, sd, dev, max_batch=1, max_ctx=N + 8, valid_ids=VALID)
+    group = [Engine(cfg, sd, dev, max_batch=1, max_ctx=N + 8, valid_ids=VALID, tp_rank=r, tp_size=2)
+             for r in range(2)]
+    g = torch.Generator(device=dev).manual_seed(6)
+    x = torch.randn(N, 1536, device=dev, generator=g).bfloat16()
+    args = (x, torch.zeros(N, **I32), torch.arange(N).to(**I32), torch.tensor([N - 1]).to(**I32))
+    h1, l1 = full.lm_forward(*args)
+    hg, lg = group[0].lm_forward_group(group[1:], *args)
+    torch.cuda.synchronize()
+    print(f"TP=2 33K prefill: rel {rel_err(hg, h1):.3e} cos {cos(hg, h1):.6f}")
+    assert rel_err(hg, h1) < 2e-2 and cos(hg, h1) > 0.999
+    for s in range(3):
+        step = torch.randn(1, 1536, device=dev, generator=g).bfloat16()
+        a = (step, torch.zeros(1, **I32), torch.tensor([N + s]).to(**I32), torch.zeros(1, **I32))
+        h1, _ = full.lm_forward(*a)
+        hg, _ = group[0].lm_forward_group(group[1:], *a)
+        torch.cuda.synchronize()
+        print(f"TP=2 33K step {s}: rel {rel_err(hg, h1):.3e} cos {cos(hg, h1):.6f}")
+        assert rel_err(hg, h1) < 2e-2 and cos(hg, h1) > 0.999
