@@ -17,6 +17,9 @@
  *   vv_codec_step        <- acoustic_tokenizer.decode :651-658, semantic_tokenizer
  *                           .encode :673-679, acoustic/semantic connectors :682-687
  *   vv_codec_reset       <- acoustic_cache/semantic_cache.set_to_zero :557-560
+ *   vv_codec_decode /    <- acoustic_tokenizer.decode / semantic_tokenizer.encode with a
+ *   vv_codec_encode /       VibeVoiceTokenizerStreamingCache (modular_vibevoice_tokenizer.py
+ *   vv_codec_reset_net      :1081-1108, :193-256), the standalone codec API
  *   vv_acoustic_encode   <- _process_speech_inputs encode :150-164 (voice prompt)
  *   vv_connector         <- SpeechConnector.forward (modeling_vibevoice.py:58-69)
  *
@@ -133,6 +136,19 @@ int vv_diffusion_sample(vv_ctx* ctx, int n, const void* pos_h, const void* neg_h
 int vv_codec_step(vv_ctx* ctx, int n, const int* slots, const void* latent, void* audio_out, void* sem_out,
                   void* embeds_out, const int* embed_rows, vv_stream st);
 int vv_codec_reset(vv_ctx* ctx, int n, const int* slots, vv_stream st);
+
+/* The standalone tokenizer API, one frame per call on codec slots slots[n]
+ * (replaces acoustic_tokenizer.decode(latents, cache, sample_indices,
+ * use_cache=True) and semantic_tokenizer.encode(audio, cache, ...),
+ * modular_vibevoice_tokenizer.py:1081-1108, with VibeVoiceTokenizerStreamingCache
+ * :193-256 as the per-slot state):
+ *   vv_codec_decode: z [n, latent] (the decoder input, already scaled) -> audio_out [n, hop]
+ *   vv_codec_encode: audio [n, hop] -> sem_out [n, semantic_dim]
+ *   vv_codec_reset_net: set_to_zero of one net's state (0 = acoustic decoder,
+ *                       1 = semantic encoder). */
+int vv_codec_decode(vv_ctx* ctx, int n, const int* slots, const void* z, void* audio_out, vv_stream st);
+int vv_codec_encode(vv_ctx* ctx, int n, const int* slots, const void* audio, void* sem_out, vv_stream st);
+int vv_codec_reset_net(vv_ctx* ctx, int net, int n, const int* slots, vv_stream st);
 
 /* Non-streaming acoustic encoder over nv voice prompts of L samples (zero
  * padded): audio [nv, L] bf16 -> mean_out [nv, ceil(L/hop), latent] bf16. */

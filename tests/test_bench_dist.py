@@ -96,6 +96,7 @@ class _FakeEngine:
     def __init__(self, cfg, sd, device, max_batch, max_ctx, tp_rank=0, tp_size=1, tp_unique_id=None):
         self.args = dict(tp_rank=tp_rank, tp_size=tp_size, uid=tp_unique_id)
         self.schedule = None
+        self.max_batch = max_batch
 
     @staticmethod
     def tp_unique_id():

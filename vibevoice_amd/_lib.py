@@ -48,6 +48,9 @@ EXPORTS = [
     ("vv_diffusion_sample", I, [P, I, P, P, P, F, P, P]),
     ("vv_codec_step", I, [P, I, P, P, P, P, P, P, P]),
     ("vv_codec_reset", I, [P, I, P, P]),
+    ("vv_codec_decode", I, [P, I, P, P, P, P]),
+    ("vv_codec_encode", I, [P, I, P, P, P, P]),
+    ("vv_codec_reset_net", I, [P, I, I, P, P]),
     ("vv_acoustic_encode", I, [P, I, I, P, P, P]),
     ("vv_vae_features", I, [P, I, I, P, P, P, P, P]),
     ("vv_connector", I, [P, I, I, P, P, P]),

@@ -337,6 +337,19 @@ int launch_cfg_dpm(int n, int D, DpmCoef k, const bf16* eps, bf16* x, bf16* m1, 
   hipLaunchKernelGGL(k_cfg_dpm, dim3(nblk(n * D, 256)), dim3(256), 0, st, n, D, k, eps, x, m1, noise);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
+// element-wise row copy src row i -> dst row i, for destinations with no
+// 16-byte alignment (an audio chunk into a conv buffer after its 6-row history)
+__global__ void k_copy_rows1(int n, int C, const bf16* src, long long lds, RowMap dst) {
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long long)n * C) return;
+  const int i = (int)(gid / C), c = (int)(gid - (long long)i * C);
+  rm_bfw(dst, i)[c] = src[(long long)i * lds + c];
+}
+int launch_copy_rows1(int n, int C, const bf16* src, long long lds, RowMap dst, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_copy_rows1, dim3(nblk((long long)n * C, 256)), dim3(256), 0, st, n, C, src, lds, dst);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
 int launch_gather_rows(int n, int C, const bf16* src, long long lds, const int* idx, RowMap dst, hipStream_t st) {
   if (n <= 0) return 0;
   if (C % 8) return 1;

@@ -145,6 +145,7 @@ struct vv_ctx {
   ConvNet dec, sem, aenc;
   DevBuf codec_ws;  // connectors
   DevBuf slot_scratch;
+  DevBuf unit_sb;   // bf16 {1, 0}: identity scaling / bias for vv_codec_decode
   // tensor parallelism of the LM (Megatron split, configuration_vibevoice.py:175-183):
   // this engine holds rank tp_rank's shard; the residual stream is all-reduced
   // after o_proj and down_proj
@@ -598,7 +599,7 @@ void vv_destroy(vv_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
   DevBuf* bufs[] = {&c->norm_ws, &c->kv_k, &c->kv_v, &c->lm_ws, &c->attn_part, &c->attn_cnt, &c->valid_ids, &c->splitk_ws, &c->splitk_cnt,
-                    &c->temb, &c->tfreq_tmp, &c->head_ws, &c->codec_ws, &c->slot_scratch};
+                    &c->temb, &c->tfreq_tmp, &c->head_ws, &c->codec_ws, &c->slot_scratch, &c->unit_sb};
   for (DevBuf* b : bufs) b->release();
   ConvNet* nets[] = {&c->dec, &c->sem, &c->aenc};
   for (ConvNet* n : nets) {
@@ -722,6 +723,11 @@ int vv_finalize(vv_ctx* c) {
   }
   CHK(c->codec_ws.ensure((size_t)k.max_batch * (4 * H + 2 * 256) * sizeof(bf16) + 4096));
   CHK(c->slot_scratch.ensure(4096));
+  {
+    const uint16_t one_zero[2] = {0x3F80, 0x0000};
+    CHK(c->unit_sb.ensure(sizeof(one_zero)));
+    HIPCHK(hipMemcpy(c->unit_sb.p, one_zero, sizeof(one_zero), hipMemcpyHostToDevice));
+  }
   HIPCHK(hipDeviceSynchronize());
   c->finalized = true;
   return 0;
@@ -1129,6 +1135,52 @@ int vv_codec_reset(vv_ctx* c, int n, const int* slots, vv_stream vst) {
   if (n <= 0) return 0;
   CHK(convnet_roll(c->dec, n, slots, 1, st));
   CHK(convnet_roll(c->sem, n, slots, 1, st));
+  return 0;
+}
+
+// The two halves of vv_codec_step as separate calls: the reference's standalone
+// tokenizer API (acoustic_tokenizer.decode / semantic_tokenizer.encode with a
+// VibeVoiceTokenizerStreamingCache, modular_vibevoice_tokenizer.py:1081-1108,
+// 193-256), one frame per call.  Slot state is the same per-slot ConvBuf
+// history vv_codec_step keeps.
+int vv_codec_decode(vv_ctx* c, int n, const int* slots, const void* z, void* audio_out, vv_stream vst) {
+  hipStream_t st = (hipStream_t)vst;
+  if (!c->finalized) FAIL("vv_codec_decode before vv_finalize");
+  if (n <= 0) return 0;
+  if (n > c->cfg.max_batch) FAIL("vv_codec_decode: n > max_batch");
+  ConvNet& dn = c->dec;
+  const int hop = dn.T[dn.nst - 1];
+  // z is already the decoder input (latent / scaling - bias, done by the caller):
+  // identity scale / bias keep the copy bit-exact
+  const bf16* one = (const bf16*)c->unit_sb.p;
+  KCHK(launch_latent_to_dec(n, c->cfg.latent_dim, (const bf16*)z, one, one + 1, buf_in_rows(dn.stem, 1, slots), st));
+  CHK(convnet_run(c, dn, n, slots, rowmap(audio_out, 1, hop, hop), RowMap{}, st));
+  CHK(convnet_roll(dn, n, slots, 0, st));
+  return 0;
+}
+
+int vv_codec_encode(vv_ctx* c, int n, const int* slots, const void* audio, void* sem_out, vv_stream vst) {
+  hipStream_t st = (hipStream_t)vst;
+  if (!c->finalized) FAIL("vv_codec_encode before vv_finalize");
+  if (n <= 0) return 0;
+  if (n > c->cfg.max_batch) FAIL("vv_codec_encode: n > max_batch");
+  ConvNet& sn = c->sem;
+  const int hop = c->dec.T[c->dec.nst - 1];
+  // audio rows [n, hop] -> the encoder stem's input rows of each slot (one row of
+  // hop channels-last samples per slot)
+  RowMap in = rowmap(sn.stem.base + (long long)sn.stem.ctx * sn.stem.C, hop, 1, sn.stem.sB, slots);
+  KCHK(launch_copy_rows1(n, hop, (const bf16*)audio, hop, in, st));
+  const int S = c->cfg.semantic_dim;
+  CHK(convnet_run(c, sn, n, slots, rowmap(sem_out, S, 1, S), RowMap{}, st));
+  CHK(convnet_roll(sn, n, slots, 0, st));
+  return 0;
+}
+
+int vv_codec_reset_net(vv_ctx* c, int net, int n, const int* slots, vv_stream vst) {
+  hipStream_t st = (hipStream_t)vst;
+  if (n <= 0) return 0;
+  if (net != 0 && net != 1) FAIL("vv_codec_reset_net: net must be 0 (acoustic decoder) or 1 (semantic encoder)");
+  CHK(convnet_roll(net == 0 ? c->dec : c->sem, n, slots, 1, st));
   return 0;
 }
 

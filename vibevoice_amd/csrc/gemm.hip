@@ -1103,9 +1103,11 @@ extern "C" int vv_gemv_tune_tpw(int tpw) {
 struct GemmPlan { int nw, ksplit, u, tpw; };
 
 // Measured on MI355X (tools/gemv_sweep.py two-pass min, profiles/r01_gemv_sweep*.txt).
-// NO cross-workgroup split-K (a hand-off costs >= 2 us in the sc1 form, up to
-// 30 us with fences — more than the extra CUs bring).  Waves per workgroup (nw)
-// and weight chunks in flight per wave (u):
+// Cross-workgroup split-K only for few-tile, long-row shapes (the M >= 8 down
+// projections and codec fc2, and the M < 8 LM down projection, listed below):
+// a hand-off costs >= 2 us in the sc1 form and up to 30 us with fences, which
+// only those shapes win back in extra CUs.  Waves per workgroup (nw) and weight
+// chunks in flight per wave (u):
 //   * >= 1024 tiles (LM gate|up, head adaLN): 2 waves — every workgroup resident
 //     in the first round (4-wave groups left a second-round tail: 16.7 -> 14.0 us)
 //   * few tiles, long rows (LM / head down): 8 waves x 4; 128 tiles x K >= 8192

@@ -190,6 +190,7 @@ int launch_head_cond(int steps, int R, int H, const bf16* condp, const bf16* tem
 int launch_silu(int n, const bf16* x, bf16* y, hipStream_t st);
 int launch_cfg_dpm(int n, int D, DpmCoef k, const bf16* eps, bf16* x, bf16* m1, const float* noise, hipStream_t st);
 int launch_gather_rows(int n, int C, const bf16* src, long long lds, const int* idx, RowMap dst, hipStream_t st);
+int launch_copy_rows1(int n, int C, const bf16* src, long long lds, RowMap dst, hipStream_t st);
 int attn_plan(int nq, int nkv, int max_len, int* chunk);
 // true: nq query rows over at most nslots distinct slots take the prefill
 // kernel (k_attn_pf: 32-row tiles share K/V; no split workspace)

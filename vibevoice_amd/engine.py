@@ -63,10 +63,13 @@ class Engine:
     """One device-resident VibeVoice model instance."""
 
     def __init__(self, cfg: VibeVoiceConfig, state_dict, device="cuda", max_batch=1, max_ctx=4096,
-                 valid_ids=None, tp_rank=0, tp_size=1, tp_unique_id=None):
+                 valid_ids=None, tp_rank=0, tp_size=1, tp_unique_id=None, packed=None):
         """tp_size > 1: rank tp_rank's shard of the LM; tp_unique_id (bytes of
         vv_tp_unique_id, shared by the group) creates its RCCL communicator, None
-        leaves it for a single-process group (lm_forward_group)."""
+        leaves it for a single-process group (lm_forward_group).
+        packed: another engine's packed weights (`Engine.w`) to bind instead of
+        packing `state_dict` again — a second context over the same device
+        weights (the standalone tokenizer API's own codec slots)."""
         L = _lib.lib()
         self.cfg = cfg
         self.device = torch.device(device)
@@ -79,7 +82,8 @@ class Engine:
         self.hop = cfg.hop
         self.tp_rank, self.tp_size = tp_rank, tp_size
         with torch.cuda.device(self.device):
-            self.w = pack(state_dict, cfg, self.device, tp_rank=tp_rank, tp_size=tp_size)
+            self.w = packed if packed is not None else pack(state_dict, cfg, self.device, tp_rank=tp_rank,
+                                                            tp_size=tp_size)
             h = ctypes.c_void_p()
             self._ecfg = engine_config(cfg, max_batch, max_ctx, tp_size)
             _lib.check(L.vv_create(ctypes.byref(self._ecfg), self.device.index or 0, ctypes.byref(h)), "create")
@@ -209,6 +213,21 @@ class Engine:
 
     def codec_reset(self, slots, stream=None):
         _lib.check(_lib.lib().vv_codec_reset(self.h, slots.shape[0], _ptr(slots), _stream(stream)), "codec_reset")
+
+    def codec_decode(self, slots, z, audio_out, stream=None):
+        """One streaming acoustic-decoder frame: z [n, latent] (decoder input) -> audio_out [n, hop]."""
+        _lib.check(_lib.lib().vv_codec_decode(self.h, slots.shape[0], _ptr(slots), _ptr(z), _ptr(audio_out),
+                                              _stream(stream)), "codec_decode")
+
+    def codec_encode(self, slots, audio, sem_out, stream=None):
+        """One streaming semantic-encoder frame: audio [n, hop] -> sem_out [n, semantic_dim]."""
+        _lib.check(_lib.lib().vv_codec_encode(self.h, slots.shape[0], _ptr(slots), _ptr(audio), _ptr(sem_out),
+                                              _stream(stream)), "codec_encode")
+
+    def codec_reset_net(self, net, slots, stream=None):
+        """set_to_zero of one net's streaming state: net 0 = acoustic decoder, 1 = semantic encoder."""
+        _lib.check(_lib.lib().vv_codec_reset_net(self.h, int(net), slots.shape[0], _ptr(slots), _stream(stream)),
+                   "codec_reset_net")
 
     # ---------------------------------------------------------------- prefill helpers
     def acoustic_encode(self, audio_bf16, stream=None):

@@ -47,12 +47,29 @@ class _LMConfigView:
 
 
 class _ModelView:
-    """`model.model.*` attributes callers touch (inference_from_file.py:315-316)."""
+    """`model.model.*` attributes callers touch: the language model's config
+    (inference_from_file.py:315-316), the noise scheduler (gradio_demo.py:114-118),
+    the tokenizers / connectors / speech scaling of VibeVoiceModel
+    (modeling_vibevoice.py:97-145) as views over the engine (tokenizer.py)."""
 
     def __init__(self, owner):
+        from . import tokenizer as tk
         self._o = owner
         self.language_model = type("LM", (), {})()
         self.language_model.config = _LMConfigView(dict(owner.config.decoder_config), owner.attn_implementation)
+        pool = tk._SlotPool(owner, max(8, owner.engine.max_batch))
+        self.acoustic_tokenizer = tk.AcousticTokenizer(owner, pool, owner.config.acoustic_tokenizer_config)
+        self.semantic_tokenizer = tk.SemanticTokenizer(owner, pool, owner.config.semantic_tokenizer_config)
+        self.acoustic_connector = tk.Connector(owner, 0)
+        self.semantic_connector = tk.Connector(owner, 1)
+
+    @property
+    def speech_scaling_factor(self):
+        return self._o.engine.w["speech_scaling_factor"]
+
+    @property
+    def speech_bias_factor(self):
+        return self._o.engine.w["speech_bias_factor"]
 
     @property
     def noise_scheduler(self):
@@ -251,6 +268,14 @@ class VibeVoiceForConditionalGenerationInference:
 
     def eval(self):
         return self
+
+    # modeling_vibevoice_inference.py:97-115
+    acoustic_tokenizer = property(lambda self: self.model.acoustic_tokenizer)
+    semantic_tokenizer = property(lambda self: self.model.semantic_tokenizer)
+    acoustic_connector = property(lambda self: self.model.acoustic_connector)
+    semantic_connector = property(lambda self: self.model.semantic_connector)
+    speech_scaling_factor = property(lambda self: self.model.speech_scaling_factor)
+    speech_bias_factor = property(lambda self: self.model.speech_bias_factor)
 
     def to(self, *args, **kwargs):
         """Moving the engine is not possible: accept only the device it lives on
