@@ -224,6 +224,23 @@ int vv_attn_tune(int chunk, int merge_in);
  * per slot of the engine -> the 32-row-tile prefill kernel), 0 = always the
  * per-row decode kernel, 1 = always the prefill kernel. */
 int vv_attn_prefill(int mode);
+/* Switch (benchmarks / tests): persistent GEMV chains (chain.hip) -- the
+ * diffusion head's S steps run as ONE launch of one workgroup per CU instead of
+ * S x (2 + 2L) GEMV launches.  0 (default, -1) = per-op launches; 1 = chains
+ * with the balanced work split; 2 = chains with the per-op launch plan mirrored
+ * (bit-identical to 0, the hand-off test).  Measured slower than 0 on MI355X
+ * (DESIGN.md "Persistent chains"), so off by default. */
+int vv_chain_tune(int mode);
+/* Tuning hook (benchmarks only): weight chunks per wave per load batch of the
+ * chain kernel (4 or 8 = built-in). */
+int vv_chain_tune_u(int u);
+/* Diagnostic: nonzero (1 + op index) if a chain launch's dependency wait gave
+ * up (a producer never signalled within ~200 ms); reading resets it. */
+int vv_chain_error(vv_ctx* c);
+/* Diagnostic (benchmarks only): chain launches write s_memrealtime stamps per
+ * (workgroup, op): wait begun, inputs ready, op signalled (uint64[G][nops][4]);
+ * NULL: off. */
+int vv_chain_stamps(void* buf);
 /* Test switch (bit mask, default 3): bit 0 folds each codec Block1D's mixer
  * (norm, depthwise conv, gamma residual, FFN norm) into its fc1 GEMV where
  * <= 16 rows fit (XF_MIX); bit 1 runs whole narrow-stage blocks (C <= 128) as

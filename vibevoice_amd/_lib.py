@@ -71,6 +71,10 @@ EXPORTS = [
     ("vv_attn_tune", I, [I, I]),
     ("vv_attn_prefill", I, [I]),
     ("vv_codec_mix_fusion", I, [I]),
+    ("vv_chain_tune", I, [I]),
+    ("vv_chain_tune_u", I, [I]),
+    ("vv_chain_error", I, [P]),
+    ("vv_chain_stamps", I, [P]),
 ]
 
 EPI = {"store": 0, "gelu": 1, "silu_mul": 2, "res": 3, "f32": 4}

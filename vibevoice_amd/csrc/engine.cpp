@@ -151,6 +151,15 @@ struct vv_ctx {
   // after o_proj and down_proj
   int tp_rank = 0, tp_size = 1;
   ncclComm_t comm = nullptr;
+  // persistent chains (chain.hip): op tables per diffusing-row count n for the
+  // current schedule; sync words (zeroed per launch), split slabs, error word
+  struct Chain {
+    DevBuf ops;
+    int nops = 0, nsync = 0, mode = -1;
+    size_t lds = 0;
+  };
+  std::unordered_map<int, Chain> head_chain;
+  DevBuf chain_sync, chain_slabs, chain_err, coef_dev;
 };
 
 // ------------------------------------------------------------------ helpers
@@ -599,8 +608,10 @@ void vv_destroy(vv_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
   DevBuf* bufs[] = {&c->norm_ws, &c->kv_k, &c->kv_v, &c->lm_ws, &c->attn_part, &c->attn_cnt, &c->valid_ids, &c->splitk_ws, &c->splitk_cnt,
-                    &c->temb, &c->tfreq_tmp, &c->head_ws, &c->codec_ws, &c->slot_scratch, &c->unit_sb};
+                    &c->temb, &c->tfreq_tmp, &c->head_ws, &c->codec_ws, &c->slot_scratch, &c->unit_sb,
+                    &c->chain_sync, &c->chain_slabs, &c->chain_err, &c->coef_dev};
   for (DevBuf* b : bufs) b->release();
+  for (auto& kv : c->head_chain) kv.second.ops.release();
   ConvNet* nets[] = {&c->dec, &c->sem, &c->aenc};
   for (ConvNet* n : nets) {
     n->state.release();
@@ -761,6 +772,13 @@ int vv_set_schedule(vv_ctx* c, int steps, const float* coef, const void* tfreq, 
   KCHK(launch_silu(steps * H, t1, t1, st));
   CHK(gemm(c, gemm_args(c, steps, H, H, rowmap(t1, H), W(c, "head.t2_w"), EPI_STORE, rowmap(c->temb.p, H)), st));
   c->steps = steps;
+  // the chain's per-step DPM coefficients (cfg is bound per call); tables are per schedule
+  CHK(c->coef_dev.ensure((size_t)1000 * sizeof(DpmCoef)));
+  HIPCHK(hipMemcpyAsync(c->coef_dev.p, c->coef.data(), (size_t)steps * sizeof(DpmCoef), hipMemcpyHostToDevice, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (!c->head_chain.empty()) g_ws_epoch.fetch_add(1);   // captured chain launches point at the old tables
+  for (auto& kv : c->head_chain) kv.second.ops.release();
+  c->head_chain.clear();
   return 0;
 }
 
@@ -984,6 +1002,82 @@ int vv_tp_init(vv_ctx* c, int rank, int size, const void* unique_id) {
   return 0;
 }
 
+// ------------------------------------------------------------------ persistent chains
+// 0 (default): per-op launches; 1: chains with the balanced plan; 2: chains
+// with the per-op launch plan mirrored (bit-identical to 0; tests).  Measured
+// on MI355X (tools/chain_bench.py, DESIGN.md "Persistent chains"): the
+// in-launch hand-off is 0.5-1.2 us, but each op's span keeps its dependent
+// memory round trips (A rows, residual, write-through drain, arrival), so a
+// 100-op head chain takes 1.05 ms against 0.87 ms of per-op launches.
+static int g_chain = 0;
+static unsigned long long* g_chain_stamps = nullptr;
+extern "C" int vv_chain_stamps(void* buf) {
+  g_chain_stamps = (unsigned long long*)buf;
+  return 0;
+}
+extern "C" int vv_chain_tune(int mode) {
+  g_chain = mode < 0 ? 0 : mode;
+  return 0;
+}
+// error word of the last chain launches (1 + the op a wait gave up on), reset on read
+extern "C" int vv_chain_error(vv_ctx* c) {
+  if (!c->chain_err.p) return 0;
+  unsigned v = 0;
+  if (hipMemcpy(&v, c->chain_err.p, 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (v) (void)hipMemset(c->chain_err.p, 0, 4);
+  return (int)v;
+}
+
+// Plan every op of `ops` (chain.hip), lay out slabs and tickets, upload.
+static int chain_upload(vv_ctx* c, std::vector<ChainOp>& ops, vv_ctx::Chain& T) {
+  const int G = chain_grid();
+  if (G <= 0) FAIL("chain: no device");
+  long long slabs = 0;
+  int tickets = 0;
+  size_t lds = 0;
+  for (ChainOp& op : ops) {
+    const size_t l = chain_plan_op(&op, G, g_chain == 2 ? 1 : 0);
+    if (!l) return 1;   // a shape the chain does not take: caller runs per-op launches
+    lds = std::max(lds, l);
+    if (op.nunit > op.nu1) {
+      const int rem = op.g.N / 16 - op.t1;
+      if (rem > CH_TMAX) return 1;
+      op.slab_off = slabs;
+      op.ticket_off = tickets;
+      slabs += (long long)rem * op.ks2 * 256;
+      tickets += rem;
+    }
+  }
+  if (lds > 151552) return 1;
+  const int nops = (int)ops.size();
+  T.nops = nops;
+  T.nsync = nops * 9 * 32 + ((tickets + 3) & ~3);
+  T.lds = lds;
+  T.mode = g_chain;
+  CHK(T.ops.ensure(ops.size() * sizeof(ChainOp)));
+  HIPCHK(hipMemcpy(T.ops.p, ops.data(), ops.size() * sizeof(ChainOp), hipMemcpyHostToDevice));
+  CHK(c->chain_sync.ensure((size_t)T.nsync * 4));
+  CHK(c->chain_slabs.ensure((size_t)std::max(slabs, 256LL) * 4));
+  if (!c->chain_err.p) {
+    CHK(c->chain_err.ensure(16));
+    HIPCHK(hipMemset(c->chain_err.p, 0, 16));
+  }
+  return 0;
+}
+
+static int chain_launch(vv_ctx* c, const vv_ctx::Chain& T, ChainArgs A, hipStream_t st) {
+  A.ops = (const ChainOp*)T.ops.p;
+  A.nops = T.nops;
+  A.done = (unsigned*)c->chain_sync.p;
+  A.tickets = A.done + (size_t)T.nops * 9 * 32;
+  A.stamps = g_chain_stamps;
+  A.slabs = (float*)c->chain_slabs.p;
+  A.err = (unsigned*)c->chain_err.p;
+  HIPCHK(hipMemsetAsync(c->chain_sync.p, 0, (size_t)T.nsync * 4, st));
+  KCHK(launch_chain(A, T.lds, st));
+  return 0;
+}
+
 int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, void* x_io, float cfg_scale,
                         const float* sde_noise, vv_stream vst) {
   hipStream_t st = (hipStream_t)vst;
@@ -1021,6 +1115,68 @@ int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, 
   // cond_proj is step-invariant: computed once per token (bit-identical to per step)
   CHK(gemm(c, gemm_args(c, R, H, H, rowmap(cond, H), W(c, "head.cond_w"), EPI_STORE, rowmap(condp, H)), st));
   RowMap xh_m = rowmap(xh, H), a_m = rowmap(a, H);
+  if (g_chain && R <= 16 && c->steps <= HEAD_SC) {
+    // all S steps (noisy, L x [gate|up, down], final + CFG + DPM) in one persistent launch
+    auto it = c->head_chain.find(n);
+    if (it == c->head_chain.end() || it->second.mode != g_chain) {
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      HIPCHK(hipStreamIsCapturing(st, &cs));
+      if (cs == hipStreamCaptureStatusNone) {   // tables are built by an eager call, never inside a capture
+        vv_ctx::Chain& T = c->head_chain[n];
+        T.ops.release();
+        std::vector<ChainOp> ops;
+        for (int s = 0; s < c->steps; ++s) {
+          const bf16* mod = mods + (size_t)(s % HEAD_SC) * R * MODW;
+          auto add = [&](const GemmArgs& g, int bind) {
+            ChainOp op;
+            memset(&op, 0, sizeof(op));
+            op.g = g;
+            op.g.keep = 1;
+            op.bind = bind;
+            op.rep = s;
+            ops.push_back(op);
+          };
+          add(gemm_args(c, R, H, D, rowmap(nullptr, D, n, 0), W(c, "head.noisy_w"), EPI_STORE, xh_m), CH_BIND_AX);
+          for (int l = 0; l < L; ++l) {
+            const std::string p = "head." + std::to_string(l);
+            const int o = 3 * H * l;
+            GemmArgs g = gemm_args(c, R, 2 * F, H, xh_m, W(c, p + ".gu_w"), EPI_SILU_MUL, rowmap(act, F));
+            g.xf = xf_norm(W(c, p + ".norm"), k.head_eps, mod, MODW, o, o + H);
+            add(g, 0);
+            g = gemm_args(c, R, H, F, rowmap(act, F), W(c, p + ".down_w"), EPI_RES, xh_m);
+            g.epi.res = xh_m;
+            g.epi.gate = rowmap(mod + o + 2 * H, MODW);
+            add(g, 0);
+          }
+          GemmArgs g = gemm_args(c, R, D, H, xh_m, W(c, "head.final_w"), EPI_CFG_DPM, rowmap(v, D));
+          g.xf = xf_norm(nullptr, k.head_eps, mod, MODW, 3 * H * L, 3 * H * L + H);
+          g.dpm.n = n;
+          g.dpm.m1 = m1;
+          add(g, CH_BIND_DPM);
+        }
+        const int rc = chain_upload(c, ops, T);
+        if (rc < 0) return rc;
+        if (rc > 0) {   // not chainable: per-op launches below
+          T.nops = 0;
+          T.mode = g_chain;
+        }
+        it = c->head_chain.find(n);
+      }
+    }
+    if (it != c->head_chain.end() && it->second.nops > 0) {
+      KCHK(launch_head_cond(c->steps, R, H, condp, (const bf16*)c->temb.p, sa, st));
+      CHK(gemm(c, gemm_args(c, c->steps * R, (int)MODW, H, rowmap(sa, H), W(c, "head.ada_w"), EPI_STORE,
+                            rowmap(mods, MODW)), st));
+      ChainArgs A;
+      memset(&A, 0, sizeof(A));
+      A.x = (bf16*)x_io;
+      A.noise = sde_noise;
+      A.noise_rep = (long long)R * D;
+      A.coef = (const DpmCoef*)c->coef_dev.p;
+      A.cfg = cfg_scale;
+      return chain_launch(c, it->second, A, st);
+    }
+  }
   for (int s = 0; s < c->steps; ++s) {
     // all adaLN modulations ([shift|scale|gate] x L, [shift|scale] final) of up to
     // HEAD_SC steps in ONE GEMM: the condition is step-invariant and the timesteps

@@ -37,6 +37,7 @@
 #include <cstdlib>
 
 #include "kernels.h"
+#include "gemv_dev.h"
 
 // Diagnostic timestamps (tools/gemv_stamps.py): 100 MHz real-time clock, one
 // lane per workgroup, to a buffer nothing else reads (a.stamps == nullptr in
@@ -46,240 +47,6 @@ DEV void stamp(const GemmArgs& a, int which) {
     const unsigned long long t = __builtin_amdgcn_s_memrealtime();
     a.stamps[((long long)blockIdx.y * gridDim.x + blockIdx.x) * 4 + which] = t;
   }
-}
-
-// Weight-stream load.  Decode weights are read once per step (GBs against a
-// 256 MB Infinity Cache), so they go out non-temporal (MI355X_MICROARCH.md
-// "nt-weights"); VV_W_NT=0 builds the default-policy variant for A/B runs.
-// KEEP (GemmArgs::keep): weights re-read soon — the diffusion head's 170 MB per
-// step is read S times per token and stays in the Infinity Cache with the
-// default policy (tools/head_mall.py: -7 % per head step).
-#ifndef VV_W_NT
-#define VV_W_NT 1
-#endif
-template <bool KEEP = false>
-DEV bf16x8 ldw(const bf16* p) {
-#if VV_W_NT
-  if (!KEEP) return __builtin_nontemporal_load((const bf16x8*)p);
-#endif
-  return *(const bf16x8*)p;
-}
-
-DEV f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
-// ------------------------------------------------------------------ A transform
-// Inverse RMS of rows [m0, m0 + nrows) (local index i -> inv_s[i]); same
-// summation order as k_rmsnorm (lane-strided 8-element chunks, wave sum).
-DEV void row_inv(const GemmArgs& a, int m0, int nrows, float* inv_s, int wave, int NW, int lane) {
-  const int nch = a.K >> 3;
-  for (int i = wave; i < nrows; i += NW) {
-    const int m = m0 + i;
-    float ss = 0.f;
-    if (m < a.M) {
-      const bf16* x = rm_bf(a.a, m);
-      for (int c = lane; c < nch; c += 64) {
-        const bf16x8 v = *(const bf16x8*)(x + c * 8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ss += bf(v[j]) * bf(v[j]);
-      }
-    }
-    ss = wave_sum(ss);
-    if (lane == 0) inv_s[i] = rsqrtf(ss / (float)a.K + a.xf.eps);
-  }
-}
-
-template <int XF>
-DEV bf16x8 xform(const GemmArgs& a, bf16x8 x, int m, int k, float inv) {
-  bf16x8 o;
-  if (XF == XF_NORM) {
-    bf16x8 wv, sh, sc;
-    if (a.xf.w) wv = *(const bf16x8*)(a.xf.w + k);
-    const bf16* md = a.xf.mod ? a.xf.mod + (long long)m * a.xf.mod_ld : nullptr;
-    if (md) {
-      sh = *(const bf16x8*)(md + a.xf.shift_off + k);
-      sc = *(const bf16x8*)(md + a.xf.scale_off + k);
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float t = rb(bf(x[j]) * inv);
-      if (a.xf.w) t = rb(t * bf(wv[j]));
-      if (md) t = rb(rb(t * rb(1.0f + bf(sc[j]))) + bf(sh[j]));
-      o[j] = tobf(t);
-    }
-  } else if (XF == XF_SILU_ADD) {
-    const bf16x8 v = *(const bf16x8*)(a.xf.vec + k);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = tobf(silu_f(rb(bf(x[j]) + bf(v[j]))));
-  } else {
-    o = x;
-  }
-  return o;
-}
-
-// ------------------------------------------------------------------ epilogues
-// One 16(n) x 16(m) MFMA tile in the C/D layout: lane l holds m = m0 + (l & 15),
-// n = n0 + 4*(l >> 4) + i, i = 0..3.  Every lane of the wave must call this
-// (cross-lane exchanges), rows m >= M are dropped inside.
-
-// RoPE epilogue (Qwen2 q/k/v projection + apply_rotary_pos_emb + cache append;
-// transformers modeling_qwen2.py:99-134, 195-247).  Packed q/k rows: tile tt of
-// head h holds dims [8tt, 8tt+8) in rows 0..7 and [64+8tt, 64+8tt+8) in rows
-// 8..15 (weights.py: _rope_pack); v rows are in natural order.
-DEV void epi_rope(const GemmArgs& a, int m, int n0, int lane, float v[4]) {
-  const RopeEpi& R = a.rope;
-  constexpr int d = 128;
-  const int g = lane >> 4;
-  if (a.epi.bias) {
-    const bf16x4 b = *(const bf16x4*)(a.epi.bias + n0 + 4 * g);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] += bf(b[i]);
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = rb(v[i]);  // q/k/v_proj output (bf16)
-  const int h = n0 / d, tt = (n0 % d) >> 4;
-  if (h < R.nh + R.nkv) {
-    float u[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) u[i] = __shfl_xor(v[i], 32);
-    if (g >= 2 || m >= a.M) return;
-    const int j = 8 * tt + 4 * g;
-    const int p = R.pos[m];
-    bf16x4 o1, o2;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float f = (float)p * R.inv_freq[j + i];
-      const float cs = rb(cosf(f)), sn = rb(sinf(f));
-      o1[i] = tobf(rb(v[i] * cs) + rb(-u[i] * sn));
-      o2[i] = tobf(rb(u[i] * cs) + rb(v[i] * sn));
-    }
-    bf16* dst = h < R.nh ? R.q_out + (long long)m * R.nh * d + h * d
-                         : R.kv.k + (long long)R.layer * R.kv.s_layer + (long long)R.slots[m] * R.kv.s_slot +
-                               (long long)(h - R.nh) * R.kv.s_head + (long long)p * d;
-    *(bf16x4*)(dst + j) = o1;
-    *(bf16x4*)(dst + j + 64) = o2;
-  } else {
-    if (m >= a.M) return;
-    // V cache in 32-position blocks of [dim][position] (common.h v_off)
-    const int hv = h - R.nh - R.nkv;
-    bf16* hb = R.kv.v + (long long)R.layer * R.kv.s_layer + (long long)R.slots[m] * R.kv.s_slot +
-               (long long)hv * R.kv.s_head;
-    const int dim0 = (n0 % d) + 4 * g, p = R.pos[m];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) hb[v_off(dim0 + i, p)] = tobf(v[i]);
-  }
-}
-
-// CFG combine + DPM-Solver++ update (sample_speech_tokens,
-// modeling_vibevoice_inference.py:717-724; DPMSolverMultistepScheduler.step,
-// dpm_solver.py:935-1022) on the final linear's rows: rows [0, n) are the
-// conditional and [n, 2n) the unconditional v-predictions, 2n <= 16 so row r and
-// its partner r + n sit in the same 16-lane group.
-DEV void epi_dpm(const GemmArgs& a, int n0, int lane, const float v[4]) {
-  const DpmEpi& P = a.dpm;
-  const int g = lane >> 4, r = lane & 15, n = P.n;
-  float e[4], u[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) e[i] = rb(v[i]);  // final_layer.linear output (bf16, no bias)
-#pragma unroll
-  for (int i = 0; i < 4; ++i) u[i] = __shfl(e[i], (lane + n) & 63);
-  if (r >= n) return;
-  const DpmCoef& k = P.k;
-  const long long off = (long long)r * a.N + n0 + 4 * g;
-  const bf16x4 xv = *(const bf16x4*)(P.x + off);
-  const bf16x4 mv = *(const bf16x4*)(P.m1 + off);
-  bf16x4 xo, mo;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float c = e[i], un = u[i];
-    const float vv = rb(un + rb(k.cfg * rb(c - un)));
-    const float xs = bf(xv[i]);
-    const float x0 = rb(rb(k.alpha_s * xs) - rb(k.sigma_s * vv));
-    float out = k.c_x * xs - rb(k.c_d0 * x0);
-    if (k.order == 2) {
-      const float d1 = rb(k.inv_r0 * rb(x0 - bf(mv[i])));
-      out = out - rb(k.c_d1 * d1);
-    }
-    if (P.noise) out = out + k.c_n * P.noise[off + i];
-    xo[i] = tobf(out);
-    mo[i] = tobf(x0);
-  }
-  *(bf16x4*)(P.x + off) = xo;
-  *(bf16x4*)(P.m1 + off) = mo;
-}
-
-DEV void epi_tile(const GemmArgs& a, int m, int n0, int lane, const float v_in[4]) {
-  const EpiArgs& e = a.epi;
-  float v[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = v_in[i];
-  const int g = lane >> 4;
-  if (e.kind == EPI_ROPE) {
-    epi_rope(a, m, n0, lane, v);
-    return;
-  }
-  if (e.kind == EPI_CFG_DPM) {
-    epi_dpm(a, n0, lane, v);
-    return;
-  }
-  if (e.kind == EPI_SILU_MUL) {
-    // rows 0..7 of the tile are gate, 8..15 the matching up rows; lane g<2 holds
-    // gate rows 4g+i, lane g+2 holds up rows 8+4g+i
-    float u[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) u[i] = __shfl_xor(v[i], 32);
-    if (g >= 2 || m >= a.M) return;
-    const int col = (n0 >> 1) + 4 * g;
-    bf16x4 o;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = tobf(rb(silu_f(rb(v[i]))) * rb(u[i]));
-    *(bf16x4*)(rm_bfw(e.out, m) + col) = o;
-    return;
-  }
-  if (m >= a.M) return;
-  const int n = n0 + 4 * g;
-  if (e.bias) {
-    bf16x4 b = *(const bf16x4*)(e.bias + n);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] += bf(b[i]);
-  }
-  if (e.kind == EPI_F32) {
-    float* o = (float*)e.out.base + rm_off(e.out, m) + n;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = v[i];
-    return;
-  }
-  bf16x4 o;
-  if (e.kind == EPI_STORE) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = tobf(v[i]);
-  } else if (e.kind == EPI_GELU) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = tobf(gelu_f(rb(v[i])));
-  } else {  // EPI_RES
-    bf16x4 r = *(const bf16x4*)(rm_bf(e.res, m) + n);
-    float s[4] = {1.f, 1.f, 1.f, 1.f};
-    bool scaled = false;
-    if (e.gamma) {
-      bf16x4 gm = *(const bf16x4*)(e.gamma + n);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) s[i] = bf(gm[i]);
-      scaled = true;
-    } else if (e.gate.base) {
-      bf16x4 gm = *(const bf16x4*)(rm_bf(e.gate, m) + n);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) s[i] = bf(gm[i]);
-      scaled = true;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float y = rb(v[i]);
-      if (scaled) y = rb(s[i] * y);
-      o[i] = tobf(bf(r[i]) + y);
-    }
-  }
-  *(bf16x4*)(rm_bfw(e.out, m) + n) = o;
 }
 
 // ------------------------------------------------------------------ GEMV
@@ -1288,6 +1055,25 @@ size_t gemv_mix_lds(int M, int T, int C) {
   const size_t xs = ((size_t)M * (C + 8) * 2 + 15) & ~(size_t)15;
   const size_t lds = xs + (size_t)rows * C * 2 + (size_t)M * n8 * 4;
   return lds <= 98304 ? lds : 0;
+}
+
+// The plan launch_gemm would run for a decode GEMV on k_gemv1 (chain.hip's
+// mirror mode reproduces it bit for bit).  Returns 1 if the shape takes another kernel.
+int gemv_plan_query(const GemmArgs& a0, int* nw, int* ksplit, int* tpw, int* fast) {
+  GemmArgs a = a0;
+  if (a.M <= 0 || a.M > 16 || a.K % 32 || a.N % 16 || a.xf.kind == XF_MIX) return 1;
+  GemmPlan p = gemv_plan(a.N, a.K, a.M);
+  if (p.nw > max_waves(1)) p.nw = max_waves(1);
+  a.ksplit = p.ksplit;
+  if (a.ksplit > 1 && (!a.ws || !a.counters || a.N / 16 > 65536)) a.ksplit = 1;
+  if (!gemv1_fits(a)) return 1;
+  int t = 1;
+  if (a.ksplit == 1 && (p.tpw == 2 || p.tpw == 4 || p.tpw == 8) && p.nw % p.tpw == 0) t = p.tpw;
+  *nw = p.nw;
+  *ksplit = a.ksplit;
+  *tpw = t;
+  *fast = 64 * p.nw;   // k_gemv1's fast staging: M * n8 <= 4 * blockDim.x
+  return 0;
 }
 
 // returns 0 ok, else an error code (see engine.cpp)

@@ -1,0 +1,287 @@
+// Device helpers of the GEMV / GEMM family shared by the per-op kernels
+// (gemm.hip) and the persistent chain kernel (chain.hip): weight-stream loads,
+// the A-operand transforms (XF_*) and the epilogues (EPI_*).
+//
+// Memory policy MP: every load of bytes that another workgroup may have written
+// in the SAME launch, and every store of such bytes, goes through MP.  MemPlain
+// (the per-op kernels: a kernel boundary publishes) is a plain access; MemWT
+// (chain.hip) is the in-launch hand-off form of MI355X_MICROARCH.md's table,
+// first row: write-through (sc1) stores, L1-bypassing (sc1) loads.
+#pragma once
+#include "kernels.h"
+
+struct MemPlain {
+  static DEV bf16x8 ld16(const bf16* p) { return *(const bf16x8*)p; }
+  static DEV bf16x4 ld8(const bf16* p) { return *(const bf16x4*)p; }
+  static DEV float ldf(const float* p) { return *p; }
+  static DEV void st8(bf16* p, bf16x4 v) { *(bf16x4*)p = v; }
+  static DEV void st2(bf16* p, bf16 v) { *p = v; }
+  static DEV void stf(float* p, float v) { *p = v; }
+};
+
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+// global (address_space 1) views: the hand-off words must be global_ accesses, never flat_
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned short gu16;
+typedef __attribute__((address_space(1))) float gf32;
+struct MemWT {
+  static DEV unsigned long long l64(const void* p) {
+    return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  static DEV bf16x8 ld16(const bf16* p) {
+    const u64x2 v = {l64(p), l64(p + 4)};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+  static DEV bf16x4 ld8(const bf16* p) { return __builtin_bit_cast(bf16x4, l64(p)); }
+  static DEV float ldf(const float* p) { return __hip_atomic_load((gf32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+  static DEV void st8(bf16* p, bf16x4 v) {
+    __hip_atomic_store((gu64*)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  static DEV void st2(bf16* p, bf16 v) {
+    __hip_atomic_store((gu16*)p, __builtin_bit_cast(unsigned short, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  static DEV void stf(float* p, float v) { __hip_atomic_store((gf32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+};
+
+// Weight-stream load.  Decode weights are read once per step (GBs against a
+// 256 MB Infinity Cache), so they go out non-temporal (MI355X_MICROARCH.md
+// "nt-weights"); VV_W_NT=0 builds the default-policy variant for A/B runs.
+// KEEP (GemmArgs::keep): weights re-read soon — the diffusion head's 170 MB per
+// step is read S times per token and stays in the Infinity Cache with the
+// default policy (tools/head_mall.py: -7 % per head step).
+#ifndef VV_W_NT
+#define VV_W_NT 1
+#endif
+template <bool KEEP = false>
+DEV bf16x8 ldw(const bf16* p) {
+#if VV_W_NT
+  if (!KEEP) return __builtin_nontemporal_load((const bf16x8*)p);
+#endif
+  return *(const bf16x8*)p;
+}
+
+DEV f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ------------------------------------------------------------------ A transform
+// Inverse RMS of rows [m0, m0 + nrows) (local index i -> inv_s[i]); same
+// summation order as k_rmsnorm (lane-strided 8-element chunks, wave sum).
+template <class MP = MemPlain>
+DEV void row_inv(const RowMap& am, int M, int K, float eps, int m0, int nrows, float* inv_s, int wave, int NW,
+                 int lane) {
+  const int nch = K >> 3;
+  for (int i = wave; i < nrows; i += NW) {
+    const int m = m0 + i;
+    float ss = 0.f;
+    if (m < M) {
+      const bf16* x = rm_bf(am, m);
+      for (int c = lane; c < nch; c += 64) {
+        const bf16x8 v = MP::ld16(x + c * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += bf(v[j]) * bf(v[j]);
+      }
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) inv_s[i] = rsqrtf(ss / (float)K + eps);
+  }
+}
+DEV void row_inv(const GemmArgs& a, int m0, int nrows, float* inv_s, int wave, int NW, int lane) {
+  row_inv<MemPlain>(a.a, a.M, a.K, a.xf.eps, m0, nrows, inv_s, wave, NW, lane);
+}
+
+template <int XF, class MP = MemPlain>
+DEV bf16x8 xform(const GemmArgs& a, bf16x8 x, int m, int k, float inv) {
+  bf16x8 o;
+  if (XF == XF_NORM) {
+    bf16x8 wv, sh, sc;
+    if (a.xf.w) wv = *(const bf16x8*)(a.xf.w + k);
+    const bf16* md = a.xf.mod ? a.xf.mod + (long long)m * a.xf.mod_ld : nullptr;
+    if (md) {
+      sh = *(const bf16x8*)(md + a.xf.shift_off + k);
+      sc = *(const bf16x8*)(md + a.xf.scale_off + k);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = rb(bf(x[j]) * inv);
+      if (a.xf.w) t = rb(t * bf(wv[j]));
+      if (md) t = rb(rb(t * rb(1.0f + bf(sc[j]))) + bf(sh[j]));
+      o[j] = tobf(t);
+    }
+  } else if (XF == XF_SILU_ADD) {
+    const bf16x8 v = *(const bf16x8*)(a.xf.vec + k);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = tobf(silu_f(rb(bf(x[j]) + bf(v[j]))));
+  } else {
+    o = x;
+  }
+  return o;
+}
+
+// ------------------------------------------------------------------ epilogues
+// One 16(n) x 16(m) MFMA tile in the C/D layout: lane l holds m = m0 + (l & 15),
+// n = n0 + 4*(l >> 4) + i, i = 0..3.  Every lane of the wave must call this
+// (cross-lane exchanges), rows m >= M are dropped inside.
+
+// RoPE epilogue (Qwen2 q/k/v projection + apply_rotary_pos_emb + cache append;
+// transformers modeling_qwen2.py:99-134, 195-247).  Packed q/k rows: tile tt of
+// head h holds dims [8tt, 8tt+8) in rows 0..7 and [64+8tt, 64+8tt+8) in rows
+// 8..15 (weights.py: _rope_pack); v rows are in natural order.
+template <class MP = MemPlain>
+DEV void epi_rope(const GemmArgs& a, int m, int n0, int lane, float v[4]) {
+  const RopeEpi& R = a.rope;
+  constexpr int d = 128;
+  const int g = lane >> 4;
+  if (a.epi.bias) {
+    const bf16x4 b = *(const bf16x4*)(a.epi.bias + n0 + 4 * g);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] += bf(b[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = rb(v[i]);  // q/k/v_proj output (bf16)
+  const int h = n0 / d, tt = (n0 % d) >> 4;
+  if (h < R.nh + R.nkv) {
+    float u[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) u[i] = __shfl_xor(v[i], 32);
+    if (g >= 2 || m >= a.M) return;
+    const int j = 8 * tt + 4 * g;
+    const int p = R.pos[m];
+    bf16x4 o1, o2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float f = (float)p * R.inv_freq[j + i];
+      const float cs = rb(cosf(f)), sn = rb(sinf(f));
+      o1[i] = tobf(rb(v[i] * cs) + rb(-u[i] * sn));
+      o2[i] = tobf(rb(u[i] * cs) + rb(v[i] * sn));
+    }
+    bf16* dst = h < R.nh ? R.q_out + (long long)m * R.nh * d + h * d
+                         : R.kv.k + (long long)R.layer * R.kv.s_layer + (long long)R.slots[m] * R.kv.s_slot +
+                               (long long)(h - R.nh) * R.kv.s_head + (long long)p * d;
+    MP::st8(dst + j, o1);
+    MP::st8(dst + j + 64, o2);
+  } else {
+    if (m >= a.M) return;
+    // V cache in 32-position blocks of [dim][position] (common.h v_off)
+    const int hv = h - R.nh - R.nkv;
+    bf16* hb = R.kv.v + (long long)R.layer * R.kv.s_layer + (long long)R.slots[m] * R.kv.s_slot +
+               (long long)hv * R.kv.s_head;
+    const int dim0 = (n0 % d) + 4 * g, p = R.pos[m];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) MP::st2(hb + v_off(dim0 + i, p), tobf(v[i]));
+  }
+}
+
+// CFG combine + DPM-Solver++ update (sample_speech_tokens,
+// modeling_vibevoice_inference.py:717-724; DPMSolverMultistepScheduler.step,
+// dpm_solver.py:935-1022) on the final linear's rows: rows [0, n) are the
+// conditional and [n, 2n) the unconditional v-predictions, 2n <= 16 so row r and
+// its partner r + n sit in the same 16-lane group.
+template <class MP = MemPlain>
+DEV void epi_dpm(const GemmArgs& a, const DpmEpi& P, int n0, int lane, const float v[4]) {
+  const int g = lane >> 4, r = lane & 15, n = P.n;
+  float e[4], u[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) e[i] = rb(v[i]);  // final_layer.linear output (bf16, no bias)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) u[i] = __shfl(e[i], (lane + n) & 63);
+  if (r >= n) return;
+  const DpmCoef& k = P.k;
+  const long long off = (long long)r * a.N + n0 + 4 * g;
+  const bf16x4 xv = MP::ld8(P.x + off);
+  const bf16x4 mv = MP::ld8(P.m1 + off);
+  bf16x4 xo, mo;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float c = e[i], un = u[i];
+    const float vv = rb(un + rb(k.cfg * rb(c - un)));
+    const float xs = bf(xv[i]);
+    const float x0 = rb(rb(k.alpha_s * xs) - rb(k.sigma_s * vv));
+    float out = k.c_x * xs - rb(k.c_d0 * x0);
+    if (k.order == 2) {
+      const float d1 = rb(k.inv_r0 * rb(x0 - bf(mv[i])));
+      out = out - rb(k.c_d1 * d1);
+    }
+    if (P.noise) out = out + k.c_n * P.noise[off + i];
+    xo[i] = tobf(out);
+    mo[i] = tobf(x0);
+  }
+  MP::st8(P.x + off, xo);
+  MP::st8(P.m1 + off, mo);
+}
+
+template <class MP = MemPlain>
+DEV void epi_tile(const GemmArgs& a, int m, int n0, int lane, const float v_in[4]) {
+  const EpiArgs& e = a.epi;
+  float v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = v_in[i];
+  const int g = lane >> 4;
+  if (e.kind == EPI_ROPE) {
+    epi_rope<MP>(a, m, n0, lane, v);
+    return;
+  }
+  if (e.kind == EPI_CFG_DPM) {
+    epi_dpm<MP>(a, a.dpm, n0, lane, v);
+    return;
+  }
+  if (e.kind == EPI_SILU_MUL) {
+    // rows 0..7 of the tile are gate, 8..15 the matching up rows; lane g<2 holds
+    // gate rows 4g+i, lane g+2 holds up rows 8+4g+i
+    float u[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) u[i] = __shfl_xor(v[i], 32);
+    if (g >= 2 || m >= a.M) return;
+    const int col = (n0 >> 1) + 4 * g;
+    bf16x4 o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = tobf(rb(silu_f(rb(v[i]))) * rb(u[i]));
+    MP::st8(rm_bfw(e.out, m) + col, o);
+    return;
+  }
+  if (m >= a.M) return;
+  const int n = n0 + 4 * g;
+  if (e.bias) {
+    bf16x4 b = *(const bf16x4*)(e.bias + n);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] += bf(b[i]);
+  }
+  if (e.kind == EPI_F32) {
+    float* o = (float*)e.out.base + rm_off(e.out, m) + n;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) MP::stf(o + i, v[i]);
+    return;
+  }
+  bf16x4 o;
+  if (e.kind == EPI_STORE) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = tobf(v[i]);
+  } else if (e.kind == EPI_GELU) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = tobf(gelu_f(rb(v[i])));
+  } else {  // EPI_RES
+    bf16x4 r = MP::ld8(rm_bf(e.res, m) + n);
+    float s[4] = {1.f, 1.f, 1.f, 1.f};
+    bool scaled = false;
+    if (e.gamma) {
+      bf16x4 gm = *(const bf16x4*)(e.gamma + n);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s[i] = bf(gm[i]);
+      scaled = true;
+    } else if (e.gate.base) {
+      bf16x4 gm = MP::ld8(rm_bf(e.gate, m) + n);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s[i] = bf(gm[i]);
+      scaled = true;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float y = rb(v[i]);
+      if (scaled) y = rb(s[i] * y);
+      o[i] = tobf(bf(r[i]) + y);
+    }
+  }
+  MP::st8(rm_bfw(e.out, m) + n, o);
+}
+

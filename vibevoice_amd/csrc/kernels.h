@@ -172,6 +172,45 @@ struct SumRows {
   bf16* p[8];
 };
 
+// ---- persistent GEMV chains (chain.hip)
+constexpr int CH_TMAX = 256;     // split-segment tiles of one op (ticket words per op)
+enum { CH_BIND_AX = 1, CH_BIND_DPM = 2 };   // per-call operands bound at launch (ChainArgs)
+
+struct ChainOp {
+  int xf, fast, bind, rep;  // A transform; k_gemv1 staging: fast path iff M * K_split / 8 <= 4 * fast;
+                            // CH_BIND_*; diffusion step of the op
+  int t1, tpw, kw;          // tiles [0, t1): units of tpw whole tiles, kw waves per tile
+  int ks2, kw2;             // tiles [t1, N/16): split ks2 ways along K, kw2 waves per split
+  int nu1, nunit;           // whole-tile units; all units
+  unsigned target;          // done[] count of a finished op (its tiles)
+  long long slab_off;       // floats into ChainArgs::slabs (split segment: [tile - t1][ks][256])
+  int ticket_off, pad_;     // words into ChainArgs::tickets (split segment: [tile - t1])
+  GemmArgs g;
+};
+
+struct ChainArgs {
+  const ChainOp* ops;
+  int nops, pad_;
+  unsigned* done;           // [nops][9][32]: 8 shard + 1 top counter lines per op, zeroed before every launch
+  unsigned* tickets;        // split-segment tiles of every op, zeroed before every launch
+  float* slabs;
+  unsigned* err;            // != 0: a wait gave up (1 + the op it waited for)
+  bf16* x;                  // CH_BIND_AX: A rows base; CH_BIND_DPM: the latents updated in place
+  const float* noise;       // CH_BIND_DPM: sde noise of step s at noise + s * noise_rep, or nullptr
+  long long noise_rep;
+  const DpmCoef* coef;      // CH_BIND_DPM: per-step coefficients (cfg from `cfg`)
+  float cfg;
+  int pad2_;
+  unsigned long long* stamps;   // diagnostics (tools/chain_bench.py): [G][nops][4] s_memrealtime, or nullptr
+};
+
+size_t chain_plan_op(ChainOp* op, int G, int mode);
+int chain_grid();
+int launch_chain(const ChainArgs& A, size_t lds, hipStream_t st);
+// the per-op kernel's plan for a decode GEMV (gemm.hip): 0 and the plan when it runs k_gemv1
+// (*fast = its workgroup's threads)
+int gemv_plan_query(const GemmArgs& a, int* nw, int* ksplit, int* tpw, int* fast);
+
 size_t gemv_mix_lds(int M, int T, int C);
 int launch_gemm(GemmArgs a, hipStream_t st);
 int launch_sum_rows(SumRows s, long long count, hipStream_t st);
