@@ -241,6 +241,9 @@ int vv_chain_error(vv_ctx* c);
  * (workgroup, op): wait begun, inputs ready, op signalled (uint64[G][nops][4]);
  * NULL: off. */
 int vv_chain_stamps(void* buf);
+/* Diagnostic (benchmarks only): vv_gemm_bf16 reads A in MFMA-fragment order
+ * (as the packed weights; the 256 x 256 tile only). */
+int vv_gemm_tune_apack(int on);
 /* Test switch (bit mask, default 3): bit 0 folds each codec Block1D's mixer
  * (norm, depthwise conv, gamma residual, FFN norm) into its fc1 GEMV where
  * <= 16 rows fit (XF_MIX); bit 1 runs whole narrow-stage blocks (C <= 128) as

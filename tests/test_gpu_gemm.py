@@ -164,17 +164,39 @@ def test_gemv_large_lds_staging(lds, M, N, K, epi):
                                        (1000, 17920, 1536, "silu_mul"), (4100, 2048, 1536, "store"),
                                        (300, 1024, 512, "gelu"), (640, 512, 128, "f32")])
 def test_gemm_big_tile(M, N, K, epi):
-    """Prefill-sized GEMMs on the LDS-staged 128 x 128 tile (k_gemm_big, two
-    stages; and its single-stage form) vs torch fp32, and vs k_gemm (same K
-    order of MFMA accumulation: bit-identical) -- ragged
-    last row tile, every epilogue kind the prefill uses."""
+    """Prefill-sized GEMMs on the LDS-staged 256 x 256 tile (k_gemm_xl, 4-stage
+    ring), the 128 x 128 tile (k_gemm_big, two stages; and its single-stage
+    form) vs torch fp32, and vs k_gemm (same K order of MFMA accumulation:
+    bit-identical) -- ragged last row tile, every epilogue kind the prefill uses."""
     L = _lib.lib()
     outs = {}
     try:
-        for mode in (6, 5, 0):   # k_gemm_big 2 / 1 stages at any tile count; k_gemm
+        for mode in (7, 6, 5, 0):   # k_gemm_xl / k_gemm_big 2 / 1 stages at any tile count; k_gemm
             L.vv_gemm_tune_big(mode)
             outs[mode], ref = run(M, N, K, epi, bias=epi != "silu_mul", res=epi == "res")
     finally:
         L.vv_gemm_tune_big(-1)
-    assert rel_err(outs[6], ref) < 5e-3
-    assert torch.equal(outs[6], outs[0]) and torch.equal(outs[5], outs[0])
+    assert rel_err(outs[7], ref) < 5e-3 and rel_err(outs[6], ref) < 5e-3
+    assert torch.equal(outs[7], outs[0]) and torch.equal(outs[6], outs[0]) and torch.equal(outs[5], outs[0])
+
+
+@pytest.mark.parametrize("handoff", [0, 1])
+@pytest.mark.parametrize("M", [1, 2, 5])
+@pytest.mark.parametrize("epi", ["res", "store", "silu_mul"])
+def test_gemv_small_m_splitk(handoff, M, epi):
+    """The M < 8 split-K plan (LM down projection: 96 tiles x K 8,960, two
+    workgroups per tile) with the residual epilogue and under both hand-off forms
+    (0: plain stores + agent release/acquire fences, 1: sc1 write-through), vs
+    torch fp32; the split-K result must equal the unsplit one bit for bit."""
+    L = _lib.lib()
+    N, K = (3072, 8960) if epi == "silu_mul" else (1536, 8960)
+    try:
+        L.vv_gemv_tune(0, 2, handoff, 0, 0)          # 2 K splits
+        Y2, ref = run(M, N, K, epi, bias=epi != "silu_mul", res=epi == "res")
+        L.vv_gemv_tune(0, 1, -1, 0, 0)               # one workgroup per tile
+        Y1, _ = run(M, N, K, epi, bias=epi != "silu_mul", res=epi == "res")
+    finally:
+        L.vv_gemv_tune(0, 0, -1, 0, 0)
+    assert rel_err(Y2, ref) < 4e-3 and max_rel(Y2, ref) < 3e-2
+    assert rel_err(Y1, ref) < 4e-3
+

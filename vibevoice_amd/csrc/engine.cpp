@@ -1384,6 +1384,13 @@ int vv_scatter_rows(vv_ctx* c, int n, int C, const void* src, int64_t lds, const
   return 0;
 }
 
+// diagnostic (vv_gemm_tune_apack): vv_gemm_bf16's A is MFMA-fragment packed (k_gemm_xl only)
+static int g_gemm_apack = 0;
+extern "C" int vv_gemm_tune_apack(int on) {
+  g_gemm_apack = on;
+  return 0;
+}
+
 int vv_gemm_bf16(int M, int N, int K, const void* A, int64_t lda, const void* Wt, const void* bias, int epi, void* Y,
                  int64_t ldy, const void* res, const void* gamma, vv_ctx* c, vv_stream vst) {
   GemmArgs g;
@@ -1400,6 +1407,7 @@ int vv_gemm_bf16(int M, int N, int K, const void* A, int64_t lda, const void* Wt
   g.epi.out = rowmap(Y, ldy);
   g.epi.res = rowmap(res, ldy);
   g.epi.gamma = (const bf16*)gamma;
+  g.apack = g_gemm_apack;
   if (c) {
     g.ws = (float*)c->splitk_ws.p;
     g.counters = (unsigned*)c->splitk_cnt.p;

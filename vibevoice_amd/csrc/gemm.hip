@@ -1010,13 +1010,161 @@ static void launch_gemv_xf(const GemmArgs& a, int mrep, int u, dim3 grid, dim3 b
   }
 }
 
+// ------------------------------------------------------------------ 256 x 256 tile (prefill, large batches)
+// cdna_hip_programming.md §5: the 128² two-barrier structure (k_gemm_big) tops
+// out near 900 TF; a 256 x 256 tile at one 8-wave workgroup per CU halves the
+// operand bytes per FLOP and keeps a 3-stage-deep LDS-DMA ring in flight across
+// raw barriers.  Here:
+//   * 8 waves as 2 (rows m) x 4 (weight rows n): wave (wr, wc) owns 128 m x 64 n
+//     = 8 x 4 accumulator tiles (128 VGPRs);
+//   * K in 32-wide stages, a ring of 4 stages in LDS (4 x 32 KB: 16 A + 16 W one-KB
+//     fragment blocks).  Step s computes stage s from registers while the wave
+//     reads stage s + 1's fragments into its second register set; stage s + 4 is
+//     issued into stage s's buffer right after the barrier that ends every wave's
+//     reads of it, so three stages are in flight; each step waits with a counted
+//     vmcnt (never 0 in the loop) and ONE raw s_barrier (a __syncthreads() would
+//     drain the ring);
+//   * the packed weight blocks are MFMA fragments already (one 1 KB glds per wave
+//     instruction, lane-linear) and A rows are gathered per lane into the same
+//     order, so every ds_read_b128 is lane-linear and conflict-free (no swizzle);
+//   * one __shared__ array (a second LDS object makes hipcc drain vmcnt(0) before
+//     every k-step, §5 item 4a); s_setprio(1) around the MFMA cluster (T5).
+// K order of accumulation per output is k_gemm's (chunk by chunk): bit-identical.
+#ifndef VV_GX_INTERLEAVE
+#define VV_GX_INTERLEAVE 1
+#endif
+// s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] |
+// vmcnt[5:4] << 14; a field at its maximum does not wait).  The builtin, unlike an
+// asm wait, is seen by hipcc's waitcnt pass, which then does not re-wait (with
+// lgkmcnt(0)) for fragments this wait already retired
+constexpr unsigned WC_VM12 = 0x0F7C, WC_VM8_LGKM0 = 0x0078, WC_LGKM0 = 0xC07F, WC_VM0 = 0x0F70;
+constexpr int GX_M = 256, GX_N = 256, GX_NS = 4;
+constexpr int GX_STAGE = 32 * 512;                       // elements per stage
+constexpr size_t GX_LDS = (size_t)GX_NS * GX_STAGE * 2;   // 128 KB
+
+__global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) bf16 smx[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int ntm = (a.M + GX_M - 1) / GX_M, ntn = a.N / GX_N, total = ntm * ntn;
+  // XCD-major remap (bijective for any total), then groups of 4 row tiles sweep the weight tiles
+  const int nb = gridDim.x, xcd = (int)(blockIdx.x & 7), q8 = nb >> 3, r8 = nb & 7;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (int)(blockIdx.x >> 3);
+  if (t >= total) return;
+  constexpr int GM = 4;
+  const int grp = t / (GM * ntn), gm = min(GM, ntm - grp * GM), tin = t - grp * GM * ntn;
+  const int tm = grp * GM + tin % gm, tn = tin / gm;
+  const int nch = a.K >> 5;
+  // staging: wave w fills A blocks 2w, 2w + 1 (row tiles) and W blocks 2w, 2w + 1 (weight tiles)
+  const bf16* asrc[2];
+  const bf16* wsrc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int j = 2 * wave + i;
+    if (a.apack) {   // packed rows: one contiguous 1 KB block per (row tile, chunk), like W
+      asrc[i] = (const bf16*)a.a.base + (long long)min(tm * 16 + j, (a.M - 1) >> 4) * nch * 512 + lane * 8;
+    } else {
+      const int m = min(tm * GX_M + j * 16 + r, a.M - 1);
+      asrc[i] = rm_bf(a.a, m) + 8 * g;
+    }
+    wsrc[i] = a.w + (long long)(tn * 16 + j) * nch * 512 + lane * 8;
+  }
+  auto issue = [&](int s) {
+    bf16* st = smx + (s & (GX_NS - 1)) * GX_STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int j = 2 * wave + i;
+      __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + (a.apack ? (long long)s * 512 : (long long)s * 32)),
+                                       (__attribute__((address_space(3))) void*)(st + j * 512), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + (long long)s * 512),
+                                       (__attribute__((address_space(3))) void*)(st + (16 + j) * 512), 16, 0, 0);
+    }
+  };
+  f32x4 acc[4][8];   // [weight tile nt][row tile mt]
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) acc[nt][mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // fragments of stage s are read into registers during step s - 1 (two register
+  // sets), so each wave's LDS reads of the next stage overlap its MFMAs
+  auto frags = [&](int s, bf16x8 (&wf)[4], bf16x8 (&xf)[8]) {
+    const bf16* st = smx + (s & (GX_NS - 1)) * GX_STAGE;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) wf[nt] = *(const bf16x8*)(st + (16 + wc * 4 + nt) * 512 + lane * 8);
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) xf[mt] = *(const bf16x8*)(st + (wr * 8 + mt) * 512 + lane * 8);
+  };
+  auto macs = [&](const bf16x8 (&wf)[4], const bf16x8 (&xf)[8]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) acc[nt][mt] = mfma(wf[nt], xf[mt], acc[nt][mt]);
+    __builtin_amdgcn_s_setprio(0);
+    // keep the MFMAs above the next step's asm waits ("memory" does not order
+    // register-only instructions, cdna_hip_programming.md §5.7 rule 18)
+    __builtin_amdgcn_sched_barrier(0);
+#if VV_GX_INTERLEAVE
+    // 4 groups: 1 glds (when issued), 3 ds_reads of the next stage, 8 MFMAs
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // VMEM read (glds)
+      __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);   // DS read
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);   // MFMA
+    }
+#endif
+  };
+  // ring: stages s + 1 .. s + 3 in flight while stage s computes; exactly 4 glds
+  // per wave per step (stages past the end re-load the last one into a buffer
+  // nothing reads again), so vmcnt(8) retires stage s + 1 at every step and each
+  // half-step below is one basic block the scheduler can interleave
+  const int last = nch - 1;
+  issue(0);
+  issue(min(1, last));
+  issue(min(2, last));
+  issue(min(3, last));
+  __builtin_amdgcn_s_waitcnt(WC_VM12);
+  __builtin_amdgcn_s_barrier();
+  bf16x8 wa[4], xa[8], wb[4], xb[8];
+  frags(0, wa, xa);
+  int s = 0;
+  for (; s + 1 < nch; s += 2) {
+    // ---- step s: compute stage s (set a), read stage s + 1 (set b)
+    __builtin_amdgcn_s_waitcnt(WC_VM8_LGKM0);
+    __builtin_amdgcn_s_barrier();   // every wave: stage s + 1 landed, stage s read (its buffer is free)
+    issue(min(s + 4, last));
+    frags(s + 1, wb, xb);
+    macs(wa, xa);
+    // ---- step s + 1: compute stage s + 1 (set b), read stage s + 2 (set a)
+    __builtin_amdgcn_s_waitcnt(WC_VM8_LGKM0);
+    __builtin_amdgcn_s_barrier();
+    issue(min(s + 5, last));
+    frags(min(s + 2, last), wa, xa);
+    macs(wb, xb);
+  }
+  if (s < nch) {   // odd stage count: the last stage is in set a
+    __builtin_amdgcn_s_waitcnt(WC_LGKM0);
+    macs(wa, xa);
+  }
+  __builtin_amdgcn_s_waitcnt(WC_VM0);   // the past-the-end re-loads land before the workgroup ends
+  // epilogue: one epi_tile body in a rolled loop, the accumulators rotated through acc[0][0]
+#pragma unroll 1
+  for (int i = 0; i < 32; ++i) {
+    float v[4] = {acc[0][0][0], acc[0][0][1], acc[0][0][2], acc[0][0][3]};
+    epi_tile(a, tm * GX_M + (wr * 8 + (i & 7)) * 16 + r, tn * GX_N + (wc * 4 + (i >> 3)) * 16, lane, v);
+#pragma unroll
+    for (int k = 0; k < 31; ++k) acc[k >> 3][k & 7] = acc[(k + 1) >> 3][(k + 1) & 7];
+  }
+}
+
 // diagnostic (vv_gemm_tune_big): 0 keeps every M > 64 GEMM on k_gemm; 1 / 2 LDS
-// stages; + 4 ignores the tile-count threshold (tests of small shapes)
-static int g_gemm_big = 2, g_gemm_big_any = 0;
+// stages of the 128² tile (k_gemm_big); 3 (built-in) = the 256² tile (k_gemm_xl)
+// where it applies, else k_gemm_big<2>; + 4 ignores the tile-count thresholds
+static int g_gemm_big = 3, g_gemm_big_any = 0;
 extern "C" int vv_gemm_tune_big(int mode) {
   g_gemm_big_any = mode >= 0 && (mode & 4) ? 1 : 0;
-  mode = mode < 0 ? 2 : mode & 3;
-  g_gemm_big = mode > 2 ? 2 : mode;
+  g_gemm_big = mode < 0 ? 3 : mode & 3;
   return 0;
 }
 
@@ -1027,6 +1175,20 @@ static int launch_gemm_xf(const GemmArgs& a, hipStream_t st) {
   // x K <= 1,024: 24 - 104 such tiles) are faster as k_gemm's 4x more 64 x 64
   // workgroups (B = 8 step 5.53 ms vs 5.83), a 1K-token prompt's o / down /
   // q|k|v projections (108 - 144 tiles, K >= 1,536) on k_gemm_big (14.5 -> 13.4 ms)
+  // k_gemm_xl with >= one 256 x 256 tile per CU (16K-token prefill: 384 - 4,480 tiles)
+  const int total_xl = ((a.M + GX_M - 1) / GX_M) * (a.N / GX_N);
+  if (XF == XF_NONE && g_gemm_big == 3 && a.M >= GEMM_BIG_M && a.N % GX_N == 0 && a.K % 32 == 0 &&
+      (total_xl >= GEMM_BIG_TILES || g_gemm_big_any)) {
+    static bool attr = false;
+    if (!attr) {
+      if (hipFuncSetAttribute((const void*)k_gemm_xl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GX_LDS) !=
+          hipSuccess)
+        return 2;
+      attr = true;
+    }
+    hipLaunchKernelGGL(k_gemm_xl, dim3(total_xl), dim3(512), GX_LDS, st, a);
+    return 0;
+  }
   const int total = ((a.M + GB_M - 1) / GB_M) * (a.N / GB_N);
   if (XF == XF_NONE && g_gemm_big && a.M >= GEMM_BIG_M && a.N % GB_N == 0 && a.K % GB_K == 0 &&
       (total >= GEMM_BIG_TILES || (long long)a.M * a.N * a.K >= (1LL << 30) || g_gemm_big_any)) {

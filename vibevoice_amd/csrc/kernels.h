@@ -73,7 +73,7 @@ struct GemmArgs {
   unsigned* counters;
   unsigned long long* stamps;  // diagnostic builds only: 4 s_memrealtime stamps per workgroup
   int keep;               // weights re-read soon (diffusion head): default cache policy, not nt
-  int pad2_;
+  int apack;              // k_gemm_xl: A rows in MFMA-fragment order (blocks (row tile, chunk) of 1 KB, as W)
 };
 
 struct NormArgs {
