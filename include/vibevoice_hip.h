@@ -244,6 +244,10 @@ int vv_chain_stamps(void* buf);
 /* Diagnostic (benchmarks only): vv_gemm_bf16 reads A in MFMA-fragment order
  * (as the packed weights; the 256 x 256 tile only). */
 int vv_gemm_tune_apack(int on);
+/* Tuning hook (benchmarks only): override the GEMV plan (waves, K splits, chunks
+ * in flight, tiles per workgroup) for one weight shape N x K at M <= mmax rows;
+ * up to 8 overrides; N <= 0 clears them. */
+int vv_gemv_tune_shape(int N, int K, int mmax, int nw, int ks, int u, int tpw);
 /* Test switch (bit mask, default 3): bit 0 folds each codec Block1D's mixer
  * (norm, depthwise conv, gamma residual, FFN norm) into its fc1 GEMV where
  * <= 16 rows fit (XF_MIX); bit 1 runs whole narrow-stage blocks (C <= 128) as

@@ -16,8 +16,15 @@ if name == "lib":
     probe = ctypes.CDLL(_lib.LIB_PATH)     # an older build may lack newer (diagnostic) exports
     _lib.EXPORTS = [e for e in _lib.EXPORTS if hasattr(probe, e[0])]
     _lib.lib()
-else:   # e.g. attn_tune 128,8
-    getattr(_lib.lib(), "vv_" + name)(*[int(v) for v in val.split(",")])
+else:   # e.g. attn_tune 128,8; gemv_tune_shape 2048,8192,1,8,2,4,1 (several: separated by ';')
+    for v in val.split(";"):
+        getattr(_lib.lib(), "vv_" + name)(*[int(x) for x in v.split(",")])
+if len(sys.argv) > 3 and sys.argv[3] == "--prefill":   # tools/prefill_bench.py instead of bench.py
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    sys.argv = ["prefill_bench.py"] + sys.argv[4:]
+    import prefill_bench  # noqa: E402
+    prefill_bench.main()
+    sys.exit(0)
 sys.argv = ["bench.py"] + sys.argv[3:]
 import bench  # noqa: E402
 

@@ -487,8 +487,14 @@ constexpr int PF_Q = 32;
 constexpr float PF_LAZY = 8.f;       // running-max slack (log2 units) before O is rescaled
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int PF_STAGE = 16 * 512;   // bf16 elements per staged step: 8 K + 8 V fragment blocks
-constexpr int PF_NS = 2;             // LDS stages: step s+1 in flight while step s computes (4, and a software
-                                     // pipeline issuing S of step s+1 before the softmax of s, measured no faster)
+// LDS stages: steps s+1 .. s+NS-2 in flight while step s computes, step
+// s+NS-1 issued after the step's one barrier.  16K-token prefill (interleaved
+// same-box runs, tools/ab_bench.py --prefill): NS 2 118.7 ms, NS 3 122.4, NS 4
+// 122.4; the former two-barrier form with NS 2 124.6 ms
+#ifndef VV_PF_NS
+#define VV_PF_NS 2
+#endif
+constexpr int PF_NS = VV_PF_NS;
 
 // max / sum over lanes {l, l^16, l^32, l^48} (one query column of an MFMA
 // tile): gfx950's v_permlane16_swap / v_permlane32_swap (VALU, a few cycles)
@@ -611,7 +617,7 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
     const bf16* K = a.kv.k + cbase;    // [ctx][128]
     const bf16* VB = a.kv.v + cbase;   // 32-position blocks of [128][32] (v_off)
     auto issue = [&](int step) {
-      bf16* st = sm + (step & (PF_NS - 1)) * PF_STAGE;
+      bf16* st = sm + (step % PF_NS) * PF_STAGE;
 #pragma unroll
       for (int i = 0; i < NI_MAX; ++i)
         if (i < ni) {
@@ -623,12 +629,14 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
     };
     for (int p = 0; p < PF_NS - 1 && p < nsteps; ++p) issue(p);
     for (int step = 0; step < nsteps; ++step) {
-      // the buffer of step + NS - 1 was released by the previous step's closing barrier
+      // this wave's loads of `step` have landed (steps step + 1 .. step + NS - 2 stay in flight)
+      wait_vm(ni * min(PF_NS - 2, nsteps - 1 - step));
+      // ONE barrier per step: every wave's loads of `step` are in LDS, and every
+      // wave has finished reading step - 1, whose buffer takes step + NS - 1
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (step + PF_NS - 1 < nsteps) issue(step + PF_NS - 1);
-      wait_vm(ni * min(PF_NS - 1, nsteps - 1 - step));   // this wave's loads of `step` have landed
-      asm volatile("s_barrier" ::: "memory");
       const int k0 = step * 32;
-      const bf16* st = sm + (step & (PF_NS - 1)) * PF_STAGE;
+      const bf16* st = sm + (step % PF_NS) * PF_STAGE;
       f32x4 s[2][2];
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
@@ -703,8 +711,8 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) o[dt][qt] = amfma(vf, pf[qt], o[dt][qt]);
       }
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // this stage is free for step + NS
     }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // the next pass restages every buffer
   }
   // lane holds O^T[dim 16dt + 4g + i][query 16qt + r]; l summed over the 4 lanes of the column
 #pragma unroll

@@ -39,6 +39,12 @@
 #include "kernels.h"
 #include "gemv_dev.h"
 
+// VV_EPI_PREFETCH=1 loads the epilogue's bias / residual / scale at kernel start:
+// measured +2.7 % B=1 step time (3.67 -> 3.77 ms, 3 interleaved same-box pairs), so off
+#ifndef VV_EPI_PREFETCH
+#define VV_EPI_PREFETCH 0
+#endif
+
 // Diagnostic timestamps (tools/gemv_stamps.py): 100 MHz real-time clock, one
 // lane per workgroup, to a buffer nothing else reads (a.stamps == nullptr in
 // every product call).
@@ -131,6 +137,11 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   // prologue loads read tile 0)
   const bf16* wrow = a.w + (long long)(tile_ok ? tile : 0) * a.K * 16 + lane * 8;
   const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+  // the epilogue's bias / residual / scale, loaded now: a round trip after the
+  // weight stream was the tail of every residual GEMV (VV_EPI_PREFETCH=0 builds the old form)
+  EpiPre pre;
+  const int etile = blockIdx.x * TPW + wave;
+  if (VV_EPI_PREFETCH && wave < TPW && etile < ntile) pre = epi_prefetch(a, r, etile * 16, lane);
 
   // ---- A staging into LDS (rows [0, M) x chunks [b0, b1), row stride padded
   // 16 B), overlapped with the first weight chunks.  vmcnt waits are in issue
@@ -441,7 +452,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     float v[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = red[wave * KW * 256 + i * 64 + lane];
-    epi_tile(a, r, (blockIdx.x * TPW + wave) * 16, lane, v);
+    epi_tile(a, r, (blockIdx.x * TPW + wave) * 16, lane, v, VV_EPI_PREFETCH ? &pre : nullptr);
     if (a.stamps) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       stamp(a, 3);
@@ -891,7 +902,26 @@ struct GemmPlan { int nw, ksplit, u, tpw; };
 //     tiles that share one staging of the A rows (tools/gemv_sweep.py --tpw,
 //     profiles/r01_gemv_sweep_tpw.txt: B = 8 LM gate|up 30.5 -> 20.0 us, head
 //     gate|up 4 tiles per group 15.6 us)
+// diagnostic (vv_gemv_tune_shape): plan overrides for one (N, K) at M <= m_max,
+// for same-box A/Bs of a single shape inside the loop (tools/ab_bench.py)
+struct ShapeTune { int N, K, mmax, nw, ks, u, tpw; };
+static ShapeTune g_shape_tune[8];
+static int g_nshape_tune = 0;
+extern "C" int vv_gemv_tune_shape(int N, int K, int mmax, int nw, int ks, int u, int tpw) {
+  if (N <= 0) {
+    g_nshape_tune = 0;
+    return 0;
+  }
+  if (g_nshape_tune >= 8) return 1;
+  g_shape_tune[g_nshape_tune++] = {N, K, mmax, nw, ks, u, tpw};
+  return 0;
+}
+
 static GemmPlan gemv_plan(int N, int K, int M) {
+  for (int i = 0; i < g_nshape_tune; ++i) {
+    const ShapeTune& s = g_shape_tune[i];
+    if (s.N == N && s.K == K && M <= s.mmax) return {s.nw, s.ks, s.u, s.tpw};
+  }
   const int chunks = K / 32, tiles = N / 16;
   int nw = 4, ks = 1, u = 4, tpw = 1;
   if (tiles <= 128 && chunks >= 128) {

@@ -211,8 +211,30 @@ DEV void epi_dpm(const GemmArgs& a, const DpmEpi& P, int n0, int lane, const flo
   MP::st8(P.m1 + off, mo);
 }
 
+// Epilogue operands a GEMV can load at kernel start instead of after its weight
+// stream (one dependent memory round trip less at the tail): bias, the
+// residual row and its per-column / per-row scale (EPI_STORE / GELU / RES / F32).
+struct EpiPre {
+  bf16x4 bias, res, scale;
+};
 template <class MP = MemPlain>
-DEV void epi_tile(const GemmArgs& a, int m, int n0, int lane, const float v_in[4]) {
+DEV EpiPre epi_prefetch(const GemmArgs& a, int m, int n0, int lane) {
+  const EpiArgs& e = a.epi;
+  EpiPre p;
+  const bool plain = e.kind == EPI_STORE || e.kind == EPI_GELU || e.kind == EPI_RES || e.kind == EPI_F32;
+  if (!plain || m >= a.M) return p;
+  const int n = n0 + 4 * (lane >> 4);
+  if (e.bias) p.bias = *(const bf16x4*)(e.bias + n);
+  if (e.kind == EPI_RES) {
+    p.res = MP::ld8(rm_bf(e.res, m) + n);
+    if (e.gamma) p.scale = *(const bf16x4*)(e.gamma + n);
+    else if (e.gate.base) p.scale = MP::ld8(rm_bf(e.gate, m) + n);
+  }
+  return p;
+}
+
+template <class MP = MemPlain>
+DEV void epi_tile(const GemmArgs& a, int m, int n0, int lane, const float v_in[4], const EpiPre* pre = nullptr) {
   const EpiArgs& e = a.epi;
   float v[4];
 #pragma unroll
@@ -243,7 +265,7 @@ DEV void epi_tile(const GemmArgs& a, int m, int n0, int lane, const float v_in[4
   if (m >= a.M) return;
   const int n = n0 + 4 * g;
   if (e.bias) {
-    bf16x4 b = *(const bf16x4*)(e.bias + n);
+    bf16x4 b = pre ? pre->bias : *(const bf16x4*)(e.bias + n);
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] += bf(b[i]);
   }
@@ -261,16 +283,16 @@ DEV void epi_tile(const GemmArgs& a, int m, int n0, int lane, const float v_in[4
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] = tobf(gelu_f(rb(v[i])));
   } else {  // EPI_RES
-    bf16x4 r = MP::ld8(rm_bf(e.res, m) + n);
+    bf16x4 r = pre ? pre->res : MP::ld8(rm_bf(e.res, m) + n);
     float s[4] = {1.f, 1.f, 1.f, 1.f};
     bool scaled = false;
     if (e.gamma) {
-      bf16x4 gm = *(const bf16x4*)(e.gamma + n);
+      bf16x4 gm = pre ? pre->scale : *(const bf16x4*)(e.gamma + n);
 #pragma unroll
       for (int i = 0; i < 4; ++i) s[i] = bf(gm[i]);
       scaled = true;
     } else if (e.gate.base) {
-      bf16x4 gm = MP::ld8(rm_bf(e.gate, m) + n);
+      bf16x4 gm = pre ? pre->scale : MP::ld8(rm_bf(e.gate, m) + n);
 #pragma unroll
       for (int i = 0; i < 4; ++i) s[i] = bf(gm[i]);
       scaled = true;
