@@ -1068,6 +1068,9 @@ static void launch_gemv_xf(const GemmArgs& a, int mrep, int u, dim3 grid, dim3 b
 // asm wait, is seen by hipcc's waitcnt pass, which then does not re-wait (with
 // lgkmcnt(0)) for fragments this wait already retired
 constexpr unsigned WC_VM12 = 0x0F7C, WC_VM8_LGKM0 = 0x0078, WC_LGKM0 = 0xC07F, WC_VM0 = 0x0F70;
+#ifndef VV_GX_ABL
+#define VV_GX_ABL 0
+#endif
 constexpr int GX_M = 256, GX_N = 256, GX_NS = 4;
 constexpr int GX_STAGE = 32 * 512;                       // elements per stage
 constexpr size_t GX_LDS = (size_t)GX_NS * GX_STAGE * 2;   // 128 KB
@@ -1101,6 +1104,9 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
     wsrc[i] = a.w + (long long)(tn * 16 + j) * nch * 512 + lane * 8;
   }
   auto issue = [&](int s) {
+#if VV_GX_ABL == 1
+    return;   // ablation (timing only): no global -> LDS staging
+#endif
     bf16* st = smx + (s & (GX_NS - 1)) * GX_STAGE;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -1119,6 +1125,9 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
   // fragments of stage s are read into registers during step s - 1 (two register
   // sets), so each wave's LDS reads of the next stage overlap its MFMAs
   auto frags = [&](int s, bf16x8 (&wf)[4], bf16x8 (&xf)[8]) {
+#if VV_GX_ABL == 2
+    return;   // ablation (timing only): no LDS fragment reads
+#endif
     const bf16* st = smx + (s & (GX_NS - 1)) * GX_STAGE;
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) wf[nt] = *(const bf16x8*)(st + (16 + wc * 4 + nt) * 512 + lane * 8);
@@ -1178,13 +1187,27 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
     macs(wa, xa);
   }
   __builtin_amdgcn_s_waitcnt(WC_VM0);   // the past-the-end re-loads land before the workgroup ends
-  // epilogue: one epi_tile body in a rolled loop, the accumulators rotated through acc[0][0]
-#pragma unroll 1
-  for (int i = 0; i < 32; ++i) {
-    float v[4] = {acc[0][0][0], acc[0][0][1], acc[0][0][2], acc[0][0][3]};
-    epi_tile(a, tm * GX_M + (wr * 8 + (i & 7)) * 16 + r, tn * GX_N + (wc * 4 + (i >> 3)) * 16, lane, v);
+  // epilogue: the accumulators go through the (now idle) LDS ring, 16 tiles per
+  // wave at a time, so ONE epi_tile body runs in a rolled loop that indexes
+  // memory (unrolled copies of the RoPE / DPM forms spill; rotating 32
+  // accumulators through one register tile cost ~4,000 moves per wave -- 30 % of
+  // a K = 1536 tile)
+  __syncthreads();   // every wave is past its reads of the last stage
+  float* ep = (float*)smx + wave * (16 * 256);
 #pragma unroll
-    for (int k = 0; k < 31; ++k) acc[k >> 3][k & 7] = acc[(k + 1) >> 3][(k + 1) & 7];
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ep[t * 256 + j * 64 + lane] = acc[2 * h + (t >> 3)][t & 7][j];
+#pragma unroll 1
+    for (int t = 0; t < 16; ++t) {
+      const int i = 16 * h + t;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = ep[t * 256 + j * 64 + lane];
+      epi_tile(a, tm * GX_M + (wr * 8 + (i & 7)) * 16 + r, tn * GX_N + (wc * 4 + (i >> 3)) * 16, lane, v);
+    }
   }
 }
 
