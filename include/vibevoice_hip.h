@@ -248,6 +248,10 @@ int vv_gemm_tune_apack(int on);
  * in flight, tiles per workgroup) for one weight shape N x K at M <= mmax rows;
  * up to 8 overrides; N <= 0 clears them. */
 int vv_gemv_tune_shape(int N, int K, int mmax, int nw, int ks, int u, int tpw);
+/* Test switch: 1 (default) = the q|k|v RoPE epilogue reads the engine's
+ * per-position bf16 cos / sin table; 0 = computes cosf / sinf inline
+ * (bit-identical by construction). */
+int vv_rope_table(int on);
 /* Test switch (bit mask, default 3): bit 0 folds each codec Block1D's mixer
  * (norm, depthwise conv, gamma residual, FFN norm) into its fc1 GEMV where
  * <= 16 rows fit (XF_MIX); bit 1 runs whole narrow-stage blocks (C <= 128) as

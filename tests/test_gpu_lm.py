@@ -111,3 +111,32 @@ def _lm_real_shapes(eng, sd, cfg, ctx):
         torch.cuda.synchronize()
         print("step", s, rel_err(h, ref), cos(h, ref))
         assert rel_err(h, ref) < 2e-2 and cos(h, ref) > 0.999
+
+
+def test_rope_table_bit_identical():
+    """The q|k|v epilogue's per-position cos / sin table (k_rope_table) vs the
+    inline cosf / sinf: identical hidden states, logits and KV caches after a
+    3,000-row prefill (the 256^2-tile GEMM path) and two decode steps."""
+    from vibevoice_amd import _lib
+    cfg = tiny_config(hidden=1536, layers=2, heads=12, kv_heads=2, inter=8960)
+    outs = []
+    for tab in (1, 0):
+        _lib.lib().vv_rope_table(tab)
+        try:
+            eng, sd = make_engine(cfg, seed=3, max_batch=1, max_ctx=4096)
+            g = torch.Generator().manual_seed(5)
+            x = torch.randn(3000, 1536, generator=g).bfloat16().to(dev)
+            h0, l0 = eng.lm_forward(x, torch.zeros(3000, **I32), torch.arange(3000).to(**I32),
+                                    torch.tensor([2999]).to(**I32))
+            hs = [h0.clone(), l0.clone()]
+            for s in range(2):
+                xs = torch.randn(1, 1536, generator=g).bfloat16().to(dev)
+                h, lg = eng.lm_forward(xs, torch.zeros(1, **I32), torch.tensor([3000 + s]).to(**I32),
+                                       torch.zeros(1, **I32))
+                hs += [h.clone(), lg.clone()]
+            torch.cuda.synchronize()
+            outs.append(hs)
+        finally:
+            _lib.lib().vv_rope_table(1)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

@@ -357,3 +357,22 @@ int launch_gather_rows(int n, int C, const bf16* src, long long lds, const int* 
                      dst);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
+
+// RoPE cos / sin table: tab[p][j] = bf16(cosf(p * inv_freq[j])), tab[p][64 + j] =
+// bf16(sinf(...)) -- the same fp32 angle and rounding as the q|k|v epilogue's
+// inline form (HF Qwen2RotaryEmbedding: fp32 angles, cos / sin cast to bf16,
+// transformers modeling_qwen2.py:99-134), computed once per engine
+__global__ void k_rope_table(int npos, const float* inv_freq, bf16* tab) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long long)npos * 64) return;
+  const int p = (int)(e >> 6), j = (int)(e & 63);
+  const float f = (float)p * inv_freq[j];
+  tab[(long long)p * 128 + j] = tobf(cosf(f));
+  tab[(long long)p * 128 + 64 + j] = tobf(sinf(f));
+}
+
+int launch_rope_table(int npos, const float* inv_freq, bf16* tab, hipStream_t st) {
+  const long long n = (long long)npos * 64;
+  hipLaunchKernelGGL(k_rope_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, npos, inv_freq, tab);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

@@ -160,6 +160,7 @@ struct vv_ctx {
   };
   std::unordered_map<int, Chain> head_chain;
   DevBuf chain_sync, chain_slabs, chain_err, coef_dev;
+  DevBuf rope_tab;   // [max_ctx][cos 64 | sin 64] bf16 (k_rope_table)
 };
 
 // ------------------------------------------------------------------ helpers
@@ -609,7 +610,7 @@ void vv_destroy(vv_ctx* c) {
   (void)hipDeviceSynchronize();
   DevBuf* bufs[] = {&c->norm_ws, &c->kv_k, &c->kv_v, &c->lm_ws, &c->attn_part, &c->attn_cnt, &c->valid_ids, &c->splitk_ws, &c->splitk_cnt,
                     &c->temb, &c->tfreq_tmp, &c->head_ws, &c->codec_ws, &c->slot_scratch, &c->unit_sb,
-                    &c->chain_sync, &c->chain_slabs, &c->chain_err, &c->coef_dev};
+                    &c->chain_sync, &c->chain_slabs, &c->chain_err, &c->coef_dev, &c->rope_tab};
   for (DevBuf* b : bufs) b->release();
   for (auto& kv : c->head_chain) kv.second.ops.release();
   ConvNet* nets[] = {&c->dec, &c->sem, &c->aenc};
@@ -715,6 +716,12 @@ int vv_finalize(vv_ctx* c) {
   const size_t kvb = (size_t)c->kv.s_layer * k.n_layers * sizeof(bf16);
   CHK(c->kv_k.ensure(kvb));
   CHK(c->kv_v.ensure(kvb + 256));
+  // RoPE cos / sin per position (the q|k|v epilogue reads it instead of cosf / sinf)
+  if (d == 128) {
+    CHK(c->rope_tab.ensure((size_t)c->kv.max_ctx * 128 * sizeof(bf16)));
+    KCHK(launch_rope_table(c->kv.max_ctx, (const float*)W(c, "lm.inv_freq"), (bf16*)c->rope_tab.p, nullptr));
+    HIPCHK(hipDeviceSynchronize());
+  }
   c->kv.k = (bf16*)c->kv_k.p;
   c->kv.v = (bf16*)c->kv_v.p;
   // ---- attention split partials for decode (2 * max_batch rows, <= 64 splits) + tickets
@@ -802,6 +809,12 @@ int vv_embed(vv_ctx* c, int n, const int* ids, void* out, vv_stream vst) {
 }
 
 // ------------------------------------------------------------------ LM pass
+// test switch (vv_rope_table): 0 = the q|k|v epilogue computes cos / sin inline
+static int g_rope_tab = 1;
+extern "C" int vv_rope_table(int on) {
+  g_rope_tab = on;
+  return 0;
+}
 // One forward of ntok token rows, split so that a tensor-parallel group can
 // interleave its ranks layer by layer (vv_lm_forward_group) or all-reduce over
 // RCCL between the halves (vv_lm_forward).
@@ -876,6 +889,7 @@ static int lm_attn_half(vv_ctx* c, LmPass& P, int l, hipStream_t st) {
     g.rope.slots = P.slot;
     g.rope.pos = P.pos;
     g.rope.inv_freq = P.inv_freq;
+    g.rope.cs_tab = g_rope_tab ? (const bf16*)c->rope_tab.p : nullptr;
     g.rope.kv = c->kv;
     CHK(gemm(c, g, st));
   }

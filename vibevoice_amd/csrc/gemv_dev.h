@@ -148,11 +148,29 @@ DEV void epi_rope(const GemmArgs& a, int m, int n0, int lane, float v[4]) {
     if (g >= 2 || m >= a.M) return;
     const int j = 8 * tt + 4 * g;
     const int p = R.pos[m];
+    // cos / sin: the engine's table holds exactly bf16(cosf / sinf(p * inv_freq))
+    // (k_rope_table), so the table and the inline form are bit-identical
+    float cs4[4], sn4[4];
+    if (R.cs_tab) {
+      const bf16x4 c4 = *(const bf16x4*)(R.cs_tab + (long long)p * d + j);
+      const bf16x4 s4 = *(const bf16x4*)(R.cs_tab + (long long)p * d + 64 + j);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        cs4[i] = bf(c4[i]);
+        sn4[i] = bf(s4[i]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float f = (float)p * R.inv_freq[j + i];
+        cs4[i] = rb(cosf(f));
+        sn4[i] = rb(sinf(f));
+      }
+    }
     bf16x4 o1, o2;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float f = (float)p * R.inv_freq[j + i];
-      const float cs = rb(cosf(f)), sn = rb(sinf(f));
+      const float cs = cs4[i], sn = sn4[i];
       o1[i] = tobf(rb(v[i] * cs) + rb(-u[i] * sn));
       o2[i] = tobf(rb(u[i] * cs) + rb(v[i] * sn));
     }

@@ -46,6 +46,7 @@ struct RopeEpi {         // EPI_ROPE
   const int* slots;      // [M] KV slot of row
   const int* pos;        // [M] position == cache index written
   const float* inv_freq; // [d/2]
+  const bf16* cs_tab;    // [max_ctx][cos d/2 | sin d/2] = bf16(cos / sin(pos * inv_freq)), or nullptr
   KVLayout kv;
 };
 
@@ -227,6 +228,7 @@ int launch_vae_features(int rows, int D, int frames, const bf16* mean, const bf1
                         const bf16* s, const bf16* b, bf16* out, hipStream_t st);
 int launch_head_cond(int steps, int R, int H, const bf16* condp, const bf16* temb, bf16* out, hipStream_t st);
 int launch_silu(int n, const bf16* x, bf16* y, hipStream_t st);
+int launch_rope_table(int npos, const float* inv_freq, bf16* tab, hipStream_t st);
 int launch_cfg_dpm(int n, int D, DpmCoef k, const bf16* eps, bf16* x, bf16* m1, const float* noise, hipStream_t st);
 int launch_gather_rows(int n, int C, const bf16* src, long long lds, const int* idx, RowMap dst, hipStream_t st);
 int launch_copy_rows1(int n, int C, const bf16* src, long long lds, RowMap dst, hipStream_t st);
