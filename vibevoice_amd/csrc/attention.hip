@@ -494,6 +494,9 @@ constexpr int PF_STAGE = 16 * 512;   // bf16 elements per staged step: 8 K + 8 V
 #ifndef VV_PF_NS
 #define VV_PF_NS 2
 #endif
+#ifndef VV_PF_ABL
+#define VV_PF_ABL 0
+#endif
 constexpr int PF_NS = VV_PF_NS;
 
 // max / sum over lanes {l, l^16, l^32, l^48} (one query column of an MFMA
@@ -572,7 +575,7 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
   // c = j & 3; lane row r' -> key 8(r' >> 2) + 4kt + (r' & 3)), j >= 8 V^T
   // fragment dt = j - 8 (dims 16dt + r', keys 8g' .. 8g'+7); both advance by
   // 128 elements per key
-  const int ni = (16 - wave + G - 1) / G;
+  const int ni = __builtin_amdgcn_readfirstlane((16 - wave + G - 1) / G);   // wave-uniform: scalar branches in issue()
   int soff[NI_MAX];   // element offset in the step's 32-key K block / V block (< 4096)
 #pragma unroll
   for (int i = 0; i < NI_MAX; ++i) {
@@ -617,6 +620,9 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
     const bf16* K = a.kv.k + cbase;    // [ctx][128]
     const bf16* VB = a.kv.v + cbase;   // 32-position blocks of [128][32] (v_off)
     auto issue = [&](int step) {
+#if VV_PF_ABL == 1
+      return;   // ablation (timing only): no K/V staging
+#endif
       bf16* st = sm + (step % PF_NS) * PF_STAGE;
 #pragma unroll
       for (int i = 0; i < NI_MAX; ++i)
@@ -630,7 +636,8 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
     for (int p = 0; p < PF_NS - 1 && p < nsteps; ++p) issue(p);
     for (int step = 0; step < nsteps; ++step) {
       // this wave's loads of `step` have landed (steps step + 1 .. step + NS - 2 stay in flight)
-      wait_vm(ni * min(PF_NS - 2, nsteps - 1 - step));
+      if (PF_NS == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (no runtime switch: n is always 0)
+      else wait_vm(ni * min(PF_NS - 2, nsteps - 1 - step));
       // ONE barrier per step: every wave's loads of `step` are in LDS, and every
       // wave has finished reading step - 1, whose buffer takes step + NS - 1
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -685,13 +692,21 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
       bf16x8 pf[2];
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
-        const bool live = m[qt] != -INFINITY;
+        // branch-free: a column with no live key yet has every x = -inf, so any
+        // finite reference gives p = 0; the raw v_exp_f32 (the libm exp2f wraps
+        // it in a denormal-range fix-up, 5 VALU per value) flushes results below
+        // 2^-126, far under a bf16 P's resolution next to the row's max of 1..2^8
+        const float mref = m[qt] != -INFINITY ? m[qt] : 0.f;
         float ps = 0.f;
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float p = live ? exp2f(x[qt][kt][i] - m[qt]) : 0.f;
+#if VV_PF_ABL == 2
+            const float p = x[qt][kt][i] - mref;   // ablation (timing only): no exp
+#else
+            const float p = __builtin_amdgcn_exp2f(x[qt][kt][i] - mref);
+#endif
             ps += p;
             pf[qt][4 * kt + i] = (bf16)p;
           }
