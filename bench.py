@@ -41,7 +41,7 @@ METRIC = "audio-sec/wall-sec (RTF) + acoustic tokens/sec, VibeVoice-1.5B at 1/2/
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=750, help="timed steps (SURVEY.md §8d C2: K = 750, 100 s of audio)")
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=1, help="dialogues per GPU")
     ap.add_argument("--speakers", type=int, default=1)

@@ -1317,14 +1317,25 @@ int launch_gemm(GemmArgs a, hipStream_t st) {
     if (a.xf.kind == XF_MIX) {
       const size_t lds = gemv_mix_lds(a.M, a.xf.T, a.K);
       if (mrep != 1 || a.ksplit != 1 || !lds || (64 * p.nw) % (a.K / 8) || a.xf.ctx != 6) return 1;
+      // tiles per workgroup (diagnostic plans only so far): the Block1D front half is
+      // recomputed once per workgroup, so fewer, wider workgroups recompute it less
+      const int mt = (p.tpw == 2 || p.tpw == 4) && p.nw % p.tpw == 0 ? p.tpw : 1;
+      a.tpw = mt;
+      grid.x = (a.N / 16 + mt - 1) / mt;
       static bool attr = false;   // > 64 KB of dynamic LDS needs the opt-in (one workgroup may hold 160 KiB)
       if (!attr) {
         if (hipFuncSetAttribute((const void*)k_gemv1<4, XF_MIX>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                98304) != hipSuccess ||
+            hipFuncSetAttribute((const void*)k_gemv1<4, XF_MIX, false, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                98304) != hipSuccess ||
+            hipFuncSetAttribute((const void*)k_gemv1<4, XF_MIX, false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 98304) != hipSuccess)
           return 2;
         attr = true;
       }
-      hipLaunchKernelGGL((k_gemv1<4, XF_MIX>), grid, block, lds, st, a);
+      if (mt == 4) hipLaunchKernelGGL((k_gemv1<4, XF_MIX, false, 4>), grid, block, lds, st, a);
+      else if (mt == 2) hipLaunchKernelGGL((k_gemv1<4, XF_MIX, false, 2>), grid, block, lds, st, a);
+      else hipLaunchKernelGGL((k_gemv1<4, XF_MIX>), grid, block, lds, st, a);
       return hipGetLastError() == hipSuccess ? 0 : 2;
     }
     switch (a.xf.kind) {
