@@ -4,8 +4,8 @@
 set -u
 pairs=$1; A=$2; B=$3
 run() {
-  if [ "$1" = base ]; then timeout -k 10 150 python bench.py --steps 200 --no-cpu-baseline
-  else timeout -k 10 150 python tools/ab_bench.py $1 --steps 200 --no-cpu-baseline; fi
+  if [ "$1" = base ]; then timeout -k 10 150 python bench.py --steps ${STEPS:-200} --no-cpu-baseline
+  else timeout -k 10 150 python tools/ab_bench.py $1 --steps ${STEPS:-200} --no-cpu-baseline; fi
 }
 for i in $(seq $pairs); do
   for v in "$A" "$B"; do

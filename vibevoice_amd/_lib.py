@@ -78,6 +78,7 @@ EXPORTS = [
     ("vv_gemm_tune_apack", I, [I]),
     ("vv_gemv_tune_shape", I, [I, I, I, I, I, I, I]),
     ("vv_rope_table", I, [I]),
+    ("vv_attn_defer", I, [I, I]),
 ]
 
 EPI = {"store": 0, "gelu": 1, "silu_mul": 2, "res": 3, "f32": 4}

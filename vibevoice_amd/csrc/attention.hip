@@ -225,7 +225,7 @@ __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
     }
     res[q] = sum;
   }
-  if (nact == 1) {
+  if (nact == 1 && !a.defer) {
 #pragma unroll
     for (int q = 0; q < NE; ++q) {
       const int e = t + q * 64 * NW;
@@ -246,7 +246,7 @@ __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
   // reads them with sc1 loads.  No release / acquire fence: an agent fence
   // writes back the XCD's whole L2 (MI355X_MICROARCH.md "publish-large", the
   // hand-off table's first row).
-  const bool wt = !a.merge;
+  const bool wt = !a.merge && !a.defer;
 #pragma unroll
   for (int q = 0; q < NE; ++q) {
     const int e = t + q * 64 * NW;
@@ -268,7 +268,7 @@ __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
       }
     }
   }
-  if (!wt) return;    // k_attn_merge runs next
+  if (!wt) return;    // k_attn_merge or the consumer's merge (defer) runs next
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t == 0) {
@@ -822,8 +822,9 @@ int launch_attn(AttnArgs a, hipStream_t st) {
   if (a.kv.d != 128 || a.nh % a.nkv || a.nh / a.nkv > ATT_GMAX) return 1;
   if (a.prefill) return launch_attn_pf(a, st);
   if (a.chunk % ATT_KC || a.nsplit > ATT_SPLITS_MAX) return 1;
-  if (a.nsplit > 1 && (!a.part_o || !a.part_ml || !a.counters)) return 1;
-  a.merge = a.nsplit > (g_att_merge_in >= 0 ? g_att_merge_in : ATT_MERGE_IN) ? 1 : 0;
+  if ((a.nsplit > 1 || a.defer) && (!a.part_o || !a.part_ml || !a.counters)) return 1;
+  if (a.defer && a.nsplit > ATT_MERGE_IN) return 1;
+  a.merge = !a.defer && a.nsplit > (g_att_merge_in >= 0 ? g_att_merge_in : ATT_MERGE_IN) ? 1 : 0;
   dim3 grid(a.nq * a.nkv, a.nsplit);
   const int nw = a.chunk >= 256 ? 8 : a.chunk >= 128 ? 4 : 2;   // 32 keys per wave step
   if (nw == 8) launch_attn_nw<8>(a, grid, st);

@@ -95,6 +95,7 @@ enum {
   XF_NORM = 1,       // a = RMSNorm(row)[*w][modulate(shift, scale)]   (row = whole K)
   XF_SILU_ADD = 2,   // a = bf16(silu(bf16(row + vec)))
   XF_MIX = 3,        // a = ffn_norm(x + gamma * dwconv(norm(x)))  (codec Block1D, M <= 16)
+  XF_ATTN_MERGE = 4, // a = the attention output merged from its key splits' partials (o_proj, M <= 16)
 };
 
 struct EpiArgs {

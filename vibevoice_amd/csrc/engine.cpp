@@ -818,8 +818,19 @@ extern "C" int vv_rope_table(int on) {
 // One forward of ntok token rows, split so that a tensor-parallel group can
 // interleave its ranks layer by layer (vv_lm_forward_group) or all-reduce over
 // RCCL between the halves (vv_lm_forward).
+// Decode attention with a deferred split merge (vv_attn_defer): contexts of 2..8
+// chunks of g_defer_chunk keys run that many splits per (row, kv head), each
+// leaves its (m, l, o) partial and o_proj merges them while staging its A rows
+// (XF_ATTN_MERGE) -- the split parallelism without a ticket or a merge pass.
+static int g_attn_defer = 1, g_defer_chunk = 256;
+extern "C" int vv_attn_defer(int on, int chunk) {
+  if (chunk % 32 || chunk < 32) return 1;
+  g_attn_defer = on;
+  g_defer_chunk = chunk;
+  return 0;
+}
 struct LmPass {
-  int ntok = 0, nsplit = 1, chunk = 64, prefill = 0;
+  int ntok = 0, nsplit = 1, chunk = 64, prefill = 0, defer = 0;
   bf16 *h = nullptr, *q = nullptr, *att = nullptr, *act = nullptr;
   RowMap in_m, hm;
   const int *slot = nullptr, *pos = nullptr;
@@ -846,6 +857,15 @@ static int lm_begin(vv_ctx* c, LmPass& P, int ntok, const void* embeds, int embe
   P.act = P.att + (size_t)ntok * nhd;
   P.prefill = attn_use_prefill(ntok, c->lm_slots) ? 1 : 0;
   P.nsplit = P.prefill ? 1 : attn_plan(ntok, k.n_kv_heads, max_pos_p1, &P.chunk);
+  P.defer = 0;
+  if (!P.prefill && g_attn_defer && ntok <= 16 && k.head_dim == 128) {
+    const int ns = (max_pos_p1 + g_defer_chunk - 1) / g_defer_chunk;
+    if (ns >= 2 && ns <= 8) {
+      P.defer = 1;
+      P.nsplit = ns;
+      P.chunk = g_defer_chunk;
+    }
+  }
   if (P.nsplit > 1) {
     if ((size_t)ntok * k.n_kv_heads > 65536) FAIL("attention split tickets exhausted");
     CHK(c->attn_part.ensure((size_t)ntok * k.n_heads * P.nsplit * (d + 2) * sizeof(float)));
@@ -903,6 +923,7 @@ static int lm_attn_half(vv_ctx* c, LmPass& P, int l, hipStream_t st) {
   at.nsplit = P.nsplit;
   at.chunk = P.chunk;
   at.prefill = P.prefill;
+  at.defer = P.defer;
   at.counters = (unsigned*)c->attn_cnt.p;
   at.scale = 1.0f / sqrtf((float)d);
   at.q = P.q;
@@ -914,6 +935,14 @@ static int lm_attn_half(vv_ctx* c, LmPass& P, int l, hipStream_t st) {
   at.part_ml = at.part_o ? at.part_o + (size_t)P.ntok * k.n_heads * P.nsplit * d : nullptr;
   KCHK(launch_attn(at, st));
   GemmArgs g = gemm_args(c, P.ntok, H, nhd, rowmap(P.att, nhd), W(c, p + ".o_w"), EPI_RES, P.hm);
+  if (P.defer) {
+    g.xf.kind = XF_ATTN_MERGE;
+    g.xf.part_o = at.part_o;
+    g.xf.part_ml = at.part_ml;
+    g.xf.qpos = P.pos;
+    g.xf.nsplit = P.nsplit;
+    g.xf.chunk = P.chunk;
+  }
   tp_residual(c, g, l == 0 ? P.in_m : P.hm);
   CHK(gemm(c, g, st));
   return 0;

@@ -156,7 +156,62 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   bf16x8 wa[U], wb[U];
   constexpr int Q = 4;                   // A items per thread on the fast path
   const bool fast = a.M * n8 <= Q * (int)blockDim.x;
-  if (XF == XF_MIX) {
+  if (XF == XF_ATTN_MERGE) {
+    // o_proj's A rows = the decode attention output, merged from the key splits'
+    // partials k_attn left (AttnArgs::defer): out = sum_s e^{m_s - M} o_s /
+    // sum_s e^{m_s - M} l_s in split order -- the attention kernel's own merge
+    // term for term (bit-identical), one round trip of partial loads here instead
+    // of a ticket + merge at the attention's tail.  Item (m, 8 dims of head hq).
+    const int nsp = a.xf.nsplit;
+#pragma unroll 1
+    for (int e = threadIdx.x; e < a.M * n8; e += blockDim.x) {
+      const int m = e / n8, k = (e - m * n8) * 8;
+      const int hq = k >> 7, j0 = k & 127;
+      const int len = a.xf.qpos[m] + 1;
+      const int cc = (len + nsp - 1) / nsp;
+      const int rch = max(a.xf.chunk, (cc + 31) / 32 * 32);
+      const int nact = (len + rch - 1) / rch;
+      const long long p0 = ((long long)m * (a.K >> 7) + hq) * nsp;
+      float mv[8], lv[8];
+      float4 o0[8], o1[8];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        if (s < nact) {
+          const float2 ml = *(const float2*)(a.xf.part_ml + (p0 + s) * 2);
+          mv[s] = ml.x;
+          lv[s] = ml.y;
+          o0[s] = *(const float4*)(a.xf.part_o + (p0 + s) * 128 + j0);
+          o1[s] = *(const float4*)(a.xf.part_o + (p0 + s) * 128 + j0 + 4);
+        }
+      }
+      float M = -INFINITY;
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+        if (s < nact) M = fmaxf(M, mv[s]);
+      float num[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, den = 0.f;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        if (s < nact) {
+          const float w = __expf(mv[s] - M);
+          num[0] += w * o0[s].x;
+          num[1] += w * o0[s].y;
+          num[2] += w * o0[s].z;
+          num[3] += w * o0[s].w;
+          num[4] += w * o1[s].x;
+          num[5] += w * o1[s].y;
+          num[6] += w * o1[s].z;
+          num[7] += w * o1[s].w;
+          den += w * lv[s];
+        }
+      }
+      bf16x8 o8;
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) o8[jj] = tobf(num[jj] / den);
+      *(bf16x8*)(xs + m * lds_ld + k) = o8;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
+  } else if (XF == XF_MIX) {
     // Codec Block1D front half for the M = ns * T rows (k_mix's math and
     // summation order, elementwise.hip): every workgroup recomputes it (a few
     // tens of KB of L2 reads next to its weight slice); workgroup 0 also stores
@@ -1336,6 +1391,15 @@ int launch_gemm(GemmArgs a, hipStream_t st) {
       if (mt == 4) hipLaunchKernelGGL((k_gemv1<4, XF_MIX, false, 4>), grid, block, lds, st, a);
       else if (mt == 2) hipLaunchKernelGGL((k_gemv1<4, XF_MIX, false, 2>), grid, block, lds, st, a);
       else hipLaunchKernelGGL((k_gemv1<4, XF_MIX>), grid, block, lds, st, a);
+      return hipGetLastError() == hipSuccess ? 0 : 2;
+    }
+    if (a.xf.kind == XF_ATTN_MERGE) {   // o_proj on the attention's split partials: one plan form
+      if (mrep != 1 || a.xf.nsplit < 1 || a.xf.nsplit > 8 || a.K % 128 || !a.xf.part_o || !a.xf.part_ml || !a.xf.qpos)
+        return 1;
+      a.ksplit = 1;
+      a.tpw = 1;
+      const size_t lds = gemv1_lds(a);
+      hipLaunchKernelGGL((k_gemv1<8, XF_ATTN_MERGE, false, 1>), dim3(a.N / 16, 1), block, lds, st, a);
       return hipGetLastError() == hipSuccess ? 0 : 2;
     }
     switch (a.xf.kind) {

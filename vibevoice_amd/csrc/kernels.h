@@ -38,6 +38,12 @@ struct ATransform {
   const int* slots;
   const bf16 *dw_w, *dw_b, *gamma, *ffn_w;
   bf16* y;               // residual rows y (fc2's residual), [M][K]
+  // XF_ATTN_MERGE: o_proj's A rows = the decode attention output, merged here
+  // from the key splits' (m, l, o) partials that k_attn left (AttnArgs::defer)
+  const float* part_o;   // [M][nh][nsplit][128]
+  const float* part_ml;  // [M][nh][nsplit][2]
+  const int* qpos;       // [M] query position (row m attends keys 0..qpos[m])
+  int nsplit, chunk;     // the attention launch's plan (row_chunk)
 };
 
 struct RopeEpi {         // EPI_ROPE
@@ -165,6 +171,7 @@ struct AttnArgs {
   unsigned* counters;   // [nq * nkv] split tickets (zero between launches)
   unsigned long long* stamps;   // diagnostics only (tools/attn_stamps.py): 4 stamps per workgroup
   int prefill;          // 1: k_attn_pf (query rows in runs sharing a slot; no splits), see attn_use_prefill
+  int defer;            // 1: every active split writes its partial, the consumer (o_proj, XF_ATTN_MERGE) merges
 };
 
 // out_r = sum_r in_r for every r (single-process tensor-parallel group)
