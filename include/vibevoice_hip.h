@@ -252,10 +252,10 @@ int vv_gemv_tune_shape(int N, int K, int mmax, int nw, int ks, int u, int tpw);
  * per-position bf16 cos / sin table; 0 = computes cosf / sinf inline
  * (bit-identical by construction). */
 int vv_rope_table(int on);
-/* Test switch: 1 (default) = decode attention over 2..8 chunks of `chunk` keys
- * (multiple of 32) runs that many key splits and leaves their partials to
- * o_proj, which merges them while staging its A rows (bit-identical to the
- * same splits merged in the attention kernel); 0 = the attn_plan splits. */
+/* Test switch: 1 (default, chunk 128) = decode attention over up to 8,192 keys
+ * runs 2..8 key splits of >= `chunk` keys (multiple of 32) and leaves their
+ * partials to o_proj, which merges them while staging its A rows (bit-identical
+ * to the same splits merged in the attention kernel); 0 = the attn_plan splits. */
 int vv_attn_defer(int on, int chunk);
 /* Test switch (bit mask, default 3): bit 0 folds each codec Block1D's mixer
  * (norm, depthwise conv, gamma residual, FFN norm) into its fc1 GEMV where

@@ -142,38 +142,41 @@ def test_rope_table_bit_identical():
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("nrows", [2, 12])
-def test_attn_defer_bit_identical(nrows):
+@pytest.mark.parametrize("nrows,chunk,maxpos", [(2, 256, 1790), (12, 256, 1790), (4, 128, 3000)])
+def test_attn_defer_bit_identical(nrows, chunk, maxpos):
     """Deferred split merge (vv_attn_defer: k_attn leaves every split's partial,
-    o_proj's XF_ATTN_MERGE staging merges them) vs the same 256-key splits merged
-    inside k_attn (vv_attn_tune): identical hidden states and logits; and close
-    to the default one-split plan.  Rows at contexts from 1 to 7 splits (nact 1
-    rows take the merge's trivial case)."""
+    o_proj's XF_ATTN_MERGE staging merges them) vs the same splits merged inside
+    k_attn (vv_attn_tune with the chunk the engine picks: `chunk`, or 8 splits
+    of ceil(max / 8) rounded to 32 keys past 8 chunks): identical hidden states
+    and logits; and close to the default 1,024-key plan.  Rows at contexts from
+    1 key to 8 splits (nact 1 rows take the merge's trivial case)."""
     from vibevoice_amd import _lib
     L = _lib.lib()
     cfg = tiny_config(hidden=1536, layers=2, heads=12, kv_heads=2, inter=8960)
-    eng, _ = make_engine(cfg, seed=4, max_batch=nrows, max_ctx=2048)
+    eng, _ = make_engine(cfg, seed=4, max_batch=nrows, max_ctx=4096)
     slots = torch.arange(nrows).to(**I32)
-    eng.kv_synthetic(slots, 0, 2048, seed=11)
+    eng.kv_synthetic(slots, 0, 4096, seed=11)
     g = torch.Generator().manual_seed(9)
     x = torch.randn(nrows, 1536, generator=g).bfloat16().to(dev)
-    pos = torch.tensor([(97 + 263 * i) % 1790 for i in range(nrows)], dtype=torch.int32).to(dev)
-    pos[0] = 1789                                  # 7 splits of 256 keys
+    pos = torch.tensor([(97 + 263 * i) % maxpos for i in range(nrows)], dtype=torch.int32).to(dev)
+    pos[0] = maxpos - 1
     if nrows > 2:
         pos[1] = 3                                 # one split
+    ns = -(-maxpos // chunk)
+    eff = chunk if ns <= 8 else (-(-maxpos // 8) + 31) // 32 * 32
     outs = {}
     try:
-        for name, defer, chunk in (("defer", 1, 0), ("inkernel", 0, 256), ("default", 0, 0)):
-            _lib.check(L.vv_attn_defer(defer, 256), "attn_defer")
-            _lib.check(L.vv_attn_tune(chunk, -1), "attn_tune")
+        for name, defer, tune in (("defer", 1, 0), ("inkernel", 0, eff), ("default", 0, 0)):
+            _lib.check(L.vv_attn_defer(defer, chunk), "attn_defer")
+            _lib.check(L.vv_attn_tune(tune, -1), "attn_tune")
             h, lg = eng.lm_forward(x, slots, pos, torch.arange(nrows).to(**I32))
             torch.cuda.synchronize()
             outs[name] = (h.clone(), lg.clone())
     finally:
-        L.vv_attn_defer(1, 256)
+        L.vv_attn_defer(1, 128)
         L.vv_attn_tune(0, -1)
     assert torch.equal(outs["defer"][0], outs["inkernel"][0])
     assert torch.equal(outs["defer"][1], outs["inkernel"][1])
     h, ref = outs["defer"][0].float(), outs["default"][0].float()
-    print("vs one split", rel_err(h, ref), cos(h, ref))
+    print("vs 1,024-key plan", rel_err(h, ref), cos(h, ref))
     assert rel_err(h, ref) < 1e-2 and cos(h, ref) > 0.9999

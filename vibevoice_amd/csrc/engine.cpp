@@ -822,7 +822,7 @@ extern "C" int vv_rope_table(int on) {
 // chunks of g_defer_chunk keys run that many splits per (row, kv head), each
 // leaves its (m, l, o) partial and o_proj merges them while staging its A rows
 // (XF_ATTN_MERGE) -- the split parallelism without a ticket or a merge pass.
-static int g_attn_defer = 1, g_defer_chunk = 256;
+static int g_attn_defer = 1, g_defer_chunk = 128;
 extern "C" int vv_attn_defer(int on, int chunk) {
   if (chunk % 32 || chunk < 32) return 1;
   g_attn_defer = on;
@@ -859,11 +859,17 @@ static int lm_begin(vv_ctx* c, LmPass& P, int ntok, const void* embeds, int embe
   P.nsplit = P.prefill ? 1 : attn_plan(ntok, k.n_kv_heads, max_pos_p1, &P.chunk);
   P.defer = 0;
   if (!P.prefill && g_attn_defer && ntok <= 16 && k.head_dim == 128) {
-    const int ns = (max_pos_p1 + g_defer_chunk - 1) / g_defer_chunk;
-    if (ns >= 2 && ns <= 8) {
+    // 2..8 splits of >= g_defer_chunk keys, up to 8 x 1,024 keys (longer contexts
+    // keep attn_plan's many 1,024-key splits: the merge input grows with them)
+    int ch = g_defer_chunk, ns = (max_pos_p1 + ch - 1) / ch;
+    if (ns > 8) {
+      ch = ((max_pos_p1 + 7) / 8 + 31) / 32 * 32;
+      ns = (max_pos_p1 + ch - 1) / ch;
+    }
+    if (ns >= 2 && ns <= 8 && ch <= 1024) {
       P.defer = 1;
       P.nsplit = ns;
-      P.chunk = g_defer_chunk;
+      P.chunk = ch;
     }
   }
   if (P.nsplit > 1) {
