@@ -1116,7 +1116,7 @@ static void launch_gemv_xf(const GemmArgs& a, int mrep, int u, dim3 grid, dim3 b
 //     every k-step, §5 item 4a); s_setprio(1) around the MFMA cluster (T5).
 // K order of accumulation per output is k_gemm's (chunk by chunk): bit-identical.
 #ifndef VV_GX_INTERLEAVE
-#define VV_GX_INTERLEAVE 1
+#define VV_GX_INTERLEAVE 2
 #endif
 // s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] |
 // vmcnt[5:4] << 14; a field at its maximum does not wait).  The builtin, unlike an
@@ -1132,7 +1132,8 @@ constexpr size_t GX_LDS = (size_t)GX_NS * GX_STAGE * 2;   // 128 KB
 
 __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16 smx[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // scalar: the glds LDS bases (M0) too
   const int r = lane & 15, g = lane >> 4;
   const int wr = wave >> 2, wc = wave & 3;
   const int ntm = (a.M + GX_M - 1) / GX_M, ntn = a.N / GX_N, total = ntm * ntn;
@@ -1163,6 +1164,9 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
     return;   // ablation (timing only): no global -> LDS staging
 #endif
     bf16* st = smx + (s & (GX_NS - 1)) * GX_STAGE;
+#if VV_GX_ABL == 3
+    s = 0;    // ablation (timing only): every stage re-loads stage 0 (L2-resident) -- issue cost without misses
+#endif
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int j = 2 * wave + i;
@@ -1171,6 +1175,23 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
       __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + (long long)s * 512),
                                        (__attribute__((address_space(3))) void*)(st + (16 + j) * 512), 16, 0, 0);
     }
+  };
+  // one of a stage's 4 glds pieces per wave (q: block i = q >> 1, A (even) or W (odd))
+  auto issue_piece = [&](int s, int q) {
+#if VV_GX_ABL == 1
+    return;
+#endif
+    bf16* st = smx + (s & (GX_NS - 1)) * GX_STAGE;
+#if VV_GX_ABL == 3
+    s = 0;
+#endif
+    const int i = q >> 1, j = 2 * wave + i;
+    if (q & 1)
+      __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + (long long)s * 512),
+                                       (__attribute__((address_space(3))) void*)(st + (16 + j) * 512), 16, 0, 0);
+    else
+      __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + (a.apack ? (long long)s * 512 : (long long)s * 32)),
+                                       (__attribute__((address_space(3))) void*)(st + j * 512), 16, 0, 0);
   };
   f32x4 acc[4][8];   // [weight tile nt][row tile mt]
 #pragma unroll
@@ -1190,24 +1211,30 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
     for (int mt = 0; mt < 8; ++mt) xf[mt] = *(const bf16x8*)(st + (wr * 8 + mt) * 512 + lane * 8);
   };
   auto macs = [&](const bf16x8 (&wf)[4], const bf16x8 (&xf)[8]) {
+#if !VV_GX_INTERLEAVE
     __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
       for (int mt = 0; mt < 8; ++mt) acc[nt][mt] = mfma(wf[nt], xf[mt], acc[nt][mt]);
-    __builtin_amdgcn_s_setprio(0);
-    // keep the MFMAs above the next step's asm waits ("memory" does not order
-    // register-only instructions, cdna_hip_programming.md §5.7 rule 18)
-    __builtin_amdgcn_sched_barrier(0);
 #if VV_GX_INTERLEAVE
-    // 4 groups: 1 glds (when issued), 3 ds_reads of the next stage, 8 MFMAs
+    // the step's 4 glds and 12 ds_reads (of the next stage) spread between its 32
+    // MFMAs, so their issue cost hides under the matrix pipe: 4 groups of 1 glds,
+    // 3 ds_reads, 8 MFMAs.  (s_setprio is a scheduling boundary: with it around the
+    // MFMAs every load issued ahead of them, the pipe idle meanwhile.)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // VMEM read (glds)
       __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);   // DS read
       __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);   // MFMA
     }
+#else
+    __builtin_amdgcn_s_setprio(0);
 #endif
+    // keep the MFMAs above the next step's asm waits ("memory" does not order
+    // register-only instructions, cdna_hip_programming.md §5.7 rule 18)
+    __builtin_amdgcn_sched_barrier(0);
   };
   // ring: stages s + 1 .. s + 3 in flight while stage s computes; exactly 4 glds
   // per wave per step (stages past the end re-load the last one into a buffer
@@ -1223,6 +1250,39 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
   bf16x8 wa[4], xa[8], wb[4], xb[8];
   frags(0, wa, xa);
   int s = 0;
+#if VV_GX_INTERLEAVE == 2
+  // A step in 4 pinned groups (sched_barrier fences): 1 glds piece of stage
+  // s + 4, 3 fragment reads of stage s + 1, then the 8 MFMAs of weight tile nt = q
+  // on stage s -- the loads' issue cost (M0 set-up, ~60+ cycles per LDS-DMA
+  // piece) sits between MFMAs instead of in front of all 32 with the matrix pipe
+  // idle.  Hand-placed: sched_group_barrier did not move the glds.
+  auto step = [&](int sis, int srd, const bf16x8 (&wf)[4], const bf16x8 (&xf)[8], bf16x8 (&wn)[4],
+                  bf16x8 (&xn)[8]) {
+    const bf16* st = smx + (srd & (GX_NS - 1)) * GX_STAGE;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      issue_piece(sis, q);
+#pragma unroll
+      for (int f = 3 * q; f < 3 * q + 3; ++f) {
+#if VV_GX_ABL != 2
+        if (f < 4) wn[f] = *(const bf16x8*)(st + (16 + wc * 4 + f) * 512 + lane * 8);
+        else xn[f - 4] = *(const bf16x8*)(st + (wr * 8 + f - 4) * 512 + lane * 8);
+#endif
+      }
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) acc[q][mt] = mfma(wf[q], xf[mt], acc[q][mt]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  for (; s + 1 < nch; s += 2) {
+    __builtin_amdgcn_s_waitcnt(WC_VM8_LGKM0);
+    __builtin_amdgcn_s_barrier();
+    step(min(s + 4, last), s + 1, wa, xa, wb, xb);
+    __builtin_amdgcn_s_waitcnt(WC_VM8_LGKM0);
+    __builtin_amdgcn_s_barrier();
+    step(min(s + 5, last), min(s + 2, last), wb, xb, wa, xa);
+  }
+#else
   for (; s + 1 < nch; s += 2) {
     // ---- step s: compute stage s (set a), read stage s + 1 (set b)
     __builtin_amdgcn_s_waitcnt(WC_VM8_LGKM0);
@@ -1237,6 +1297,7 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
     frags(min(s + 2, last), wa, xa);
     macs(wb, xb);
   }
+#endif
   if (s < nch) {   // odd stage count: the last stage is in set a
     __builtin_amdgcn_s_waitcnt(WC_LGKM0);
     macs(wa, xa);
@@ -1248,6 +1309,48 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
   // accumulators through one register tile cost ~4,000 moves per wave -- 30 % of
   // a K = 1536 tile)
   __syncthreads();   // every wave is past its reads of the last stage
+#if VV_GX_ABL != 4
+  if (epi_row8_ok(a)) {
+    // row-contiguous form: per wave and pass, 4 m-tiles x its 4 n-tiles -> LDS
+    // [64 rows][64 cols] f32 (16 KB per wave, the whole ring for 8 waves; odd rows'
+    // float4 slots XOR-shifted by one so the b128 reads below are conflict-free),
+    // then every lane takes 8 consecutive columns of a row: 16-byte stores, 8 rows
+    // x 128 bytes per instruction (SiLU*up: 16 rows x 64 bytes).  A wave reads
+    // only its own region and its LDS ops run in order: no barrier between passes.
+    float* ep = (float*)smx + wave * (64 * 64);
+    auto sw = [](int row, int col) { return row * 64 + (col ^ ((row & 1) << 2)); };
+    const int mb = tm * GX_M + wr * 128, nb = tn * GX_N + wc * 64;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+#pragma unroll
+      for (int mq = 0; mq < 4; ++mq)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) *(f32x4*)(ep + sw(mq * 16 + r, nt * 16 + 4 * g)) = acc[nt][4 * p + mq];
+      if (a.epi.kind == EPI_SILU_MUL) {
+#pragma unroll 1
+        for (int it = 0; it < 4; ++it) {
+          const int row = it * 16 + (lane >> 2), a4 = lane & 3, m = mb + 64 * p + row;
+          float gt[8], up[8];
+          *(f32x4*)gt = *(const f32x4*)(ep + sw(row, 16 * a4));
+          *(f32x4*)(gt + 4) = *(const f32x4*)(ep + sw(row, 16 * a4 + 4));
+          *(f32x4*)up = *(const f32x4*)(ep + sw(row, 16 * a4 + 8));
+          *(f32x4*)(up + 4) = *(const f32x4*)(ep + sw(row, 16 * a4 + 12));
+          if (m < a.M) epi_silu8(a, m, (nb >> 1) + 8 * a4, gt, up);
+        }
+      } else {
+#pragma unroll 1
+        for (int it = 0; it < 8; ++it) {
+          const int row = it * 8 + (lane >> 3), c8 = lane & 7, m = mb + 64 * p + row;
+          float v[8];
+          *(f32x4*)v = *(const f32x4*)(ep + sw(row, 8 * c8));
+          *(f32x4*)(v + 4) = *(const f32x4*)(ep + sw(row, 8 * c8 + 4));
+          if (m < a.M) epi_row8(a, m, nb + 8 * c8, v);
+        }
+      }
+    }
+    return;
+  }
+#endif
   float* ep = (float*)smx + wave * (16 * 256);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -1261,6 +1364,9 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
       float v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = ep[t * 256 + j * 64 + lane];
+#if VV_GX_ABL == 4
+      if (v[0] == 12345.f)   // ablation (timing only): no epilogue stores
+#endif
       epi_tile(a, tm * GX_M + (wr * 8 + (i & 7)) * 16 + r, tn * GX_N + (wc * 4 + (i >> 3)) * 16, lane, v);
     }
   }

@@ -251,6 +251,66 @@ DEV EpiPre epi_prefetch(const GemmArgs& a, int m, int n0, int lane) {
   return p;
 }
 
+// Row-contiguous epilogue forms for tiles staged through LDS (k_gemm_xl): 8
+// consecutive output columns n .. n+7 of row m per lane, so the stores are 16
+// bytes and a wave instruction covers whole 128-byte row segments (epi_tile's
+// lane holds 4 columns x 1 row: 16 rows x 32 bytes per instruction, 16 x 16 for
+// SiLU*up -- the 16K-token gate|up GEMM spent 30 % of its time in those stores).
+// Same arithmetic as epi_tile, value for value.
+DEV bool a16(const void* p) { return ((unsigned long long)p & 15) == 0; }
+DEV bool rm8(const RowMap& r) { return a16(r.base) && r.sT % 8 == 0 && r.sB % 8 == 0; }
+DEV bool epi_row8_ok(const GemmArgs& a) {
+  const EpiArgs& e = a.epi;
+  if (e.kind != EPI_STORE && e.kind != EPI_GELU && e.kind != EPI_RES && e.kind != EPI_SILU_MUL) return false;
+  if (!rm8(e.out) || (e.bias && !a16(e.bias))) return false;
+  if (e.kind == EPI_RES && (!rm8(e.res) || (e.gamma && !a16(e.gamma)) || (e.gate.base && !rm8(e.gate)))) return false;
+  return true;
+}
+DEV void epi_row8(const GemmArgs& a, int m, int n, const float v_in[8]) {
+  const EpiArgs& e = a.epi;
+  float v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = v_in[i];
+  if (e.bias) {
+    const bf16x8 b = *(const bf16x8*)(e.bias + n);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] += bf(b[i]);
+  }
+  bf16x8 o;
+  if (e.kind == EPI_STORE) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = tobf(v[i]);
+  } else if (e.kind == EPI_GELU) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = tobf(gelu_f(rb(v[i])));
+  } else {  // EPI_RES
+    const bf16x8 r = *(const bf16x8*)(rm_bf(e.res, m) + n);
+    float s[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+    bool scaled = false;
+    if (e.gamma || e.gate.base) {
+      const bf16x8 gm = e.gamma ? *(const bf16x8*)(e.gamma + n) : *(const bf16x8*)(rm_bf(e.gate, m) + n);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[i] = bf(gm[i]);
+      scaled = true;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float y = rb(v[i]);
+      if (scaled) y = rb(s[i] * y);
+      o[i] = tobf(bf(r[i]) + y);
+    }
+  }
+  *(bf16x8*)(rm_bfw(e.out, m) + n) = o;
+}
+// SiLU(gate) * up for act columns col .. col+7 of row m (gate / up: the 16-column
+// tile's rows 0..7 / 8..15, epi_tile's EPI_SILU_MUL pairing)
+DEV void epi_silu8(const GemmArgs& a, int m, int col, const float gt[8], const float up[8]) {
+  bf16x8 o;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = tobf(rb(silu_f(rb(gt[i]))) * rb(up[i]));
+  *(bf16x8*)(rm_bfw(a.epi.out, m) + col) = o;
+}
+
 template <class MP = MemPlain>
 DEV void epi_tile(const GemmArgs& a, int m, int n0, int lane, const float v_in[4], const EpiPre* pre = nullptr) {
   const EpiArgs& e = a.epi;
