@@ -11,6 +11,8 @@
 // for one 32-key step are one 8 KB contiguous block.  A row's cache holds only the entries its
 // attention mask keeps, in order, so cache index == RoPE position (SURVEY.md
 // §8a rows a3, a7).
+#include <type_traits>
+
 #include "kernels.h"
 
 
@@ -536,7 +538,10 @@ DEV void wait_vm(int n) {
 }
 
 template <int G>
-__global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >= 4 ? 3 : 1))) k_attn_pf(AttnArgs a) {
+#ifndef VV_PF_WPE
+#define VV_PF_WPE 2
+#endif
+__global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >= 4 ? VV_PF_WPE : 1))) k_attn_pf(AttnArgs a) {
   constexpr int d = 128;
   constexpr int NI_MAX = (16 + G - 1) / G;   // staging instructions per wave and step
   // one LDS array (a second __shared__ object can make hipcc drain the
@@ -644,39 +649,62 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
       if (step + PF_NS - 1 < nsteps) issue(step + PF_NS - 1);
       const int k0 = step * 32;
       const bf16* st = sm + (step % PF_NS) * PF_STAGE;
+      // all 8 K fragments, then the 16 S MFMAs (one LDS round trip, not one per key tile)
+      bf16x8 kf[8];
+#pragma unroll
+      for (int f = 0; f < 8; ++f) kf[f] = *(const bf16x8*)(st + f * 512 + lane * 8);
       f32x4 s[2][2];
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        bf16x8 kf[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) kf[c] = *(const bf16x8*)(st + (kt * 4 + c) * 512 + lane * 8);
+      for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) {
           s[kt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int c = 0; c < 4; ++c) s[kt][qt] = amfma(kf[c], qf[qt][c], s[kt][qt]);
+          for (int c = 0; c < 4; ++c) s[kt][qt] = amfma(kf[kt * 4 + c], qf[qt][c], s[kt][qt]);
         }
-      }
+      // the V^T fragments do not depend on P: issued now, they land under the softmax
+      // (read one at a time after it, each read's latency was exposed 8 times a step)
+      bf16x8 vf[8];
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) vf[dt] = *(const bf16x8*)(st + (8 + dt) * 512 + lane * 8);
+      __builtin_amdgcn_sched_barrier(0);
       // online softmax with a lazy running max: a column's m (log2 units) moves
       // only when a score exceeds it by > PF_LAZY, so P <= 2^PF_LAZY and the
       // O / l rescale (64 multiplies per column pair) runs only on the steps
-      // where some column of the wave moved (a wave-uniform branch)
+      // where some column of the wave moved (a wave-uniform branch).  Steps every
+      // row attends in full (all but the diagonal ones) skip the mask selects.
       const bool full = k0 + 32 <= kfull;
       float x[2][2][4], al[2];
       bool move[2];
+      if (full) {   // raw scores: the max commutes with the positive scale, exp2 takes fma(s, sl2, -m)
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[qt][kt][i] = s[kt][qt][i];
+      } else {
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          const bool in = qt == 0 ? in0 : in1;
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int key = k0 + 8 * g + 4 * kt + i;
+              x[qt][kt][i] = in && key <= qpos[qt] ? s[kt][qt][i] * sl2 : -INFINITY;
+            }
+        }
+      }
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
-        const bool in = qt == 0 ? in0 : in1;
         float mx = -INFINITY;
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int key = k0 + 8 * g + 4 * kt + i;
-            x[qt][kt][i] = full || (in && key <= qpos[qt]) ? s[kt][qt][i] * sl2 : -INFINITY;
-            mx = fmaxf(mx, x[qt][kt][i]);
-          }
+          for (int i = 0; i < 4; ++i) mx = fmaxf(mx, x[qt][kt][i]);
         mx = col_max(mx);
+        if (full) mx *= sl2;
         move[qt] = mx > m[qt] + PF_LAZY;   // also the first live step (m = -inf); lanes of a column agree
         al[qt] = move[qt] ? exp2f(m[qt] - mx) : 1.f;
         if (move[qt]) m[qt] = mx;
@@ -690,42 +718,48 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
         }
       }
       bf16x8 pf[2];
+      // branch-free within a step: a column with no live key yet has every x =
+      // -inf, so any finite reference gives p = 0; the raw v_exp_f32 (the libm
+      // exp2f wraps it in a denormal-range fix-up, 5 VALU per value) flushes
+      // results below 2^-126, far under a bf16 P's resolution next to the row's
+      // max of 1..2^8.  Full steps: p = 2^fma(s, scale, -m) (one VALU less per score)
+      auto probs = [&](auto full_c) {
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        // branch-free: a column with no live key yet has every x = -inf, so any
-        // finite reference gives p = 0; the raw v_exp_f32 (the libm exp2f wraps
-        // it in a denormal-range fix-up, 5 VALU per value) flushes results below
-        // 2^-126, far under a bf16 P's resolution next to the row's max of 1..2^8
-        const float mref = m[qt] != -INFINITY ? m[qt] : 0.f;
-        float ps = 0.f;
+        for (int qt = 0; qt < 2; ++qt) {
+          const float mref = m[qt] != -INFINITY ? m[qt] : 0.f;
+          float ps = 0.f;
 #pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
+          for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < 4; ++i) {
+              const float e = decltype(full_c)::value ? __builtin_fmaf(x[qt][kt][i], sl2, -mref) : x[qt][kt][i] - mref;
 #if VV_PF_ABL == 2
-            const float p = x[qt][kt][i] - mref;   // ablation (timing only): no exp
+              const float p = e;   // ablation (timing only): no exp
 #else
-            const float p = __builtin_amdgcn_exp2f(x[qt][kt][i] - mref);
+              const float p = __builtin_amdgcn_exp2f(e);
 #endif
-            ps += p;
-            pf[qt][4 * kt + i] = (bf16)p;
-          }
-        l[qt] += ps;
+              ps += p;
+              pf[qt][4 * kt + i] = (bf16)p;
+            }
+          l[qt] += ps;
+        }
+      };
+      if (full) probs(std::true_type{});
+      else probs(std::false_type{});
+      // the last step's V past the last key (unwritten cache) would meet P = 0:
+      // zero it (0 * NaN) with a bit mask over the lane's keys 8g .. 8g+7
+      if (k0 + 32 > nk) {
+        const int lim = nk - k0 - 8 * g;
+        u32x4 vm;
+#pragma unroll
+        for (int p2 = 0; p2 < 4; ++p2) vm[p2] = (2 * p2 < lim ? 0xFFFFu : 0u) | (2 * p2 + 1 < lim ? 0xFFFF0000u : 0u);
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) vf[dt] = __builtin_bit_cast(bf16x8, __builtin_bit_cast(u32x4, vf[dt]) & vm);
       }
-      // unwritten V past the last key would meet P = 0: zero it (0 * NaN) with a
-      // bit mask over the lane's keys 8g .. 8g+7 (branch-free: a uniform branch
-      // per fragment serialised the LDS reads)
-      const int lim = nk - k0 - 8 * g;
-      u32x4 vm;
 #pragma unroll
-      for (int p2 = 0; p2 < 4; ++p2) vm[p2] = (2 * p2 < lim ? 0xFFFFu : 0u) | (2 * p2 + 1 < lim ? 0xFFFF0000u : 0u);
+      for (int dt = 0; dt < 8; ++dt)
 #pragma unroll
-      for (int dt = 0; dt < 8; ++dt) {
-        const u32x4 raw = *(const u32x4*)(st + (8 + dt) * 512 + lane * 8);
-        const bf16x8 vf = __builtin_bit_cast(bf16x8, raw & vm);
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt) o[dt][qt] = amfma(vf, pf[qt], o[dt][qt]);
-      }
+        for (int qt = 0; qt < 2; ++qt) o[dt][qt] = amfma(vf[dt], pf[qt], o[dt][qt]);
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // the next pass restages every buffer
   }
