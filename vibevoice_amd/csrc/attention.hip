@@ -537,13 +537,16 @@ DEV void wait_vm(int n) {
   }
 }
 
-template <int G>
-#ifndef VV_PF_WPE
-#define VV_PF_WPE 2
-#endif
-__global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >= 4 ? VV_PF_WPE : 1))) k_attn_pf(AttnArgs a) {
+// QW = 16-query tiles per wave: 2 -> G waves (one per head); 1 -> 2G waves (a
+// head's two tiles on two waves).  At G = 6 the 6-wave form leaves two SIMDs
+// with one wave and two with two (the per-step barrier waits for the loaded
+// ones), and 215 VGPRs allow no second workgroup; 12 waves of ~150 VGPRs fill
+// every SIMD with three.
+template <int G, int QW>
+__global__ void __launch_bounds__(64 * G * 2 / QW) __attribute__((amdgpu_waves_per_eu(QW == 1 ? (G * 2 + 3) / 4 : (G >= 4 ? 2 : 1)))) k_attn_pf(AttnArgs a) {
   constexpr int d = 128;
-  constexpr int NI_MAX = (16 + G - 1) / G;   // staging instructions per wave and step
+  constexpr int NW = G * 2 / QW;             // waves
+  constexpr int NI_MAX = (16 + NW - 1) / NW;   // staging instructions per wave and step
   // one LDS array (a second __shared__ object can make hipcc drain the
   // prefetch early, cdna_hip_programming.md §5 trap 4a): 2 stages + row table
   __shared__ __attribute__((aligned(16))) bf16 sm[PF_NS * PF_STAGE + 4 * PF_Q];
@@ -553,38 +556,39 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
   const int r = lane & 15, g = lane >> 4;
   const int ntile = (a.nq + PF_Q - 1) / PF_Q;
   const int q0 = (ntile - 1 - (int)blockIdx.x) * PF_Q;   // late (long) tiles first
-  const int kh = blockIdx.y, h = kh * G + wave;
+  const int kh = blockIdx.y, h = kh * G + (QW == 2 ? wave : wave >> 1);
+  const int qt0 = QW == 2 ? 0 : (wave & 1);   // the wave's first 16-query tile
   if (threadIdx.x < PF_Q) {
     const int qi = q0 + threadIdx.x;
     s_slot[threadIdx.x] = qi < a.nq ? a.slots[qi] : -1;
     s_pos[threadIdx.x] = qi < a.nq ? a.pos[qi] : -1;
   }
   const bf16x8 z8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-  bf16x8 qf[2][4];   // B operand of S^T: column = query 16qt + r, k = dims 32c + 8g .. +7
+  bf16x8 qf[QW][4];   // B operand of S^T: column = query 16(qt0 + qt) + r, k = dims 32c + 8g .. +7
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int qi = q0 + 16 * qt + r;
+  for (int qt = 0; qt < QW; ++qt) {
+    const int qi = q0 + 16 * (qt0 + qt) + r;
 #pragma unroll
     for (int c = 0; c < 4; ++c)
       qf[qt][c] = qi < a.nq ? *(const bf16x8*)(a.q + (long long)qi * a.nh * d + h * d + 32 * c + 8 * g) : z8;
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // no plain loads in flight beside the staging
   __syncthreads();
-  int qslot[2], qpos[2];
+  int qslot[QW], qpos[QW];
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    qslot[qt] = s_slot[16 * qt + r];
-    qpos[qt] = s_pos[16 * qt + r];
+  for (int qt = 0; qt < QW; ++qt) {
+    qslot[qt] = s_slot[16 * (qt0 + qt) + r];
+    qpos[qt] = s_pos[16 * (qt0 + qt) + r];
   }
-  // this wave's staging blocks j = wave + G * i: j < 8 K fragment (kt = j >> 2,
+  // this wave's staging blocks j = wave + NW * i: j < 8 K fragment (kt = j >> 2,
   // c = j & 3; lane row r' -> key 8(r' >> 2) + 4kt + (r' & 3)), j >= 8 V^T
   // fragment dt = j - 8 (dims 16dt + r', keys 8g' .. 8g'+7); both advance by
   // 128 elements per key
-  const int ni = __builtin_amdgcn_readfirstlane((16 - wave + G - 1) / G);   // wave-uniform: scalar branches in issue()
+  const int ni = __builtin_amdgcn_readfirstlane((16 - wave + NW - 1) / NW);   // wave-uniform: scalar branches in issue()
   int soff[NI_MAX];   // element offset in the step's 32-key K block / V block (< 4096)
 #pragma unroll
   for (int i = 0; i < NI_MAX; ++i) {
-    const int j = wave + G * i;
+    const int j = wave + NW * i;
     if (j < 8) {
       const int kt = j >> 2, c = j & 3;
       soff[i] = (8 * (r >> 2) + 4 * kt + (r & 3)) * d + 32 * c + 8 * g;
@@ -592,12 +596,17 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
       soff[i] = (int)v_off(16 * (j - 8) + r, 8 * g);
     }
   }
-  f32x4 o[8][2];
+  f32x4 o[8][QW];
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt)
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) o[dt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+    for (int qt = 0; qt < QW; ++qt) o[dt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m[QW], l[QW];
+#pragma unroll
+  for (int qt = 0; qt < QW; ++qt) {
+    m[qt] = -INFINITY;
+    l[qt] = 0.f;
+  }
   const float sl2 = a.scale * 1.4426950408889634f;   // scores in log2 units
   unsigned valid = 0;
   for (int j = 0; j < PF_Q; ++j)
@@ -619,7 +628,9 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
     // past nq are never stored)
     const int kfull = seg == valid ? kmin + 1 : 0;
     const int nk = kmax + 1, nsteps = (nk + 31) >> 5;
-    const bool in0 = qslot[0] == slot, in1 = qslot[1] == slot;
+    bool inq[QW];
+#pragma unroll
+    for (int qt = 0; qt < QW; ++qt) inq[qt] = qslot[qt] == slot;
     const long long cbase = (long long)a.layer * a.kv.s_layer + (long long)slot * a.kv.s_slot +
                             (long long)kh * a.kv.s_head;
     const bf16* K = a.kv.k + cbase;    // [ctx][128]
@@ -632,9 +643,9 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
 #pragma unroll
       for (int i = 0; i < NI_MAX; ++i)
         if (i < ni) {
-          const bf16* src = (wave + G * i >= 8 ? VB : K) + (long long)step * 32 * d + soff[i];
+          const bf16* src = (wave + NW * i >= 8 ? VB : K) + (long long)step * 32 * d + soff[i];
           __builtin_amdgcn_global_load_lds((const void*)src,
-                                           (__attribute__((address_space(3))) void*)(st + (wave + G * i) * 512),
+                                           (__attribute__((address_space(3))) void*)(st + (wave + NW * i) * 512),
                                            16, 0, 0);
         }
     };
@@ -653,11 +664,11 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
       bf16x8 kf[8];
 #pragma unroll
       for (int f = 0; f < 8; ++f) kf[f] = *(const bf16x8*)(st + f * 512 + lane * 8);
-      f32x4 s[2][2];
+      f32x4 s[2][QW];
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
+        for (int qt = 0; qt < QW; ++qt) {
           s[kt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int c = 0; c < 4; ++c) s[kt][qt] = amfma(kf[kt * 4 + c], qf[qt][c], s[kt][qt]);
@@ -674,19 +685,19 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
       // where some column of the wave moved (a wave-uniform branch).  Steps every
       // row attends in full (all but the diagonal ones) skip the mask selects.
       const bool full = k0 + 32 <= kfull;
-      float x[2][2][4], al[2];
-      bool move[2];
+      float x[QW][2][4], al[QW];
+      bool move[QW];
       if (full) {   // raw scores: the max commutes with the positive scale, exp2 takes fma(s, sl2, -m)
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt)
+        for (int qt = 0; qt < QW; ++qt)
 #pragma unroll
           for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
             for (int i = 0; i < 4; ++i) x[qt][kt][i] = s[kt][qt][i];
       } else {
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
-          const bool in = qt == 0 ? in0 : in1;
+        for (int qt = 0; qt < QW; ++qt) {
+          const bool in = inq[qt];
 #pragma unroll
           for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -696,8 +707,9 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
             }
         }
       }
+      bool anymove = false;
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
+      for (int qt = 0; qt < QW; ++qt) {
         float mx = -INFINITY;
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
@@ -708,16 +720,17 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
         move[qt] = mx > m[qt] + PF_LAZY;   // also the first live step (m = -inf); lanes of a column agree
         al[qt] = move[qt] ? exp2f(m[qt] - mx) : 1.f;
         if (move[qt]) m[qt] = mx;
+        anymove |= move[qt];
       }
-      if (__builtin_amdgcn_ballot_w64(move[0] || move[1])) {
+      if (__builtin_amdgcn_ballot_w64(anymove)) {
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
+        for (int qt = 0; qt < QW; ++qt) {
           l[qt] *= al[qt];
 #pragma unroll
           for (int dt = 0; dt < 8; ++dt) o[dt][qt] *= al[qt];
         }
       }
-      bf16x8 pf[2];
+      bf16x8 pf[QW];
       // branch-free within a step: a column with no live key yet has every x =
       // -inf, so any finite reference gives p = 0; the raw v_exp_f32 (the libm
       // exp2f wraps it in a denormal-range fix-up, 5 VALU per value) flushes
@@ -725,7 +738,7 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
       // max of 1..2^8.  Full steps: p = 2^fma(s, scale, -m) (one VALU less per score)
       auto probs = [&](auto full_c) {
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
+        for (int qt = 0; qt < QW; ++qt) {
           const float mref = m[qt] != -INFINITY ? m[qt] : 0.f;
           float ps = 0.f;
 #pragma unroll
@@ -759,15 +772,15 @@ __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(G >
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt)
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) o[dt][qt] = amfma(vf[dt], pf[qt], o[dt][qt]);
+        for (int qt = 0; qt < QW; ++qt) o[dt][qt] = amfma(vf[dt], pf[qt], o[dt][qt]);
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // the next pass restages every buffer
   }
   // lane holds O^T[dim 16dt + 4g + i][query 16qt + r]; l summed over the 4 lanes of the column
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
+  for (int qt = 0; qt < QW; ++qt) {
     const float L = col_sum(l[qt]);
-    const int qi = q0 + 16 * qt + r;
+    const int qi = q0 + 16 * (qt0 + qt) + r;
     if (qi < a.nq) {
       const float inv = 1.f / L;
       bf16* op = a.out + (long long)qi * a.nh * d + h * d + 4 * g;
@@ -795,17 +808,21 @@ bool attn_use_prefill(int nq, int nslots) {
   return nq >= 256 && nq >= PF_Q * nslots;
 }
 
+#ifndef VV_PF_QW1
+#define VV_PF_QW1 1   // 0: one wave per head at every G (diagnostic builds)
+#endif
 static int launch_attn_pf(const AttnArgs& a, hipStream_t st) {
   const dim3 grid((a.nq + PF_Q - 1) / PF_Q, a.nkv);
+  // two waves per head (QW = 1) while that keeps <= 3 waves per SIMD (G <= 6)
   switch (a.nh / a.nkv) {
-    case 1: hipLaunchKernelGGL((k_attn_pf<1>), grid, dim3(64), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((k_attn_pf<2>), grid, dim3(128), 0, st, a); break;
-    case 3: hipLaunchKernelGGL((k_attn_pf<3>), grid, dim3(192), 0, st, a); break;
-    case 4: hipLaunchKernelGGL((k_attn_pf<4>), grid, dim3(256), 0, st, a); break;
-    case 5: hipLaunchKernelGGL((k_attn_pf<5>), grid, dim3(320), 0, st, a); break;
-    case 6: hipLaunchKernelGGL((k_attn_pf<6>), grid, dim3(384), 0, st, a); break;
-    case 7: hipLaunchKernelGGL((k_attn_pf<7>), grid, dim3(448), 0, st, a); break;
-    default: hipLaunchKernelGGL((k_attn_pf<8>), grid, dim3(512), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((k_attn_pf<1, VV_PF_QW1 ? 1 : 2>), grid, dim3(VV_PF_QW1 ? 128 : 64), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((k_attn_pf<2, VV_PF_QW1 ? 1 : 2>), grid, dim3(VV_PF_QW1 ? 256 : 128), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((k_attn_pf<3, VV_PF_QW1 ? 1 : 2>), grid, dim3(VV_PF_QW1 ? 384 : 192), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((k_attn_pf<4, VV_PF_QW1 ? 1 : 2>), grid, dim3(VV_PF_QW1 ? 512 : 256), 0, st, a); break;
+    case 5: hipLaunchKernelGGL((k_attn_pf<5, VV_PF_QW1 ? 1 : 2>), grid, dim3(VV_PF_QW1 ? 640 : 320), 0, st, a); break;
+    case 6: hipLaunchKernelGGL((k_attn_pf<6, VV_PF_QW1 ? 1 : 2>), grid, dim3(VV_PF_QW1 ? 768 : 384), 0, st, a); break;
+    case 7: hipLaunchKernelGGL((k_attn_pf<7, 2>), grid, dim3(448), 0, st, a); break;
+    default: hipLaunchKernelGGL((k_attn_pf<8, 2>), grid, dim3(512), 0, st, a); break;
   }
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
