@@ -180,3 +180,30 @@ def test_attn_defer_bit_identical(nrows, chunk, maxpos):
     h, ref = outs["defer"][0].float(), outs["default"][0].float()
     print("vs 1,024-key plan", rel_err(h, ref), cos(h, ref))
     assert rel_err(h, ref) < 1e-2 and cos(h, ref) > 0.9999
+
+
+def test_norm_pack_bit_identical():
+    """The prefill's RMSNorm producer writing MFMA-fragment-packed rows for the
+    256 x 256-tile q|k|v and gate|up GEMMs (vv_norm_pack) vs row-major rows:
+    identical hidden states and logits after a ragged 8,200-row prefill (both
+    GEMMs on the 256 x 256 tile, last row tile partial) and one decode step."""
+    from vibevoice_amd import _lib
+    L = _lib.lib()
+    cfg = tiny_config(hidden=1536, layers=2, heads=12, kv_heads=2, inter=8960)
+    outs = []
+    try:
+        for pack in (1, 0):
+            L.vv_norm_pack(pack)
+            eng, _ = make_engine(cfg, seed=6, max_batch=1, max_ctx=8448)
+            g = torch.Generator().manual_seed(8)
+            x = torch.randn(8200, 1536, generator=g).bfloat16().to(dev)
+            h0, l0 = eng.lm_forward(x, torch.zeros(8200, **I32), torch.arange(8200).to(**I32),
+                                    torch.tensor([0, 5170, 8199]).to(**I32))
+            xs = torch.randn(1, 1536, generator=g).bfloat16().to(dev)
+            h1, l1 = eng.lm_forward(xs, torch.zeros(1, **I32), torch.tensor([8200]).to(**I32), torch.zeros(1, **I32))
+            torch.cuda.synchronize()
+            outs.append([h0.clone(), l0.clone(), h1.clone(), l1.clone()])
+    finally:
+        L.vv_norm_pack(1)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

@@ -79,6 +79,7 @@ EXPORTS = [
     ("vv_gemv_tune_shape", I, [I, I, I, I, I, I, I]),
     ("vv_rope_table", I, [I]),
     ("vv_attn_defer", I, [I, I]),
+    ("vv_norm_pack", I, [I]),
 ]
 
 EPI = {"store": 0, "gelu": 1, "silu_mul": 2, "res": 3, "f32": 4}

@@ -23,7 +23,7 @@ __global__ void __launch_bounds__(256) k_rmsnorm(NormArgs a) {
   }
   ss = wave_sum(ss);
   const float inv = rsqrtf(ss / (float)a.C + a.eps);
-  bf16* y = rm_bfw(a.out, m);
+  bf16* y = a.pack ? (bf16*)a.out.base + (long long)(m >> 4) * a.C * 16 + (m & 15) * 8 : rm_bfw(a.out, m);
   const bf16* md = a.has_mod ? a.mod + (long long)m * a.mod_ld : nullptr;
   for (int c = lane; c < nch; c += 64) {
     bf16x8 v = *(const bf16x8*)(x + c * 8);
@@ -41,7 +41,8 @@ __global__ void __launch_bounds__(256) k_rmsnorm(NormArgs a) {
       if (md) t = rb(rb(t * rb(1.0f + bf(sc[j]))) + bf(sh[j]));
       o[j] = tobf(t);
     }
-    *(bf16x8*)(y + c * 8) = o;
+    // packed: columns 8c .. 8c+7 are chunk c >> 2, lane (m & 15) + 16 (c & 3) of the row's tile
+    *(bf16x8*)(y + (a.pack ? (c >> 2) * 512 + (c & 3) * 128 : c * 8)) = o;
   }
 }
 

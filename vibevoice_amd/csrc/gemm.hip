@@ -1382,6 +1382,13 @@ extern "C" int vv_gemm_tune_big(int mode) {
   return 0;
 }
 
+bool gemm_uses_xl(const GemmArgs& a) {
+  const int total_xl = ((a.M + GX_M - 1) / GX_M) * (a.N / GX_N);
+  return !(a.M <= 64 && (a.M <= 16 || a.M <= g_gemv_max_m || a.epi.kind == EPI_CFG_DPM)) && a.epi.kind != EPI_CFG_DPM &&
+         g_gemm_big == 3 && a.M >= GEMM_BIG_M && a.N % GX_N == 0 && a.K % 32 == 0 &&
+         (total_xl >= GEMM_BIG_TILES || g_gemm_big_any);
+}
+
 template <int XF>
 static int launch_gemm_xf(const GemmArgs& a, hipStream_t st) {
   // k_gemm_big only with >= one 128 x 128 tile per CU or >= 2^30 MACs: the
@@ -1456,6 +1463,7 @@ int gemv_plan_query(const GemmArgs& a0, int* nw, int* ksplit, int* tpw, int* fas
 int launch_gemm(GemmArgs a, hipStream_t st) {
   if (a.M <= 0) return 0;
   if (a.K % 32 != 0 || a.N % 16 != 0) return 1;
+  if (a.apack && (a.xf.kind != XF_NONE || !gemm_uses_xl(a))) return 1;   // only k_gemm_xl reads packed A rows
   if (a.xf.kind == XF_NORM && a.K % 8 != 0) return 1;
   if (a.epi.kind == EPI_ROPE && (a.rope.kv.d != 128 || !a.rope.pos || !a.rope.slots)) return 1;
   if (a.epi.kind == EPI_CFG_DPM && (a.M > 16 || 2 * a.dpm.n != a.M)) return 1;

@@ -92,6 +92,9 @@ struct NormArgs {
   const bf16* mod;      // row m: mod + m * mod_ld
   long long mod_ld;
   int shift_off, scale_off;
+  int pack;             // 1: out.base receives the rows in MFMA-fragment order (16-row tiles x
+                        // 32-column chunks of 1 KB, weights.py mfma_pack), the A layout
+                        // k_gemm_xl stages with one contiguous 1 KB load per block
 };
 
 struct DwArgs {
@@ -235,6 +238,8 @@ int launch_vae_features(int rows, int D, int frames, const bf16* mean, const bf1
                         const bf16* s, const bf16* b, bf16* out, hipStream_t st);
 int launch_head_cond(int steps, int R, int H, const bf16* condp, const bf16* temb, bf16* out, hipStream_t st);
 int launch_silu(int n, const bf16* x, bf16* y, hipStream_t st);
+// true: launch_gemm would run this (XF-free) GEMM on the 256 x 256 tile
+bool gemm_uses_xl(const GemmArgs& a);
 int launch_rope_table(int npos, const float* inv_freq, bf16* tab, hipStream_t st);
 int launch_cfg_dpm(int n, int D, DpmCoef k, const bf16* eps, bf16* x, bf16* m1, const float* noise, hipStream_t st);
 int launch_gather_rows(int n, int C, const bf16* src, long long lds, const int* idx, RowMap dst, hipStream_t st);
