@@ -257,9 +257,10 @@ int vv_rope_table(int on);
  * partials to o_proj, which merges them while staging its A rows (bit-identical
  * to the same splits merged in the attention kernel); 0 = the attn_plan splits. */
 int vv_attn_defer(int on, int chunk);
-/* Test switch: 1 (default) = RMSNorm rows feeding a 256 x 256-tile GEMM (the
- * prefill's q|k|v and gate|up) are written MFMA-fragment-packed for it;
- * 0 = row-major.  Both give the same bits. */
+/* Test switch: 1 (default) = the A rows of the prefill's 256 x 256-tile GEMMs
+ * are written MFMA-fragment-packed by their producers (RMSNorm rows for q|k|v
+ * and gate|up, gate|up's SiLU*up rows for down); 0 = row-major.  Both give the
+ * same bits. */
 int vv_norm_pack(int on);
 /* Test switch (bit mask, default 3): bit 0 folds each codec Block1D's mixer
  * (norm, depthwise conv, gamma residual, FFN norm) into its fc1 GEMV where

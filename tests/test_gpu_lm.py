@@ -183,8 +183,9 @@ def test_attn_defer_bit_identical(nrows, chunk, maxpos):
 
 
 def test_norm_pack_bit_identical():
-    """The prefill's RMSNorm producer writing MFMA-fragment-packed rows for the
-    256 x 256-tile q|k|v and gate|up GEMMs (vv_norm_pack) vs row-major rows:
+    """The prefill's producers writing MFMA-fragment-packed A rows for the
+    256 x 256-tile GEMMs (vv_norm_pack: RMSNorm rows for q|k|v and gate|up,
+    gate|up's SiLU*up rows for down) vs row-major rows:
     identical hidden states and logits after a ragged 8,200-row prefill (both
     GEMMs on the 256 x 256 tile, last row tile partial) and one decode step."""
     from vibevoice_amd import _lib

@@ -100,7 +100,8 @@ enum {
 
 struct EpiArgs {
   int kind;
-  int pad_;
+  int pack;             // EPI_SILU_MUL on the 256 x 256 tile: out.base receives the act rows
+                        // MFMA-fragment-packed (the next GEMM's A, GemmArgs::apack)
   const bf16* bias;     // [N] or nullptr
   RowMap out;           // bf16 (float for EPI_F32)
   RowMap res;           // residual rows (EPI_RES), may alias out

@@ -1464,6 +1464,9 @@ int launch_gemm(GemmArgs a, hipStream_t st) {
   if (a.M <= 0) return 0;
   if (a.K % 32 != 0 || a.N % 16 != 0) return 1;
   if (a.apack && (a.xf.kind != XF_NONE || !gemm_uses_xl(a))) return 1;   // only k_gemm_xl reads packed A rows
+  if (a.epi.pack && (a.epi.kind != EPI_SILU_MUL || a.xf.kind != XF_NONE || !gemm_uses_xl(a) || (a.N >> 1) % 32 ||
+                     ((unsigned long long)a.epi.out.base & 15)))
+    return 1;   // ... and only its row-contiguous SiLU*up epilogue writes them
   if (a.xf.kind == XF_NORM && a.K % 8 != 0) return 1;
   if (a.epi.kind == EPI_ROPE && (a.rope.kv.d != 128 || !a.rope.pos || !a.rope.slots)) return 1;
   if (a.epi.kind == EPI_CFG_DPM && (a.M > 16 || 2 * a.dpm.n != a.M)) return 1;

@@ -261,6 +261,7 @@ DEV bool a16(const void* p) { return ((unsigned long long)p & 15) == 0; }
 DEV bool rm8(const RowMap& r) { return a16(r.base) && r.sT % 8 == 0 && r.sB % 8 == 0; }
 DEV bool epi_row8_ok(const GemmArgs& a) {
   const EpiArgs& e = a.epi;
+  if (e.pack) return true;   // host-checked (launch_gemm): EPI_SILU_MUL, 16-byte aligned base
   if (e.kind != EPI_STORE && e.kind != EPI_GELU && e.kind != EPI_RES && e.kind != EPI_SILU_MUL) return false;
   if (!rm8(e.out) || (e.bias && !a16(e.bias))) return false;
   if (e.kind == EPI_RES && (!rm8(e.res) || (e.gamma && !a16(e.gamma)) || (e.gate.base && !rm8(e.gate)))) return false;
@@ -308,7 +309,14 @@ DEV void epi_silu8(const GemmArgs& a, int m, int col, const float gt[8], const f
   bf16x8 o;
 #pragma unroll
   for (int i = 0; i < 8; ++i) o[i] = tobf(rb(silu_f(rb(gt[i]))) * rb(up[i]));
-  *(bf16x8*)(rm_bfw(a.epi.out, m) + col) = o;
+  if (a.epi.pack) {   // act row length N / 2; columns col .. col+7 = one lane's 16 bytes of a block
+    const int na = a.N >> 1;
+    bf16* p = (bf16*)a.epi.out.base + ((long long)(m >> 4) * (na >> 5) + (col >> 5)) * 512 +
+              ((m & 15) + 16 * ((col & 31) >> 3)) * 8;
+    *(bf16x8*)p = o;
+  } else {
+    *(bf16x8*)(rm_bfw(a.epi.out, m) + col) = o;
+  }
 }
 
 template <class MP = MemPlain>
