@@ -185,16 +185,21 @@ def test_attn_defer_bit_identical(nrows, chunk, maxpos):
 def test_norm_pack_bit_identical():
     """The prefill's producers writing MFMA-fragment-packed A rows for the
     256 x 256-tile GEMMs (vv_norm_pack: RMSNorm rows for q|k|v and gate|up,
-    gate|up's SiLU*up rows for down) vs row-major rows:
-    identical hidden states and logits after a ragged 8,200-row prefill (both
-    GEMMs on the 256 x 256 tile, last row tile partial) and one decode step."""
+    gate|up's SiLU*up rows for down) vs row-major rows, and the 256 x 256 tile's
+    row-contiguous epilogues (q|k|v RoPE + K / V cache append, SiLU*up,
+    residual) vs the 128 x 128 tile's per-lane ones: identical hidden states and
+    logits after a ragged 8,200-row prefill (last row tile partial) and one
+    decode step that reads the prefill's K / V cache."""
     from vibevoice_amd import _lib
     L = _lib.lib()
     cfg = tiny_config(hidden=1536, layers=2, heads=12, kv_heads=2, inter=8960)
     outs = []
     try:
-        for pack in (1, 0):
+        # packed / row-major A rows on the 256^2 tile (its row-contiguous RoPE + KV
+        # epilogue), then the 128^2 tile with epi_tile's per-lane epilogue
+        for pack, big in ((1, -1), (0, -1), (0, 2)):
             L.vv_norm_pack(pack)
+            L.vv_gemm_tune_big(big)
             eng, _ = make_engine(cfg, seed=6, max_batch=1, max_ctx=8448)
             g = torch.Generator().manual_seed(8)
             x = torch.randn(8200, 1536, generator=g).bfloat16().to(dev)
@@ -206,5 +211,7 @@ def test_norm_pack_bit_identical():
             outs.append([h0.clone(), l0.clone(), h1.clone(), l1.clone()])
     finally:
         L.vv_norm_pack(1)
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
+        L.vv_gemm_tune_big(-1)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)

@@ -1310,6 +1310,44 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
   // a K = 1536 tile)
   __syncthreads();   // every wave is past its reads of the last stage
 #if VV_GX_ABL != 4
+  if (rope_row8_ok(a)) {
+    // q|k|v + RoPE + KV append in the same row-contiguous staging: a q / k lane
+    // takes one row's 16-column tile (its two RoPE halves), a V lane one column
+    // over 8 consecutive rows (one 16-byte store into the [dim][32 pos] block)
+    float* ep = (float*)smx + wave * (64 * 64);
+    auto sw = [](int row, int col) { return row * 64 + (col ^ ((row & 1) << 2)); };
+    const int mb = tm * GX_M + wr * 128, nb = tn * GX_N + wc * 64;
+    const bool vhead = (nb >> 7) >= a.rope.nh + a.rope.nkv;   // a wave's 64 columns lie in one head
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+#pragma unroll
+      for (int mq = 0; mq < 4; ++mq)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) *(f32x4*)(ep + sw(mq * 16 + r, nt * 16 + 4 * g)) = acc[nt][4 * p + mq];
+      if (!vhead) {
+#pragma unroll 1
+        for (int it = 0; it < 4; ++it) {
+          const int row = it * 16 + (lane >> 2), tq = lane & 3, m = mb + 64 * p + row;
+          float lo[8], hi[8];
+          *(f32x4*)lo = *(const f32x4*)(ep + sw(row, 16 * tq));
+          *(f32x4*)(lo + 4) = *(const f32x4*)(ep + sw(row, 16 * tq + 4));
+          *(f32x4*)hi = *(const f32x4*)(ep + sw(row, 16 * tq + 8));
+          *(f32x4*)(hi + 4) = *(const f32x4*)(ep + sw(row, 16 * tq + 12));
+          if (m < a.M) rope_qk8(a, m, nb + 16 * tq, lo, hi);
+        }
+      } else {
+#pragma unroll 1
+        for (int it = 0; it < 8; ++it) {
+          const int r0 = it * 8, m0 = mb + 64 * p + r0;
+          float vv[8];
+#pragma unroll
+          for (int k2 = 0; k2 < 8; ++k2) vv[k2] = ep[sw(r0 + k2, lane)];
+          if (m0 < a.M) rope_v8(a, m0, nb + lane, vv);
+        }
+      }
+    }
+    return;
+  }
   if (epi_row8_ok(a)) {
     // row-contiguous form: per wave and pass, 4 m-tiles x its 4 n-tiles -> LDS
     // [64 rows][64 cols] f32 (16 KB per wave, the whole ring for 8 waves; odd rows'

@@ -319,6 +319,94 @@ DEV void epi_silu8(const GemmArgs& a, int m, int col, const float gt[8], const f
   }
 }
 
+// Row-contiguous RoPE epilogue (k_gemm_xl, the prefill's q|k|v projection):
+// epi_rope's arithmetic for one row m and one 16-column q/k tile at n0 (lo = its
+// columns 0..7 = dims j..j+7, hi = columns 8..15 = dims 64+j..), 16-byte stores
+DEV bool rope_row8_ok(const GemmArgs& a) {
+  const RopeEpi& R = a.rope;
+  return a.epi.kind == EPI_ROPE && a16(R.q_out) && a16(R.kv.k) && a16(R.kv.v) && (!a.epi.bias || a16(a.epi.bias)) &&
+         (!R.cs_tab || a16(R.cs_tab)) && R.kv.s_layer % 8 == 0 && R.kv.s_slot % 8 == 0 && R.kv.s_head % 8 == 0;
+}
+DEV void rope_qk8(const GemmArgs& a, int m, int n0, const float lo[8], const float hi[8]) {
+  const RopeEpi& R = a.rope;
+  constexpr int d = 128;
+  float v[8], u[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    v[i] = lo[i];
+    u[i] = hi[i];
+  }
+  if (a.epi.bias) {
+    const bf16x8 b0 = *(const bf16x8*)(a.epi.bias + n0), b1 = *(const bf16x8*)(a.epi.bias + n0 + 8);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      v[i] += bf(b0[i]);
+      u[i] += bf(b1[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    v[i] = rb(v[i]);
+    u[i] = rb(u[i]);
+  }
+  const int h = n0 / d, j = ((n0 % d) >> 4) * 8, p = R.pos[m];
+  float cs[8], sn[8];
+  if (R.cs_tab) {
+    const bf16x8 c8 = *(const bf16x8*)(R.cs_tab + (long long)p * d + j);
+    const bf16x8 s8 = *(const bf16x8*)(R.cs_tab + (long long)p * d + 64 + j);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      cs[i] = bf(c8[i]);
+      sn[i] = bf(s8[i]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float f = (float)p * R.inv_freq[j + i];
+      cs[i] = rb(cosf(f));
+      sn[i] = rb(sinf(f));
+    }
+  }
+  bf16x8 o1, o2;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    o1[i] = tobf(rb(v[i] * cs[i]) + rb(-u[i] * sn[i]));
+    o2[i] = tobf(rb(u[i] * cs[i]) + rb(v[i] * sn[i]));
+  }
+  bf16* dst = h < R.nh ? R.q_out + (long long)m * R.nh * d + h * d
+                       : R.kv.k + (long long)R.layer * R.kv.s_layer + (long long)R.slots[m] * R.kv.s_slot +
+                             (long long)(h - R.nh) * R.kv.s_head + (long long)p * d;
+  *(bf16x8*)(dst + j) = o1;
+  *(bf16x8*)(dst + j + 64) = o2;
+}
+// V column n (one dim) of rows m0 .. m0+7 into the blocked V cache: one 16-byte
+// store when the 8 rows are consecutive positions p0 .. p0+7 (p0 % 8 == 0) of one
+// slot -- a prompt's rows -- else 8 two-byte stores (epi_rope's form)
+DEV void rope_v8(const GemmArgs& a, int m0, int n, const float vin[8]) {
+  const RopeEpi& R = a.rope;
+  const float b = a.epi.bias ? bf(a.epi.bias[n]) : 0.f;
+  const int dim = n % 128, hv = n / 128 - R.nh - R.nkv;
+  bf16x8 o;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o[k] = tobf(rb(vin[k] + b));
+  const long long hoff = (long long)R.layer * R.kv.s_layer + (long long)hv * R.kv.s_head;
+  bool run = m0 + 7 < a.M;
+  const int s0 = run ? R.slots[m0] : 0, p0 = run ? R.pos[m0] : 0;
+  run = run && (p0 & 7) == 0;
+  if (run) {
+#pragma unroll
+    for (int k = 1; k < 8; ++k) run = run && R.slots[m0 + k] == s0 && R.pos[m0 + k] == p0 + k;
+  }
+  if (run) {
+    *(bf16x8*)(R.kv.v + hoff + (long long)s0 * R.kv.s_slot + v_off(dim, p0)) = o;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (m0 + k < a.M)
+        R.kv.v[hoff + (long long)R.slots[m0 + k] * R.kv.s_slot + v_off(dim, R.pos[m0 + k])] = o[k];
+  }
+}
+
 template <class MP = MemPlain>
 DEV void epi_tile(const GemmArgs& a, int m, int n0, int lane, const float v_in[4], const EpiPre* pre = nullptr) {
   const EpiArgs& e = a.epi;
