@@ -488,7 +488,12 @@ int launch_final_head(int R, int H, const bf16* h, const int* idx, const bf16* n
 constexpr int PF_Q = 32;
 constexpr float PF_LAZY = 8.f;       // running-max slack (log2 units) before O is rescaled
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-constexpr int PF_STAGE = 16 * 512;   // bf16 elements per staged step: 8 K + 8 V fragment blocks
+#ifndef VV_PF_SUB
+#define VV_PF_SUB 2
+#endif
+// 32-key steps per LDS stage (one barrier and one vmcnt wait per stage)
+constexpr int PF_SUB = VV_PF_SUB;
+constexpr int PF_STAGE = PF_SUB * 16 * 512;   // bf16 elements per stage: per step 8 K + 8 V fragment blocks
 // LDS stages: steps s+1 .. s+NS-2 in flight while step s computes, step
 // s+NS-1 issued after the step's one barrier.  16K-token prefill (interleaved
 // same-box runs, tools/ab_bench.py --prefill): NS 2 118.7 ms, NS 3 122.4, NS 4
@@ -546,23 +551,20 @@ template <int G, int QW>
 __global__ void __launch_bounds__(64 * G * 2 / QW) __attribute__((amdgpu_waves_per_eu(QW == 1 ? (G * 2 + 3) / 4 : (G >= 4 ? 2 : 1)))) k_attn_pf(AttnArgs a) {
   constexpr int d = 128;
   constexpr int NW = G * 2 / QW;             // waves
-  constexpr int NI_MAX = (16 + NW - 1) / NW;   // staging instructions per wave and step
+  constexpr int NI_MAX = (16 * PF_SUB + NW - 1) / NW;   // staging instructions per wave and stage
   // one LDS array (a second __shared__ object can make hipcc drain the
   // prefetch early, cdna_hip_programming.md §5 trap 4a): 2 stages + row table
-  __shared__ __attribute__((aligned(16))) bf16 sm[PF_NS * PF_STAGE + 4 * PF_Q];
-  int* s_slot = (int*)(sm + PF_NS * PF_STAGE);
-  int* s_pos = s_slot + PF_Q;
+  __shared__ __attribute__((aligned(16))) bf16 sm[PF_NS * PF_STAGE];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int ntile = (a.nq + PF_Q - 1) / PF_Q;
   const int q0 = (ntile - 1 - (int)blockIdx.x) * PF_Q;   // late (long) tiles first
+  // the tile's row slots / positions come from global (uniform addresses: scalar
+  // loads); an LDS table beside the 64 KB ring would not fit
+  auto s_slot = [&](int j) { return q0 + j < a.nq ? a.slots[q0 + j] : -1; };
+  auto s_pos = [&](int j) { return q0 + j < a.nq ? a.pos[q0 + j] : -1; };
   const int kh = blockIdx.y, h = kh * G + (QW == 2 ? wave : wave >> 1);
   const int qt0 = QW == 2 ? 0 : (wave & 1);   // the wave's first 16-query tile
-  if (threadIdx.x < PF_Q) {
-    const int qi = q0 + threadIdx.x;
-    s_slot[threadIdx.x] = qi < a.nq ? a.slots[qi] : -1;
-    s_pos[threadIdx.x] = qi < a.nq ? a.pos[qi] : -1;
-  }
   const bf16x8 z8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
   bf16x8 qf[QW][4];   // B operand of S^T: column = query 16(qt0 + qt) + r, k = dims 32c + 8g .. +7
 #pragma unroll
@@ -577,23 +579,23 @@ __global__ void __launch_bounds__(64 * G * 2 / QW) __attribute__((amdgpu_waves_p
   int qslot[QW], qpos[QW];
 #pragma unroll
   for (int qt = 0; qt < QW; ++qt) {
-    qslot[qt] = s_slot[16 * (qt0 + qt) + r];
-    qpos[qt] = s_pos[16 * (qt0 + qt) + r];
+    qslot[qt] = s_slot(16 * (qt0 + qt) + r);
+    qpos[qt] = s_pos(16 * (qt0 + qt) + r);
   }
   // this wave's staging blocks j = wave + NW * i: j < 8 K fragment (kt = j >> 2,
   // c = j & 3; lane row r' -> key 8(r' >> 2) + 4kt + (r' & 3)), j >= 8 V^T
   // fragment dt = j - 8 (dims 16dt + r', keys 8g' .. 8g'+7); both advance by
   // 128 elements per key
-  const int ni = __builtin_amdgcn_readfirstlane((16 - wave + NW - 1) / NW);   // wave-uniform: scalar branches in issue()
+  const int ni = __builtin_amdgcn_readfirstlane((16 * PF_SUB - wave + NW - 1) / NW);   // wave-uniform: scalar branches in issue()
   int soff[NI_MAX];   // element offset in the step's 32-key K block / V block (< 4096)
 #pragma unroll
   for (int i = 0; i < NI_MAX; ++i) {
-    const int j = wave + NW * i;
+    const int j = (wave + NW * i) & 15, sub = (wave + NW * i) >> 4;   // block j of step `sub` of the stage
     if (j < 8) {
       const int kt = j >> 2, c = j & 3;
-      soff[i] = (8 * (r >> 2) + 4 * kt + (r & 3)) * d + 32 * c + 8 * g;
+      soff[i] = (sub * 32 + 8 * (r >> 2) + 4 * kt + (r & 3)) * d + 32 * c + 8 * g;
     } else {
-      soff[i] = (int)v_off(16 * (j - 8) + r, 8 * g);
+      soff[i] = (int)v_off(16 * (j - 8) + r, sub * 32 + 8 * g);
     }
   }
   f32x4 o[8][QW];
@@ -610,24 +612,24 @@ __global__ void __launch_bounds__(64 * G * 2 / QW) __attribute__((amdgpu_waves_p
   const float sl2 = a.scale * 1.4426950408889634f;   // scores in log2 units
   unsigned valid = 0;
   for (int j = 0; j < PF_Q; ++j)
-    if (s_slot[j] >= 0) valid |= 1u << j;
+    if (s_slot(j) >= 0) valid |= 1u << j;
   unsigned done = 0;
   while (done != valid) {
     // one pass per distinct slot of the tile
-    const int slot = s_slot[__builtin_ctz(valid & ~done)];
+    const int slot = s_slot(__builtin_ctz(valid & ~done));
     int kmax = 0, kmin = 1 << 30;
     unsigned seg = 0;
     for (int j = 0; j < PF_Q; ++j)
-      if (s_slot[j] == slot) {
+      if (s_slot(j) == slot) {
         seg |= 1u << j;
-        kmax = max(kmax, s_pos[j]);
-        kmin = min(kmin, s_pos[j]);
+        kmax = max(kmax, s_pos(j));
+        kmin = min(kmin, s_pos(j));
       }
     done |= seg;
     // steps whose keys every valid row of the tile attends need no mask (rows
     // past nq are never stored)
     const int kfull = seg == valid ? kmin + 1 : 0;
-    const int nk = kmax + 1, nsteps = (nk + 31) >> 5;
+    const int nk = kmax + 1, nsteps = (nk + 32 * PF_SUB - 1) / (32 * PF_SUB);   // stages
     bool inq[QW];
 #pragma unroll
     for (int qt = 0; qt < QW; ++qt) inq[qt] = qslot[qt] == slot;
@@ -643,7 +645,7 @@ __global__ void __launch_bounds__(64 * G * 2 / QW) __attribute__((amdgpu_waves_p
 #pragma unroll
       for (int i = 0; i < NI_MAX; ++i)
         if (i < ni) {
-          const bf16* src = (wave + NW * i >= 8 ? VB : K) + (long long)step * 32 * d + soff[i];
+          const bf16* src = (((wave + NW * i) & 15) >= 8 ? VB : K) + (long long)step * 32 * PF_SUB * d + soff[i];
           __builtin_amdgcn_global_load_lds((const void*)src,
                                            (__attribute__((address_space(3))) void*)(st + (wave + NW * i) * 512),
                                            16, 0, 0);
@@ -658,8 +660,11 @@ __global__ void __launch_bounds__(64 * G * 2 / QW) __attribute__((amdgpu_waves_p
       // wave has finished reading step - 1, whose buffer takes step + NS - 1
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (step + PF_NS - 1 < nsteps) issue(step + PF_NS - 1);
-      const int k0 = step * 32;
-      const bf16* st = sm + (step % PF_NS) * PF_STAGE;
+#pragma unroll
+      for (int sub = 0; sub < PF_SUB; ++sub) {
+      const int k0 = (step * PF_SUB + sub) * 32;
+      if (k0 >= nk) break;
+      const bf16* st = sm + (step % PF_NS) * PF_STAGE + sub * 16 * 512;
       // all 8 K fragments, then the 16 S MFMAs (one LDS round trip, not one per key tile)
       bf16x8 kf[8];
 #pragma unroll
@@ -773,6 +778,7 @@ __global__ void __launch_bounds__(64 * G * 2 / QW) __attribute__((amdgpu_waves_p
       for (int dt = 0; dt < 8; ++dt)
 #pragma unroll
         for (int qt = 0; qt < QW; ++qt) o[dt][qt] = amfma(vf[dt], pf[qt], o[dt][qt]);
+      }   // sub-step
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // the next pass restages every buffer
   }
