@@ -252,10 +252,11 @@ int vv_gemv_tune_shape(int N, int K, int mmax, int nw, int ks, int u, int tpw);
  * per-position bf16 cos / sin table; 0 = computes cosf / sinf inline
  * (bit-identical by construction). */
 int vv_rope_table(int on);
-/* Test switch: 1 (default, chunk 128) = decode attention over up to 8,192 keys
- * runs 2..8 key splits of >= `chunk` keys (multiple of 32) and leaves their
- * partials to o_proj, which merges them while staging its A rows (bit-identical
- * to the same splits merged in the attention kernel); 0 = the attn_plan splits. */
+/* Test switch: on = 1 (default, chunk 128): decode passes of <= 4 rows over up
+ * to 8,192 keys run 2..8 key splits of >= `chunk` keys (multiple of 32) and
+ * leave their partials to o_proj, which merges them while staging its A rows
+ * (bit-identical to the same splits merged in the attention kernel); on = n >= 2:
+ * passes of <= n rows (n <= 16); 0 = the attn_plan splits everywhere. */
 int vv_attn_defer(int on, int chunk);
 /* Test switch: 1 (default) = the A rows of the prefill's 256 x 256-tile GEMMs
  * are written MFMA-fragment-packed by their producers (RMSNorm rows for q|k|v

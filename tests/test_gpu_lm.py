@@ -167,7 +167,7 @@ def test_attn_defer_bit_identical(nrows, chunk, maxpos):
     outs = {}
     try:
         for name, defer, tune in (("defer", 1, 0), ("inkernel", 0, eff), ("default", 0, 0)):
-            _lib.check(L.vv_attn_defer(defer, chunk), "attn_defer")
+            _lib.check(L.vv_attn_defer(16 if defer else 0, chunk), "attn_defer")   # <= 16 rows defer
             _lib.check(L.vv_attn_tune(tune, -1), "attn_tune")
             h, lg = eng.lm_forward(x, slots, pos, torch.arange(nrows).to(**I32))
             torch.cuda.synchronize()

@@ -837,10 +837,13 @@ extern "C" int vv_rope_table(int on) {
 // chunks of g_defer_chunk keys run that many splits per (row, kv head), each
 // leaves its (m, l, o) partial and o_proj merges them while staging its A rows
 // (XF_ATTN_MERGE) -- the split parallelism without a ticket or a merge pass.
-static int g_attn_defer = 1, g_defer_chunk = 128;
+// Rows: B = 1 (2 rows) gains 1.5 % at K = 750; at B = 8 (16 rows) o_proj's
+// staging of 16 rows' partials cost more than the splits saved (5.79 vs 5.67 ms),
+// so by default only <= 4 rows defer.
+static int g_attn_defer = 4, g_defer_chunk = 128;
 extern "C" int vv_attn_defer(int on, int chunk) {
-  if (chunk % 32 || chunk < 32) return 1;
-  g_attn_defer = on;
+  if (chunk % 32 || chunk < 32 || on < 0) return 1;
+  g_attn_defer = on == 1 ? 4 : on;   // 1: the default row limit; n >= 2: up to n rows (<= 16)
   g_defer_chunk = chunk;
   return 0;
 }
@@ -874,7 +877,7 @@ static int lm_begin(vv_ctx* c, LmPass& P, int ntok, const void* embeds, int embe
   P.prefill = attn_use_prefill(ntok, c->lm_slots) ? 1 : 0;
   P.nsplit = P.prefill ? 1 : attn_plan(ntok, k.n_kv_heads, max_pos_p1, &P.chunk);
   P.defer = 0;
-  if (!P.prefill && g_attn_defer && ntok <= 16 && k.head_dim == 128) {
+  if (!P.prefill && g_attn_defer && ntok <= g_attn_defer && ntok <= 16 && k.head_dim == 128) {
     // 2..8 splits of >= g_defer_chunk keys, up to 8 x 1,024 keys (longer contexts
     // keep attn_plan's many 1,024-key splits: the merge input grows with them)
     int ch = g_defer_chunk, ns = (max_pos_p1 + ch - 1) / ch;
