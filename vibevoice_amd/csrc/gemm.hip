@@ -1427,6 +1427,9 @@ bool gemm_uses_xl(const GemmArgs& a) {
          (total_xl >= GEMM_BIG_TILES || g_gemm_big_any);
 }
 
+#ifndef VV_GEMM_BN32
+#define VV_GEMM_BN32 128
+#endif
 template <int XF>
 static int launch_gemm_xf(const GemmArgs& a, hipStream_t st) {
   // k_gemm_big only with >= one 128 x 128 tile per CU or >= 2^30 MACs: the
@@ -1455,7 +1458,10 @@ static int launch_gemm_xf(const GemmArgs& a, hipStream_t st) {
     else hipLaunchKernelGGL(k_gemm_big<2>, dim3(((total + 7) >> 3) * 8), dim3(256), 0, st, a);
     return 0;
   }
-  if (a.N % 64 == 0) {
+  // 64-wide tiles unless that leaves fewer than VV_GEMM_BN32 workgroups (the
+  // codec's 200-row stage: fc2 N = 256 is 16 workgroups of K = 1,024)
+  const int wg64 = ((a.M + 63) / 64) * (a.N / 64);
+  if (a.N % 64 == 0 && wg64 >= VV_GEMM_BN32) {
     dim3 grid((a.M + 63) / 64, a.N / 64);
     hipLaunchKernelGGL((k_gemm<64, XF>), grid, dim3(256), 0, st, a);
   } else if (a.N % 32 == 0) {
