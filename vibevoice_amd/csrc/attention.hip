@@ -55,6 +55,31 @@ DEV int row_chunk(const AttnArgs& a, int len) {
 
 DEV f32x4 amfma(bf16x8 a, bf16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
 
+// max / sum over the 16 lanes of a DPP row (one MFMA tile column group) with
+// row-local DPP moves on the VALU: quad xor 1, quad xor 2, half-row mirror,
+// row mirror (a butterfly: every lane ends with the whole row's value; each step
+// adds a lane pair in both orders, so all lanes agree bit for bit).  Four
+// __shfl_xor were four dependent ds_bpermute LDS round trips.
+template <int CTRL>
+DEV float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+DEV float row16_max(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  return fmaxf(v, dpp_f<0x140>(v));
+}
+DEV float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  return v + dpp_f<0x140>(v);
+}
+#ifndef VV_ATT_DPP
+#define VV_ATT_DPP 1
+#endif
+
 DEV void astamp(const AttnArgs& a, int which) {
   if (a.stamps && threadIdx.x == 0)
     a.stamps[((long long)blockIdx.y * gridDim.x + blockIdx.x) * 4 + which] = __builtin_amdgcn_s_memrealtime();
@@ -160,19 +185,27 @@ __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
       float s0 = c0 + r < w1 ? sacc[0][i] * a.scale : -INFINITY;
       float s1 = c0 + 16 + r < w1 ? sacc[1][i] * a.scale : -INFINITY;
       float mx = fmaxf(s0, s1);
+#if VV_ATT_DPP
+      mx = row16_max(mx);
+#else
       mx = fmaxf(mx, __shfl_xor(mx, 1));
       mx = fmaxf(mx, __shfl_xor(mx, 2));
       mx = fmaxf(mx, __shfl_xor(mx, 4));
       mx = fmaxf(mx, __shfl_xor(mx, 8));
+#endif
       const float mnew = fmaxf(m[i], mx);
       const float al = __expf(m[i] - mnew);
       p[0][i] = __expf(s0 - mnew);
       p[1][i] = __expf(s1 - mnew);
       float ps = p[0][i] + p[1][i];
+#if VV_ATT_DPP
+      ps = row16_sum(ps);
+#else
       ps += __shfl_xor(ps, 1);
       ps += __shfl_xor(ps, 2);
       ps += __shfl_xor(ps, 4);
       ps += __shfl_xor(ps, 8);
+#endif
       l[i] = l[i] * al + ps;
       m[i] = mnew;
 #pragma unroll
