@@ -45,10 +45,25 @@ DEV float silu_f(float x) { return x / (1.0f + __expf(-x)); }
 // GELU, exact erf form (transformers ACT2FN["gelu"]; modular_vibevoice_tokenizer.py:589)
 DEV float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
+// Whole-wave sum: the four 16-lane rows by DPP butterflies (quad xor 1, 2,
+// half-row and row mirror), then across rows by gfx950's v_permlane16_swap /
+// v_permlane32_swap -- VALU moves instead of six dependent ds_bpermute LDS round
+// trips (every normalising GEMV prologue and k_rmsnorm run one per row).  Each
+// step adds a lane pair in both orders, so every lane ends with the same bits.
+// Call with the whole wave active.
+template <int CTRL>
+DEV float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
 DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  v += dpp_mov<0xB1>(v);
+  v += dpp_mov<0x4E>(v);
+  v += dpp_mov<0x141>(v);
+  v += dpp_mov<0x140>(v);
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 DEV float wave_max(float v) {
 #pragma unroll
