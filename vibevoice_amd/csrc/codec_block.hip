@@ -92,7 +92,7 @@ DEV void mix_rows(const MixArgs& a, unsigned char* smem, bf16* a_lds, int a_ld) 
   for (int i = gi; i < rows && gi < ng; i += ng) {   // row sums in a fixed order
     float ss = 0.f;
     for (int c = gl; c < n8; c += LPR) ss += ssp[i * n8 + c];
-    for (int o = LPR >> 1; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+    ss = group_sum_n(ss, LPR);   // DPP / permlane (common.h), XF_MIX's wave_sum order at LPR 64
     if (gl == 0) inv[i] = rsqrtf(ss / (float)C + a.eps);
   }
   __syncthreads();
@@ -139,7 +139,7 @@ DEV void mix_rows(const MixArgs& a, unsigned char* smem, bf16* a_lds, int a_ld) 
   for (int i = gi; i < a.R && gi < ng; i += ng) {
     float ss = 0.f;
     for (int c = gl; c < n8; c += LPR) ss += ssp[i * n8 + c];
-    for (int o = LPR >> 1; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+    ss = group_sum_n(ss, LPR);
     if (gl == 0) inv[i] = rsqrtf(ss / (float)C + a.eps);
   }
   __syncthreads();

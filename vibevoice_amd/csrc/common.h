@@ -55,15 +55,40 @@ template <int CTRL>
 DEV float dpp_mov(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
-DEV float wave_sum(float v) {
-  v += dpp_mov<0xB1>(v);
-  v += dpp_mov<0x4E>(v);
-  v += dpp_mov<0x141>(v);
-  v += dpp_mov<0x140>(v);
-  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
-  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+// sum over aligned groups of N lanes (N = 2 .. 64), same step order for every N
+template <int N>
+DEV float group_sum(float v) {
+  if (N >= 2) v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]
+  if (N >= 4) v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]
+  if (N >= 8) v += dpp_mov<0x141>(v);   // row_half_mirror
+  if (N >= 16) v += dpp_mov<0x140>(v);  // row_mirror
+  if (N >= 32) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  }
+  if (N >= 64) {
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(b[0]) + __uint_as_float(b[1]);
+  }
+  return v;
+}
+DEV float wave_sum(float v) { return group_sum<64>(v); }
+// runtime group width (a wave-uniform power of two <= 64; every lane of a group active)
+DEV float group_sum_n(float v, int n) {
+  switch (n) {
+    case 64: return group_sum<64>(v);
+    case 32: return group_sum<32>(v);
+    case 16: return group_sum<16>(v);
+    case 8: return group_sum<8>(v);
+    case 4: return group_sum<4>(v);
+    case 2: return group_sum<2>(v);
+    default: return v;
+  }
+}
+// the lane 32 apart (lane l < 32: l + 32, else l - 32), by v_permlane32_swap
+DEV float xor32(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float((__lane_id() & 32) ? a[0] : a[1]);
 }
 DEV float wave_max(float v) {
 #pragma unroll

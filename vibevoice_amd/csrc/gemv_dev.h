@@ -144,7 +144,7 @@ DEV void epi_rope(const GemmArgs& a, int m, int n0, int lane, float v[4]) {
   if (h < R.nh + R.nkv) {
     float u[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) u[i] = __shfl_xor(v[i], 32);
+    for (int i = 0; i < 4; ++i) u[i] = xor32(v[i]);
     if (g >= 2 || m >= a.M) return;
     const int j = 8 * tt + 4 * g;
     const int p = R.pos[m];
@@ -427,7 +427,7 @@ DEV void epi_tile(const GemmArgs& a, int m, int n0, int lane, const float v_in[4
     // gate rows 4g+i, lane g+2 holds up rows 8+4g+i
     float u[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) u[i] = __shfl_xor(v[i], 32);
+    for (int i = 0; i < 4; ++i) u[i] = xor32(v[i]);
     if (g >= 2 || m >= a.M) return;
     const int col = (n0 >> 1) + 4 * g;
     bf16x4 o;
