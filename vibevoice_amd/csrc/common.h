@@ -90,12 +90,6 @@ DEV float xor32(float v) {
   const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float((__lane_id() & 32) ? a[0] : a[1]);
 }
-DEV float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  return v;
-}
-
 // Row addressing shared by every kernel that reads or writes "rows".
 // Logical row m belongs to group g = m / T (a sample), row t = m % T inside it.
 // The group's storage slot is idx[g] when idx != nullptr (streaming state is
