@@ -29,60 +29,67 @@ DEV size_t mix_lds_bytes(int R, int ctx, int C) {
   return (size_t)(2 * R + ctx) * C * sizeof(bf16) + (size_t)(R + ctx) * (C / 8 + 1) * sizeof(float);
 }
 
-template <bool TO_LDS>
-DEV void mix_rows(const MixArgs& a, unsigned char* smem, bf16* a_lds, int a_ld) {
+// Every global load is issued in the kernel's first batch: the per-channel
+// operands, the QB row items per thread (branch-free, clamped addresses, so
+// the waits are counted), then `issue` (k_block's fc1 / fc2 weights, biases and
+// output slot) -- one exposed memory round trip before the LDS phases instead
+// of one per phase.  The raw x rows the workgroup owns stay in ybuf for the
+// gamma residual (they were re-read from global).  blockDim.x % n8 == 0 (host
+// check), so a thread's channel chunk is the same in every loop: c2.
+template <bool TO_LDS, int QB, typename Issue>
+DEV void mix_rows(const MixArgs& a, unsigned char* smem, bf16* a_lds, int a_ld, Issue&& issue) {
   const int t0 = blockIdx.x * a.R, smp = blockIdx.y;
   const int C = a.C, n8 = C >> 3;
   const int rows = a.R + a.ctx;
   bf16* nrm = (bf16*)smem;                       // [rows][C] normalised inputs of the conv
-  bf16* ybuf = nrm + (size_t)rows * C;           // [R][C]
+  bf16* ybuf = nrm + (size_t)rows * C;           // [R][C] raw x rows, then y
   float* ssp = (float*)(ybuf + (size_t)a.R * C); // [rows][n8] partial sums of squares
   float* inv = ssp + (size_t)rows * n8;          // [rows] inverse RMS (x rows, then y rows)
   const bf16* X = a.x + (long long)smp * a.T * C;
   bf16* buf = a.buf + (long long)a.slots[smp] * a.buf_sB;
   const int LPR = n8 < 64 ? n8 : 64;
   const int gi = threadIdx.x / LPR, gl = threadIdx.x - gi * LPR, ng = blockDim.x / LPR;
-  // ---- this thread's conv item (row i, chunk c): its per-channel operands go
-  // out first, in one batch with the row loads below (vmcnt waits are in order)
+  // ---- this thread's conv item (row i, chunk c2)
   const int e2 = threadIdx.x;
   const int i2 = e2 / n8, c2 = e2 - i2 * n8;
   const bool own = e2 < a.R * n8 && t0 + i2 < a.T;
-  bf16x8 wk[7], bb, gv, wf;
-  if (own) {
+  bf16x8 wk[7], bb, gv, wf, wn;
 #pragma unroll
-    for (int k = 0; k < 7; ++k) wk[k] = *(const bf16x8*)(a.dw_w + (size_t)c2 * 56 + k * 8);
-    bb = *(const bf16x8*)(a.dw_b + c2 * 8);
-    gv = *(const bf16x8*)(a.gamma + c2 * 8);
-    wf = *(const bf16x8*)(a.ffn_norm_w + c2 * 8);
-  }
+  for (int k = 0; k < 7; ++k) wk[k] = *(const bf16x8*)(a.dw_w + (size_t)c2 * 56 + k * 8);
+  bb = *(const bf16x8*)(a.dw_b + c2 * 8);
+  gv = *(const bf16x8*)(a.gamma + c2 * 8);
+  wf = *(const bf16x8*)(a.ffn_norm_w + c2 * 8);
+  wn = *(const bf16x8*)(a.norm_w + c2 * 8);
   // ---- phase 1: rows t0 - ctx .. t0 + R - 1 (history rows t < 0 are already
   // normalised in the buffer; halo rows t >= 0 are recomputed from x)
-  // 8 items per thread per batch: all loads first, then the LDS stores
+  // QB items per thread per batch: all loads first, then the LDS stores
   const bf16x8 z8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-  for (int e0 = threadIdx.x; e0 < rows * n8; e0 += 8 * blockDim.x) {
-    bf16x8 v[8];
+  const int nitem = rows * n8;
+  for (int e0 = threadIdx.x, first = 1; e0 < nitem; e0 += QB * blockDim.x, first = 0) {
+    bf16x8 v[QB];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < QB; ++q) {
       const int e = e0 + q * blockDim.x;
-      v[q] = z8;
-      if (e < rows * n8) {
-        const int i = e / n8, c = e - i * n8;
-        const int t = t0 - a.ctx + i;
-        if (t < 0) v[q] = *(const bf16x8*)(buf + (long long)(a.ctx + t) * C + c * 8);
-        else if (t < a.T) v[q] = *(const bf16x8*)(X + (long long)t * C + c * 8);
-      }
+      const int ee = e < nitem ? e : e0;
+      const int i = ee / n8, c = ee - i * n8;
+      const int t = t0 - a.ctx + i;
+      const bf16* src = t < 0 ? buf + (long long)(a.ctx + t) * C + c * 8 : X + (long long)min(t, a.T - 1) * C + c * 8;
+      v[q] = *(const bf16x8*)src;
     }
+    if (first) issue();
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < QB; ++q) {
       const int e = e0 + q * blockDim.x;
-      if (e < rows * n8) {
+      if (e < nitem) {
         const int i = e / n8, c = e - i * n8;
         const int t = t0 - a.ctx + i;
-        *(bf16x8*)(nrm + i * C + c * 8) = v[q];   // history: normalised; else raw, normalised below
+        const bf16x8 vq = t < a.T ? v[q] : z8;
+        *(bf16x8*)(nrm + i * C + c * 8) = vq;   // history: normalised; else raw, normalised below
+        if (i >= a.ctx) *(bf16x8*)(ybuf + (i - a.ctx) * C + c * 8) = vq;
         float ss = 0.f;
         if (t >= 0) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) ss += bf(v[q][j]) * bf(v[q][j]);
+          for (int j = 0; j < 8; ++j) ss += bf(vq[j]) * bf(vq[j]);
         }
         ssp[e] = ss;
       }
@@ -101,11 +108,10 @@ DEV void mix_rows(const MixArgs& a, unsigned char* smem, bf16* a_lds, int a_ld) 
     const int t = t0 - a.ctx + i;
     if (t < 0 || t >= a.T) continue;
     const bf16x8 v = *(const bf16x8*)(nrm + i * C + c * 8);
-    const bf16x8 w = *(const bf16x8*)(a.norm_w + c * 8);
     const float r = inv[i];
     bf16x8 o8;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o8[j] = tobf(rb(rb(bf(v[j]) * r) * bf(w[j])));
+    for (int j = 0; j < 8; ++j) o8[j] = tobf(rb(rb(bf(v[j]) * r) * bf(wn[j])));
     *(bf16x8*)(nrm + i * C + c * 8) = o8;
     if (i >= a.ctx) *(bf16x8*)(buf + (long long)(a.ctx + t) * C + c * 8) = o8;
   }
@@ -123,7 +129,7 @@ DEV void mix_rows(const MixArgs& a, unsigned char* smem, bf16* a_lds, int a_ld) 
         acc[j] += bf(wk[f >> 3][f & 7]) * bf(v[j]);
       }
     }
-    const bf16x8 xv = *(const bf16x8*)(X + (long long)t * C + c2 * 8);
+    const bf16x8 xv = *(const bf16x8*)(ybuf + i2 * C + c2 * 8);   // raw x row (phase 1)
     bf16x8 y8;
     float ss = 0.f;
 #pragma unroll
@@ -158,7 +164,7 @@ DEV void mix_rows(const MixArgs& a, unsigned char* smem, bf16* a_lds, int a_ld) 
 
 __global__ void __launch_bounds__(256) k_mix(MixArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  mix_rows<false>(a, smem, nullptr, 0);
+  mix_rows<false, 4>(a, smem, nullptr, 0, [] {});
 }
 
 // ---------------------------------------------------------------- whole block
@@ -182,7 +188,43 @@ __global__ void __launch_bounds__(256) k_block(BlockArgs b) {
   const int r = lane & 15, g = lane >> 4;
   const int t0 = blockIdx.x * R, smp = blockIdx.y;
 
-  mix_rows<true>(a, smem, alds, a_ld);
+  // fc1's weights / biases, fc2's biases / gamma and the output row base go out
+  // with the mixer's first loads (fc2's weights too while registers allow:
+  // C <= 64; at C = 128 they are issued before fc1's MFMAs instead)
+  constexpr bool W2_EARLY = C <= 64;
+  bf16x8 wf[NTW1][NK1];
+  bf16x4 bv1[NTW1];
+  bf16x8 w2f[2][NK2];
+  bf16x4 bv2[2], gm2[2];
+  long long obase = 0;
+  auto load_w2 = [&]() {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int nt = (2 * wave + j) / MT;
+#pragma unroll
+      for (int c = 0; c < NK2; ++c) w2f[j][c] = *(const bf16x8*)(b.w2 + ((long long)nt * NK2 + c) * 512 + lane * 8);
+    }
+  };
+  auto issue = [&]() {
+#pragma unroll
+    for (int j = 0; j < NTW1; ++j)
+#pragma unroll
+      for (int c = 0; c < NK1; ++c)
+        wf[j][c] = *(const bf16x8*)(b.w1 + ((long long)(wave * NTW1 + j) * NK1 + c) * 512 + lane * 8);
+#pragma unroll
+    for (int j = 0; j < NTW1; ++j) bv1[j] = *(const bf16x4*)(b.b1 + (wave * NTW1 + j) * 16 + 4 * g);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = ((2 * wave + j) / MT) * 16 + 4 * g;
+      bv2[j] = *(const bf16x4*)(b.b2 + n);
+      gm2[j] = *(const bf16x4*)(b.g2 + n);
+    }
+    obase = rm_off(b.out, smp * a.T);   // row t of this sample: + t * out.sT (host: out.T == T)
+    if (W2_EARLY) load_w2();
+  };
+
+  mix_rows<true, 2>(a, smem, alds, a_ld, issue);
+  if (!W2_EARLY) load_w2();
   __syncthreads();
   if (b.dbg_a)
     for (int e = threadIdx.x; e < R * C / 8; e += blockDim.x) {
@@ -193,16 +235,10 @@ __global__ void __launch_bounds__(256) k_block(BlockArgs b) {
 
   // ---- fc1 + GELU -> hidden rows (LDS): wave w owns hidden tiles w*NTW1 .. +NTW1
   {
-    bf16x8 wf[NTW1][NK1];
-#pragma unroll
-    for (int j = 0; j < NTW1; ++j)
-#pragma unroll
-      for (int c = 0; c < NK1; ++c)
-        wf[j][c] = *(const bf16x8*)(b.w1 + ((long long)(wave * NTW1 + j) * NK1 + c) * 512 + lane * 8);
 #pragma unroll
     for (int j = 0; j < NTW1; ++j) {
       const int n = (wave * NTW1 + j) * 16 + 4 * g;
-      const bf16x4 bv = *(const bf16x4*)(b.b1 + n);
+      const bf16x4 bv = bv1[j];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const bf16* xrow = alds + (mt * 16 + r) * a_ld + 8 * g;
@@ -218,14 +254,6 @@ __global__ void __launch_bounds__(256) k_block(BlockArgs b) {
       }
     }
   }
-  // fc2's weights go out before the barrier (they do not depend on the hidden rows)
-  bf16x8 w2f[2][NK2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int nt = (2 * wave + j) / MT;
-#pragma unroll
-    for (int c = 0; c < NK2; ++c) w2f[j][c] = *(const bf16x8*)(b.w2 + ((long long)nt * NK2 + c) * 512 + lane * 8);
-  }
   __syncthreads();
   // ---- fc2 + ffn_gamma + residual -> out: wave w owns tiles 2w, 2w + 1
 #pragma unroll
@@ -238,8 +266,8 @@ __global__ void __launch_bounds__(256) k_block(BlockArgs b) {
     const int m = mt * 16 + r, t = t0 + m;
     if (t >= a.T) continue;
     const int n = nt * 16 + 4 * g;
-    const bf16x4 bv = *(const bf16x4*)(b.b2 + n);
-    const bf16x4 gm = *(const bf16x4*)(b.g2 + n);
+    const bf16x4 bv = bv2[j];
+    const bf16x4 gm = gm2[j];
     const bf16x4 yv = *(const bf16x4*)(ybuf + m * C + n);
     bf16x4 o;
 #pragma unroll
@@ -247,7 +275,7 @@ __global__ void __launch_bounds__(256) k_block(BlockArgs b) {
       const float v = rb(bf(gm[i]) * rb(acc[i] + bf(bv[i])));
       o[i] = tobf(bf(yv[i]) + v);
     }
-    *(bf16x4*)(rm_bfw(b.out, (long long)smp * a.T + t) + n) = o;
+    *(bf16x4*)((bf16*)b.out.base + obase + (long long)t * b.out.sT + n) = o;
   }
 }
 
@@ -258,7 +286,7 @@ static size_t mix_lds_host(int R, int ctx, int C) {
 
 int launch_mix(MixArgs a, hipStream_t st) {
   if (a.n <= 0 || a.T <= 0) return 0;
-  if (a.C % 8 || a.C > 2048 || (256 % (a.C / 8 < 64 ? a.C / 8 : 64)) || a.ctx != 6) return 1;
+  if (a.C % 8 || a.C > 2048 || 256 % (a.C / 8) || a.ctx != 6) return 1;   // mix_rows: 256 % n8 == 0
   if (a.R * (a.C / 8) != 256 && !(a.R == a.T && a.R * (a.C / 8) < 256)) return 1;   // one conv item per thread
   const size_t lds = mix_lds_host(a.R, a.ctx, a.C);
   if (lds > 65536) return 1;
@@ -276,7 +304,7 @@ int launch_block(BlockArgs b, hipStream_t st) {
   const MixArgs& a = b.mix;
   if (a.n <= 0 || a.T <= 0) return 0;
   const size_t lds = block_lds(a.R, a.C);
-  if (!lds || a.ctx != 6 || lds > 65536 || !b.w1 || !b.w2 || !b.b1 || !b.b2 || !b.g2) return 1;
+  if (!lds || a.ctx != 6 || lds > 65536 || !b.w1 || !b.w2 || !b.b1 || !b.b2 || !b.g2 || b.out.T != a.T) return 1;
   const dim3 grid((a.T + a.R - 1) / a.R, a.n);
   switch (a.C) {
     case 32: hipLaunchKernelGGL(k_block<32>, grid, dim3(256), lds, st, b); break;
