@@ -1008,6 +1008,8 @@ static GemmPlan gemv_plan(int N, int K, int M) {
     nw = 2;
   } else if (tiles <= 128) {
     u = 8;
+  } else if (tiles >= 512 && chunks <= 64) {
+    u = 2;   // head gate|up (576 tiles x K 1,536): 6 interleaved in-loop pairs, B = 1 step -13 us vs u = 4
   }
   if (g_tune_waves > 0) {
     int wpt = (g_tune_waves + tiles - 1) / tiles;
