@@ -988,7 +988,8 @@ static GemmPlan gemv_plan(int N, int K, int M) {
       ks = 2;
       nw = 8;
     } else if (tiles == 128 && chunks >= 256) {
-      u = 8;
+      if (chunks == 256) nw = 8;   // codec fc2 at C = 2,048 (K 8,192): 8 x 4 (in-loop A/Bs below)
+      else u = 8;
     } else {
       nw = 8;
     }
@@ -1007,7 +1008,10 @@ static GemmPlan gemv_plan(int N, int K, int M) {
   } else if (tiles >= 1024) {
     nw = 2;
   } else if (tiles <= 128) {
-    u = 8;
+    // LM q|k|v (128 tiles x K 1,536) with codec fc2 above: 8 waves x 4 chunks
+    // instead of 4 x 8, interleaved in-loop pairs -5 .. -26 us per B = 1 step
+    if (tiles == 128 && chunks <= 64) nw = 8;
+    else u = 8;
   } else if (tiles >= 512 && chunks <= 64) {
     u = 2;   // head gate|up (576 tiles x K 1,536): 6 interleaved in-loop pairs, B = 1 step -13 us vs u = 4
   }
