@@ -982,7 +982,8 @@ static GemmPlan gemv_plan(int N, int K, int M) {
   if (tiles <= 128 && chunks >= 128) {
     if (M >= 8) {   // batched rows: 2-way split-K (sc1 hand-off) reaches 2x the CUs
       ks = 2;
-      if (chunks >= 256) u = 8;
+      if (chunks == 256 && tiles == 128) nw = 8;   // codec fc2, C = 2,048: 8 x 4 (B = 8 in-loop A/B: -53 us per step)
+      else if (chunks >= 256) u = 8;
       else nw = 8;
     } else if (tiles < 128 && chunks >= 256) {   // M < 8 LM down: 2-way split-K, 8 waves x 4
       ks = 2;
