@@ -49,7 +49,8 @@ def parse():
     ap.add_argument("--model", default="1.5B", choices=["1.5B", "Large"])
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel ranks per model replica (RCCL)")
     ap.add_argument("--context", type=int, default=0,
-                    help="grow the positive context to this many positions with synthetic K/V before timing "
+                    help="prompt length in tokens: a long script prefilled through the product path "
+                         "(k_attn_pf + k_gemm_xl) before timing decode at that context "
                          "(SURVEY.md §8d config 5: 64K-position decode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-tokens", type=int, default=8, help="timed tokens of the CPU oracle sample")
@@ -186,6 +187,55 @@ def measure_gemv(model, B, iters=6):
                 avg_us=round(avg_s * 1e6, 2), alg_bytes_per_launch=alg)
 
 
+# ------------------------------------------------------------------ TP collective share
+def measure_tp_collective(make_pass, n_layers, world, dev, iters=20):
+    """Time of one LM pass with its 2 x n_layers RCCL all-reduces and with
+    them skipped (vv_tp_null_collective: the outputs are then wrong, so this
+    runs after the timed loop), max over ranks; their difference is the
+    collectives' share of the pass.  make_pass(null) returns a callable that
+    runs one pass (a hipGraph replay of the loop's LM phase, captured with the
+    switch set as given)."""
+    def timed(null):
+        run = make_pass(null)
+        run()
+        barrier(world)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            run()
+        barrier(world)
+        return max_over_ranks(time.perf_counter() - t0, world, dev) / iters
+    on, off = timed(False), timed(True)
+    return dict(lm_pass_us=round(on * 1e6, 2), lm_pass_us_null_collective=round(off * 1e6, 2),
+                allreduce_us_per_pass=round(max(0.0, on - off) * 1e6, 2), allreduce_calls_per_pass=2 * n_layers,
+                allreduce_share=round(max(0.0, on - off) / on, 4) if on > 0 else None,
+                note="RCCL all-reduce (sum, bf16, in place) of the [2B, H] residual after o_proj and down_proj; "
+                     "max over ranks of graph-replayed LM passes with / without the collectives")
+
+
+def lm_pass_maker(model, sess):
+    """make_pass for measure_tp_collective: the loop's LM phase body on the
+    session's static buffers, captured into a hipGraph per switch setting."""
+    from vibevoice_amd import _lib
+    eng, B = model.engine, sess.B
+    L = _lib.lib()
+
+    def body():
+        eng.lm_forward(sess.x_in2[:B], sess.rows2, sess.pos_dev, sess.rows2, hidden_out=sess.hid,
+                       logits_out=sess.logits, max_pos=eng.max_ctx - 1, ntok=2 * B)
+
+    def make(null):
+        L.vv_tp_null_collective(1 if null else 0)
+        try:
+            body()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                body()
+        finally:
+            L.vv_tp_null_collective(0)
+        return g.replay
+    return make
+
+
 # ------------------------------------------------------------------ CPU baseline (oracle)
 def cpu_baseline(cfg, tokens, S):
     """The oracle's fp32 eager restatement of the reference loop (the
@@ -284,25 +334,30 @@ def main():
     B, S, K, W = args.batch, args.ddpm_steps, args.steps, args.warmup
     T = args.tp
     tp_group, replica, replicas = tp_groups(world, rank, T)
-    inp = synthetic_inputs(batch=B, speakers=args.speakers, voice_seconds=3.0, text_tokens=64, seed=100 + replica)
-    L = inp["input_ids"].shape[1]
     total = W + K + 4
-    if args.context:   # the timed steps end at most at max_position_embeddings (65,536 for the 1.5B LM)
+    text_tokens = 64
+    if args.context:   # a long script: the timed steps end at most at max_position_embeddings (65,536 at 1.5B)
         from vibevoice_amd.config import VibeVoiceConfig
         mpe = VibeVoiceConfig.builtin(args.model).decoder_config.max_position_embeddings
         args.context = min(args.context, mpe - total - 8)
+        base = synthetic_inputs(batch=1, speakers=args.speakers, voice_seconds=3.0, text_tokens=0, seed=0)
+        text_tokens = max(64, args.context - base["input_ids"].shape[1])
+    inp = synthetic_inputs(batch=B, speakers=args.speakers, voice_seconds=3.0, text_tokens=text_tokens,
+                           seed=100 + replica)
+    L = inp["input_ids"].shape[1]
     model = VibeVoiceForConditionalGenerationInference.from_pretrained(
         f"synthetic:{args.model}", device_map=str(dev), synthetic_seed=0, max_batch=B,
-        max_ctx=max(L, args.context) + total + 8,
-        tp_group=tp_group)
+        max_ctx=L + total + 8, tp_group=tp_group)
     model.set_ddpm_inference_steps(S)
     tk = tokenizer_ids()
     forced = [[tk.speech_diffusion_id] * total for _ in range(B)]
     torch.manual_seed(1234)
+    torch.cuda.synchronize()
+    t_pf = time.perf_counter()
     sess = model.generate_session(**inp, tokenizer=tk, cfg_scale=1.3, generation_config={"do_sample": False},
                                   forced_tokens=forced, max_length_times=total / L + 1, max_new_tokens=total + 2)
-    if args.context:
-        sess.extend_context(args.context)
+    torch.cuda.synchronize()
+    prefill_ms = (time.perf_counter() - t_pf) * 1e3
     for _ in range(W):
         assert sess.step()
     ctx0 = int(sess.pos_len.float().mean())
@@ -322,6 +377,10 @@ def main():
     bpt = bytes_per_token(wb, model.config, B, S, ctx_avg, (ctx0 + ctx1) / 2 - L)
     step_ach = bpt * B / (dt / K) / 1e9
     roof = measure_gemv(model, B)
+    tp_coll = None
+    if T > 1:   # after the timed loop: the null-collective passes corrupt the session's state
+        tp_coll = measure_tp_collective(lm_pass_maker(model, sess), model.config.decoder_config.num_hidden_layers,
+                                        world, dev)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:   # bounded CPU sample, N=1 only
@@ -345,16 +404,20 @@ def main():
                     "speech_diffusion schedule (constrained argmax still computed and read back each step)",
             "config": {"workload": f"VibeVoice-{args.model} bf16, {B} dialogue(s)/replica x {args.speakers} "
                                    f"speaker(s), {S} diffusion steps, TP={T}, prompt {L} tokens"
-                                   + (f", positive context grown to {args.context} positions (synthetic K/V)"
+                                   + (f", long-form context: a {L}-token script prefilled through the product "
+                                      f"path ({prefill_ms:.0f} ms incl. the voice encoder), decode timed from there"
                                       if args.context else ""),
                        "model": f"VibeVoice-{args.model}", "global_batch": B * replicas, "seq_len": L,
-                       "diffusion_steps": S, "parallelism": f"dp{replicas} (independent replicas), tp{T}"},
+                       "diffusion_steps": S, "parallelism": f"dp{replicas} (independent replicas), tp{T}",
+                       "context_start": ctx0, "context_end": ctx1},
             "roofline": roof,
             "step_roofline": {"bound": "hbm", "achieved": round(step_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(step_ach / HBM_PEAK_GBS, 4),
                               "alg_bytes_per_token": int(bpt), "note": "whole loop iteration, SURVEY.md §8d bytes"},
             "cpu_baseline": cpu,
         }
+        if tp_coll is not None:
+            line["tp_collective"] = tp_coll
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
@@ -372,12 +435,19 @@ def plumbing(args, world, rank, dev):
     barrier(world)
     dt = max_over_ranks(time.perf_counter() - t0, world, dev)
     tps, audio_per_s = throughput(dt, args.batch, args.steps, replicas)
+    tp_coll = None
+    if args.tp > 1:   # the field's plumbing: a "pass" of 1 ms, 0.25 ms of it the collective
+        tp_coll = measure_tp_collective(lambda null: (lambda: time.sleep(0.75e-3 if null else 1e-3)), 2, world,
+                                        dev, iters=10)
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": round(audio_per_s, 3), "unit": "audio-sec/wall-sec",
-                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                          "ms_per_step": round(dt / args.steps * 1e3, 4), "scaling": "weak",
-                          "data": "plumbing (empty step)", "config": {"parallelism": f"dp{replicas}, tp{args.tp}"},
-                          "backend": torch.distributed.get_backend() if world > 1 else None}), flush=True)
+        line = {"metric": METRIC, "value": round(audio_per_s, 3), "unit": "audio-sec/wall-sec",
+                "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": round(dt / args.steps * 1e3, 4), "scaling": "weak",
+                "data": "plumbing (empty step)", "config": {"parallelism": f"dp{replicas}, tp{args.tp}"},
+                "backend": torch.distributed.get_backend() if world > 1 else None}
+        if tp_coll is not None:
+            line["tp_collective"] = tp_coll
+        print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 

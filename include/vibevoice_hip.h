@@ -111,6 +111,10 @@ int vv_tp_init(vv_ctx* ctx, int rank, int size, const void* unique_id);
 int vv_lm_forward_group(int n, vv_ctx* const* ctxs, int ntok, const void* embeds, int embed_rows, const int* slot,
                         const int* pos, int max_pos_p1, int nout, const int* out_idx, void* hidden_out,
                         float* logits_out, vv_stream st);
+/* Switch (benchmarks only): 1 = skip the RCCL all-reduces of communicator
+ * engines (outputs wrong), so bench.py --tp can time an LM pass with and
+ * without its 2 x n_layers collectives and report their share. */
+int vv_tp_null_collective(int on);
 
 /* Copy the K/V cache entry src[i] -> dst[i] of slot slots[i] (all layers). */
 int vv_kv_copy(vv_ctx* ctx, int n, const int* slots, const int* src, const int* dst, vv_stream st);

@@ -63,7 +63,7 @@ class StreamState:
 
     def get(self, key, slots, C, ctx, like):
         if key not in self.buf:
-            self.buf[key] = torch.zeros(self.n, C, ctx, dtype=like.dtype)
+            self.buf[key] = torch.zeros(self.n, C, ctx, dtype=like.dtype, device=like.device)
         return self.buf[key][slots]
 
     def put(self, key, slots, val):

@@ -24,7 +24,7 @@ def rms_norm(x, eps, weight=None):
 def timestep_freq(t, dim=256, max_period=10000):
     """TimestepEmbedder.timestep_embedding (:66-88): cos||sin, cast to t.dtype."""
     half = dim // 2
-    freqs = torch.exp(-math.log(max_period) * torch.arange(0, half, dtype=torch.float32) / half)
+    freqs = torch.exp(-math.log(max_period) * torch.arange(0, half, dtype=torch.float32, device=t.device) / half)
     args = t[:, None].float() * freqs[None]
     return torch.cat([torch.cos(args), torch.sin(args)], dim=-1).to(t.dtype)
 
@@ -68,7 +68,7 @@ def sample_speech_tokens(sd, cond, neg_cond, noise, steps, cfg_scale, n_layers, 
     for si, t in enumerate(sched.timesteps):
         half = speech[:n]
         combined = torch.cat([half, half], dim=0)
-        eps_ = head_forward(sd, combined, t.repeat(2 * n).to(combined.dtype), condition, n_layers, eps)
+        eps_ = head_forward(sd, combined, t.repeat(2 * n).to(device=combined.device, dtype=combined.dtype), condition, n_layers, eps)
         c_eps, u_eps = torch.split(eps_, n, dim=0)
         half_eps = u_eps + cfg_scale * (c_eps - u_eps)
         speech = sched.step(torch.cat([half_eps, half_eps], dim=0), speech,

@@ -42,14 +42,15 @@ def voice_embeds(sd, cfg, speech_tensors, speech_masks, dtype, voice_noise=None)
     reference does there)."""
     asd = _sub(sd, "model.acoustic_tokenizer.")
     ed = codec.codec_dims(cfg.acoustic_tokenizer_config, "encoder")
-    mean = codec.encode(asd, ed, speech_tensors.to(dtype).unsqueeze(1), None, None, streaming=False)
+    dev = sd["model.speech_scaling_factor"].device
+    mean = codec.encode(asd, ed, speech_tensors.to(device=dev, dtype=dtype).unsqueeze(1), None, None, streaming=False)
     value = cfg.acoustic_tokenizer_config.fix_std / 0.8
     if voice_noise is None:
-        std = torch.randn(mean.shape[0], dtype=mean.dtype) * value
-        eps = torch.randn_like(mean)
+        std = torch.randn(mean.shape[0], dtype=mean.dtype).to(mean.device) * value
+        eps = torch.randn_like(mean.cpu()).to(mean.device)              # randn_like keeps mean's (permuted) strides
     else:
-        std = voice_noise[0].to(mean.dtype) * value
-        eps = voice_noise[1].to(mean.dtype).reshape(mean.shape)
+        std = voice_noise[0].to(device=mean.device, dtype=mean.dtype) * value
+        eps = voice_noise[1].to(device=mean.device, dtype=mean.dtype).reshape(mean.shape)
     z = mean + std[:, None, None] * eps
     feats = (z + sd["model.speech_bias_factor"]) * sd["model.speech_scaling_factor"]
     return connector(sd, "model.acoustic_connector.", feats)[speech_masks]
@@ -97,6 +98,7 @@ def generate(sd, cfg, input_ids, attention_mask, tokenizer_ids, ddpm_steps=10, c
     start, end, diff, eos = (tokenizer_ids[k] for k in ("start", "end", "diffusion", "eos"))
     valid = sorted([start, end, diff, eos])
     emb_w = lsd["embed_tokens.weight"]
+    dev = emb_w.device        # the oracle runs where its weights are (a GPU only as a test's checker)
     lm_head = sd.get("lm_head.weight", emb_w)
     scale, bias = sd["model.speech_scaling_factor"], sd["model.speech_bias_factor"]
 
@@ -139,7 +141,7 @@ def generate(sd, cfg, input_ids, attention_mask, tokenizer_ids, ddpm_steps=10, c
             hs = []
             if teacher is not None:
                 emb0 = emb0.clone()
-                emb0[attention_mask.bool()] = teacher["prompt_embeds"].to(emb0.dtype)
+                emb0[attention_mask.bool()] = teacher["prompt_embeds"].to(device=dev, dtype=emb0.dtype)
             if record is not None:
                 record["prompt_embeds"] = emb0[attention_mask.bool()].clone()
             for b in range(B):
@@ -162,10 +164,10 @@ def generate(sd, cfg, input_ids, attention_mask, tokenizer_ids, ddpm_steps=10, c
                 nxt = torch.multinomial(F.softmax(scores, dim=-1), num_samples=1).squeeze(1)
             else:
                 p = F.softmax(scores[:, valid], dim=-1)
-                nxt = torch.tensor(valid)[(p / sample_q(step)).argmax(-1)]
+                nxt = torch.tensor(valid)[(p / sample_q(step).to(p.device)).argmax(-1).cpu()]
         else:
             sub = lg[:, valid]
-            nxt = torch.tensor(valid)[sub.argmax(-1)]
+            nxt = torch.tensor(valid)[sub.argmax(-1).cpu()]
         nxt[finished] = eos                                           # :509
         seqs = torch.cat([seqs, nxt[:, None]], dim=1)
 
@@ -216,7 +218,7 @@ def generate(sd, cfg, input_ids, attention_mask, tokenizer_ids, ddpm_steps=10, c
                             t[li] = torch.cat([t[li][:, :c + 1], t[li][:, c:-1]], dim=1)
             correct_cnt[nd] += 1
             n = didx.numel()
-            noise = torch.randn(2 * n, cfg.acoustic_vae_dim).to(dtype)  # :716
+            noise = torch.randn(2 * n, cfg.acoustic_vae_dim).to(device=dev, dtype=dtype)  # :716
             if record is not None:
                 record.setdefault("noise", []).append(noise.clone())
             lat = head.sample_speech_tokens(hsd, hpos[didx], hneg[didx], noise, ddpm_steps, cfg_scale,
@@ -224,7 +226,7 @@ def generate(sd, cfg, input_ids, attention_mask, tokenizer_ids, ddpm_steps=10, c
                                             cfg.diffusion_head_config.rms_norm_eps)
             own_lat = lat
             if teacher is not None:
-                lat = teacher["latents"][dstep].to(lat.dtype)
+                lat = teacher["latents"][dstep].to(device=dev, dtype=lat.dtype)
             dstep += 1
             z = (lat / scale - bias).unsqueeze(-1)                    # :651
             a = codec.decode(asd, dd, z, a_state, didx)
@@ -241,7 +243,7 @@ def generate(sd, cfg, input_ids, attention_mask, tokenizer_ids, ddpm_steps=10, c
             record.setdefault("didx", []).append(didx.clone())
             record.setdefault("next_embeds", []).append(next_embeds.clone())
         if teacher is not None:
-            next_embeds = teacher["next_embeds"][step].to(next_embeds.dtype)
+            next_embeds = teacher["next_embeds"][step].to(device=dev, dtype=next_embeds.dtype)
         inputs_embeds = next_embeds
     outs = [torch.cat(c, dim=-1) if c else None for c in audio]
     return seqs, outs, reach

@@ -80,6 +80,12 @@ def test_bench_tp_groups_are_replicas():
     rc, line, err = _run_bench(["--gpus", "4", "--tp", "2", "--plumbing", "--steps", "5"])
     assert rc == 0, err[-2000:]
     assert line["n_gpus"] == 4 and line["config"]["parallelism"] == "dp2, tp2"
+    # the collective-share field --tp adds (plumbing pass: 1 ms, 0.75 ms without the "collective")
+    tc = line["tp_collective"]
+    assert tc["allreduce_calls_per_pass"] == 4
+    assert 900 <= tc["lm_pass_us"] and 650 <= tc["lm_pass_us_null_collective"] < tc["lm_pass_us"]
+    assert abs(tc["allreduce_us_per_pass"] - (tc["lm_pass_us"] - tc["lm_pass_us_null_collective"])) < 0.02
+    assert 0 < tc["allreduce_share"] < 1
 
 
 def test_bench_world_size_mismatch_refused():

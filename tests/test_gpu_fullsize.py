@@ -3,28 +3,25 @@
 σ-VAE codec, hop 3200) against oracle/loop.py, the CPU restatement pinned to
 the reference's own generate() by golden G8.
 
-Workloads (BASELINE.json configs[1] and configs[2]):
-  * B = 1, one 3 s voice prompt (72,000 samples -> 23 latent frames through the
-    real acoustic encoder), 10 diffusion steps, cfg 1.3;
-  * B = 8 two-speaker dialogues, ragged voice clips (3.0 / 2.2 / 1.3 / 2.7 s)
-    and ragged, left-padded scripts, forced schedules mixing speech_diffusion,
-    speech_end (codec reset), speech_start (negative-stream reset), the skip
-    correction and eos.
+Workloads (BASELINE.json configs):
+  * configs[1]: B = 1, one 3 s voice prompt (72,000 samples -> 23 latent frames
+    through the real acoustic encoder), 10 diffusion steps, cfg 1.3;
+  * configs[0]'s workload (1 speaker, 1-sentence script, 5 diffusion steps) on
+    the HIP path — the product has no CPU branch, so its CPU leg is the oracle;
+  * configs[2]: B = 8 two-speaker dialogues, ragged voice clips (3.0 / 2.2 /
+    1.3 / 2.7 s) and ragged, left-padded scripts, forced schedules mixing
+    speech_diffusion, speech_end (codec reset), speech_start (negative-stream
+    reset), the skip correction and eos.
 Weights: seeded synthetic, mode "test" (fan-in-scaled linears, random norms,
 biases and layer-scale gammas, so every term of every kernel contributes).
 
-Teacher forcing (the per-step check `north_star` names: acoustic-latent L2):
-the oracle runs the loop in bf16 (the reference's GPU dtype) and records each
-step's inputs.  The product loop is then driven with exactly those inputs —
-the prompt embeddings, every step's next input embedding and, for the codec,
-every step's latent — so each step's outputs (positive / negative hidden
-states, the 4 legal logits, the diffusion latents, the audio chunk) measure
-one step of arithmetic, not accumulated drift.  The reference's own bf16
-error is measured the same way: the oracle in fp32, teacher-forced on the bf16
-run.  Bound, per step and quantity: rel L2 < max(floor, 2 x that bf16
-self-deviation), floors: hidden 2e-2, latents 2e-2, audio 2e-2.
-Free-running (no forcing): token sequences equal, audio within
-max(5e-2, 2 x the free-running bf16 self-deviation), as the tiny-config tests.
+Teacher forcing (tests/teacher.py): per step and quantity, rel L2 against FIXED
+bounds — hidden 3e-2, logits (the 4 legal ones) 5e-2, acoustic latents 6e-2,
+audio 3e-2, next-step connector embeddings 3e-2.
+Free-running (no forcing): an unforced greedy run of 40 steps whose token
+sequence equals the oracle's, and forced-diffusion audio within rel 0.30 /
+cosine 0.95 after 8 autoregressive frames (the bf16 reference's own drift from
+fp32 over those frames is 0.31).
 """
 import os
 import types
@@ -35,6 +32,7 @@ import torch
 from gpu_util import cos, rel_err
 from oracle import codec as ocodec
 from oracle import loop as oloop
+from teacher import BOUND, oracle_run, per_step_check, teacher_forced
 from vibevoice_amd.config import VibeVoiceConfig
 from vibevoice_amd.modeling_vibevoice_inference import VibeVoiceForConditionalGenerationInference
 from vibevoice_amd.synthetic import synthetic_inputs, tokenizer_ids
@@ -45,9 +43,11 @@ dev = "cuda"
 TK = tokenizer_ids()
 IDS = dict(eos=TK.eos_token_id, start=TK.speech_start_id, end=TK.speech_end_id, diffusion=TK.speech_diffusion_id)
 D, E, S, X = IDS["diffusion"], IDS["end"], IDS["start"], IDS["eos"]
-FLOOR = dict(hpos=2e-2, hneg=2e-2, latents=2e-2, audio=2e-2)
+VALID = sorted(IDS.values())
 STEPS = 10
 SEED = 1234
+GREEDY_W_SEED = 6          # legal lm_head rows of the greedy runs (see _greedy_model)
+GREEDY_STEPS = 40
 
 
 def _cpu_copy(sd_dev):
@@ -69,7 +69,7 @@ def m15():
     model = VibeVoiceForConditionalGenerationInference(cfg, sd_dev, dev, max_batch=8, max_ctx=1024)
     model.set_ddpm_inference_steps(STEPS)
     sd = _cpu_copy(sd_dev)
-    return types.SimpleNamespace(cfg=cfg, model=model, sd=sd, sd32=None)
+    return types.SimpleNamespace(cfg=cfg, model=model, sd=sd, sd_dev=sd_dev, sd32=None, greedy=None)
 
 
 def _sd32(m):
@@ -84,82 +84,10 @@ def _voice_noise(inp, D_lat, seed=9):
     return torch.randn(nv, generator=g), torch.randn(nv, fr, D_lat, generator=g)
 
 
-def _oracle(m, inp, sched, vn, dtype=torch.bfloat16, teacher=None, max_new=None):
-    rec = {}
-    sd = m.sd if dtype == torch.bfloat16 else _sd32(m)
-    torch.manual_seed(SEED)
-    seqs, audio, reach = oloop.generate(sd, m.cfg, inp["input_ids"], inp["attention_mask"], IDS, ddpm_steps=STEPS,
-                                        cfg_scale=1.3, forced=sched, dtype=dtype, record=rec, voice_noise=vn,
-                                        teacher=teacher, max_new_tokens=max_new,
-                                        speech_tensors=inp["speech_tensors"], speech_masks=inp["speech_masks"],
-                                        speech_input_mask=inp["speech_input_mask"])
-    return rec, seqs, audio, reach
-
-
-def _teacher_forced(model, inp, sched, rec):
-    """Drive the product loop with the oracle run's inputs (see module doc).
-    Returns the per-step outputs the product computed."""
-    B = inp["input_ids"].shape[0]
-    got = dict(hpos=[], hneg=[], logits=[], latents=[], audio=[])
-    pe = rec["prompt_embeds"].to(dev, torch.bfloat16)
-    orig = model._prompt_embeds
-    model._prompt_embeds = lambda *a, **k: pe.clone()
-    try:
-        torch.manual_seed(SEED)
-        sess = model.generate_session(input_ids=inp["input_ids"], attention_mask=inp["attention_mask"], tokenizer=TK,
-                                      cfg_scale=1.3, forced_tokens=sched, show_progress_bar=False,
-                                      max_new_tokens=max(len(s) for s in sched) + 2)
-    finally:
-        model._prompt_embeds = orig
-    post = sess._post_phase
-
-    def hooked(n):
-        k = sess.step_idx
-        got["hpos"].append(sess.hid[:B].float().cpu())
-        got["hneg"].append(sess.hid[B:].float().cpu())
-        got["logits"].append(sess.logits_pin.clone()[:, sess.order])          # sorted ids, as the oracle records
-        if n:
-            got["latents"].append(sess.noise_dev[:n].float().cpu())
-            sess.noise_dev[:n].copy_(rec["latents"][len(got["latents"]) - 1].to(dev, torch.bfloat16))
-        post(n)
-        if n:
-            got["audio"].append(sess.audio_dev[:n].float().cpu())
-        sess.x_in2[:B].copy_(rec["next_embeds"][k].to(dev, torch.bfloat16))
-    sess._post_phase = hooked
-    while sess.step():
-        pass
-    torch.cuda.synchronize()
-    return got, sess
-
-
-def _per_step_check(got, rec16, rec32, tag):
-    """rel L2 per step and quantity vs the bf16 oracle; bound max(floor, 2 x
-    the fp32-vs-bf16 deviation of the oracle on the same inputs)."""
-    worst = {}
-    fails = []
-    dsteps = [k for k, d in enumerate(rec16["didx"]) if d.numel()]
-    for q in ("hpos", "hneg", "latents", "audio"):
-        for j in range(len(got[q]) if q in ("latents", "audio") else len(rec16["hpos"])):
-            if q in ("latents", "audio"):
-                r, r32 = rec16[q][j], rec32[q][j]
-                g = got[q][j].reshape(r.shape)
-            elif q == "hneg":
-                if rec16["hneg"][j] is None or j not in dsteps:
-                    continue
-                rows = rec16["didx"][j]                 # the rows the head consumes
-                g, r, r32 = got[q][j][rows], rec16[q][j][rows], rec32[q][j][rows]
-            else:
-                g, r, r32 = got[q][j], rec16[q][j], rec32[q][j]
-            e, self_dev = rel_err(g, r), rel_err(r32, r)
-            bound = max(FLOOR[q], 2 * self_dev)
-            worst[q] = max(worst.get(q, (0, 0, 0)), (e, self_dev, bound))
-            if not e < bound:
-                fails.append(f"{q}[{j}] rel {e:.3e} >= {bound:.3e} (bf16 self-dev {self_dev:.3e})")
-    for q, (e, sd_, b) in worst.items():
-        print(f"{tag} {q}: worst rel {e:.3e} (bf16 reference self-deviation {sd_:.3e}, bound {b:.3e})")
-    lg = max(rel_err(g, r) for g, r in zip(got["logits"], rec16["logits"]))
-    print(f"{tag} logits(4 legal): worst rel {lg:.3e}")
-    assert not fails, "\n".join(fails)
+def _oracle(m, inp, sched, vn, dtype=torch.bfloat16, teacher=None, max_new=None, steps=STEPS, sd=None):
+    if sd is None:
+        sd = m.sd if dtype == torch.bfloat16 else _sd32(m)
+    return oracle_run(sd, m.cfg, inp, sched, IDS, steps, vn, SEED, dtype=dtype, teacher=teacher, max_new=max_new)
 
 
 def test_acoustic_encoder_real_shape(m15):
@@ -213,17 +141,25 @@ def test_prompt_embeds_real_shape(m15):
     assert e < 2e-2
 
 
-def test_teacher_forced_1p5b_b1(m15):
-    """configs[1]: B = 1, 3 s voice, S = 10, 6 diffusion steps then eos."""
+@pytest.mark.parametrize("steps", [10, 5])
+def test_teacher_forced_1p5b_b1(m15, steps):
+    """configs[1] (S = 10) and configs[0]'s workload (S = 5: 1 speaker, a
+    1-sentence script; demo/inference_from_file.py runs it on the CPU in fp32,
+    the product on the GPU in bf16): 3 s voice, 6 diffusion steps, speech_end /
+    speech_start, 2 more, eos."""
     inp = synthetic_inputs(batch=1, speakers=1, voice_seconds=3.0, text_tokens=64, seed=100)
-    sched = [[D] * 6 + [X]]
+    sched = [[D] * 6 + [E, S, D, D, X]]
     vn = _voice_noise(inp, m15.cfg.acoustic_vae_dim)
-    rec16, seqs, _, _ = _oracle(m15, inp, sched, vn)
-    rec32, _, _, _ = _oracle(m15, inp, sched, vn, dtype=torch.float32, teacher=rec16)
-    got, sess = _teacher_forced(m15.model, inp, sched, rec16)
-    assert len(got["latents"]) == len(rec16["latents"]) == 6
+    rec16, seqs, _, _ = _oracle(m15, inp, sched, vn, steps=steps)
+    rec32, _, _, _ = _oracle(m15, inp, sched, vn, dtype=torch.float32, teacher=rec16, steps=steps)
+    m15.model.set_ddpm_inference_steps(steps)
+    try:
+        got, sess = teacher_forced(m15.model, inp, sched, rec16, TK, SEED)
+    finally:
+        m15.model.set_ddpm_inference_steps(STEPS)
+    assert len(got["latents"]) == len(rec16["latents"]) == 8
     assert torch.equal(sess.result().sequences, seqs)
-    _per_step_check(got, rec16, rec32, "1.5B B=1")
+    per_step_check(got, rec16, rec32, f"1.5B B=1 S={steps}")
 
 
 def test_teacher_forced_1p5b_b8_two_speakers(m15):
@@ -245,36 +181,116 @@ def test_teacher_forced_1p5b_b8_two_speakers(m15):
     vn = _voice_noise(inp, m15.cfg.acoustic_vae_dim)
     rec16, seqs, _, reach = _oracle(m15, inp, sched, vn)
     rec32, _, _, _ = _oracle(m15, inp, sched, vn, dtype=torch.float32, teacher=rec16)
-    got, sess = _teacher_forced(m15.model, inp, sched, rec16)
+    got, sess = teacher_forced(m15.model, inp, sched, rec16, TK, SEED)
     out = sess.result()
     assert torch.equal(out.sequences, seqs) and torch.equal(out.reach_max_step_sample.cpu(), reach)
-    _per_step_check(got, rec16, rec32, "1.5B B=8 two-speaker")
+    per_step_check(got, rec16, rec32, "1.5B B=8 two-speaker")
+
+
+def _greedy_model(m):
+    """The 1.5B test model with its 4 legal lm_head rows re-drawn (seed
+    GREEDY_W_SEED; eos's row = -(the other three), so eos never wins and the
+    run lasts GREEDY_STEPS), untied from the embedding so the inputs are
+    unchanged.  With the synthetic rows the hidden state after a speech_start
+    input always picks speech_start (a fixed point, margins ~240); these rows
+    give a greedy path that mixes speech_diffusion and speech_end, whose
+    speech_end -> speech_start transitions reset the negative stream and the
+    codec state."""
+    if m.greedy is None:
+        emb = m.sd["model.language_model.embed_tokens.weight"]
+        W = torch.randn(4, emb.shape[1], generator=torch.Generator().manual_seed(GREEDY_W_SEED))
+        W[0] = -(W[1] + W[2] + W[3])                     # VALID is sorted: eos first
+        lm_head = emb.clone()
+        lm_head[VALID] = W.to(emb.dtype)
+        sd = dict(m.sd)
+        sd["lm_head.weight"] = lm_head
+        sd_dev = dict(m.sd_dev)
+        sd_dev["lm_head.weight"] = lm_head.to(dev)
+        model = VibeVoiceForConditionalGenerationInference(m.cfg, sd_dev, dev, max_batch=1, max_ctx=1024)
+        model.set_ddpm_inference_steps(STEPS)
+        m.greedy = types.SimpleNamespace(sd=sd, model=model)
+    return m.greedy
+
+
+def _margins(logits):
+    """Top-2 margin of each step's 4 legal logits, relative to their L2 norm."""
+    out = []
+    for lg in logits:
+        s = lg[0].float().sort().values
+        out.append(float((s[-1] - s[-2]) / lg[0].float().norm()))
+    return out
+
+
+def test_greedy_tokens_teacher_forced_1p5b(m15):
+    """Unforced greedy token choice over 40 steps (:494-509), teacher-forced:
+    the oracle chooses greedily; the product is driven with the oracle's inputs
+    and its OWN constrained argmax (k_final_head over the 4 legal rows, read
+    back every step) must equal the oracle's choice wherever the oracle's
+    top-2 margin exceeds 2 x the logits bound (rel 0.1 of the logits' norm —
+    a margin the bounded logit error cannot flip); every step's logits are
+    within that bound.  The path mixes diffusion, speech_end and speech_start."""
+    g = _greedy_model(m15)
+    inp = synthetic_inputs(batch=1, speakers=1, voice_seconds=3.0, text_tokens=64, seed=102)
+    vn = _voice_noise(inp, m15.cfg.acoustic_vae_dim)
+    rec, seqs, _, _ = _oracle(m15, inp, None, vn, max_new=GREEDY_STEPS, sd=g.sd)
+    L = inp["input_ids"].shape[1]
+    toks = seqs[0, L:].tolist()
+    margins = _margins(rec["logits"])
+    print("greedy tokens", [t - 151640 for t in toks])
+    print("oracle margins", [round(x, 3) for x in margins])
+    assert len(toks) >= 32, len(toks)
+    assert {D, E, S} <= set(toks), "the greedy path should exercise diffusion, speech_end and speech_start"
+    seen = []
+    got, sess = teacher_forced(g.model, inp, [toks], rec, TK, SEED)
+    for k, lg in enumerate(got["logits"]):
+        mine = VALID[int(lg[0].argmax())]
+        seen.append(mine)
+        if margins[k] > 2 * BOUND["logits"]:
+            assert mine == toks[k], f"step {k}: product argmax {mine} != oracle {toks[k]} (margin {margins[k]:.3f})"
+    print("product argmax", [t - 151640 for t in seen])
+    per_step_check(got, rec, None, "1.5B greedy (teacher-forced)")
 
 
 def test_free_running_1p5b(m15):
-    """No teacher forcing.  (1) Greedy, unforced, 8 steps from a 3 s voice
-    prompt: the token sequence equals the oracle's.  (2) A forced 8-step
-    diffusion run: audio within max(5e-2, 2 x the bf16 reference's own
-    free-running deviation from fp32) — bf16 noise compounds through the
-    autoregressive feedback."""
-    model = m15.model
+    """No teacher forcing.  (1) Greedy, unforced, from a 3 s voice prompt with
+    the greedy rows of _greedy_model: the product's token sequence equals the
+    oracle's, except that the two may part at a step whose oracle margin is
+    under 0.1 of the logits' norm (where bounded bf16 drift may legitimately
+    pick the other token); the comparison ends there.  (2) A forced 8-step
+    diffusion run: audio within rel L2 0.30 and cosine 0.95 of the bf16 oracle
+    (fixed bound; bf16 noise compounds through the autoregressive feedback —
+    the bf16 reference's own free-running deviation from fp32 is printed
+    beside it)."""
+    g = _greedy_model(m15)
+    model = g.model
     inp = synthetic_inputs(batch=1, speakers=1, voice_seconds=3.0, text_tokens=64, seed=102)
     nv, fr = inp["speech_masks"].shape
+    L = inp["input_ids"].shape[1]
     # (1) greedy token choice: the device's prefill draws replayed into the oracle
     torch.manual_seed(SEED)
-    out = model.generate(**inp, tokenizer=TK, cfg_scale=1.3, max_new_tokens=8, show_progress_bar=False)
+    out = model.generate(**inp, tokenizer=TK, cfg_scale=1.3, max_new_tokens=GREEDY_STEPS, show_progress_bar=False)
     torch.cuda.manual_seed(SEED)
     vn = (torch.randn(nv, device=dev, dtype=torch.bfloat16).cpu(),
           torch.randn(nv, fr, m15.cfg.acoustic_vae_dim, device=dev, dtype=torch.bfloat16).cpu())
-    rec, seqs, _, _ = _oracle(m15, inp, None, vn, max_new=8)
-    print("greedy tokens", (out.sequences[0, inp["input_ids"].shape[1]:] - 151640).tolist(),
-          "oracle logit margins", [round(float(l.sort().values[0, -1] - l.sort().values[0, -2]), 2)
-                                   for l in rec["logits"]])
-    assert torch.equal(out.sequences, seqs)
+    rec, seqs, _, _ = _oracle(m15, inp, None, vn, max_new=GREEDY_STEPS, sd=g.sd)
+    mine, ref = out.sequences[0, L:].tolist(), seqs[0, L:].tolist()
+    margins = _margins(rec["logits"])
+    print("greedy tokens  ", [t - 151640 for t in mine])
+    print("oracle tokens  ", [t - 151640 for t in ref])
+    print("oracle margins ", [round(x, 3) for x in margins])
+    n = 0
+    while n < min(len(mine), len(ref)) and mine[n] == ref[n]:
+        n += 1
+    print(f"greedy tokens equal for {n} of {len(ref)} steps")
+    if n < len(ref):
+        assert n < len(margins) and margins[n] < 0.1, \
+            f"greedy tokens part at step {n} where the oracle margin is {margins[n]:.3f} (>= 0.1)"
+    else:
+        assert len(mine) == len(ref)
     # (2) forced diffusion, free-running audio
     sched = [[D] * 8 + [X]]
     torch.manual_seed(SEED)
-    out = model.generate(**inp, tokenizer=TK, cfg_scale=1.3, forced_tokens=sched, show_progress_bar=False)
+    out = m15.model.generate(**inp, tokenizer=TK, cfg_scale=1.3, forced_tokens=sched, show_progress_bar=False)
     _, seqs16, a16, _ = _oracle(m15, inp, sched, vn)
     _, _, a32, _ = _oracle(m15, inp, sched, vn, dtype=torch.float32)
     assert torch.equal(out.sequences, seqs16)
@@ -282,4 +298,4 @@ def test_free_running_1p5b(m15):
     assert got.shape == ref.shape == (1, 8 * 3200)
     e, c, noise = rel_err(got, ref), cos(got, ref), rel_err(ref, a32[0])
     print(f"1.5B free-running audio rel {e:.3e} cos {c:.6f} (bf16 reference vs fp32: {noise:.3e})")
-    assert e < max(5e-2, 2 * noise)
+    assert e < 0.30 and c > 0.95

@@ -11,8 +11,10 @@ context (BASELINE.json configs[3] and configs[4]) on the MI355X.
   ranks' shards interleaved layer by layer on one GPU, on-device sum as the
   all-reduce) — vs the TP = 1 engine.
 * configs[4]: a 65,000-token 1.5B-shape prefill followed by decode steps vs
-  oracle/lm.py run as the checker on the GPU (chunked causal prefill), and
-  TP = 2 at a 33,000-token context vs the TP = 1 engine.
+  oracle/lm.py run as the checker on the GPU (chunked causal prefill); the
+  decode step captured into a hipGraph (the loop's max_ctx plan) and replayed
+  at 65K keys, bitwise equal to eager launches; TP = 2 at a 65,000-token
+  context vs the TP = 1 engine, and its graph-replayed decode vs its eager one.
 Tolerance: rel L2 < 2e-2 and cosine > 0.999 (bf16), as test_gpu_lm.py.
 """
 import pytest
@@ -179,15 +181,95 @@ def test_64k_context_prefill_and_decode_vs_oracle():
         assert rel_err(h, ref) < 2e-2 and cos(h, ref) > 0.999
 
 
+def _graph_vs_eager(run, set_step, n_steps):
+    """Eager decode steps, then the same call captured into a hipGraph and
+    replayed on the same static buffers: bitwise equal outputs.  Re-running a
+    step at its position rewrites that position's K/V with the same values and
+    attends keys [0, pos], so the replays see exactly the eager state."""
+    eager = []
+    for s in range(n_steps):
+        set_step(s)
+        eager.append(run())
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        run()
+    replayed = []
+    for s in range(n_steps):
+        set_step(s)
+        g.replay()
+        replayed.append(run.out())
+    torch.cuda.synchronize()
+    return eager, replayed
+
+
+class _Dec:
+    """Static-buffer decode call (one row) for graph capture."""
+
+    def __init__(self, eng, peers=None):
+        self.eng, self.peers = eng, peers
+        self.x = torch.zeros(1, eng.hidden, dtype=torch.bfloat16, device=dev)
+        self.pos = torch.zeros(1, **I32)
+        self.rows = torch.zeros(1, **I32)
+        self.h = torch.zeros(1, eng.hidden, dtype=torch.bfloat16, device=dev)
+        self.lg = torch.zeros(1, 4, dtype=torch.float32, device=dev)
+
+    def __call__(self):
+        a = (self.x, self.rows, self.pos, self.rows)
+        kw = dict(hidden_out=self.h, logits_out=self.lg, max_pos=self.eng.max_ctx - 1)   # the loop's graph plan
+        if self.peers is None:
+            self.eng.lm_forward(*a, **kw)
+        else:
+            self.eng.lm_forward_group(self.peers, *a, **kw)
+        return self.out()
+
+    def out(self):
+        return self.h.clone(), self.lg.clone()
+
+
+def test_64k_graph_decode_matches_eager():
+    """configs[4]'s decode step as the loop runs it — captured into a hipGraph
+    with the max_ctx split plan and replayed — at a real 65,000-token context
+    (prefilled by k_attn_pf / k_gemm_xl, 1.5B layer shapes, 2 layers): bitwise
+    equal to eager launches, and the first replayed step vs oracle/lm.py."""
+    cfg = tiny_config(hidden=1536, layers=2, heads=12, kv_heads=2, inter=8960)
+    cfg.decoder_config["max_position_embeddings"] = 65536
+    sd = synthetic_state_dict(cfg, seed=26, device="cpu", mode="test", with_acoustic_encoder=False)
+    N = 65000
+    eng = Engine(cfg, sd, dev, max_batch=1, max_ctx=N + 40, valid_ids=VALID)
+    g = torch.Generator(device=dev).manual_seed(7)
+    x = torch.randn(N, 1536, device=dev, generator=g).bfloat16()
+    eng.lm_forward(x, torch.zeros(N, **I32), torch.arange(N).to(**I32), torch.tensor([N - 1]).to(**I32))
+    steps = torch.randn(4, 1536, device=dev, generator=g).bfloat16()
+    dec = _Dec(eng)
+
+    def set_step(s):
+        dec.x.copy_(steps[s:s + 1])
+        dec.pos.fill_(N + s)
+    eager, replayed = _graph_vs_eager(dec, set_step, 4)
+    for s, ((he, le), (hg, lg)) in enumerate(zip(eager, replayed)):
+        print(f"64K graph step {s} (attends {N + s + 1} keys): bitwise {torch.equal(he, hg) and torch.equal(le, lg)}")
+        assert torch.equal(he, hg) and torch.equal(le, lg)
+    osd, lcfg = oracle_sd(sd, dev), dict(cfg.decoder_config)
+    kv = olm.RowKV(2)
+    with torch.no_grad():
+        _oracle_prefill_gpu(osd, lcfg, x, kv)
+        ref = olm.forward_rows(osd, lcfg, steps[None, :1], [kv])[0, -1]
+    print(f"64K graph step 0 vs oracle: rel {rel_err(replayed[0][0], ref):.3e} cos {cos(replayed[0][0], ref):.6f}")
+    assert rel_err(replayed[0][0], ref) < 2e-2 and cos(replayed[0][0], ref) > 0.999
+
+
 def test_tp2_long_context_matches_single_engine():
     """configs[4] under TP = 2 (1.5B: 2 kv heads -> one per rank): a
-    33,000-token prefill and decode steps, group vs the TP = 1 engine."""
+    65,000-token prefill and decode steps, group vs the TP = 1 engine; then the
+    group's decode captured into a hipGraph and replayed, bitwise equal to the
+    group's eager launches."""
     cfg = tiny_config(hidden=1536, layers=2, heads=12, kv_heads=2, inter=8960)
     cfg.decoder_config["max_position_embeddings"] = 65536
     sd = synthetic_state_dict(cfg, seed=25, device="cpu", mode="test", with_acoustic_encoder=False)
-    N = 33000
-    full = Engine(cfg, sd, dev, max_batch=1, max_ctx=N + 8, valid_ids=VALID)
-    group = [Engine(cfg, sd, dev, max_batch=1, max_ctx=N + 8, valid_ids=VALID, tp_rank=r, tp_size=2)
+    N = 65000
+    full = Engine(cfg, sd, dev, max_batch=1, max_ctx=N + 40, valid_ids=VALID)
+    group = [Engine(cfg, sd, dev, max_batch=1, max_ctx=N + 40, valid_ids=VALID, tp_rank=r, tp_size=2)
              for r in range(2)]
     g = torch.Generator(device=dev).manual_seed(6)
     x = torch.randn(N, 1536, device=dev, generator=g).bfloat16()
@@ -195,13 +277,22 @@ def test_tp2_long_context_matches_single_engine():
     h1, l1 = full.lm_forward(*args)
     hg, lg = group[0].lm_forward_group(group[1:], *args)
     torch.cuda.synchronize()
-    print(f"TP=2 33K prefill: rel {rel_err(hg, h1):.3e} cos {cos(hg, h1):.6f}")
+    print(f"TP=2 65K prefill: rel {rel_err(hg, h1):.3e} cos {cos(hg, h1):.6f}")
     assert rel_err(hg, h1) < 2e-2 and cos(hg, h1) > 0.999
+    steps = torch.randn(3, 1536, device=dev, generator=g).bfloat16()
     for s in range(3):
-        step = torch.randn(1, 1536, device=dev, generator=g).bfloat16()
-        a = (step, torch.zeros(1, **I32), torch.tensor([N + s]).to(**I32), torch.zeros(1, **I32))
+        a = (steps[s:s + 1], torch.zeros(1, **I32), torch.tensor([N + s]).to(**I32), torch.zeros(1, **I32))
         h1, _ = full.lm_forward(*a)
         hg, _ = group[0].lm_forward_group(group[1:], *a)
         torch.cuda.synchronize()
-        print(f"TP=2 33K step {s}: rel {rel_err(hg, h1):.3e} cos {cos(hg, h1):.6f}")
+        print(f"TP=2 65K step {s}: rel {rel_err(hg, h1):.3e} cos {cos(hg, h1):.6f}")
         assert rel_err(hg, h1) < 2e-2 and cos(hg, h1) > 0.999
+    dec = _Dec(group[0], group[1:])
+
+    def set_step(s):
+        dec.x.copy_(steps[s:s + 1])
+        dec.pos.fill_(N + s)
+    eager, replayed = _graph_vs_eager(dec, set_step, 3)
+    for s, ((he, le), (hr, lr)) in enumerate(zip(eager, replayed)):
+        print(f"TP=2 65K graph step {s}: bitwise {torch.equal(he, hr) and torch.equal(le, lr)}")
+        assert torch.equal(he, hr) and torch.equal(le, lr)

@@ -110,3 +110,28 @@ def test_api_frames_bit_identical_to_codec_step(setup):
         s2 = model.model.semantic_tokenizer.encode(a2, cache=sc, sample_indices=torch.arange(2), use_cache=True).mean
         torch.cuda.synchronize()
         assert torch.equal(a1, a2[:, 0]) and torch.equal(s1, s2[:, 0])
+
+
+def test_tokenizer_views_on_a_tp_shard():
+    """The tokenizer views of a tensor-parallel rank bind the rank's packed LM
+    shards (the view engine used tp_size = 1 and failed the shape
+    check on every TP model).  A TP = 2 rank-0 owner (single-process group, no
+    communicator) decodes and encodes bit-identically to the TP = 1 model."""
+    import types
+    from vibevoice_amd import tokenizer as tk
+    from vibevoice_amd.engine import Engine
+    cfg = tiny_config(hidden=256, layers=1, heads=4, kv_heads=2, inter=512, ratios=(8, 5, 5, 4, 2, 2),
+                      depths="3-3-3-3-3-3-8", nf=32)
+    sd = synthetic_state_dict(cfg, seed=43, device="cpu", mode="test", with_acoustic_encoder=False)
+    model = VibeVoiceForConditionalGenerationInference(cfg, sd, dev, max_batch=4, max_ctx=64)
+    shard = Engine(cfg, sd, dev, max_batch=4, max_ctx=64, tp_rank=0, tp_size=2)
+    owner = types.SimpleNamespace(engine=shard, config=cfg, device=model.device, tp_rank=0, tp_size=2)
+    pool = tk._SlotPool(owner, 4)
+    ac = tk.AcousticTokenizer(owner, pool, cfg.acoustic_tokenizer_config)
+    sc = tk.SemanticTokenizer(owner, pool, cfg.semantic_tokenizer_config)
+    g = torch.Generator().manual_seed(9)
+    z = torch.randn(2, 64, 3, generator=g).bfloat16().to(dev)
+    a_tp = ac.decode(z)
+    a_1 = model.model.acoustic_tokenizer.decode(z)
+    assert torch.equal(a_tp, a_1)
+    assert torch.equal(sc.encode(a_tp).mean, model.model.semantic_tokenizer.encode(a_1).mean)

@@ -43,6 +43,7 @@ EXPORTS = [
     ("vv_kv_synthetic", I, [P, I, P, I, I, ctypes.c_uint, P]),
     ("vv_tp_unique_id", I, [P, I]),
     ("vv_tp_init", I, [P, I, I, P]),
+    ("vv_tp_null_collective", I, [I]),
     ("vv_lm_forward_group", I, [I, ctypes.POINTER(P), I, P, I, P, P, I, I, P, P, P, P]),
     ("vv_embed", I, [P, I, P, P, P]),
     ("vv_diffusion_sample", I, [P, I, P, P, P, F, P, P]),

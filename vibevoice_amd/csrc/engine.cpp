@@ -996,11 +996,20 @@ static int lm_mlp_half(vv_ctx* c, LmPass& P, int l, hipStream_t st) {
   return 0;
 }
 
+// Benchmarks only (bench.py --tp: the collective's share of an LM pass):
+// skip the all-reduces of a communicator engine — the outputs are then wrong.
+static int g_tp_null = 0;
+extern "C" int vv_tp_null_collective(int on) {
+  g_tp_null = on ? 1 : 0;
+  return 0;
+}
+
 static int tp_allreduce(vv_ctx* c, LmPass& P, hipStream_t st) {
   if (!c->comm) {
     if (c->tp_size > 1) FAIL("tensor-parallel engine without a communicator (vv_tp_init)");
     return 0;
   }
+  if (g_tp_null) return 0;
   const ncclResult_t r = ncclAllReduce(P.h, P.h, (size_t)P.ntok * c->cfg.hidden, ncclBfloat16, ncclSum, c->comm, st);
   if (r != ncclSuccess) FAIL(std::string("ncclAllReduce: ") + ncclGetErrorString(r));
   return 0;
@@ -1151,6 +1160,18 @@ static int chain_launch(vv_ctx* c, const vv_ctx::Chain& T, ChainArgs A, hipStrea
   A.err = (unsigned*)c->chain_err.p;
   HIPCHK(hipMemsetAsync(c->chain_sync.p, 0, (size_t)T.nsync * 4, st));
   KCHK(launch_chain(A, T.lds, st));
+  // Eager launches (the chain is an opt-in switch): a dependency wait that gave
+  // up (not every workgroup co-resident, e.g. CUs held by another stream) left
+  // latents built from stale inputs — report it instead of returning success.
+  // Inside a graph capture the caller checks vv_chain_error after replay.
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  HIPCHK(hipStreamIsCapturing(st, &cap));
+  if (cap == hipStreamCaptureStatusNone) {
+    HIPCHK(hipStreamSynchronize(st));
+    const int e = vv_chain_error(c);
+    if (e) FAIL("persistent chain: a dependency wait gave up at op " + std::to_string(e - 1) +
+                " (workgroups not co-resident); outputs are invalid");
+  }
   return 0;
 }
 

@@ -165,8 +165,9 @@ class Engine:
         if logits_out is None:
             logits_out = torch.empty(nout, self.n_valid, dtype=torch.float32, device=self.device)
         if getattr(self, "_valid", None):
-            for p in peers:
-                p.set_valid_ids(self._valid)
+            for p in peers:      # only on change: the copy is synchronous (not allowed inside a graph capture)
+                if getattr(p, "_valid", None) != self._valid:
+                    p.set_valid_ids(self._valid)
         mp = int(max_pos if max_pos is not None else pos.max().item()) + 1
         ctxs = (ctypes.c_void_p * (1 + len(peers)))(self.h, *[p.h for p in peers])
         _lib.check(_lib.lib().vv_lm_forward_group(1 + len(peers), ctxs, ntok, _ptr(embeds), rows, _ptr(slots),

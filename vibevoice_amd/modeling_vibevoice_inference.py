@@ -486,23 +486,6 @@ class GenerateSession:
         eng.lm_forward(step_in, tok_slot.to(**i32), tok_pos.to(**i32), out_idx.to(**i32), hidden_out=self.hid,
                        logits_out=self.logits, max_pos=int(tok_pos.max()))
 
-    def extend_context(self, n_pos, seed=0):
-        """Benchmarks only: grow every positive row's
-        context to n_pos positions with synthetic K/V (vv_kv_synthetic) instead of
-        a long prefill, so decode is timed attending n_pos keys.  Positions stay
-        consistent (cache index == RoPE position); the values are not a
-        reference computation."""
-        i32 = dict(device=self.dev, dtype=torch.int32)
-        for b in range(self.B):
-            p0 = int(self.pos_len[b])
-            if n_pos <= p0:
-                continue
-            if n_pos + self.max_steps + 2 > self.eng.max_ctx:
-                raise RuntimeError(f"extend_context({n_pos}) needs max_ctx >= {n_pos + self.max_steps + 2}")
-            self.eng.kv_synthetic(torch.tensor([b], **i32), p0, n_pos, seed=seed + b)
-            self.pos_len[b] = n_pos
-        self.pos_pushed = False
-
     # ---------------------------------------------------------------- device phases
     def _replay(self, key, fn):
         """Run `fn` (device work only, on static buffers).  With graphs on, the

@@ -94,7 +94,10 @@ class _SlotPool:
     def eng(self):
         if self._eng is None:
             m = self.model.engine
-            self._eng = Engine(self.model.config, None, m.device, max_batch=self.n, max_ctx=64, packed=m.w)
+            # same TP coordinates as the owner: its packed LM weights are this rank's shards
+            # (no communicator: the views only run the replicated codec / connectors)
+            self._eng = Engine(self.model.config, None, m.device, max_batch=self.n, max_ctx=64, packed=m.w,
+                               tp_rank=m.tp_rank, tp_size=m.tp_size)
         return self._eng
 
     def _i32(self, xs):
@@ -207,7 +210,10 @@ class SemanticTokenizer(_TokenizerView):
     @torch.no_grad()
     def encode(self, audio, cache=None, sample_indices=None, use_cache=False, debug=False):
         """audio [n, 1, L], L a multiple of the hop (whole frames, as generate()
-        feeds it, :673-679) -> output with mean [n, L / hop, semantic_dim]."""
+        feeds it, :673-679) -> output with mean [n, L / hop, semantic_dim].
+        A partial last frame raises: the reference pads it per conv layer
+        (extra right padding of each strided conv, :127-133), which no fixture
+        pins; INTEGRATION.md lists this difference."""
         eng = self._pool.eng
         a = audio.reshape(audio.shape[0], -1).to(self.device, torch.bfloat16)
         n, L = a.shape
