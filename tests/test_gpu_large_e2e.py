@@ -80,10 +80,14 @@ def test_teacher_forced_large_4_speakers(large):
     assert inp["speech_tensors"].shape[0] == 4
     sched = [[D, D, D, D, E, S, D, D, D, X]]
     vn = _voice_noise(inp, large.cfg.acoustic_vae_dim)
-    with torch.no_grad():
-        rec16, seqs, _, _ = oracle_run(large.sd, large.cfg, inp, sched, IDS, STEPS, vn, SEED)
     print(f"Large prompt: {int(inp['attention_mask'].sum())} tokens, "
           f"{int(inp['speech_masks'].sum())} voice frames from 4 speakers")
+    with torch.no_grad():
+        rec16, seqs, _, _ = oracle_run(large.sd, large.cfg, inp, sched, IDS, STEPS, vn, SEED)
+        sd32 = {k: v.float() for k, v in large.sd.items()}     # the bf16 reference's own deviation, for scale
+        rec32, _, _, _ = oracle_run(sd32, large.cfg, inp, sched, IDS, STEPS, vn, SEED, dtype=torch.float32,
+                                    teacher=rec16)
+        del sd32
     got, sess = teacher_forced(large.model, inp, sched, rec16, TK, SEED)
     assert torch.equal(sess.result().sequences, seqs)
-    per_step_check(got, rec16, None, "Large 4-speaker")
+    per_step_check(got, rec16, rec32, "Large 4-speaker")

@@ -17,7 +17,9 @@ from vibevoice_amd.weights import mfma_pack  # noqa: E402
 
 SHAPES = [("lm.gu", 2, 17920, 1536, "silu_mul"), ("head.gu", 2, 9216, 1536, "silu_mul"),
           ("lm.down", 2, 1536, 8960, "res"), ("lm.o", 2, 1536, 1536, "res"), ("lm.qkv", 2, 2048, 1536, "store"),
-          ("codec.fc1", 1, 8192, 2048, "gelu"), ("codec.fc2", 1, 2048, 8192, "res")]
+          ("codec.fc1", 1, 8192, 2048, "gelu"), ("codec.fc2", 1, 2048, 8192, "res"),
+          ("lm.gu+norm", 2, 17920, 1536, "silu_mul"), ("lm.gu.b8", 16, 17920, 1536, "silu_mul"),
+          ("lm.gu.b8+norm", 16, 17920, 1536, "silu_mul"), ("head.gu.b8+norm", 16, 9216, 1536, "silu_mul")]
 
 
 def P(t):
@@ -26,7 +28,11 @@ def P(t):
 
 def main():
     L = _lib.lib()
+    only = sys.argv[sys.argv.index("--only") + 1].split(",") if "--only" in sys.argv else None
     for name, M, N, K, epi in SHAPES:
+        if only and name not in only:
+            continue
+        norm = name.endswith("+norm")
         ncopy = max(2, (512 << 20) // (N * K * 2) + 1)
         Ws = [mfma_pack((torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()) for _ in range(ncopy)]
         A = torch.randn(M, K, device="cuda").bfloat16()
@@ -37,10 +43,17 @@ def main():
         G = N // 16
         st = torch.zeros(reps, G, 4, dtype=torch.int64, device="cuda")
 
+        nw_ = (1 + 0.1 * torch.randn(K, device="cuda")).bfloat16()
+
         def run(i):
             L.vv_gemv_stamps(ctypes.c_void_p(st[i].data_ptr()))
-            _lib.check(L.vv_gemm_bf16(M, N, K, P(A), K, P(Ws[i % ncopy]), None, _lib.EPI[epi], P(Y), outN, P(R),
-                                      None, None, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+            sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+            if norm:
+                _lib.check(L.vv_gemm_bf16_norm(M, N, K, P(A), K, P(nw_), 1e-6, P(Ws[i % ncopy]), _lib.EPI[epi],
+                                               P(Y), outN, None, sp))
+            else:
+                _lib.check(L.vv_gemm_bf16(M, N, K, P(A), K, P(Ws[i % ncopy]), None, _lib.EPI[epi], P(Y), outN,
+                                          P(R), None, None, sp))
             L.vv_gemv_stamps(None)
         run(0)
         g = torch.cuda.CUDAGraph()
@@ -51,7 +64,8 @@ def main():
         g.replay()
         torch.cuda.synchronize()
         s = st.cpu().double() * 10e-3                                 # us
-        s = s[reps // 4:]                                             # steady state
+        G = int((s[0, :, 0] > 0).sum())                               # launched workgroups (tiles per group, K splits)
+        s = s[reps // 4:, :G]                                         # steady state
         first = s[:, :, 0].min(1).values
         last_end = s[:, :, 3].max(1).values
         span = (last_end - first).mean().item()

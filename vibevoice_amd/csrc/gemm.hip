@@ -108,6 +108,16 @@ DEV bool splitk_handoff(const GemmArgs& a, float* red, int TILE, unsigned* last_
 // M <= 16: the workgroup's A rows (its K range, transformed) are staged once in
 // LDS; each wave streams its weight chunks with a two-deep register ping-pong
 // (U chunks = U KB per wave in flight while the previous U are multiplied).
+// VV_G1_PRE2: both halves of the ping-pong (2U chunks) are issued before the A
+// prologue, so twice the weight bytes are in flight while the A rows arrive and
+// are normalised.  VV_G1_QW: A items per thread of the single-round-trip
+// ("fast") prologue of the multi-tile (TPW > 1, M >= 8) form.
+#ifndef VV_G1_PRE2
+#define VV_G1_PRE2 0
+#endif
+#ifndef VV_G1_QW
+#define VV_G1_QW 4
+#endif
 template <int U, int XF, bool KEEP = false, int TPW = 1>
 __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -154,7 +164,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   bf16* xs = (bf16*)smem;
   float* part = (float*)(smem + (((size_t)a.M * lds_ld * 2 + 15) & ~(size_t)15));
   bf16x8 wa[U], wb[U];
-  constexpr int Q = 4;                   // A items per thread on the fast path
+  constexpr int Q = TPW > 1 ? VV_G1_QW : 4;   // A items per thread on the fast path
   const bool fast = a.M * n8 <= Q * (int)blockDim.x;
   if (XF == XF_ATTN_MERGE) {
     // o_proj's A rows = the decode attention output, merged from the key splits'
@@ -211,6 +221,10 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
+    if (VV_G1_PRE2) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) wb[u] = ldw<KEEP>(wrow + min(c0 + U + u, max(c1 - 1, 0)) * 512);
+    }
   } else if (XF == XF_MIX) {
     // Codec Block1D front half for the M = ns * T rows (k_mix's math and
     // summation order, elementwise.hip): every workgroup recomputes it (a few
@@ -254,6 +268,10 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
       if (first) {
 #pragma unroll
         for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
+        if (VV_G1_PRE2) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) wb[u] = ldw<KEEP>(wrow + min(c0 + U + u, max(c1 - 1, 0)) * 512);
+        }
       }
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -362,6 +380,10 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
+    if (VV_G1_PRE2) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) wb[u] = ldw<KEEP>(wrow + min(c0 + U + u, max(c1 - 1, 0)) * 512);
+    }
     if (XF == XF_NORM) {
       // per-item sums of squares -> LDS, rows reduced in a fixed order
 #pragma unroll
@@ -413,6 +435,10 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     // many rows (B >= 8 batches): weights first, then the A rows in batches
 #pragma unroll
     for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
+    if (VV_G1_PRE2) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) wb[u] = ldw<KEEP>(wrow + min(c0 + U + u, max(c1 - 1, 0)) * 512);
+    }
     for (int e0 = threadIdx.x; e0 < a.M * n8; e0 += 4 * blockDim.x) {
       bf16x8 xv[4];
 #pragma unroll
@@ -481,11 +507,20 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
 #pragma unroll
     for (int u = 0; u < U; ++u) wf[u] = ldw<KEEP>(wrow + min(c + u, max(c1 - 1, 0)) * 512);
   };
-  for (int c = c0; c < c1; c += 2 * U) {
-    load(wb, c + U);
-    compute(wa, c);
-    load(wa, c + 2 * U);
-    compute(wb, c + U);
+  if (VV_G1_PRE2) {   // wb(c0 + U) is already in flight: the same ping-pong, loads after the computes
+    for (int c = c0; c < c1; c += 2 * U) {
+      compute(wa, c);
+      load(wa, c + 2 * U);
+      compute(wb, c + U);
+      load(wb, c + 3 * U);
+    }
+  } else {
+    for (int c = c0; c < c1; c += 2 * U) {
+      load(wb, c + U);
+      compute(wa, c);
+      load(wa, c + 2 * U);
+      compute(wb, c + U);
+    }
   }
   stamp(a, 2);
 
@@ -1133,6 +1168,21 @@ constexpr unsigned WC_VM12 = 0x0F7C, WC_VM8_LGKM0 = 0x0078, WC_LGKM0 = 0xC07F, W
 #ifndef VV_GX_ABL
 #define VV_GX_ABL 0
 #endif
+// VV_GX_M32: the wave's 128 x 64 tile on v_mfma_f32_32x32x16_bf16 (8 accumulators
+// of 32 x 32, 16 MFMAs per 32-deep stage) instead of 16x16x32 (32 accumulators of
+// 16 x 16, 32 MFMAs).  Same LDS images: a 32 x 16 operand fragment of lane l
+// (row l & 31, k 8 (l >> 5) .. +7 of a 16-deep half) is 16 contiguous bytes of the
+// 16-row block that holds row l & 31, so every read stays one lane-linear
+// ds_read_b128 per 16 lanes.  Fragment bytes read per stage are the same (the
+// wave tile sets them); the MFMA count halves.  K order differs from k_gemm
+// (two K = 16 halves per chunk): equal to torch fp32 within rounding, not bitwise.
+#ifndef VV_GX_M32
+#define VV_GX_M32 0
+#endif
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+DEV f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
 constexpr int GX_M = 256, GX_N = 256, GX_NS = 4;
 constexpr int GX_STAGE = 32 * 512;                       // elements per stage
 constexpr size_t GX_LDS = (size_t)GX_NS * GX_STAGE * 2;   // 128 KB
@@ -1200,11 +1250,30 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
       __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + (a.apack ? (long long)s * 512 : (long long)s * 32)),
                                        (__attribute__((address_space(3))) void*)(st + j * 512), 16, 0, 0);
   };
+#if VV_GX_M32
+  f32x16 acc2[2][4];   // [32-row weight tile][32-row row tile]
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc2[nt][mt][i] = 0.f;
+  // fragment f of a stage: W (f < 4): weight tile f >> 1, k-half f & 1; A (f >= 4):
+  // row tile (f - 4) >> 1, k-half (f - 4) & 1.  Lane offset inside the 16-row block
+  // of row l & 31: ((2 kk + (l >> 5)) * 16 + (l & 15)) * 8 elements.
+  const int off32 = ((lane >> 5) * 16 + (lane & 15)) * 8 + ((lane >> 4) & 1) * 512;
+  auto frag32 = [&](const bf16* st, int f) -> bf16x8 {
+    const int blk = f < 4 ? 16 + wc * 4 + 2 * (f >> 1) : wr * 8 + 2 * ((f - 4) >> 1);
+    const int kk = f < 4 ? (f & 1) : ((f - 4) & 1);
+    return *(const bf16x8*)(st + blk * 512 + kk * 256 + off32);
+  };
+#else
   f32x4 acc[4][8];   // [weight tile nt][row tile mt]
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) acc[nt][mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#endif
   // fragments of stage s are read into registers during step s - 1 (two register
   // sets), so each wave's LDS reads of the next stage overlap its MFMAs
   auto frags = [&](int s, bf16x8 (&wf)[4], bf16x8 (&xf)[8]) {
@@ -1212,19 +1281,35 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
     return;   // ablation (timing only): no LDS fragment reads
 #endif
     const bf16* st = smx + (s & (GX_NS - 1)) * GX_STAGE;
+#if VV_GX_M32
+#pragma unroll
+    for (int f = 0; f < 4; ++f) wf[f] = frag32(st, f);
+#pragma unroll
+    for (int f = 0; f < 8; ++f) xf[f] = frag32(st, 4 + f);
+#else
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) wf[nt] = *(const bf16x8*)(st + (16 + wc * 4 + nt) * 512 + lane * 8);
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) xf[mt] = *(const bf16x8*)(st + (wr * 8 + mt) * 512 + lane * 8);
+#endif
   };
   auto macs = [&](const bf16x8 (&wf)[4], const bf16x8 (&xf)[8]) {
 #if !VV_GX_INTERLEAVE
     __builtin_amdgcn_s_setprio(1);
 #endif
+#if VV_GX_M32
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc2[nt][mt] = mfma32(wf[2 * nt + kk], xf[2 * mt + kk], acc2[nt][mt]);
+#else
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
       for (int mt = 0; mt < 8; ++mt) acc[nt][mt] = mfma(wf[nt], xf[mt], acc[nt][mt]);
+#endif
 #if VV_GX_INTERLEAVE
     // the step's 4 glds and 12 ds_reads (of the next stage) spread between its 32
     // MFMAs, so their issue cost hides under the matrix pipe: 4 groups of 1 glds,
@@ -1272,12 +1357,25 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
 #pragma unroll
       for (int f = 3 * q; f < 3 * q + 3; ++f) {
 #if VV_GX_ABL != 2
+#if VV_GX_M32
+        if (f < 4) wn[f] = frag32(st, f);
+        else xn[f - 4] = frag32(st, f);
+#else
         if (f < 4) wn[f] = *(const bf16x8*)(st + (16 + wc * 4 + f) * 512 + lane * 8);
         else xn[f - 4] = *(const bf16x8*)(st + (wr * 8 + f - 4) * 512 + lane * 8);
 #endif
+#endif
       }
+#if VV_GX_M32
+      {   // group q: k-half q >> 1, weight tile q & 1, the 4 row tiles
+        const int kk = q >> 1, nt = q & 1;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc2[nt][mt] = mfma32(wf[2 * nt + kk], xf[2 * mt + kk], acc2[nt][mt]);
+      }
+#else
 #pragma unroll
       for (int mt = 0; mt < 8; ++mt) acc[q][mt] = mfma(wf[q], xf[mt], acc[q][mt]);
+#endif
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -1316,6 +1414,28 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
   // accumulators through one register tile cost ~4,000 moves per wave -- 30 % of
   // a K = 1536 tile)
   __syncthreads();   // every wave is past its reads of the last stage
+  // pass p (row tiles 64 p .. 64 p + 63 of the wave's 128) -> this wave's LDS
+  // region as [64 rows][64 cols] f32, odd rows' float4 slots XOR-shifted by one
+  auto stage_ep = [&](float* ep, int p) {
+    auto sw = [](int row, int col) { return row * 64 + (col ^ ((row & 1) << 2)); };
+#if VV_GX_M32
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          const f32x16& c = acc2[nt][2 * p + mt];
+          *(f32x4*)(ep + sw(mt * 32 + (lane & 31), nt * 32 + 8 * q4 + 4 * (lane >> 5))) =
+              (f32x4){c[4 * q4], c[4 * q4 + 1], c[4 * q4 + 2], c[4 * q4 + 3]};
+        }
+#else
+#pragma unroll
+    for (int mq = 0; mq < 4; ++mq)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) *(f32x4*)(ep + sw(mq * 16 + r, nt * 16 + 4 * g)) = acc[nt][4 * p + mq];
+#endif
+  };
 #if VV_GX_ABL != 4
   if (rope_row8_ok(a)) {
     // q|k|v + RoPE + KV append in the same row-contiguous staging: a q / k lane
@@ -1327,10 +1447,7 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
     const bool vhead = (nb >> 7) >= a.rope.nh + a.rope.nkv;   // a wave's 64 columns lie in one head
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
-#pragma unroll
-      for (int mq = 0; mq < 4; ++mq)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) *(f32x4*)(ep + sw(mq * 16 + r, nt * 16 + 4 * g)) = acc[nt][4 * p + mq];
+      stage_ep(ep, p);
       if (!vhead) {
 #pragma unroll 1
         for (int it = 0; it < 4; ++it) {
@@ -1367,10 +1484,7 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
     const int mb = tm * GX_M + wr * 128, nb = tn * GX_N + wc * 64;
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
-#pragma unroll
-      for (int mq = 0; mq < 4; ++mq)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) *(f32x4*)(ep + sw(mq * 16 + r, nt * 16 + 4 * g)) = acc[nt][4 * p + mq];
+      stage_ep(ep, p);
       if (a.epi.kind == EPI_SILU_MUL) {
 #pragma unroll 1
         for (int it = 0; it < 4; ++it) {
@@ -1396,6 +1510,25 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
     return;
   }
 #endif
+#if VV_GX_M32
+  {   // any other epilogue: 16 x 16 tiles read back from the staged pass
+    float* ep = (float*)smx + wave * (64 * 64);
+    auto sw = [](int row, int col) { return row * 64 + (col ^ ((row & 1) << 2)); };
+    const int mb = tm * GX_M + wr * 128, nb = tn * GX_N + wc * 64;
+#pragma unroll 1
+    for (int p = 0; p < 2; ++p) {
+      stage_ep(ep, p);
+#pragma unroll 1
+      for (int t = 0; t < 16; ++t) {
+        const int mq = t & 3, nt = t >> 2;
+        float v[4];
+        *(f32x4*)v = *(const f32x4*)(ep + sw(mq * 16 + r, nt * 16 + 4 * g));
+        epi_tile(a, mb + 64 * p + mq * 16 + r, nb + nt * 16, lane, v);
+      }
+    }
+    return;
+  }
+#else
   float* ep = (float*)smx + wave * (16 * 256);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -1415,6 +1548,7 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
       epi_tile(a, tm * GX_M + (wr * 8 + (i & 7)) * 16 + r, tn * GX_N + (wc * 4 + (i >> 3)) * 16, lane, v);
     }
   }
+#endif
 }
 
 // diagnostic (vv_gemm_tune_big): 0 keeps every M > 64 GEMM on k_gemm; 1 / 2 LDS
