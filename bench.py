@@ -123,8 +123,14 @@ def bytes_per_token(wb, cfg, B, S, ctx_pos, ctx_neg):
 
 
 # ------------------------------------------------------------------ dominant kernel, live
-ROOF_KERNEL = "k_gemv1<4, 1, false>"   # U = 4 chunks in flight, XF_NORM, non-temporal weights; 2-wave groups (gemm.hip gemv_plan)
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+# U = 4 chunks in flight, XF_NORM, non-temporal weights, tiles per workgroup (gemm.hip gemv_plan: 1 at M < 8,
+# 8 at 8 <= M <= 16); HBM traffic per launch from tools/pmc_traffic.py (rocprofv3 PMC, committed per M)
+def roof_kernel(M):
+    return f"k_gemv1<4, 1, false, {8 if M >= 8 else 1}>"
+
+
+def pmc_file(M):
+    return os.path.join(ROOT, "profiles", f"r03_pmc_traffic_m{M}.json")
 
 
 def measure_gemv(model, B, iters=6):
@@ -173,12 +179,12 @@ def measure_gemv(model, B, iters=6):
     ach = alg / avg_s / 1e9
     shape = f"M={M} N={2 * I} K={H}"
     traffic = None
-    if os.path.exists(PMC_FILE):
-        with open(PMC_FILE) as f:
+    if os.path.exists(pmc_file(M)):
+        with open(pmc_file(M)) as f:
             pmc = json.load(f)
-        if pmc.get("kernel") == ROOF_KERNEL and pmc.get("shape") == shape:
+        if pmc.get("kernel") == roof_kernel(M) and pmc.get("shape") == shape:
             traffic = pmc["hbm_bytes_per_launch"]
-    kernel = (f"{ROOF_KERNEL} (LM post-norm + gate|up + SiLU*up, graph-replayed)" if M <= 16 else
+    kernel = (f"{roof_kernel(M)} (LM post-norm + gate|up + SiLU*up, graph-replayed)" if M <= 16 else
               "k_rmsnorm + k_gemv/k_gemvw (the engine's M > 16 dispatch: post-norm once, then gate|up + SiLU*up; "
               "graph-replayed, both launches timed)")
     return dict(kernel=kernel, shape=shape,

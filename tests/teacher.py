@@ -43,9 +43,10 @@ def oracle_run(sd, cfg, inp, sched, ids, steps, vn, seed, dtype=torch.bfloat16, 
     return rec, seqs, audio, reach
 
 
-def teacher_forced(model, inp, sched, rec, tok, seed):
+def teacher_forced(model, inp, sched, rec, tok, seed, max_new=None):
     """Drive the product loop with the oracle run's inputs.  Returns the
-    per-step outputs the product computed, and the session."""
+    per-step outputs the product computed, and the session.  max_new: the
+    oracle run's max_new_tokens when its length cap ended it."""
     B = inp["input_ids"].shape[0]
     got = dict(hpos=[], hneg=[], logits=[], latents=[], audio=[], next=[])
     pe = rec["prompt_embeds"].to(dev, torch.bfloat16)
@@ -55,7 +56,7 @@ def teacher_forced(model, inp, sched, rec, tok, seed):
         torch.manual_seed(seed)
         sess = model.generate_session(input_ids=inp["input_ids"], attention_mask=inp["attention_mask"], tokenizer=tok,
                                       cfg_scale=1.3, forced_tokens=sched, show_progress_bar=False,
-                                      max_new_tokens=max(len(s) for s in sched) + 2)
+                                      max_new_tokens=max_new or max(len(s) for s in sched) + 2)
     finally:
         model._prompt_embeds = orig
     post = sess._post_phase

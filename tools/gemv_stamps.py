@@ -27,12 +27,27 @@ def P(t):
 
 
 def main():
+    if "--lib" in sys.argv:   # another build of the library (tools/build_variant.sh)
+        _lib.LIB_PATH = os.path.abspath(sys.argv[sys.argv.index("--lib") + 1])
     L = _lib.lib()
     only = sys.argv[sys.argv.index("--only") + 1].split(",") if "--only" in sys.argv else None
-    for name, M, N, K, epi in SHAPES:
+    # --tune nw,u,tpw[;nw,u,tpw...]: GEMV plans to stamp (vv_gemv_tune / vv_gemv_tune_tpw), built-in first
+    tunes = [None] + ([tuple(int(x) for x in t.split(",")) for t in sys.argv[sys.argv.index("--tune") + 1].split(";")]
+                      if "--tune" in sys.argv else [])
+    if len(tunes) > 1:
+        tunes.append(None)    # the built-in plan again, last (the first configuration of a shape can read slow)
+    for (name, M, N, K, epi), tune in [(sh, t) for sh in SHAPES for t in tunes]:
         if only and name not in only:
             continue
+        if tune is None:
+            L.vv_gemv_tune(0, 0, -1, 0, 0)
+            L.vv_gemv_tune_tpw(0)
+        else:
+            L.vv_gemv_tune(tune[0], 1, 1, 0, tune[1])
+            L.vv_gemv_tune_tpw(tune[2])
         norm = name.endswith("+norm")
+        if tune is not None:
+            name = f"{name}[nw{tune[0]} u{tune[1]} tpw{tune[2]}]"
         ncopy = max(2, (512 << 20) // (N * K * 2) + 1)
         Ws = [mfma_pack((torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()) for _ in range(ncopy)]
         A = torch.randn(M, K, device="cuda").bfloat16()

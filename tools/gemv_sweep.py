@@ -32,6 +32,10 @@ SHAPES = [  # name, M, N, K, epi
     ("codec.t8.fc2", 8, 1024, 4096, "res"),
     ("head.down.b8", 16, 1536, 4608, "res"), ("codec.fc2.b8", 8, 2048, 8192, "res"), ("lm.o.b8", 16, 1536, 1536, "res"),
     ("head.down.b4", 8, 1536, 4608, "res"), ("lm.down.b4", 8, 1536, 8960, "res"),
+    # VibeVoice-Large (H 3584, I 18944, 28 q / 4 kv heads; head FFN 10752), B = 1
+    ("L.lm.qkv", 2, 4608, 3584, "store"), ("L.lm.o", 2, 3584, 3584, "res"), ("L.lm.gu", 2, 37888, 3584, "silu_mul"),
+    ("L.lm.down", 2, 3584, 18944, "res"), ("L.head.gu", 2, 21504, 3584, "silu_mul"),
+    ("L.head.down", 2, 3584, 10752, "res"), ("L.head.cond", 2, 3584, 3584, "store"),
 ]
 
 
@@ -120,6 +124,8 @@ def main():
         if "--ks" in sys.argv:    # cross-workgroup split-K x hand-off form x waves x chunks in flight
             configs += [(nw, ks, h, 0, u, 0) for nw, ks, h, u in itertools.product((4, 8), (1, 2, 3), (0, 1), (4, 8))
                         if ks > 1 or h == 1]
+        elif "--large" in sys.argv:   # waves x chunks in flight x split-K (sc1 hand-off)
+            configs += [(nw, ks, 1, 0, u, 0) for nw, ks, u in itertools.product((2, 4, 8), (1, 2, 4), (2, 4, 8))]
         elif "--tpw" in sys.argv:   # tiles per workgroup x waves x chunks in flight
             configs += [(nw, 1, 1, 0, u, t) for nw, u, t in itertools.product((2, 4, 8), (2, 4, 8), (1, 2, 4, 8))
                         if nw % t == 0]

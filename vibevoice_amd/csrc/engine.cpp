@@ -1204,9 +1204,11 @@ int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, 
   }
   // the per-step head weights (noisy, gate|up, down, final: 170 MB at 1.5B) are
   // re-read by every diffusion step: default cache policy keeps them in the
-  // Infinity Cache across the S steps
+  // Infinity Cache (256 MB) across the S steps.  VibeVoice-Large's (925 MB per
+  // step) cannot stay there: they stream non-temporal like the LM's
+  const bool head_keep = (size_t)L * 3 * F * H * sizeof(bf16) <= (192ull << 20);
   auto hgemm = [&](GemmArgs g) {
-    g.keep = 1;
+    g.keep = head_keep ? 1 : 0;
     return gemm(c, g, st);
   };
   // cond_proj is step-invariant: computed once per token (bit-identical to per step)

@@ -118,6 +118,11 @@ DEV bool splitk_handoff(const GemmArgs& a, float* red, int TILE, unsigned* last_
 #ifndef VV_G1_QW
 #define VV_G1_QW 4
 #endif
+// VV_G1_PSTAMP (diagnostic builds): the 4 per-workgroup stamps time the A
+// prologue instead (start, A rows in registers / LDS, row norms done, staged)
+#ifndef VV_G1_PSTAMP
+#define VV_G1_PSTAMP 0
+#endif
 template <int U, int XF, bool KEEP = false, int TPW = 1>
 __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -396,6 +401,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
           part[e] = ss;
         }
       }
+      if (VV_G1_PSTAMP) stamp(a, 1);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (a.ksplit == 1) {
         for (int m = wave; m < a.M; m += NW) {
@@ -408,6 +414,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
         row_inv(a, 0, a.M, inv_s, wave, NW, lane);
       }
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (VV_G1_PSTAMP) stamp(a, 2);
     }
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
@@ -459,6 +466,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
       }
     }
     if (XF != XF_NONE) {
+      if (VV_G1_PSTAMP) stamp(a, 1);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (XF == XF_NORM) {
         if (a.ksplit == 1) {
@@ -476,6 +484,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
           row_inv(a, 0, a.M, inv_s, wave, NW, lane);
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (VV_G1_PSTAMP) stamp(a, 2);
       }
       for (int e = threadIdx.x; e < a.M * n8; e += blockDim.x) {
         const int m = e / n8, k8 = (e - m * n8) * 8;
@@ -485,7 +494,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  stamp(a, 1);
+  stamp(a, VV_G1_PSTAMP ? 3 : 1);
 
   f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
   // A fragment reads are unconditional (a guarded LDS read compiled to an
@@ -522,7 +531,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
       compute(wb, c + U);
     }
   }
-  stamp(a, 2);
+  if (!VV_G1_PSTAMP) stamp(a, 2);
 
   // ---- reduce each tile's K-slice waves (tile t's sum lands in slab t * KW)
 #pragma unroll
@@ -543,7 +552,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = red[wave * KW * 256 + i * 64 + lane];
     epi_tile(a, r, (blockIdx.x * TPW + wave) * 16, lane, v, VV_EPI_PREFETCH ? &pre : nullptr);
-    if (a.stamps) {
+    if (a.stamps && !VV_G1_PSTAMP) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       stamp(a, 3);
     }
@@ -1043,6 +1052,14 @@ static GemmPlan gemv_plan(int N, int K, int M) {
     }
   } else if (tiles >= 1024) {
     nw = 2;
+    // VibeVoice-Large's long rows (K 3,584: the LM gate|up, 2,368 tiles; the head
+    // gate|up, 1,344): 4 waves x 2 chunks (tools/gemv_sweep.py --large: 46.1 ->
+    // 43.8 us), which also keeps the fused RMSNorm prologue on its one-round-trip
+    // form (2 rows x 448 items fit 256 threads x 4)
+    if (chunks >= 96) {
+      nw = 4;
+      u = 2;
+    }
   } else if (tiles <= 128) {
     // LM q|k|v (128 tiles x K 1,536) with codec fc2 above: 8 waves x 4 chunks
     // instead of 4 x 8, interleaved in-loop pairs -5 .. -26 us per B = 1 step
@@ -1666,6 +1683,20 @@ int launch_gemm(GemmArgs a, hipStream_t st) {
     if (p.nw > max_waves(mrep)) p.nw = max_waves(mrep);
     a.ksplit = p.ksplit;
     if (a.ksplit > 1 && (!a.ws || !a.counters || a.N / 16 > 65536)) a.ksplit = 1;
+    // Rows too long for one workgroup to stage in k_gemv1's LDS at one K split
+    // (VibeVoice-Large's LM down projection, M = 2 x K 18,944 = 76 KB): split K
+    // until the slice fits, 8 waves x 4 chunks (tools/gemv_sweep.py --large: 48.4 ->
+    // 27.1 us), instead of k_gemv re-loading A fragments from L2 per chunk.
+    if (mrep == 1 && a.M < 8 && a.xf.kind == XF_NONE && !g_tune_ks && a.ws && a.counters && a.N / 16 <= 65536 &&
+        !gemv1_fits(a)) {
+      GemmArgs t = a;
+      while (!gemv1_fits(t) && t.ksplit < 4) t.ksplit *= 2;
+      if (gemv1_fits(t)) {
+        a.ksplit = t.ksplit;
+        if (!g_tune_nw) p.nw = 8;
+        if (!g_tune_u) p.u = 4;
+      }
+    }
     a.handoff = g_tune_handoff >= 0 ? g_tune_handoff : 1;
     a.tpw = 1;
     if (mrep == 1 && a.ksplit == 1 && a.xf.kind != XF_MIX && (p.tpw == 2 || p.tpw == 4 || p.tpw == 8) && p.nw % p.tpw == 0 && gemv1_fits(a))
