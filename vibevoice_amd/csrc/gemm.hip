@@ -1051,15 +1051,9 @@ static GemmPlan gemv_plan(int N, int K, int M) {
       u = 4;
     }
   } else if (tiles >= 1024) {
+    // (VibeVoice-Large's K 3,584 rows too: 4 waves x 2 chunks won the bare-GEMV
+    // sweep, 46.1 -> 43.8 us, but lost in the loop, 7.07 -> 7.15 ms per step)
     nw = 2;
-    // VibeVoice-Large's long rows (K 3,584: the LM gate|up, 2,368 tiles; the head
-    // gate|up, 1,344): 4 waves x 2 chunks (tools/gemv_sweep.py --large: 46.1 ->
-    // 43.8 us), which also keeps the fused RMSNorm prologue on its one-round-trip
-    // form (2 rows x 448 items fit 256 threads x 4)
-    if (chunks >= 96) {
-      nw = 4;
-      u = 2;
-    }
   } else if (tiles <= 128) {
     // LM q|k|v (128 tiles x K 1,536) with codec fc2 above: 8 waves x 4 chunks
     // instead of 4 x 8, interleaved in-loop pairs -5 .. -26 us per B = 1 step
