@@ -91,3 +91,38 @@ def test_teacher_forced_large_4_speakers(large):
     got, sess = teacher_forced(large.model, inp, sched, rec16, TK, SEED)
     assert torch.equal(sess.result().sequences, seqs)
     per_step_check(got, rec16, rec32, "Large 4-speaker")
+
+
+def test_large_tp4_group_28_layers(large):
+    """configs[3]'s parallelism at full depth: the 28-layer Large backbone split
+    over 4 ranks (Megatron split of configuration_vibevoice.py:175-183, whole KV
+    heads per rank: 4 kv heads -> 1 per rank), driven as one group on this GPU
+    (vv_lm_forward_group: an on-device sum stands in for the RCCL all-reduce)
+    vs the TP = 1 engine: a 300-token prefill and 3 decode steps."""
+    from vibevoice_amd.engine import Engine
+    VALID = sorted(IDS.values())
+    full = large.model.engine
+    full.set_valid_ids(VALID)
+    group = [Engine(large.cfg, large.sd, dev, max_batch=1, max_ctx=512, valid_ids=VALID, tp_rank=r, tp_size=4)
+             for r in range(4)]
+    i32 = dict(dtype=torch.int32, device=dev)
+    g = torch.Generator(device=dev).manual_seed(12)
+    N = 300
+    x = torch.randn(N, 3584, device=dev, generator=g).bfloat16()
+    args = (x, torch.zeros(N, **i32), torch.arange(N).to(**i32), torch.tensor([N - 1]).to(**i32))
+    h1, l1 = full.lm_forward(*args)
+    hg, lg = group[0].lm_forward_group(group[1:], *args)
+    torch.cuda.synchronize()
+    print(f"Large 28-layer TP=4 prefill: rel {rel_err(hg, h1):.3e} cos {cos(hg, h1):.6f}")
+    assert rel_err(hg, h1) < 3e-2 and cos(hg, h1) > 0.999
+    for s in range(3):
+        step = torch.randn(1, 3584, device=dev, generator=g).bfloat16()
+        a = (step, torch.zeros(1, **i32), torch.tensor([N + s]).to(**i32), torch.zeros(1, **i32))
+        h1, l1 = full.lm_forward(*a)
+        hg, lg = group[0].lm_forward_group(group[1:], *a)
+        torch.cuda.synchronize()
+        print(f"Large 28-layer TP=4 step {s}: rel {rel_err(hg, h1):.3e} cos {cos(hg, h1):.6f}")
+        assert rel_err(hg, h1) < 3e-2 and cos(hg, h1) > 0.999
+        assert torch.allclose(lg, l1, rtol=5e-2, atol=5e-2 * l1.abs().max().item())
+    for e in group:
+        e.close()

@@ -17,7 +17,16 @@ from vibevoice_amd.weights import synthetic_state_dict  # noqa: E402
 
 
 def main():
-    ns = [int(a) for a in sys.argv[1:]] or [1, 4, 8]
+    # --lib <so>: another build (tools/build_variant.sh); --timeline: the per-op stamps
+    # of one launch (needs the default one-workgroup-per-CU grid: the stamp buffer is sized by CUs)
+    args = sys.argv[1:]
+    if "--lib" in args:
+        i = args.index("--lib")
+        _lib.LIB_PATH = os.path.abspath(args[i + 1])
+        del args[i:i + 2]
+    timeline = "--timeline" in args
+    args = [a for a in args if a != "--timeline"]
+    ns = [int(a) for a in args] or [1, 4, 8]
     g = torch.Generator().manual_seed(21)
     sd_head, hc, H = real_head_sd(g)
     cfg = tiny_config(hidden=H, layers=1, heads=12, kv_heads=2, inter=256)
@@ -53,6 +62,8 @@ def main():
                 best = min(best, e0.elapsed_time(e1) / 20 * 1e3)
             err = L.vv_chain_error(eng.h)
             print(f"n={n} mode={mode} u={u}: {best:8.1f} us per diffusion_sample (S=10)  err={err}", flush=True)
+    if not timeline:
+        return
     # per-op timeline of one chain launch (n = first n): last signal of op j-1 ->
     # first workgroup past its wait for op j (hand-off latency), and op spans
     n = ns[0]

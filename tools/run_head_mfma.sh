@@ -8,7 +8,10 @@ R=${GRAFT_REPO_ROOT:-/root/repo}
 OUT=$R/gpurun_out/head_mfma
 mkdir -p $OUT
 CTR="SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_BF16 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
-for cfg in "--n 1" "--n 8" "--n 32" "--m 128" "--m 256" "--m 512" "--m 1024" "--m 2048" "--m 4096"; do
+# configurations: the script's arguments (e.g. "--m 8192" "--m 16384"), else the round-2 set
+if [ $# -gt 0 ]; then CFGS=("$@"); else
+  CFGS=("--n 1" "--n 8" "--n 32" "--m 128" "--m 256" "--m 512" "--m 1024" "--m 2048" "--m 4096"); fi
+for cfg in "${CFGS[@]}"; do
   tag=$(echo $cfg | tr -d ' -')
   timeout -s KILL 120 rocprofv3 --pmc $CTR -d $OUT/$tag -o run --output-format csv -- python3 $R/tools/head_mfma.py $cfg > $OUT/$tag.log 2>&1
   rc=$?

@@ -37,7 +37,16 @@
 
 #include "gemv_dev.h"
 
-constexpr int CH_NW = 8;          // waves per workgroup
+// waves per workgroup and workgroups per CU (co-resident: VGPRs allow 8 waves
+// per CU, LDS 2 x 80 KB).  VV_CH_NW=4 VV_CH_WGPC=2: two units in flight per CU
+// (diagnostic builds; the default is one 8-wave workgroup per CU)
+#ifndef VV_CH_NW
+#define VV_CH_NW 8
+#endif
+#ifndef VV_CH_WGPC
+#define VV_CH_WGPC 1
+#endif
+constexpr int CH_NW = VV_CH_NW;
 
 // global (address_space 1) loads: a flat load also counts in lgkmcnt, so every
 // LDS wait would wait for the weight stream in flight
@@ -284,7 +293,7 @@ DEV void chain_stamp(const ChainArgs& A, int j, int which) {
 }
 
 template <int U>
-__global__ void __launch_bounds__(512) k_chain(ChainArgs A) {
+__global__ void __launch_bounds__(64 * CH_NW) k_chain(ChainArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ float inv_s[16];
   __shared__ float red[CH_NW * 256];
@@ -445,6 +454,7 @@ size_t chain_plan_op(ChainOp* op, int G, int mode) {
   if (mode == 1) {
     int nw, ks, tp;
     if (gemv_plan_query(a, &nw, &ks, &tp, &fast)) return 0;
+    if (nw > CH_NW) return 0;   // the per-op plan's workgroup is wider than the chain's
     if (ks > 1) {
       t1 = 0;
       tpw = 1;
@@ -488,7 +498,7 @@ size_t chain_plan_op(ChainOp* op, int G, int mode) {
       }
       t1 = ks2 > 1 ? 0 : T;
     }
-    fast = 512;
+    fast = 64 * CH_NW;
     if (ks2 > 1 && T - t1 > CH_TMAX) return 0;
   }
   op->xf = a.xf.kind;
@@ -518,7 +528,7 @@ int chain_grid() {
     int dev = 0;
     hipDeviceProp_t p;
     if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return 0;
-    g = p.multiProcessorCount;
+    g = p.multiProcessorCount * VV_CH_WGPC;
   }
   return g;
 }
@@ -543,7 +553,7 @@ int launch_chain(const ChainArgs& A, size_t lds, hipStream_t st) {
   }
   const int G = chain_grid();
   if (G <= 0) return 2;
-  if (g_chain_u == 4) hipLaunchKernelGGL(k_chain<4>, dim3(G), dim3(512), lds, st, A);
-  else hipLaunchKernelGGL(k_chain<8>, dim3(G), dim3(512), lds, st, A);
+  if (g_chain_u == 4) hipLaunchKernelGGL(k_chain<4>, dim3(G), dim3(64 * CH_NW), lds, st, A);
+  else hipLaunchKernelGGL(k_chain<8>, dim3(G), dim3(64 * CH_NW), lds, st, A);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
