@@ -700,8 +700,15 @@ __global__ void __launch_bounds__(64 * G * 2 / QW) __attribute__((amdgpu_waves_p
       const bf16* st = sm + (step % PF_NS) * PF_STAGE + sub * 16 * 512;
       // all 8 K fragments, then the 16 S MFMAs (one LDS round trip, not one per key tile)
       bf16x8 kf[8];
+#if VV_PF_ABL == 3
+      // ablation (timing only): every step reuses one 16-byte LDS read per fragment
+      // slot (the first K row's), so the step's LDS read traffic drops 8-fold
+#pragma unroll
+      for (int f = 0; f < 8; ++f) kf[f] = *(const bf16x8*)(st + lane * 8);
+#else
 #pragma unroll
       for (int f = 0; f < 8; ++f) kf[f] = *(const bf16x8*)(st + f * 512 + lane * 8);
+#endif
       f32x4 s[2][QW];
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
@@ -714,8 +721,13 @@ __global__ void __launch_bounds__(64 * G * 2 / QW) __attribute__((amdgpu_waves_p
       // the V^T fragments do not depend on P: issued now, they land under the softmax
       // (read one at a time after it, each read's latency was exposed 8 times a step)
       bf16x8 vf[8];
+#if VV_PF_ABL == 3
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) vf[dt] = kf[dt];
+#else
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt) vf[dt] = *(const bf16x8*)(st + (8 + dt) * 512 + lane * 8);
+#endif
       __builtin_amdgcn_sched_barrier(0);
       // online softmax with a lazy running max: a column's m (log2 units) moves
       // only when a score exceeds it by > PF_LAZY, so P <= 2^PF_LAZY and the
