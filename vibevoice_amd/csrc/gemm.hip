@@ -1040,6 +1040,14 @@ static GemmPlan gemv_plan(int N, int K, int M) {
     }
   } else if (M > 16) {
     nw = tiles >= 1024 ? 1 : 4;   // k_gemv (A from L2 per chunk): batched head adaLN 35 -> 20.5 us
+  } else if (M >= 8 && tiles <= 8 && chunks >= 32) {
+    // the head's final layer (N 64, K 1,536: 4 tiles) at B = 8: 8-way split-K so 32
+    // workgroups share the 16-row RMSNorm prologue and the stream (interleaved
+    // in-loop pairs: B = 8 step -20..-40 us; at M = 2 the hand-off costs more
+    // than it saves, +20..+50 us)
+    nw = 8;
+    u = 2;
+    ks = 8;
   } else if (M >= 8) {
     nw = 8;
     u = 2;
