@@ -194,15 +194,18 @@ def measure_gemv(model, B, iters=6):
 
 
 # ------------------------------------------------------------------ TP collective share
-def measure_tp_collective(make_pass, n_layers, world, dev, iters=20):
+def measure_tp_collective(make_pass, n_layers, world, dev, iters=20, reps=3):
     """Time of one LM pass with its 2 x n_layers RCCL all-reduces and with
     them skipped (vv_tp_null_collective: the outputs are then wrong, so this
     runs after the timed loop), max over ranks; their difference is the
     collectives' share of the pass.  make_pass(null) returns a callable that
     runs one pass (a hipGraph replay of the loop's LM phase, captured with the
-    switch set as given)."""
-    def timed(null):
-        run = make_pass(null)
+    switch set as given).  Each figure is the best of `reps` interleaved
+    blocks of `iters` passes (a block's time is the slowest rank's), so a
+    noisy block on a shared host does not invert the two."""
+    runs = {null: make_pass(null) for null in (False, True)}
+
+    def timed(run):
         run()
         barrier(world)
         t0 = time.perf_counter()
@@ -210,7 +213,11 @@ def measure_tp_collective(make_pass, n_layers, world, dev, iters=20):
             run()
         barrier(world)
         return max_over_ranks(time.perf_counter() - t0, world, dev) / iters
-    on, off = timed(False), timed(True)
+    best = {False: float("inf"), True: float("inf")}
+    for _ in range(reps):
+        for null in (False, True):
+            best[null] = min(best[null], timed(runs[null]))
+    on, off = best[False], best[True]
     return dict(lm_pass_us=round(on * 1e6, 2), lm_pass_us_null_collective=round(off * 1e6, 2),
                 allreduce_us_per_pass=round(max(0.0, on - off) * 1e6, 2), allreduce_calls_per_pass=2 * n_layers,
                 allreduce_share=round(max(0.0, on - off) / on, 4) if on > 0 else None,
