@@ -206,6 +206,10 @@ int vv_gemv_tune_wide(int on);
  * GEMV may stage its A slice in before it falls back to per-wave A fragment
  * loads, up to 148 KiB (per-kernel opt-in above 64 KB); 0 = built-in (64 KB). */
 int vv_gemv_tune_lds(int bytes);
+/* Tuning hook (benchmarks only): fused-RMSNorm GEMVs with at least min_m rows
+ * (and an eligible shape) stage whole A rows per wave (k_gemv1's RW form: the
+ * norm applied in registers, one barrier); 0 restores the built-in 1. */
+int vv_gemv_tune_rw(int min_m);
 /* Tuning hook (benchmarks / tests): XF-free GEMMs with >= 256 rows,
  * N % 128 == 0, K % 64 == 0 and >= 256 such tiles (or >= 2^30 MACs) take the
  * LDS-staged 128 x 128 tile (k_gemm_big, the prefill projections) with 2 LDS

@@ -66,6 +66,7 @@ EXPORTS = [
     ("vv_gemv_tune_maxm", I, [I]),
     ("vv_gemv_tune_wide", I, [I]),
     ("vv_gemv_tune_lds", I, [I]),
+    ("vv_gemv_tune_rw", I, [I]),
     ("vv_gemm_tune_big", I, [I]),
     ("vv_gemv_stamps", I, [P]),
     ("vv_attn_stamps", I, [P]),

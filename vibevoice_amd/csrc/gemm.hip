@@ -35,6 +35,7 @@
 //            tile, 4 waves of 32 x BN/2, operands straight from L2.
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 #include "kernels.h"
 #include "gemv_dev.h"
@@ -123,7 +124,17 @@ DEV bool splitk_handoff(const GemmArgs& a, float* red, int TILE, unsigned* last_
 #ifndef VV_G1_PSTAMP
 #define VV_G1_PSTAMP 0
 #endif
-template <int U, int XF, bool KEEP = false, int TPW = 1>
+// VV_G1_RW: the fused RMSNorm prologue with whole rows per wave.  Wave w loads
+// rows w*RPW .. w*RPW+RPW-1 (lane l: 8-column items l, l+64, ...), so a row's
+// sum of squares is one in-register accumulation + wave_sum and the norm is
+// applied before the A rows ever reach LDS: one barrier instead of three and no
+// LDS round trip of partial sums.  Each row's summation order is the one the
+// item-per-thread form used (per-item partials when that form was "fast", one
+// running sum otherwise = k_rmsnorm's), so both forms are bit-identical.
+#ifndef VV_G1_RW
+#define VV_G1_RW 1
+#endif
+template <int U, int XF, bool KEEP = false, int TPW = 1, bool RW = false>
 __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ float inv_s[16];
@@ -171,7 +182,85 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   bf16x8 wa[U], wb[U];
   constexpr int Q = TPW > 1 ? VV_G1_QW : 4;   // A items per thread on the fast path
   const bool fast = a.M * n8 <= Q * (int)blockDim.x;
-  if (XF == XF_ATTN_MERGE) {
+  // row-per-wave norm prologue: items per lane per row (IPR) x rows per wave (RPW)
+  // (RW instantiations only; the host picks them for eligible shapes, gemv1_rw)
+  const int ipr = n8 >> 6, rpw = (a.M + NW - 1) / NW;
+  const int rw = ipr == 3 && rpw == 1 ? 31 : ipr == 3 ? 32 : 71;
+  // whole rows per wave: loads (A, norm weight, adaLN shift / scale; all
+  // unconditional, clamped to valid rows, so no branch join waits on them),
+  // then the weight stream, then sums, wave_sum and the norm in registers
+  auto stage_rw = [&](auto ipr_c, auto rpw_c, auto mod_c) {
+    constexpr int IPR = decltype(ipr_c)::value, RPW = decltype(rpw_c)::value, QR = IPR * RPW;
+    constexpr bool MOD = decltype(mod_c)::value;   // adaLN operands possible (their registers reserved)
+    bf16x8 xv[QR], wv[QR], sh[MOD ? QR : 1], sc[MOD ? QR : 1];
+    const bool has_w = a.xf.w != nullptr, has_mod = MOD && a.xf.mod != nullptr;
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const int m = min(wave * RPW + r, a.M - 1);
+      const bf16* xr = rm_bf(a.a, m);
+      const bf16* wp = has_w ? a.xf.w : xr;
+      const bf16* md = has_mod ? a.xf.mod + (long long)m * a.xf.mod_ld : xr;
+      const int so = has_mod ? a.xf.shift_off : 0, co = has_mod ? a.xf.scale_off : 0;
+#pragma unroll
+      for (int i = 0; i < IPR; ++i) {
+        const int k = (lane + 64 * i) * 8;
+        xv[r * IPR + i] = *(const bf16x8*)(xr + k);
+        wv[r * IPR + i] = *(const bf16x8*)(wp + k);
+        if (has_mod) {
+          sh[MOD ? r * IPR + i : 0] = *(const bf16x8*)(md + so + k);
+          sc[MOD ? r * IPR + i : 0] = *(const bf16x8*)(md + co + k);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
+    if (VV_G1_PRE2) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) wb[u] = ldw<KEEP>(wrow + min(c0 + U + u, max(c1 - 1, 0)) * 512);
+    }
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      float ss = 0.f;
+#pragma unroll
+      for (int i = 0; i < IPR; ++i) {
+        if (fast) {   // the item-per-thread fast form: per-item partials, then items in order
+          float p = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) p += bf(xv[r * IPR + i][j]) * bf(xv[r * IPR + i][j]);
+          ss += p;
+        } else {      // the staged form / k_rmsnorm: one running sum
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss += bf(xv[r * IPR + i][j]) * bf(xv[r * IPR + i][j]);
+        }
+      }
+      ss = wave_sum(ss);
+      const float inv = rsqrtf(ss / (float)a.K + a.xf.eps);
+      const int m = wave * RPW + r;
+      if (m < a.M) {
+#pragma unroll
+        for (int i = 0; i < IPR; ++i) {
+          const int q = r * IPR + i;
+          bf16x8 o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float t = rb(bf(xv[q][j]) * inv);
+            if (has_w) t = rb(t * bf(wv[q][j]));
+            if (has_mod) t = rb(rb(t * rb(1.0f + bf(sc[MOD ? q : 0][j]))) + bf(sh[MOD ? q : 0][j]));
+            o[j] = tobf(t);
+          }
+          *(bf16x8*)(xs + m * lds_ld + (lane + 64 * i) * 8) = o;
+        }
+      }
+    }
+  };
+  if constexpr (RW) {
+    if (VV_G1_PSTAMP) stamp(a, 1);
+    using I = std::true_type;
+    if (rw == 31) stage_rw(std::integral_constant<int, 3>(), std::integral_constant<int, 1>(), I());
+    else if (rw == 32) stage_rw(std::integral_constant<int, 3>(), std::integral_constant<int, 2>(), I());
+    else stage_rw(std::integral_constant<int, 7>(), std::integral_constant<int, 1>(), std::false_type());
+    if (VV_G1_PSTAMP) stamp(a, 2);
+  } else if (XF == XF_ATTN_MERGE) {
     // o_proj's A rows = the decode attention output, merged from the key splits'
     // partials k_attn left (AttnArgs::defer): out = sum_s e^{m_s - M} o_s /
     // sum_s e^{m_s - M} l_s in split order -- the attention kernel's own merge
@@ -1109,30 +1198,56 @@ static size_t gemv1_lds(const GemmArgs& a) {
 }
 static bool gemv1_fits(const GemmArgs& a) { return gemv1_lds(a) <= g_gemv1_lds_max; }
 
-template <int U, int XF, bool KEEP, int TPW>
+template <int U, int XF, bool KEEP, int TPW, bool RW>
 static void go_gemv1(const GemmArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t st) {
   if (lds > 65536) {   // > 64 KB of dynamic LDS needs the opt-in, once per instantiation
-    static const bool attr = hipFuncSetAttribute((const void*)k_gemv1<U, XF, KEEP, TPW>,
+    static const bool attr = hipFuncSetAttribute((const void*)k_gemv1<U, XF, KEEP, TPW, RW>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
                                                  (int)GEMV1_LDS_MAX) == hipSuccess;
     (void)attr;   // a refused opt-in surfaces as the launch error
   }
-  hipLaunchKernelGGL((k_gemv1<U, XF, KEEP, TPW>), grid, block, lds, st, a);
+  hipLaunchKernelGGL((k_gemv1<U, XF, KEEP, TPW, RW>), grid, block, lds, st, a);
+}
+
+// Row-per-wave norm prologue (k_gemv1's RW form) for this launch?  Whole rows
+// of K = 1,536 (3 items per lane) at up to 2 rows per wave, or K = 3,584 (7
+// items) at one row per wave without adaLN operands (their registers would cost
+// occupancy).  A separate instantiation: compiled into the item-per-thread
+// kernels it cost them registers / SGPR spills (B = 1 step 3.57 -> 3.66 ms).
+// Interleaved same-box runs (profiles/r03_gemv_rw_ab.txt): B = 8 step 5.45-5.47
+// -> 5.14-5.16 ms (M = 16 LM gate|up 19.98 -> 17.11 us, q|k|v 11.20 -> 8.63,
+// head gate|up 15.62 -> 12.45 in tools/gemv_variants.py), VibeVoice-Large B = 1
+// 7.14 -> 6.85 ms (K = 3,584 rows), 1.5B B = 1 3.597 -> 3.588 ms.
+// Diagnostic: vv_gemv_tune_rw(min rows; 99 = off).
+static int g_rw_min_m = 1;
+extern "C" int vv_gemv_tune_rw(int min_m) {
+  g_rw_min_m = min_m > 0 ? min_m : 1;
+  return 0;
+}
+static bool gemv1_rw(const GemmArgs& a, int nw) {
+  if (!VV_G1_RW || a.xf.kind != XF_NORM || a.ksplit != 1 || a.M < g_rw_min_m || a.K % 512) return false;
+  const int ipr = a.K / 512, rpw = (a.M + nw - 1) / nw;
+  return (ipr == 3 && rpw <= 2) || (ipr == 7 && rpw == 1 && !a.xf.mod);
 }
 
 // TPW is a template argument so the one-tile form (every M < 8 launch) keeps
 // its straight-line index math (a runtime tiles-per-group cost 1 us per launch)
+template <int XF, int TPW, bool RW>
+static void launch_gemv1_rw(const GemmArgs& a, int u, dim3 grid, dim3 block, size_t lds, hipStream_t st) {
+  if (a.keep) {
+    if (u == 4) go_gemv1<4, XF, true, TPW, RW>(a, grid, block, lds, st);
+    else if (u == 2) go_gemv1<2, XF, true, TPW, RW>(a, grid, block, lds, st);
+    else go_gemv1<8, XF, true, TPW, RW>(a, grid, block, lds, st);
+  } else {
+    if (u == 4) go_gemv1<4, XF, false, TPW, RW>(a, grid, block, lds, st);
+    else if (u == 2) go_gemv1<2, XF, false, TPW, RW>(a, grid, block, lds, st);
+    else go_gemv1<8, XF, false, TPW, RW>(a, grid, block, lds, st);
+  }
+}
 template <int XF, int TPW>
 static void launch_gemv1(const GemmArgs& a, int u, dim3 grid, dim3 block, size_t lds, hipStream_t st) {
-  if (a.keep) {
-    if (u == 4) go_gemv1<4, XF, true, TPW>(a, grid, block, lds, st);
-    else if (u == 2) go_gemv1<2, XF, true, TPW>(a, grid, block, lds, st);
-    else go_gemv1<8, XF, true, TPW>(a, grid, block, lds, st);
-  } else {
-    if (u == 4) go_gemv1<4, XF, false, TPW>(a, grid, block, lds, st);
-    else if (u == 2) go_gemv1<2, XF, false, TPW>(a, grid, block, lds, st);
-    else go_gemv1<8, XF, false, TPW>(a, grid, block, lds, st);
-  }
+  if (XF == XF_NORM && gemv1_rw(a, block.x / 64)) launch_gemv1_rw<XF_NORM, TPW, true>(a, u, grid, block, lds, st);
+  else launch_gemv1_rw<XF, TPW, false>(a, u, grid, block, lds, st);
 }
 
 template <int XF>
