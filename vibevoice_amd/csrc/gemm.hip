@@ -134,7 +134,7 @@ DEV bool splitk_handoff(const GemmArgs& a, float* red, int TILE, unsigned* last_
 #ifndef VV_G1_RW
 #define VV_G1_RW 1
 #endif
-template <int U, int XF, bool KEEP = false, int TPW = 1, bool RW = false>
+template <int U, int XF, bool KEEP = false, int TPW = 1, int RW = 0>
 __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ float inv_s[16];
@@ -253,7 +253,78 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
       }
     }
   };
-  if constexpr (RW) {
+  // K = 3,584 rows with adaLN operands (VibeVoice-Large head): the raw A row
+  // goes straight to its LDS row by 16-byte LDS DMA (lane l's item i lands at
+  // (l + 64 i) * 8, the row layout), so only the norm weight and shift / scale
+  // take registers; the row is read back by its own lanes after a counted vmcnt
+  // (the 21 operand loads and the U weight loads issued after it stay in flight)
+  auto stage_rw_dma = [&]() {
+    constexpr int IPR = 7;
+    bf16x8 wv[IPR], sh[IPR], sc[IPR];
+    const bool has_w = a.xf.w != nullptr;
+    const int m = min(wave, a.M - 1);
+    bf16* xrow_l = xs + m * lds_ld;
+    if (wave < a.M) {
+      const bf16* xr = rm_bf(a.a, m);
+      const bf16* wp = has_w ? a.xf.w : xr;
+      const bf16* md = a.xf.mod + (long long)m * a.xf.mod_ld;
+#pragma unroll
+      for (int i = 0; i < IPR; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(xr + (lane + 64 * i) * 8),
+                                         (__attribute__((address_space(3))) void*)(xrow_l + 64 * i * 8), 16, 0, 0);
+#pragma unroll
+      for (int i = 0; i < IPR; ++i) {
+        const int k = (lane + 64 * i) * 8;
+        wv[i] = *(const bf16x8*)(wp + k);
+        sh[i] = *(const bf16x8*)(md + a.xf.shift_off + k);
+        sc[i] = *(const bf16x8*)(md + a.xf.scale_off + k);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
+    if (VV_G1_PRE2) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) wb[u] = ldw<KEEP>(wrow + min(c0 + U + u, max(c1 - 1, 0)) * 512);
+    }
+    if (wave < a.M) {
+      // the DMA is older than 3 * IPR operand loads and the weight loads
+      constexpr int after = 3 * IPR + U * (VV_G1_PRE2 ? 2 : 1);
+      __builtin_amdgcn_s_waitcnt((after & 15) | ((after >> 4) << 14) | (7 << 4) | (15 << 8));
+      bf16x8 xv[IPR];
+#pragma unroll
+      for (int i = 0; i < IPR; ++i) xv[i] = *(const bf16x8*)(xrow_l + (lane + 64 * i) * 8);
+      float ss = 0.f;
+#pragma unroll
+      for (int i = 0; i < IPR; ++i) {
+        if (fast) {
+          float p = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) p += bf(xv[i][j]) * bf(xv[i][j]);
+          ss += p;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss += bf(xv[i][j]) * bf(xv[i][j]);
+        }
+      }
+      ss = wave_sum(ss);
+      const float inv = rsqrtf(ss / (float)a.K + a.xf.eps);
+#pragma unroll
+      for (int i = 0; i < IPR; ++i) {
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float t = rb(bf(xv[i][j]) * inv);
+          if (has_w) t = rb(t * bf(wv[i][j]));
+          t = rb(rb(t * rb(1.0f + bf(sc[i][j]))) + bf(sh[i][j]));
+          o[j] = tobf(t);
+        }
+        *(bf16x8*)(xrow_l + (lane + 64 * i) * 8) = o;
+      }
+    }
+  };
+  if constexpr (RW == 2) {   // its own instantiation: its registers would cost the others occupancy
+    stage_rw_dma();
+  } else if constexpr (RW == 1) {
     if (VV_G1_PSTAMP) stamp(a, 1);
     using I = std::true_type;
     if (rw == 31) stage_rw(std::integral_constant<int, 3>(), std::integral_constant<int, 1>(), I());
@@ -1116,7 +1187,15 @@ static GemmPlan gemv_plan(int N, int K, int M) {
     if (M >= 8) {   // batched rows: 2-way split-K (sc1 hand-off) reaches 2x the CUs
       ks = 2;
       if (chunks == 256 && tiles == 128) nw = 8;   // codec fc2, C = 2,048: 8 x 4 (B = 8 in-loop A/B: -53 us per step)
-      else if (chunks >= 256) u = 8;
+      else if (chunks >= 256 && M <= 16) {
+        // long rows: split K until the workgroup's A slice fits k_gemv1's 64 KB of
+        // LDS (staged once) instead of k_gemv's per-wave A fragment reads from L2
+        // (LM down at B = 8, M 16 x K 8,960: 5 ways; B = 8 step 5.15 -> 5.05 ms in
+        // interleaved in-loop runs, profiles/r03_gemv_rw_ab.txt; the same rule for
+        // the codec fc2 above cost +20 us); 8 waves x 4 chunks
+        while (ks < 8 && (size_t)M * ((chunks + ks - 1) / ks * 32 + 8) * 2 > 65536) ++ks;
+        nw = 8;
+      } else if (chunks >= 256) u = 8;
       else nw = 8;
     } else if (tiles < 128 && chunks >= 256) {   // M < 8 LM down: 2-way split-K, 8 waves x 4
       ks = 2;
@@ -1198,7 +1277,7 @@ static size_t gemv1_lds(const GemmArgs& a) {
 }
 static bool gemv1_fits(const GemmArgs& a) { return gemv1_lds(a) <= g_gemv1_lds_max; }
 
-template <int U, int XF, bool KEEP, int TPW, bool RW>
+template <int U, int XF, bool KEEP, int TPW, int RW>
 static void go_gemv1(const GemmArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t st) {
   if (lds > 65536) {   // > 64 KB of dynamic LDS needs the opt-in, once per instantiation
     static const bool attr = hipFuncSetAttribute((const void*)k_gemv1<U, XF, KEEP, TPW, RW>,
@@ -1219,20 +1298,26 @@ static void go_gemv1(const GemmArgs& a, dim3 grid, dim3 block, size_t lds, hipSt
 // head gate|up 15.62 -> 12.45 in tools/gemv_variants.py), VibeVoice-Large B = 1
 // 7.14 -> 6.85 ms (K = 3,584 rows), 1.5B B = 1 3.597 -> 3.588 ms.
 // Diagnostic: vv_gemv_tune_rw(min rows; 99 = off).
+// The K = 3,584 adaLN rows (VibeVoice-Large head) take the LDS-DMA form (RW 2).
+// Diagnostic: vv_gemv_tune_rw(min rows; 99 = off; -1 = built-in without RW 2).
 static int g_rw_min_m = 1;
+static bool g_rw_dma = true;
 extern "C" int vv_gemv_tune_rw(int min_m) {
   g_rw_min_m = min_m > 0 ? min_m : 1;
+  g_rw_dma = min_m >= 0;
   return 0;
 }
-static bool gemv1_rw(const GemmArgs& a, int nw) {
-  if (!VV_G1_RW || a.xf.kind != XF_NORM || a.ksplit != 1 || a.M < g_rw_min_m || a.K % 512) return false;
+static int gemv1_rw(const GemmArgs& a, int nw) {
+  if (!VV_G1_RW || a.xf.kind != XF_NORM || a.ksplit != 1 || a.M < g_rw_min_m || a.K % 512) return 0;
   const int ipr = a.K / 512, rpw = (a.M + nw - 1) / nw;
-  return (ipr == 3 && rpw <= 2) || (ipr == 7 && rpw == 1 && !a.xf.mod);
+  if (ipr == 3 && rpw <= 2) return 1;
+  if (ipr == 7 && rpw == 1) return !a.xf.mod ? 1 : g_rw_dma ? 2 : 0;
+  return 0;
 }
 
 // TPW is a template argument so the one-tile form (every M < 8 launch) keeps
 // its straight-line index math (a runtime tiles-per-group cost 1 us per launch)
-template <int XF, int TPW, bool RW>
+template <int XF, int TPW, int RW>
 static void launch_gemv1_rw(const GemmArgs& a, int u, dim3 grid, dim3 block, size_t lds, hipStream_t st) {
   if (a.keep) {
     if (u == 4) go_gemv1<4, XF, true, TPW, RW>(a, grid, block, lds, st);
@@ -1246,8 +1331,10 @@ static void launch_gemv1_rw(const GemmArgs& a, int u, dim3 grid, dim3 block, siz
 }
 template <int XF, int TPW>
 static void launch_gemv1(const GemmArgs& a, int u, dim3 grid, dim3 block, size_t lds, hipStream_t st) {
-  if (XF == XF_NORM && gemv1_rw(a, block.x / 64)) launch_gemv1_rw<XF_NORM, TPW, true>(a, u, grid, block, lds, st);
-  else launch_gemv1_rw<XF, TPW, false>(a, u, grid, block, lds, st);
+  const int rw = XF == XF_NORM ? gemv1_rw(a, block.x / 64) : 0;
+  if (rw == 1) launch_gemv1_rw<XF_NORM, TPW, 1>(a, u, grid, block, lds, st);
+  else if (rw == 2 && TPW == 1) launch_gemv1_rw<XF_NORM, 1, 2>(a, u, grid, block, lds, st);
+  else launch_gemv1_rw<XF, TPW, 0>(a, u, grid, block, lds, st);
 }
 
 template <int XF>
