@@ -124,9 +124,10 @@ def bytes_per_token(wb, cfg, B, S, ctx_pos, ctx_neg):
 
 # ------------------------------------------------------------------ dominant kernel, live
 # U = 4 chunks in flight, XF_NORM, non-temporal weights, tiles per workgroup (gemm.hip gemv_plan: 1 at M < 8,
-# 8 at 8 <= M <= 16); HBM traffic per launch from tools/pmc_traffic.py (rocprofv3 PMC, committed per M)
+# 8 at 8 <= M <= 16), row-per-wave norm prologue (RW = 1); HBM traffic per launch from tools/pmc_traffic.py
+# (rocprofv3 PMC, committed per M)
 def roof_kernel(M):
-    return f"k_gemv1<4, 1, false, {8 if M >= 8 else 1}>"
+    return f"k_gemv1<4, 1, false, {8 if M >= 8 else 1}, 1>"
 
 
 def pmc_file(M):

@@ -1,4 +1,4 @@
-"""HBM traffic of bench.py's roofline kernel (the LM gate|up GEMV, k_gemv1<4, 1, false>,
+"""HBM traffic of bench.py's roofline kernel (the LM gate|up GEMV, k_gemv1<4, 1, false, tpw, 1>,
 M=2 N=17920 K=1536 at 1.5B, B=1) from rocprofv3 PMC counters, collected the way
 MI355X_MICROARCH.md "HBM" / "rocprofv3 PMC slots" prescribe: FETCH_SIZE and
 WRITE_SIZE in separate passes (they do not fit one TCC pass), FETCH_SIZE
@@ -22,7 +22,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 M = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 N, K, NL = 17920, 1536, 28
-KERNEL = f"k_gemv1<4, 1, false, {8 if M >= 8 else 1}>"     # U, XF_NORM, non-temporal, tiles per workgroup
+KERNEL = f"k_gemv1<4, 1, false, {8 if M >= 8 else 1}, 1>"  # U, XF_NORM, non-temporal, tiles per workgroup, RW form
 
 
 def run():
