@@ -208,7 +208,8 @@ int vv_gemv_tune_wide(int on);
 int vv_gemv_tune_lds(int bytes);
 /* Tuning hook (benchmarks only): fused-RMSNorm GEMVs with at least min_m rows
  * (and an eligible shape) stage whole A rows per wave (k_gemv1's RW form: the
- * norm applied in registers, one barrier); 0 restores the built-in 1. */
+ * norm applied in registers, one barrier); 0 restores the built-in 1; -1 = the
+ * built-in without the LDS-DMA form for K = 3,584 adaLN rows; 99 = off. */
 int vv_gemv_tune_rw(int min_m);
 /* Tuning hook (benchmarks / tests): XF-free GEMMs with >= 256 rows,
  * N % 128 == 0, K % 64 == 0 and >= 256 such tiles (or >= 2^30 MACs) take the
