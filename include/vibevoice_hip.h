@@ -211,6 +211,14 @@ int vv_gemv_tune_lds(int bytes);
  * norm applied in registers, one barrier); 0 restores the built-in 1; -1 = the
  * built-in without the LDS-DMA form for K = 3,584 adaLN rows; 99 = off. */
 int vv_gemv_tune_rw(int min_m);
+/* Host-only plan query (no device work; tests and tools): the kernel form and
+ * launch plan the library uses for an M <= 16 GEMV (xf: 0 none, 1 RMSNorm, 2
+ * SiLU-add; has_w / has_mod: norm weight, adaLN shift / scale present).
+ * out[7] = {kernel (0 = A staged in LDS, 1 = A fragments from L2), waves, K
+ * splits, weight chunks in flight, tiles per workgroup, norm prologue form
+ * (0 item per thread, 1 row per wave, 2 row per wave + LDS-DMA rows), dynamic
+ * LDS bytes}. Replaces nothing in the reference (the plan is this engine's). */
+int vv_gemv_plan(int M, int N, int K, int xf, int has_w, int has_mod, int* out);
 /* Tuning hook (benchmarks / tests): XF-free GEMMs with >= 256 rows,
  * N % 128 == 0, K % 64 == 0 and >= 256 such tiles (or >= 2^30 MACs) take the
  * LDS-staged 128 x 128 tile (k_gemm_big, the prefill projections) with 2 LDS

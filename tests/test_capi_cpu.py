@@ -38,3 +38,43 @@ def test_create_rejects_bad_config():
     h = ctypes.c_void_p()
     assert L.vv_create(ctypes.byref(c), 0, ctypes.byref(h)) != 0
     assert b"head_dim" in L.vv_last_error()
+
+
+def _plan(M, N, K, xf=0, w=False, mod=False):
+    out = (ctypes.c_int * 7)()
+    assert _lib.lib().vv_gemv_plan(M, N, K, xf, int(w), int(mod), out) == 0
+    return dict(zip(("kernel", "waves", "ksplit", "u", "tpw", "rw", "lds"), list(out)))
+
+
+def test_gemv_plan_rules():
+    """The decode-GEMV launch plans DESIGN.md §3 documents (host logic only)."""
+    NORM = 1
+    # B = 1 (M = 2): LM gate|up, 2-wave one-tile workgroups, row-per-wave norm
+    p = _plan(2, 17920, 1536, NORM, w=True)
+    assert (p["kernel"], p["waves"], p["ksplit"], p["u"], p["tpw"], p["rw"]) == (0, 2, 1, 4, 1, 1)
+    # B = 8 (M = 16): 8 tiles per 8-wave workgroup, two rows per wave
+    p = _plan(16, 17920, 1536, NORM, w=True)
+    assert (p["waves"], p["tpw"], p["rw"]) == (8, 8, 1)
+    # B = 8 LM down: K split until the A slice fits 64 KB of LDS (5 ways), staged once
+    p = _plan(16, 1536, 8960)
+    assert (p["kernel"], p["ksplit"], p["waves"]) == (0, 5, 8) and p["lds"] <= 65536
+    # codec fc2 at C = 2,048 keeps its 2-way split on k_gemv (the split-to-fit rule cost 20 us there)
+    p = _plan(16, 2048, 8192)
+    assert (p["kernel"], p["ksplit"], p["waves"]) == (1, 2, 8)
+    # VibeVoice-Large LM down at M = 2: split until the 76 KB of A rows fit
+    p = _plan(2, 3584, 18944)
+    assert (p["kernel"], p["ksplit"], p["waves"]) == (0, 2, 8)
+    # Large head layers (K 3,584, norm weight + adaLN): the LDS-DMA row form; no adaLN: registers
+    assert _plan(2, 21504, 3584, NORM, w=True, mod=True)["rw"] == 2
+    assert _plan(2, 37888, 3584, NORM, w=True)["rw"] == 1
+    # the RW form is an XF_NORM-only, unsplit-K form
+    assert _plan(2, 1536, 8960)["rw"] == 0
+    assert _plan(16, 64, 1536, NORM, mod=True)["ksplit"] == 8 and _plan(16, 64, 1536, NORM, mod=True)["rw"] == 0
+    # the diagnostic switch turns it off and back on
+    L = _lib.lib()
+    L.vv_gemv_tune_rw(99)
+    try:
+        assert _plan(2, 17920, 1536, NORM, w=True)["rw"] == 0
+    finally:
+        L.vv_gemv_tune_rw(0)
+    assert _plan(2, 17920, 1536, NORM, w=True)["rw"] == 1

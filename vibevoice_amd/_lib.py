@@ -67,6 +67,7 @@ EXPORTS = [
     ("vv_gemv_tune_wide", I, [I]),
     ("vv_gemv_tune_lds", I, [I]),
     ("vv_gemv_tune_rw", I, [I]),
+    ("vv_gemv_plan", I, [I, I, I, I, I, I, P]),
     ("vv_gemm_tune_big", I, [I]),
     ("vv_gemv_stamps", I, [P]),
     ("vv_attn_stamps", I, [P]),

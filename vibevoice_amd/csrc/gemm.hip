@@ -1865,6 +1865,66 @@ int gemv_plan_query(const GemmArgs& a0, int* nw, int* ksplit, int* tpw, int* fas
   return 0;
 }
 
+// The decode-GEMV launch plan for a (M <= 64): waves, K split, tiles per
+// workgroup; sets a.ksplit / a.handoff / a.tpw (launch_gemm, vv_gemv_plan).
+static GemmPlan gemv_resolve(GemmArgs& a) {
+  const int mrep = (a.M + 15) / 16;
+  GemmPlan p = gemv_plan(a.N, a.K, a.M);
+  if (p.nw > max_waves(mrep)) p.nw = max_waves(mrep);
+  a.ksplit = p.ksplit;
+  if (a.ksplit > 1 && (!a.ws || !a.counters || a.N / 16 > 65536)) a.ksplit = 1;
+  // Rows too long for one workgroup to stage in k_gemv1's LDS at one K split
+  // (VibeVoice-Large's LM down projection, M = 2 x K 18,944 = 76 KB): split K
+  // until the slice fits, 8 waves x 4 chunks (tools/gemv_sweep.py --large: 48.4 ->
+  // 27.1 us), instead of k_gemv re-loading A fragments from L2 per chunk.
+  if (mrep == 1 && a.M < 8 && a.xf.kind == XF_NONE && !g_tune_ks && a.ws && a.counters && a.N / 16 <= 65536 &&
+      !gemv1_fits(a)) {
+    GemmArgs t = a;
+    while (!gemv1_fits(t) && t.ksplit < 4) t.ksplit *= 2;
+    if (gemv1_fits(t)) {
+      a.ksplit = t.ksplit;
+      if (!g_tune_nw) p.nw = 8;
+      if (!g_tune_u) p.u = 4;
+    }
+  }
+  a.handoff = g_tune_handoff >= 0 ? g_tune_handoff : 1;
+  a.tpw = 1;
+  if (mrep == 1 && a.ksplit == 1 && a.xf.kind != XF_MIX && (p.tpw == 2 || p.tpw == 4 || p.tpw == 8) && p.nw % p.tpw == 0 && gemv1_fits(a))
+    a.tpw = p.tpw;
+  return p;
+}
+
+// Host-only plan query (no device work; tests and tools): the kernel form and
+// launch plan launch_gemm would use for an M <= 16 GEMV.  out[7] = {kernel
+// (0 k_gemv1, 1 k_gemv: A fragments from L2), waves, K splits, chunks in flight,
+// tiles per workgroup, norm prologue form (0 item per thread, 1 row per wave,
+// 2 row per wave with LDS-DMA rows), dynamic LDS bytes}.
+extern "C" int vv_gemv_plan(int M, int N, int K, int xf, int has_w, int has_mod, int* out) {
+  if (M <= 0 || M > 16 || K % 32 || N % 16 || !out || (xf != XF_NONE && xf != XF_NORM && xf != XF_SILU_ADD)) return 1;
+  static const bf16 dummy[8] = {};
+  static unsigned dummy_ctr[1];
+  GemmArgs a{};
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.xf.kind = xf;
+  a.xf.w = has_w ? dummy : nullptr;
+  a.xf.mod = has_mod ? dummy : nullptr;
+  static float dummy_ws[1];
+  a.ws = dummy_ws;   // planning only tests these for null
+  a.counters = dummy_ctr;
+  const GemmPlan p = gemv_resolve(a);
+  const bool g1 = gemv1_fits(a);
+  out[0] = g1 ? 0 : 1;
+  out[1] = p.nw;
+  out[2] = a.ksplit;
+  out[3] = p.u;
+  out[4] = a.tpw;
+  out[5] = g1 && xf == XF_NORM ? gemv1_rw(a, p.nw) : 0;
+  out[6] = g1 ? (int)gemv1_lds(a) : 0;
+  return 0;
+}
+
 // returns 0 ok, else an error code (see engine.cpp)
 int launch_gemm(GemmArgs a, hipStream_t st) {
   if (a.M <= 0) return 0;
@@ -1883,28 +1943,7 @@ int launch_gemm(GemmArgs a, hipStream_t st) {
   if (a.M <= 64 && (a.M <= 16 || a.M <= g_gemv_max_m || a.epi.kind == EPI_CFG_DPM)) {
     if (launch_gemvw(a, st)) return hipGetLastError() == hipSuccess ? 0 : 2;
     const int mrep = (a.M + 15) / 16;
-    GemmPlan p = gemv_plan(a.N, a.K, a.M);
-    if (p.nw > max_waves(mrep)) p.nw = max_waves(mrep);
-    a.ksplit = p.ksplit;
-    if (a.ksplit > 1 && (!a.ws || !a.counters || a.N / 16 > 65536)) a.ksplit = 1;
-    // Rows too long for one workgroup to stage in k_gemv1's LDS at one K split
-    // (VibeVoice-Large's LM down projection, M = 2 x K 18,944 = 76 KB): split K
-    // until the slice fits, 8 waves x 4 chunks (tools/gemv_sweep.py --large: 48.4 ->
-    // 27.1 us), instead of k_gemv re-loading A fragments from L2 per chunk.
-    if (mrep == 1 && a.M < 8 && a.xf.kind == XF_NONE && !g_tune_ks && a.ws && a.counters && a.N / 16 <= 65536 &&
-        !gemv1_fits(a)) {
-      GemmArgs t = a;
-      while (!gemv1_fits(t) && t.ksplit < 4) t.ksplit *= 2;
-      if (gemv1_fits(t)) {
-        a.ksplit = t.ksplit;
-        if (!g_tune_nw) p.nw = 8;
-        if (!g_tune_u) p.u = 4;
-      }
-    }
-    a.handoff = g_tune_handoff >= 0 ? g_tune_handoff : 1;
-    a.tpw = 1;
-    if (mrep == 1 && a.ksplit == 1 && a.xf.kind != XF_MIX && (p.tpw == 2 || p.tpw == 4 || p.tpw == 8) && p.nw % p.tpw == 0 && gemv1_fits(a))
-      a.tpw = p.tpw;
+    const GemmPlan p = gemv_resolve(a);
     dim3 grid((a.N / 16 + a.tpw - 1) / a.tpw, a.ksplit), block(64 * p.nw);
     if (a.xf.kind == XF_MIX) {
       const size_t lds = gemv_mix_lds(a.M, a.xf.T, a.K);
