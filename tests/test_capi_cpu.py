@@ -1,5 +1,7 @@
 """CPU-side checks of the C ABI library: it builds, loads and exports every
-entry point declared in include/vibevoice_hip.h (no GPU compute here)."""
+entry point declared in include/vibevoice_hip.h (the product interface) and
+include/vibevoice_hip_diag.h (kernel entry points, tuning hooks, stamps), and
+the product header declares none of the diagnostics (no GPU compute here)."""
 import ctypes
 import os
 import re
@@ -9,15 +11,37 @@ from vibevoice_amd import _lib
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_symbols():
-    src = open(os.path.join(ROOT, "include", "vibevoice_hip.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:const char\*|int|void)\s+(vv_\w+)\(", src, re.M)))
+def declared_symbols(headers=("vibevoice_hip.h", "vibevoice_hip_diag.h")):
+    names = set()
+    for h in headers:
+        src = open(os.path.join(ROOT, "include", h)).read()
+        names |= set(re.findall(r"^\s*(?:const char\*|int|void)\s+(vv_\w+)\(", src, re.M))
+    return sorted(names)
 
 
 def test_header_declares_entry_points():
     names = declared_symbols()
     assert "vv_lm_forward" in names and "vv_diffusion_sample" in names and "vv_codec_step" in names
     assert set(names) == {n for n, _, _ in _lib.EXPORTS}
+
+
+def test_product_header_has_no_diagnostics():
+    """Tuning hooks, stamps, kernel entry points and benchmark-only switches
+    (process-wide state) live in the diag header only."""
+    product = set(declared_symbols(("vibevoice_hip.h",)))
+    diag = set(declared_symbols(("vibevoice_hip_diag.h",)))
+    assert not product & diag
+    for n in product:
+        assert not re.search(r"tune|stamps|null_collective|synthetic|_bf16$|plan|chain|pack|rope_table|defer|"
+                             r"mix_fusion|attn_prefill", n), n
+    assert {"vv_tp_null_collective", "vv_kv_synthetic", "vv_gemv_tune", "vv_gemm_bf16"} <= diag
+    # nothing in the product package calls a diagnostic entry point
+    pkg = os.path.join(ROOT, "vibevoice_amd")
+    for f in os.listdir(pkg):
+        if f.endswith(".py") and f != "_lib.py":
+            src = open(os.path.join(pkg, f)).read()
+            for n in diag:
+                assert n + "(" not in src, (f, n)
 
 
 def test_library_loads_and_exports_all_symbols():

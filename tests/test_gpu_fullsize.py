@@ -20,7 +20,7 @@ bounds — hidden 3e-2, logits (the 4 legal ones) 7e-2, acoustic latents 7e-2,
 audio 3e-2, next-step connector embeddings 3e-2.
 Token choice: an unforced greedy run of 40 steps, teacher-forced, where the
 product's own argmax must equal the oracle's at every step whose margin the
-bounded logit error cannot flip.  Free-running (no forcing): greedy tokens equal
+bounded logit error cannot flip (>= 30 such steps asserted).  Free-running (no forcing): greedy tokens equal
 for the first 8 steps, and forced-diffusion audio within rel 0.30 / cosine 0.95
 after 8 autoregressive frames (the bf16 reference's own drift from fp32 over
 those frames is 0.31).
@@ -240,9 +240,13 @@ def test_greedy_tokens_teacher_forced_1p5b(m15):
     the oracle chooses greedily; the product is driven with the oracle's inputs
     and its OWN constrained argmax (k_final_head over the 4 legal rows, read
     back every step) must equal the oracle's choice wherever the oracle's
-    top-2 margin exceeds 2 x the logits bound (rel 0.1 of the logits' norm —
-    a margin the bounded logit error cannot flip); every step's logits are
-    within that bound.  The path mixes diffusion, speech_end and speech_start."""
+    top-2 margin exceeds sqrt(2) x the logits bound: every step's logits are
+    asserted within rel L2 BOUND["logits"] of the oracle's, and two entries of
+    an error vector e differ by at most sqrt(2) |e|, so such a margin cannot
+    flip.  At least 30 of the 40 steps must clear that gate and be compared
+    (the seeded path: 33), including a non-diffusion choice (speech_start at
+    step 38, margin 0.35).  The path mixes diffusion, speech_end and
+    speech_start."""
     g = _greedy_model(m15)
     inp = synthetic_inputs(batch=1, speakers=1, voice_seconds=3.0, text_tokens=64, seed=102)
     vn = _voice_noise(inp, m15.cfg.acoustic_vae_dim)
@@ -254,14 +258,20 @@ def test_greedy_tokens_teacher_forced_1p5b(m15):
     print("oracle margins", [round(x, 3) for x in margins])
     assert len(toks) >= 32, len(toks)
     assert {D, E, S} <= set(toks), "the greedy path should exercise diffusion, speech_end and speech_start"
-    seen = []
+    seen, compared = [], []
+    gate = 2 ** 0.5 * BOUND["logits"]
     got, sess = teacher_forced(g.model, inp, [toks], rec, TK, SEED, max_new=GREEDY_STEPS)
+    assert len(got["logits"]) == len(toks)
     for k, lg in enumerate(got["logits"]):
         mine = VALID[int(lg[0].argmax())]
         seen.append(mine)
-        if margins[k] > 2 * BOUND["logits"]:
+        if margins[k] > gate:
+            compared.append(k)
             assert mine == toks[k], f"step {k}: product argmax {mine} != oracle {toks[k]} (margin {margins[k]:.3f})"
     print("product argmax", [t - 151640 for t in seen])
+    print(f"argmax compared at {len(compared)} of {len(toks)} steps (margin > {gate:.3f}): {compared}")
+    assert len(compared) >= 30, f"only {len(compared)} steps cleared the margin gate"
+    assert any(toks[k] != D for k in compared), "no speech_end / speech_start / eos choice among the compared steps"
     per_step_check(got, rec, None, "1.5B greedy (teacher-forced)")
 
 

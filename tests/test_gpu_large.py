@@ -296,3 +296,46 @@ def test_tp2_long_context_matches_single_engine():
     for s, ((he, le), (hr, lr)) in enumerate(zip(eager, replayed)):
         print(f"TP=2 65K graph step {s}: bitwise {torch.equal(he, hr) and torch.equal(le, lr)}")
         assert torch.equal(he, hr) and torch.equal(le, lr)
+
+
+def test_28_layer_32k_prefill_graph_decode_vs_oracle():
+    """configs[4]'s long-context path at FULL depth: VibeVoice-1.5B's 28 Qwen2
+    layers (H 1536, 12 q / 2 kv heads, I 8960), a 32,768-token causal prefill
+    through the product path (k_attn_pf + k_gemm_xl), then 3 decode steps
+    captured into ONE hipGraph with the loop's max_ctx split plan and replayed
+    (k_attn splits + merge over 32K keys) — bitwise equal to the eager
+    launches, and every replayed step's final-norm hidden state within rel L2
+    3e-2 of oracle/lm.py (the full-size hidden bound, tests/teacher.py) run as
+    the checker on the GPU."""
+    cfg = tiny_config(hidden=1536, layers=28, heads=12, kv_heads=2, inter=8960)
+    cfg.decoder_config["max_position_embeddings"] = 65536
+    sd = synthetic_state_dict(cfg, seed=27, device=dev, mode="test", with_acoustic_encoder=False)
+    N = 32768
+    eng = Engine(cfg, sd, dev, max_batch=1, max_ctx=N + 40, valid_ids=VALID)
+    g = torch.Generator(device=dev).manual_seed(8)
+    x = torch.randn(N, 1536, device=dev, generator=g).bfloat16()
+    hp, _ = eng.lm_forward(x, torch.zeros(N, **I32), torch.arange(N).to(**I32), torch.tensor([N - 1]).to(**I32))
+    steps = torch.randn(3, 1536, device=dev, generator=g).bfloat16()
+    dec = _Dec(eng)
+
+    def set_step(s):
+        dec.x.copy_(steps[s:s + 1])
+        dec.pos.fill_(N + s)
+    eager, replayed = _graph_vs_eager(dec, set_step, 3)
+    osd, lcfg = oracle_sd(sd, dev), dict(cfg.decoder_config)
+    kv = olm.RowKV(28)
+    with torch.no_grad():
+        ref_p = _oracle_prefill_gpu(osd, lcfg, x, kv)
+    e = rel_err(hp, ref_p)
+    print(f"28-layer 32K prefill: rel {e:.3e} cos {cos(hp, ref_p):.6f}")
+    assert e < 3e-2 and cos(hp, ref_p) > 0.999
+    for s, ((he, le), (hr, lr)) in enumerate(zip(eager, replayed)):
+        with torch.no_grad():
+            ref = olm.forward_rows(osd, lcfg, steps[None, s:s + 1], [kv])[0, -1]
+        torch.cuda.synchronize()
+        e = rel_err(hr, ref)
+        same = torch.equal(he, hr) and torch.equal(le, lr)
+        print(f"28-layer 32K graph step {s} (attends {N + s + 1} keys): bitwise-eager {same} "
+              f"rel {e:.3e} cos {cos(hr, ref):.6f}")
+        assert same
+        assert e < 3e-2 and cos(hr, ref) > 0.999

@@ -11,7 +11,7 @@ import pytest
 import torch
 
 from golden_io import load, t, weights
-from gpu_util import cos, rel_err
+from gpu_util import cos, kv_synthetic, rel_err
 from oracle import lm as olm
 from tiny import tiny_config
 from vibevoice_amd.engine import Engine
@@ -155,7 +155,7 @@ def test_attn_defer_bit_identical(nrows, chunk, maxpos):
     cfg = tiny_config(hidden=1536, layers=2, heads=12, kv_heads=2, inter=8960)
     eng, _ = make_engine(cfg, seed=4, max_batch=nrows, max_ctx=4096)
     slots = torch.arange(nrows).to(**I32)
-    eng.kv_synthetic(slots, 0, 4096, seed=11)
+    kv_synthetic(eng, slots, 0, 4096, seed=11)
     g = torch.Generator().manual_seed(9)
     x = torch.randn(nrows, 1536, generator=g).bfloat16().to(dev)
     pos = torch.tensor([(97 + 263 * i) % maxpos for i in range(nrows)], dtype=torch.int32).to(dev)

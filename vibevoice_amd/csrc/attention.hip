@@ -11,6 +11,7 @@
 // for one 32-key step are one 8 KB contiguous block.  A row's cache holds only the entries its
 // attention mask keeps, in order, so cache index == RoPE position (SURVEY.md
 // §8a rows a3, a7).
+#include <atomic>
 #include <type_traits>
 
 #include "kernels.h"
@@ -76,9 +77,6 @@ DEV float row16_sum(float v) {
   v += dpp_f<0x141>(v);
   return v + dpp_f<0x140>(v);
 }
-#ifndef VV_ATT_DPP
-#define VV_ATT_DPP 1
-#endif
 
 DEV void astamp(const AttnArgs& a, int which) {
   if (a.stamps && threadIdx.x == 0)
@@ -185,27 +183,13 @@ __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
       float s0 = c0 + r < w1 ? sacc[0][i] * a.scale : -INFINITY;
       float s1 = c0 + 16 + r < w1 ? sacc[1][i] * a.scale : -INFINITY;
       float mx = fmaxf(s0, s1);
-#if VV_ATT_DPP
       mx = row16_max(mx);
-#else
-      mx = fmaxf(mx, __shfl_xor(mx, 1));
-      mx = fmaxf(mx, __shfl_xor(mx, 2));
-      mx = fmaxf(mx, __shfl_xor(mx, 4));
-      mx = fmaxf(mx, __shfl_xor(mx, 8));
-#endif
       const float mnew = fmaxf(m[i], mx);
       const float al = __expf(m[i] - mnew);
       p[0][i] = __expf(s0 - mnew);
       p[1][i] = __expf(s1 - mnew);
       float ps = p[0][i] + p[1][i];
-#if VV_ATT_DPP
       ps = row16_sum(ps);
-#else
-      ps += __shfl_xor(ps, 1);
-      ps += __shfl_xor(ps, 2);
-      ps += __shfl_xor(ps, 4);
-      ps += __shfl_xor(ps, 8);
-#endif
       l[i] = l[i] * al + ps;
       m[i] = mnew;
 #pragma unroll
@@ -521,23 +505,14 @@ int launch_final_head(int R, int H, const bf16* h, const int* idx, const bf16* n
 constexpr int PF_Q = 32;
 constexpr float PF_LAZY = 8.f;       // running-max slack (log2 units) before O is rescaled
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-#ifndef VV_PF_SUB
-#define VV_PF_SUB 2
-#endif
 // 32-key steps per LDS stage (one barrier and one vmcnt wait per stage)
-constexpr int PF_SUB = VV_PF_SUB;
+constexpr int PF_SUB = 2;
 constexpr int PF_STAGE = PF_SUB * 16 * 512;   // bf16 elements per stage: per step 8 K + 8 V fragment blocks
 // LDS stages: steps s+1 .. s+NS-2 in flight while step s computes, step
 // s+NS-1 issued after the step's one barrier.  16K-token prefill (interleaved
 // same-box runs, tools/ab_bench.py --prefill): NS 2 118.7 ms, NS 3 122.4, NS 4
 // 122.4; the former two-barrier form with NS 2 124.6 ms
-#ifndef VV_PF_NS
-#define VV_PF_NS 2
-#endif
-#ifndef VV_PF_ABL
-#define VV_PF_ABL 0
-#endif
-constexpr int PF_NS = VV_PF_NS;
+constexpr int PF_NS = 2;
 
 // max / sum over lanes {l, l^16, l^32, l^48} (one query column of an MFMA
 // tile): gfx950's v_permlane16_swap / v_permlane32_swap (VALU, a few cycles)
@@ -671,9 +646,6 @@ __global__ void __launch_bounds__(64 * G * 2 / QW) __attribute__((amdgpu_waves_p
     const bf16* K = a.kv.k + cbase;    // [ctx][128]
     const bf16* VB = a.kv.v + cbase;   // 32-position blocks of [128][32] (v_off)
     auto issue = [&](int step) {
-#if VV_PF_ABL == 1
-      return;   // ablation (timing only): no K/V staging
-#endif
       bf16* st = sm + (step % PF_NS) * PF_STAGE;
 #pragma unroll
       for (int i = 0; i < NI_MAX; ++i)
@@ -700,15 +672,8 @@ __global__ void __launch_bounds__(64 * G * 2 / QW) __attribute__((amdgpu_waves_p
       const bf16* st = sm + (step % PF_NS) * PF_STAGE + sub * 16 * 512;
       // all 8 K fragments, then the 16 S MFMAs (one LDS round trip, not one per key tile)
       bf16x8 kf[8];
-#if VV_PF_ABL == 3
-      // ablation (timing only): every step reuses one 16-byte LDS read per fragment
-      // slot (the first K row's), so the step's LDS read traffic drops 8-fold
-#pragma unroll
-      for (int f = 0; f < 8; ++f) kf[f] = *(const bf16x8*)(st + lane * 8);
-#else
 #pragma unroll
       for (int f = 0; f < 8; ++f) kf[f] = *(const bf16x8*)(st + f * 512 + lane * 8);
-#endif
       f32x4 s[2][QW];
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
@@ -721,13 +686,8 @@ __global__ void __launch_bounds__(64 * G * 2 / QW) __attribute__((amdgpu_waves_p
       // the V^T fragments do not depend on P: issued now, they land under the softmax
       // (read one at a time after it, each read's latency was exposed 8 times a step)
       bf16x8 vf[8];
-#if VV_PF_ABL == 3
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) vf[dt] = kf[dt];
-#else
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt) vf[dt] = *(const bf16x8*)(st + (8 + dt) * 512 + lane * 8);
-#endif
       __builtin_amdgcn_sched_barrier(0);
       // online softmax with a lazy running max: a column's m (log2 units) moves
       // only when a score exceeds it by > PF_LAZY, so P <= 2^PF_LAZY and the
@@ -796,11 +756,7 @@ __global__ void __launch_bounds__(64 * G * 2 / QW) __attribute__((amdgpu_waves_p
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const float e = decltype(full_c)::value ? __builtin_fmaf(x[qt][kt][i], sl2, -mref) : x[qt][kt][i] - mref;
-#if VV_PF_ABL == 2
-              const float p = e;   // ablation (timing only): no exp
-#else
               const float p = __builtin_amdgcn_exp2f(e);
-#endif
               ps += p;
               pf[qt][4 * kt + i] = (bf16)p;
             }
@@ -846,7 +802,7 @@ __global__ void __launch_bounds__(64 * G * 2 / QW) __attribute__((amdgpu_waves_p
   }
 }
 
-static int g_att_prefill = -1;   // diagnostic override (vv_attn_prefill): -1 auto, 0 never, 1 always
+static std::atomic<int> g_att_prefill{-1};   // diagnostic override (vv_attn_prefill): -1 auto, 0 never, 1 always
 extern "C" int vv_attn_prefill(int mode) {
   g_att_prefill = mode < 0 ? -1 : mode > 0 ? 1 : 0;
   return 0;
@@ -859,19 +815,16 @@ bool attn_use_prefill(int nq, int nslots) {
   return nq >= 256 && nq >= PF_Q * nslots;
 }
 
-#ifndef VV_PF_QW1
-#define VV_PF_QW1 1   // 0: one wave per head at every G (diagnostic builds)
-#endif
 static int launch_attn_pf(const AttnArgs& a, hipStream_t st) {
   const dim3 grid((a.nq + PF_Q - 1) / PF_Q, a.nkv);
   // two waves per head (QW = 1) while that keeps <= 3 waves per SIMD (G <= 6)
   switch (a.nh / a.nkv) {
-    case 1: hipLaunchKernelGGL((k_attn_pf<1, VV_PF_QW1 ? 1 : 2>), grid, dim3(VV_PF_QW1 ? 128 : 64), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((k_attn_pf<2, VV_PF_QW1 ? 1 : 2>), grid, dim3(VV_PF_QW1 ? 256 : 128), 0, st, a); break;
-    case 3: hipLaunchKernelGGL((k_attn_pf<3, VV_PF_QW1 ? 1 : 2>), grid, dim3(VV_PF_QW1 ? 384 : 192), 0, st, a); break;
-    case 4: hipLaunchKernelGGL((k_attn_pf<4, VV_PF_QW1 ? 1 : 2>), grid, dim3(VV_PF_QW1 ? 512 : 256), 0, st, a); break;
-    case 5: hipLaunchKernelGGL((k_attn_pf<5, VV_PF_QW1 ? 1 : 2>), grid, dim3(VV_PF_QW1 ? 640 : 320), 0, st, a); break;
-    case 6: hipLaunchKernelGGL((k_attn_pf<6, VV_PF_QW1 ? 1 : 2>), grid, dim3(VV_PF_QW1 ? 768 : 384), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((k_attn_pf<1, 1>), grid, dim3(128), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((k_attn_pf<2, 1>), grid, dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((k_attn_pf<3, 1>), grid, dim3(384), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((k_attn_pf<4, 1>), grid, dim3(512), 0, st, a); break;
+    case 5: hipLaunchKernelGGL((k_attn_pf<5, 1>), grid, dim3(640), 0, st, a); break;
+    case 6: hipLaunchKernelGGL((k_attn_pf<6, 1>), grid, dim3(768), 0, st, a); break;
     case 7: hipLaunchKernelGGL((k_attn_pf<7, 2>), grid, dim3(448), 0, st, a); break;
     default: hipLaunchKernelGGL((k_attn_pf<8, 2>), grid, dim3(512), 0, st, a); break;
   }
@@ -882,7 +835,7 @@ static int launch_attn_pf(const AttnArgs& a, hipStream_t st) {
 // ATT_SPLITS_MAX; beyond that the splits grow in ATT_CHUNK steps).  Each row
 // sizes its own splits from its length (row_chunk), so a plan made for
 // max_ctx serves every step of a captured graph.
-static int g_att_chunk = 0, g_att_merge_in = -1;   // diagnostic overrides (vv_attn_tune)
+static std::atomic<int> g_att_chunk{0}, g_att_merge_in{-1};   // diagnostic overrides (vv_attn_tune)
 extern "C" int vv_attn_tune(int chunk, int merge_in) {
   if (chunk % ATT_KC) return 1;
   g_att_chunk = chunk;
@@ -893,7 +846,8 @@ extern "C" int vv_attn_tune(int chunk, int merge_in) {
 int attn_plan(int nq, int nkv, int max_len, int* chunk) {
   (void)nq;
   (void)nkv;
-  int c = g_att_chunk > 0 ? g_att_chunk : ATT_CHUNK;
+  const int tc = g_att_chunk;
+  int c = tc > 0 ? tc : ATT_CHUNK;
   int ns = (max_len + c - 1) / c;
   if (ns > ATT_SPLITS_MAX) {
     c = ((max_len + ATT_SPLITS_MAX - 1) / ATT_SPLITS_MAX + ATT_CHUNK - 1) / ATT_CHUNK * ATT_CHUNK;
@@ -926,7 +880,8 @@ int launch_attn(AttnArgs a, hipStream_t st) {
   if (a.chunk % ATT_KC || a.nsplit > ATT_SPLITS_MAX) return 1;
   if ((a.nsplit > 1 || a.defer) && (!a.part_o || !a.part_ml || !a.counters)) return 1;
   if (a.defer && a.nsplit > ATT_MERGE_IN) return 1;
-  a.merge = !a.defer && a.nsplit > (g_att_merge_in >= 0 ? g_att_merge_in : ATT_MERGE_IN) ? 1 : 0;
+  const int mi = g_att_merge_in;
+  a.merge = !a.defer && a.nsplit > (mi >= 0 ? mi : ATT_MERGE_IN) ? 1 : 0;
   dim3 grid(a.nq * a.nkv, a.nsplit);
   const int nw = a.chunk >= 256 ? 8 : a.chunk >= 128 ? 4 : 2;   // 32 keys per wave step
   if (nw == 8) launch_attn_nw<8>(a, grid, st);

@@ -32,21 +32,15 @@
 // and split summation order, same epilogues.  With the per-op launch plan
 // mirrored (vv_chain_tune(2)) the chain is bit-identical to the per-op kernels;
 // the default plan re-splits K to balance the 256 CUs.
+#include <atomic>
 #include <cstdio>
 #include <vector>
 
 #include "gemv_dev.h"
 
-// waves per workgroup and workgroups per CU (co-resident: VGPRs allow 8 waves
-// per CU, LDS 2 x 80 KB).  VV_CH_NW=4 VV_CH_WGPC=2: two units in flight per CU
-// (diagnostic builds; the default is one 8-wave workgroup per CU)
-#ifndef VV_CH_NW
-#define VV_CH_NW 8
-#endif
-#ifndef VV_CH_WGPC
-#define VV_CH_WGPC 1
-#endif
-constexpr int CH_NW = VV_CH_NW;
+// waves per workgroup and workgroups per CU: one 8-wave workgroup per CU (two
+// 4-wave workgroups per CU measured slower, DESIGN.md "Persistent chains")
+constexpr int CH_NW = 8, CH_WGPC = 1;
 
 // global (address_space 1) loads: a flat load also counts in lgkmcnt, so every
 // LDS wait would wait for the weight stream in flight
@@ -523,17 +517,14 @@ size_t chain_plan_op(ChainOp* op, int G, int mode) {
 }
 
 int chain_grid() {
-  static int g = 0;
-  if (!g) {
-    int dev = 0;
-    hipDeviceProp_t p;
-    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return 0;
-    g = p.multiProcessorCount * VV_CH_WGPC;
-  }
-  return g;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  return cus * CH_WGPC;
 }
 
-static int g_chain_u = 8;   // weight chunks per wave per batch (diagnostic hook vv_chain_tune_u)
+static std::atomic<int> g_chain_u{8};   // weight chunks per wave per batch (diagnostic hook vv_chain_tune_u)
 extern "C" int vv_chain_tune_u(int u) {
   g_chain_u = u == 4 ? 4 : 8;
   return 0;
@@ -542,15 +533,12 @@ extern "C" int vv_chain_tune_u(int u) {
 int launch_chain(const ChainArgs& A, size_t lds, hipStream_t st) {
   constexpr size_t LDS_MAX = 151552;
   if (lds > LDS_MAX) return 1;
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute((const void*)k_chain<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX) !=
-            hipSuccess ||
-        hipFuncSetAttribute((const void*)k_chain<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX) !=
-            hipSuccess)
-      return 2;
-    attr = true;
-  }
+  static const bool attr =   // once (thread-safe static init)
+      hipFuncSetAttribute((const void*)k_chain<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX) ==
+          hipSuccess &&
+      hipFuncSetAttribute((const void*)k_chain<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX) ==
+          hipSuccess;
+  if (!attr) return 2;
   const int G = chain_grid();
   if (G <= 0) return 2;
   if (g_chain_u == 4) hipLaunchKernelGGL(k_chain<4>, dim3(G), dim3(64 * CH_NW), lds, st, A);

@@ -16,7 +16,7 @@
 #include <unordered_map>
 #include <vector>
 
-#include "../../include/vibevoice_hip.h"
+#include "../../include/vibevoice_hip_diag.h"
 #include "kernels.h"
 
 static thread_local std::string g_err;
@@ -113,7 +113,7 @@ struct ConvNet {
 }  // namespace
 
 // diagnostic: attention launches record per-workgroup timestamps (nullptr: off)
-static unsigned long long* g_attn_stamps = nullptr;
+static std::atomic<unsigned long long*> g_attn_stamps{nullptr};
 extern "C" int vv_attn_stamps(void* buf) {
   g_attn_stamps = (unsigned long long*)buf;
   return 0;
@@ -223,7 +223,7 @@ static int rmsnorm(int M, int C, RowMap in, RowMap out, const bf16* w, float eps
 // test switch (vv_norm_pack): 1 = the normalised rows feeding a 256 x 256-tile
 // GEMM are written MFMA-fragment-packed (16K-token gate|up 1055 -> 948 us, q|k|v
 // 98 -> 92: one contiguous 1 KB load per A block instead of 16 row pieces)
-static int g_norm_pack = 1;
+static std::atomic<int> g_norm_pack{1};
 extern "C" int vv_norm_pack(int on) {
   g_norm_pack = on;
   return 0;
@@ -418,7 +418,7 @@ static RowMap buf_in_rows(const ConvBuf& b, int T, const int* slots) {
 
 // Codec Block1D front half folded into fc1's prologue where it fits (XF_MIX);
 // off only for the bit-exactness test against the k_mix path.
-static int g_mix_fusion = 3;   // bit 0: XF_MIX, bit 1: k_block
+static std::atomic<int> g_mix_fusion{3};   // bit 0: XF_MIX, bit 1: k_block
 extern "C" int vv_codec_mix_fusion(int mask) {
   g_mix_fusion = mask & 3;
   return 0;
@@ -825,7 +825,7 @@ int vv_embed(vv_ctx* c, int n, const int* ids, void* out, vv_stream vst) {
 
 // ------------------------------------------------------------------ LM pass
 // test switch (vv_rope_table): 0 = the q|k|v epilogue computes cos / sin inline
-static int g_rope_tab = 1;
+static std::atomic<int> g_rope_tab{1};
 extern "C" int vv_rope_table(int on) {
   g_rope_tab = on;
   return 0;
@@ -840,7 +840,7 @@ extern "C" int vv_rope_table(int on) {
 // Rows: B = 1 (2 rows) gains 1.5 % at K = 750; at B = 8 (16 rows) o_proj's
 // staging of 16 rows' partials cost more than the splits saved (5.79 vs 5.67 ms),
 // so by default only <= 4 rows defer.
-static int g_attn_defer = 4, g_defer_chunk = 128;
+static std::atomic<int> g_attn_defer{4}, g_defer_chunk{128};
 extern "C" int vv_attn_defer(int on, int chunk) {
   if (chunk % 32 || chunk < 32 || on < 0) return 1;
   g_attn_defer = on == 1 ? 4 : on;   // 1: the default row limit; n >= 2: up to n rows (<= 16)
@@ -998,7 +998,7 @@ static int lm_mlp_half(vv_ctx* c, LmPass& P, int l, hipStream_t st) {
 
 // Benchmarks only (bench.py --tp: the collective's share of an LM pass):
 // skip the all-reduces of a communicator engine — the outputs are then wrong.
-static int g_tp_null = 0;
+static std::atomic<int> g_tp_null{0};
 extern "C" int vv_tp_null_collective(int on) {
   g_tp_null = on ? 1 : 0;
   return 0;
@@ -1094,8 +1094,8 @@ int vv_tp_init(vv_ctx* c, int rank, int size, const void* unique_id) {
 // in-launch hand-off is 0.5-1.2 us, but each op's span keeps its dependent
 // memory round trips (A rows, residual, write-through drain, arrival), so a
 // 100-op head chain takes 1.05 ms against 0.87 ms of per-op launches.
-static int g_chain = 0;
-static unsigned long long* g_chain_stamps = nullptr;
+static std::atomic<int> g_chain{0};
+static std::atomic<unsigned long long*> g_chain_stamps{nullptr};
 extern "C" int vv_chain_stamps(void* buf) {
   g_chain_stamps = (unsigned long long*)buf;
   return 0;
@@ -1484,7 +1484,7 @@ int vv_scatter_rows(vv_ctx* c, int n, int C, const void* src, int64_t lds, const
 }
 
 // diagnostic (vv_gemm_tune_apack): vv_gemm_bf16's A is MFMA-fragment packed (k_gemm_xl only)
-static int g_gemm_apack = 0;
+static std::atomic<int> g_gemm_apack{0};
 extern "C" int vv_gemm_tune_apack(int on) {
   g_gemm_apack = on;
   return 0;

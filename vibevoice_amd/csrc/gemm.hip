@@ -33,18 +33,13 @@
 //            release / ticket / acquire, Guideline 16) only for few-tile shapes.
 //   k_gemm : M > 64 (codec stages at T >= 8, LM prefill).  64 x BN workgroup
 //            tile, 4 waves of 32 x BN/2, operands straight from L2.
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <type_traits>
 
 #include "kernels.h"
 #include "gemv_dev.h"
-
-// VV_EPI_PREFETCH=1 loads the epilogue's bias / residual / scale at kernel start:
-// measured +2.7 % B=1 step time (3.67 -> 3.77 ms, 3 interleaved same-box pairs), so off
-#ifndef VV_EPI_PREFETCH
-#define VV_EPI_PREFETCH 0
-#endif
 
 // Diagnostic timestamps (tools/gemv_stamps.py): 100 MHz real-time clock, one
 // lane per workgroup, to a buffer nothing else reads (a.stamps == nullptr in
@@ -109,31 +104,16 @@ DEV bool splitk_handoff(const GemmArgs& a, float* red, int TILE, unsigned* last_
 // M <= 16: the workgroup's A rows (its K range, transformed) are staged once in
 // LDS; each wave streams its weight chunks with a two-deep register ping-pong
 // (U chunks = U KB per wave in flight while the previous U are multiplied).
-// VV_G1_PRE2: both halves of the ping-pong (2U chunks) are issued before the A
-// prologue, so twice the weight bytes are in flight while the A rows arrive and
-// are normalised.  VV_G1_QW: A items per thread of the single-round-trip
-// ("fast") prologue of the multi-tile (TPW > 1, M >= 8) form.
-#ifndef VV_G1_PRE2
-#define VV_G1_PRE2 0
-#endif
-#ifndef VV_G1_QW
-#define VV_G1_QW 4
-#endif
-// VV_G1_PSTAMP (diagnostic builds): the 4 per-workgroup stamps time the A
-// prologue instead (start, A rows in registers / LDS, row norms done, staged)
-#ifndef VV_G1_PSTAMP
-#define VV_G1_PSTAMP 0
-#endif
-// VV_G1_RW: the fused RMSNorm prologue with whole rows per wave.  Wave w loads
-// rows w*RPW .. w*RPW+RPW-1 (lane l: 8-column items l, l+64, ...), so a row's
-// sum of squares is one in-register accumulation + wave_sum and the norm is
-// applied before the A rows ever reach LDS: one barrier instead of three and no
-// LDS round trip of partial sums.  Each row's summation order is the one the
+// RW instantiations: the fused RMSNorm prologue with whole rows per wave.  Wave
+// w loads rows w*RPW .. w*RPW+RPW-1 (lane l: 8-column items l, l+64, ...), so a
+// row's sum of squares is one in-register accumulation + wave_sum and the norm
+// is applied before the A rows ever reach LDS: one barrier instead of three and
+// no LDS round trip of partial sums.  Each row's summation order is the one the
 // item-per-thread form used (per-item partials when that form was "fast", one
 // running sum otherwise = k_rmsnorm's), so both forms are bit-identical.
-#ifndef VV_G1_RW
-#define VV_G1_RW 1
-#endif
+// (Rejected variants -- weights issued twice as deep before the prologue, a
+// one-round-trip M = 16 prologue, epilogue operands prefetched at kernel start --
+// are recorded with their measurements in DESIGN.md and no longer built.)
 template <int U, int XF, bool KEEP = false, int TPW = 1, int RW = 0>
 __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -163,11 +143,6 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   // prologue loads read tile 0)
   const bf16* wrow = a.w + (long long)(tile_ok ? tile : 0) * a.K * 16 + lane * 8;
   const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-  // the epilogue's bias / residual / scale, loaded now: a round trip after the
-  // weight stream was the tail of every residual GEMV (VV_EPI_PREFETCH=0 builds the old form)
-  EpiPre pre;
-  const int etile = blockIdx.x * TPW + wave;
-  if (VV_EPI_PREFETCH && wave < TPW && etile < ntile) pre = epi_prefetch(a, r, etile * 16, lane);
 
   // ---- A staging into LDS (rows [0, M) x chunks [b0, b1), row stride padded
   // 16 B), overlapped with the first weight chunks.  vmcnt waits are in issue
@@ -180,7 +155,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   bf16* xs = (bf16*)smem;
   float* part = (float*)(smem + (((size_t)a.M * lds_ld * 2 + 15) & ~(size_t)15));
   bf16x8 wa[U], wb[U];
-  constexpr int Q = TPW > 1 ? VV_G1_QW : 4;   // A items per thread on the fast path
+  constexpr int Q = 4;   // A items per thread on the fast path
   const bool fast = a.M * n8 <= Q * (int)blockDim.x;
   // row-per-wave norm prologue: items per lane per row (IPR) x rows per wave (RPW)
   // (RW instantiations only; the host picks them for eligible shapes, gemv1_rw)
@@ -214,10 +189,6 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
-    if (VV_G1_PRE2) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) wb[u] = ldw<KEEP>(wrow + min(c0 + U + u, max(c1 - 1, 0)) * 512);
-    }
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
       float ss = 0.f;
@@ -282,13 +253,9 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
-    if (VV_G1_PRE2) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) wb[u] = ldw<KEEP>(wrow + min(c0 + U + u, max(c1 - 1, 0)) * 512);
-    }
     if (wave < a.M) {
       // the DMA is older than 3 * IPR operand loads and the weight loads
-      constexpr int after = 3 * IPR + U * (VV_G1_PRE2 ? 2 : 1);
+      constexpr int after = 3 * IPR + U;
       __builtin_amdgcn_s_waitcnt((after & 15) | ((after >> 4) << 14) | (7 << 4) | (15 << 8));
       bf16x8 xv[IPR];
 #pragma unroll
@@ -325,12 +292,10 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   if constexpr (RW == 2) {   // its own instantiation: its registers would cost the others occupancy
     stage_rw_dma();
   } else if constexpr (RW == 1) {
-    if (VV_G1_PSTAMP) stamp(a, 1);
     using I = std::true_type;
     if (rw == 31) stage_rw(std::integral_constant<int, 3>(), std::integral_constant<int, 1>(), I());
     else if (rw == 32) stage_rw(std::integral_constant<int, 3>(), std::integral_constant<int, 2>(), I());
     else stage_rw(std::integral_constant<int, 7>(), std::integral_constant<int, 1>(), std::false_type());
-    if (VV_G1_PSTAMP) stamp(a, 2);
   } else if (XF == XF_ATTN_MERGE) {
     // o_proj's A rows = the decode attention output, merged from the key splits'
     // partials k_attn left (AttnArgs::defer): out = sum_s e^{m_s - M} o_s /
@@ -386,10 +351,6 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
-    if (VV_G1_PRE2) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) wb[u] = ldw<KEEP>(wrow + min(c0 + U + u, max(c1 - 1, 0)) * 512);
-    }
   } else if (XF == XF_MIX) {
     // Codec Block1D front half for the M = ns * T rows (k_mix's math and
     // summation order, elementwise.hip): every workgroup recomputes it (a few
@@ -433,10 +394,6 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
       if (first) {
 #pragma unroll
         for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
-        if (VV_G1_PRE2) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) wb[u] = ldw<KEEP>(wrow + min(c0 + U + u, max(c1 - 1, 0)) * 512);
-        }
       }
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -545,10 +502,6 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
-    if (VV_G1_PRE2) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) wb[u] = ldw<KEEP>(wrow + min(c0 + U + u, max(c1 - 1, 0)) * 512);
-    }
     if (XF == XF_NORM) {
       // per-item sums of squares -> LDS, rows reduced in a fixed order
 #pragma unroll
@@ -561,7 +514,6 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
           part[e] = ss;
         }
       }
-      if (VV_G1_PSTAMP) stamp(a, 1);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (a.ksplit == 1) {
         for (int m = wave; m < a.M; m += NW) {
@@ -574,7 +526,6 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
         row_inv(a, 0, a.M, inv_s, wave, NW, lane);
       }
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if (VV_G1_PSTAMP) stamp(a, 2);
     }
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
@@ -602,10 +553,6 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     // many rows (B >= 8 batches): weights first, then the A rows in batches
 #pragma unroll
     for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
-    if (VV_G1_PRE2) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) wb[u] = ldw<KEEP>(wrow + min(c0 + U + u, max(c1 - 1, 0)) * 512);
-    }
     for (int e0 = threadIdx.x; e0 < a.M * n8; e0 += 4 * blockDim.x) {
       bf16x8 xv[4];
 #pragma unroll
@@ -626,7 +573,6 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
       }
     }
     if (XF != XF_NONE) {
-      if (VV_G1_PSTAMP) stamp(a, 1);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (XF == XF_NORM) {
         if (a.ksplit == 1) {
@@ -644,8 +590,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
           row_inv(a, 0, a.M, inv_s, wave, NW, lane);
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if (VV_G1_PSTAMP) stamp(a, 2);
-      }
+        }
       for (int e = threadIdx.x; e < a.M * n8; e += blockDim.x) {
         const int m = e / n8, k8 = (e - m * n8) * 8;
         bf16x8* px = (bf16x8*)(xs + m * lds_ld + k8);
@@ -654,7 +599,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  stamp(a, VV_G1_PSTAMP ? 3 : 1);
+  stamp(a, 1);
 
   f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
   // A fragment reads are unconditional (a guarded LDS read compiled to an
@@ -676,22 +621,13 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
 #pragma unroll
     for (int u = 0; u < U; ++u) wf[u] = ldw<KEEP>(wrow + min(c + u, max(c1 - 1, 0)) * 512);
   };
-  if (VV_G1_PRE2) {   // wb(c0 + U) is already in flight: the same ping-pong, loads after the computes
-    for (int c = c0; c < c1; c += 2 * U) {
-      compute(wa, c);
-      load(wa, c + 2 * U);
-      compute(wb, c + U);
-      load(wb, c + 3 * U);
-    }
-  } else {
-    for (int c = c0; c < c1; c += 2 * U) {
-      load(wb, c + U);
-      compute(wa, c);
-      load(wa, c + 2 * U);
-      compute(wb, c + U);
-    }
+  for (int c = c0; c < c1; c += 2 * U) {
+    load(wb, c + U);
+    compute(wa, c);
+    load(wa, c + 2 * U);
+    compute(wb, c + U);
   }
-  if (!VV_G1_PSTAMP) stamp(a, 2);
+  stamp(a, 2);
 
   // ---- reduce each tile's K-slice waves (tile t's sum lands in slab t * KW)
 #pragma unroll
@@ -711,8 +647,8 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     float v[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = red[wave * KW * 256 + i * 64 + lane];
-    epi_tile(a, r, (blockIdx.x * TPW + wave) * 16, lane, v, VV_EPI_PREFETCH ? &pre : nullptr);
-    if (a.stamps && !VV_G1_PSTAMP) {
+    epi_tile(a, r, (blockIdx.x * TPW + wave) * 16, lane, v);
+    if (a.stamps) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       stamp(a, 3);
     }
@@ -902,7 +838,7 @@ static void launch_gemvw_t(const GemmArgs& a, hipStream_t st) {
   else hipLaunchKernelGGL((k_gemvw<MREP, TPW, false>), grid, dim3(512), 0, st, a);
 }
 
-static int g_gemvw = 1;   // diagnostic: 0 = k_gemv for every 16 < M <= 64 (vv_gemv_tune_wide)
+static std::atomic<int> g_gemvw{1};   // diagnostic: 0 = k_gemv for every 16 < M <= 64 (vv_gemv_tune_wide)
 extern "C" int vv_gemv_tune_wide(int on) {
   g_gemvw = on;
   return 0;
@@ -1107,13 +1043,13 @@ __global__ void __launch_bounds__(256) k_gemm_big(GemmArgs a) {
 }
 
 // ------------------------------------------------------------------ host launch
-static int g_tune_nw = 0, g_tune_ks = 0, g_tune_handoff = -1, g_tune_waves = 0, g_tune_u = 0, g_tune_tpw = 0;
-static int g_gemv_max_m = 64;   // more rows than this: the tiled k_gemm (vv_gemv_tune_maxm)
+static std::atomic<int> g_tune_nw{0}, g_tune_ks{0}, g_tune_handoff{-1}, g_tune_waves{0}, g_tune_u{0}, g_tune_tpw{0};
+static std::atomic<int> g_gemv_max_m{64};   // more rows than this: the tiled k_gemm (vv_gemv_tune_maxm)
 extern "C" int vv_gemv_tune_maxm(int m) {
   g_gemv_max_m = m > 0 ? m : 64;
   return 0;
 }
-static unsigned long long* g_stamps = nullptr;
+static std::atomic<unsigned long long*> g_stamps{nullptr};
 static const bool g_shape_log = getenv("VV_GEMM_LOG") != nullptr;
 
 // diagnostic: GEMV launches record per-workgroup timestamps into buf (nullptr: off)
@@ -1165,19 +1101,22 @@ struct GemmPlan { int nw, ksplit, u, tpw; };
 // for same-box A/Bs of a single shape inside the loop (tools/ab_bench.py)
 struct ShapeTune { int N, K, mmax, nw, ks, u, tpw; };
 static ShapeTune g_shape_tune[8];
-static int g_nshape_tune = 0;
+static std::atomic<int> g_nshape_tune{0};
 extern "C" int vv_gemv_tune_shape(int N, int K, int mmax, int nw, int ks, int u, int tpw) {
   if (N <= 0) {
     g_nshape_tune = 0;
     return 0;
   }
-  if (g_nshape_tune >= 8) return 1;
-  g_shape_tune[g_nshape_tune++] = {N, K, mmax, nw, ks, u, tpw};
+  const int n = g_nshape_tune;
+  if (n >= 8) return 1;
+  g_shape_tune[n] = {N, K, mmax, nw, ks, u, tpw};
+  g_nshape_tune = n + 1;   // published after the entry (seq_cst store)
   return 0;
 }
 
 static GemmPlan gemv_plan(int N, int K, int M) {
-  for (int i = 0; i < g_nshape_tune; ++i) {
+  const int ntune = g_nshape_tune;
+  for (int i = 0; i < ntune; ++i) {
     const ShapeTune& s = g_shape_tune[i];
     if (s.N == N && s.K == K && M <= s.mmax) return {s.nw, s.ks, s.u, s.tpw};
   }
@@ -1264,7 +1203,7 @@ static int max_waves(int) { return 8; }
 // per-wave fragment loads -- measured slower (B = 8 step 5.51 -> 5.83 ms: one
 // workgroup per CU leaves too few weight loads in flight), so it stays a hook.
 constexpr size_t GEMV1_LDS_MAX = 151552, GEMV1_LDS_DEFAULT = 65536;
-static size_t g_gemv1_lds_max = GEMV1_LDS_DEFAULT;   // diagnostic (vv_gemv_tune_lds)
+static std::atomic<size_t> g_gemv1_lds_max{GEMV1_LDS_DEFAULT};   // diagnostic (vv_gemv_tune_lds)
 extern "C" int vv_gemv_tune_lds(int bytes) {
   g_gemv1_lds_max = bytes > 0 && (size_t)bytes <= GEMV1_LDS_MAX ? (size_t)bytes : GEMV1_LDS_DEFAULT;
   return 0;
@@ -1300,15 +1239,15 @@ static void go_gemv1(const GemmArgs& a, dim3 grid, dim3 block, size_t lds, hipSt
 // Diagnostic: vv_gemv_tune_rw(min rows; 99 = off).
 // The K = 3,584 adaLN rows (VibeVoice-Large head) take the LDS-DMA form (RW 2).
 // Diagnostic: vv_gemv_tune_rw(min rows; 99 = off; -1 = built-in without RW 2).
-static int g_rw_min_m = 1;
-static bool g_rw_dma = true;
+static std::atomic<int> g_rw_min_m{1};
+static std::atomic<bool> g_rw_dma{true};
 extern "C" int vv_gemv_tune_rw(int min_m) {
   g_rw_min_m = min_m > 0 ? min_m : 1;
   g_rw_dma = min_m >= 0;
   return 0;
 }
 static int gemv1_rw(const GemmArgs& a, int nw) {
-  if (!VV_G1_RW || a.xf.kind != XF_NORM || a.ksplit != 1 || a.M < g_rw_min_m || a.K % 512) return 0;
+  if (a.xf.kind != XF_NORM || a.ksplit != 1 || a.M < g_rw_min_m || a.K % 512) return 0;
   const int ipr = a.K / 512, rpw = (a.M + nw - 1) / nw;
   if (ipr == 3 && rpw <= 2) return 1;
   if (ipr == 7 && rpw == 1) return !a.xf.mod ? 1 : g_rw_dma ? 2 : 0;
@@ -1376,34 +1315,16 @@ static void launch_gemv_xf(const GemmArgs& a, int mrep, int u, dim3 grid, dim3 b
 //     instruction, lane-linear) and A rows are gathered per lane into the same
 //     order, so every ds_read_b128 is lane-linear and conflict-free (no swizzle);
 //   * one __shared__ array (a second LDS object makes hipcc drain vmcnt(0) before
-//     every k-step, §5 item 4a); s_setprio(1) around the MFMA cluster (T5).
+//     every k-step, §5 item 4a); loads hand-interleaved between the MFMAs.
 // K order of accumulation per output is k_gemm's (chunk by chunk): bit-identical.
-#ifndef VV_GX_INTERLEAVE
-#define VV_GX_INTERLEAVE 2
-#endif
 // s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] |
 // vmcnt[5:4] << 14; a field at its maximum does not wait).  The builtin, unlike an
 // asm wait, is seen by hipcc's waitcnt pass, which then does not re-wait (with
 // lgkmcnt(0)) for fragments this wait already retired
 constexpr unsigned WC_VM12 = 0x0F7C, WC_VM8_LGKM0 = 0x0078, WC_LGKM0 = 0xC07F, WC_VM0 = 0x0F70;
-#ifndef VV_GX_ABL
-#define VV_GX_ABL 0
-#endif
-// VV_GX_M32: the wave's 128 x 64 tile on v_mfma_f32_32x32x16_bf16 (8 accumulators
-// of 32 x 32, 16 MFMAs per 32-deep stage) instead of 16x16x32 (32 accumulators of
-// 16 x 16, 32 MFMAs).  Same LDS images: a 32 x 16 operand fragment of lane l
-// (row l & 31, k 8 (l >> 5) .. +7 of a 16-deep half) is 16 contiguous bytes of the
-// 16-row block that holds row l & 31, so every read stays one lane-linear
-// ds_read_b128 per 16 lanes.  Fragment bytes read per stage are the same (the
-// wave tile sets them); the MFMA count halves.  K order differs from k_gemm
-// (two K = 16 halves per chunk): equal to torch fp32 within rounding, not bitwise.
-#ifndef VV_GX_M32
-#define VV_GX_M32 0
-#endif
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-DEV f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
+// (Measured and rejected, DESIGN.md "Prefill": the wave tile on
+// v_mfma_f32_32x32x16_bf16 -- 0.305 vs 0.443 of peak on gate|up -- and the
+// ablation builds that located the ceiling; neither is built any more.)
 constexpr int GX_M = 256, GX_N = 256, GX_NS = 4;
 constexpr int GX_STAGE = 32 * 512;                       // elements per stage
 constexpr size_t GX_LDS = (size_t)GX_NS * GX_STAGE * 2;   // 128 KB
@@ -1438,13 +1359,7 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
     wsrc[i] = a.w + (long long)(tn * 16 + j) * nch * 512 + lane * 8;
   }
   auto issue = [&](int s) {
-#if VV_GX_ABL == 1
-    return;   // ablation (timing only): no global -> LDS staging
-#endif
     bf16* st = smx + (s & (GX_NS - 1)) * GX_STAGE;
-#if VV_GX_ABL == 3
-    s = 0;    // ablation (timing only): every stage re-loads stage 0 (L2-resident) -- issue cost without misses
-#endif
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int j = 2 * wave + i;
@@ -1456,13 +1371,7 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
   };
   // one of a stage's 4 glds pieces per wave (q: block i = q >> 1, A (even) or W (odd))
   auto issue_piece = [&](int s, int q) {
-#if VV_GX_ABL == 1
-    return;
-#endif
     bf16* st = smx + (s & (GX_NS - 1)) * GX_STAGE;
-#if VV_GX_ABL == 3
-    s = 0;
-#endif
     const int i = q >> 1, j = 2 * wave + i;
     if (q & 1)
       __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + (long long)s * 512),
@@ -1471,80 +1380,31 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
       __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + (a.apack ? (long long)s * 512 : (long long)s * 32)),
                                        (__attribute__((address_space(3))) void*)(st + j * 512), 16, 0, 0);
   };
-#if VV_GX_M32
-  f32x16 acc2[2][4];   // [32-row weight tile][32-row row tile]
-#pragma unroll
-  for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc2[nt][mt][i] = 0.f;
-  // fragment f of a stage: W (f < 4): weight tile f >> 1, k-half f & 1; A (f >= 4):
-  // row tile (f - 4) >> 1, k-half (f - 4) & 1.  Lane offset inside the 16-row block
-  // of row l & 31: ((2 kk + (l >> 5)) * 16 + (l & 15)) * 8 elements.
-  const int off32 = ((lane >> 5) * 16 + (lane & 15)) * 8 + ((lane >> 4) & 1) * 512;
-  auto frag32 = [&](const bf16* st, int f) -> bf16x8 {
-    const int blk = f < 4 ? 16 + wc * 4 + 2 * (f >> 1) : wr * 8 + 2 * ((f - 4) >> 1);
-    const int kk = f < 4 ? (f & 1) : ((f - 4) & 1);
-    return *(const bf16x8*)(st + blk * 512 + kk * 256 + off32);
-  };
-#else
   f32x4 acc[4][8];   // [weight tile nt][row tile mt]
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) acc[nt][mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#endif
   // fragments of stage s are read into registers during step s - 1 (two register
   // sets), so each wave's LDS reads of the next stage overlap its MFMAs
   auto frags = [&](int s, bf16x8 (&wf)[4], bf16x8 (&xf)[8]) {
-#if VV_GX_ABL == 2
-    return;   // ablation (timing only): no LDS fragment reads
-#endif
     const bf16* st = smx + (s & (GX_NS - 1)) * GX_STAGE;
-#if VV_GX_M32
-#pragma unroll
-    for (int f = 0; f < 4; ++f) wf[f] = frag32(st, f);
-#pragma unroll
-    for (int f = 0; f < 8; ++f) xf[f] = frag32(st, 4 + f);
-#else
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) wf[nt] = *(const bf16x8*)(st + (16 + wc * 4 + nt) * 512 + lane * 8);
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) xf[mt] = *(const bf16x8*)(st + (wr * 8 + mt) * 512 + lane * 8);
-#endif
   };
   auto macs = [&](const bf16x8 (&wf)[4], const bf16x8 (&xf)[8]) {
-#if !VV_GX_INTERLEAVE
-    __builtin_amdgcn_s_setprio(1);
-#endif
-#if VV_GX_M32
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) acc2[nt][mt] = mfma32(wf[2 * nt + kk], xf[2 * mt + kk], acc2[nt][mt]);
-#else
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
       for (int mt = 0; mt < 8; ++mt) acc[nt][mt] = mfma(wf[nt], xf[mt], acc[nt][mt]);
-#endif
-#if VV_GX_INTERLEAVE
-    // the step's 4 glds and 12 ds_reads (of the next stage) spread between its 32
-    // MFMAs, so their issue cost hides under the matrix pipe: 4 groups of 1 glds,
-    // 3 ds_reads, 8 MFMAs.  (s_setprio is a scheduling boundary: with it around the
-    // MFMAs every load issued ahead of them, the pipe idle meanwhile.)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // VMEM read (glds)
       __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);   // DS read
       __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);   // MFMA
     }
-#else
-    __builtin_amdgcn_s_setprio(0);
-#endif
     // keep the MFMAs above the next step's asm waits ("memory" does not order
     // register-only instructions, cdna_hip_programming.md §5.7 rule 18)
     __builtin_amdgcn_sched_barrier(0);
@@ -1563,12 +1423,13 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
   bf16x8 wa[4], xa[8], wb[4], xb[8];
   frags(0, wa, xa);
   int s = 0;
-#if VV_GX_INTERLEAVE == 2
   // A step in 4 pinned groups (sched_barrier fences): 1 glds piece of stage
   // s + 4, 3 fragment reads of stage s + 1, then the 8 MFMAs of weight tile nt = q
   // on stage s -- the loads' issue cost (M0 set-up, ~60+ cycles per LDS-DMA
   // piece) sits between MFMAs instead of in front of all 32 with the matrix pipe
-  // idle.  Hand-placed: sched_group_barrier did not move the glds.
+  // idle.  Hand-placed: sched_group_barrier did not move the glds, and
+  // s_setprio is a scheduling boundary (with it around the MFMAs every load
+  // issued ahead of all 32).
   auto step = [&](int sis, int srd, const bf16x8 (&wf)[4], const bf16x8 (&xf)[8], bf16x8 (&wn)[4],
                   bf16x8 (&xn)[8]) {
     const bf16* st = smx + (srd & (GX_NS - 1)) * GX_STAGE;
@@ -1577,26 +1438,11 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
       issue_piece(sis, q);
 #pragma unroll
       for (int f = 3 * q; f < 3 * q + 3; ++f) {
-#if VV_GX_ABL != 2
-#if VV_GX_M32
-        if (f < 4) wn[f] = frag32(st, f);
-        else xn[f - 4] = frag32(st, f);
-#else
         if (f < 4) wn[f] = *(const bf16x8*)(st + (16 + wc * 4 + f) * 512 + lane * 8);
         else xn[f - 4] = *(const bf16x8*)(st + (wr * 8 + f - 4) * 512 + lane * 8);
-#endif
-#endif
       }
-#if VV_GX_M32
-      {   // group q: k-half q >> 1, weight tile q & 1, the 4 row tiles
-        const int kk = q >> 1, nt = q & 1;
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) acc2[nt][mt] = mfma32(wf[2 * nt + kk], xf[2 * mt + kk], acc2[nt][mt]);
-      }
-#else
 #pragma unroll
       for (int mt = 0; mt < 8; ++mt) acc[q][mt] = mfma(wf[q], xf[mt], acc[q][mt]);
-#endif
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -1608,22 +1454,6 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
     __builtin_amdgcn_s_barrier();
     step(min(s + 5, last), min(s + 2, last), wb, xb, wa, xa);
   }
-#else
-  for (; s + 1 < nch; s += 2) {
-    // ---- step s: compute stage s (set a), read stage s + 1 (set b)
-    __builtin_amdgcn_s_waitcnt(WC_VM8_LGKM0);
-    __builtin_amdgcn_s_barrier();   // every wave: stage s + 1 landed, stage s read (its buffer is free)
-    issue(min(s + 4, last));
-    frags(s + 1, wb, xb);
-    macs(wa, xa);
-    // ---- step s + 1: compute stage s + 1 (set b), read stage s + 2 (set a)
-    __builtin_amdgcn_s_waitcnt(WC_VM8_LGKM0);
-    __builtin_amdgcn_s_barrier();
-    issue(min(s + 5, last));
-    frags(min(s + 2, last), wa, xa);
-    macs(wb, xb);
-  }
-#endif
   if (s < nch) {   // odd stage count: the last stage is in set a
     __builtin_amdgcn_s_waitcnt(WC_LGKM0);
     macs(wa, xa);
@@ -1639,25 +1469,11 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
   // region as [64 rows][64 cols] f32, odd rows' float4 slots XOR-shifted by one
   auto stage_ep = [&](float* ep, int p) {
     auto sw = [](int row, int col) { return row * 64 + (col ^ ((row & 1) << 2)); };
-#if VV_GX_M32
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4) {
-          const f32x16& c = acc2[nt][2 * p + mt];
-          *(f32x4*)(ep + sw(mt * 32 + (lane & 31), nt * 32 + 8 * q4 + 4 * (lane >> 5))) =
-              (f32x4){c[4 * q4], c[4 * q4 + 1], c[4 * q4 + 2], c[4 * q4 + 3]};
-        }
-#else
 #pragma unroll
     for (int mq = 0; mq < 4; ++mq)
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) *(f32x4*)(ep + sw(mq * 16 + r, nt * 16 + 4 * g)) = acc[nt][4 * p + mq];
-#endif
   };
-#if VV_GX_ABL != 4
   if (rope_row8_ok(a)) {
     // q|k|v + RoPE + KV append in the same row-contiguous staging: a q / k lane
     // takes one row's 16-column tile (its two RoPE halves), a V lane one column
@@ -1730,26 +1546,6 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
     }
     return;
   }
-#endif
-#if VV_GX_M32
-  {   // any other epilogue: 16 x 16 tiles read back from the staged pass
-    float* ep = (float*)smx + wave * (64 * 64);
-    auto sw = [](int row, int col) { return row * 64 + (col ^ ((row & 1) << 2)); };
-    const int mb = tm * GX_M + wr * 128, nb = tn * GX_N + wc * 64;
-#pragma unroll 1
-    for (int p = 0; p < 2; ++p) {
-      stage_ep(ep, p);
-#pragma unroll 1
-      for (int t = 0; t < 16; ++t) {
-        const int mq = t & 3, nt = t >> 2;
-        float v[4];
-        *(f32x4*)v = *(const f32x4*)(ep + sw(mq * 16 + r, nt * 16 + 4 * g));
-        epi_tile(a, mb + 64 * p + mq * 16 + r, nb + nt * 16, lane, v);
-      }
-    }
-    return;
-  }
-#else
   float* ep = (float*)smx + wave * (16 * 256);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -1763,19 +1559,15 @@ __global__ void __launch_bounds__(512) k_gemm_xl(GemmArgs a) {
       float v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = ep[t * 256 + j * 64 + lane];
-#if VV_GX_ABL == 4
-      if (v[0] == 12345.f)   // ablation (timing only): no epilogue stores
-#endif
       epi_tile(a, tm * GX_M + (wr * 8 + (i & 7)) * 16 + r, tn * GX_N + (wc * 4 + (i >> 3)) * 16, lane, v);
     }
   }
-#endif
 }
 
 // diagnostic (vv_gemm_tune_big): 0 keeps every M > 64 GEMM on k_gemm; 1 / 2 LDS
 // stages of the 128² tile (k_gemm_big); 3 (built-in) = the 256² tile (k_gemm_xl)
 // where it applies, else k_gemm_big<2>; + 4 ignores the tile-count thresholds
-static int g_gemm_big = 3, g_gemm_big_any = 0;
+static std::atomic<int> g_gemm_big{3}, g_gemm_big_any{0};
 extern "C" int vv_gemm_tune_big(int mode) {
   g_gemm_big_any = mode >= 0 && (mode & 4) ? 1 : 0;
   g_gemm_big = mode < 0 ? 3 : mode & 3;
@@ -1789,9 +1581,7 @@ bool gemm_uses_xl(const GemmArgs& a) {
          (total_xl >= GEMM_BIG_TILES || g_gemm_big_any);
 }
 
-#ifndef VV_GEMM_BN32
-#define VV_GEMM_BN32 128
-#endif
+constexpr int GEMM_BN32 = 128;   // fewer 64-wide-tile workgroups than this: 32-wide tiles
 template <int XF>
 static int launch_gemm_xf(const GemmArgs& a, hipStream_t st) {
   // k_gemm_big only with >= one 128 x 128 tile per CU or >= 2^30 MACs: the
@@ -1803,13 +1593,9 @@ static int launch_gemm_xf(const GemmArgs& a, hipStream_t st) {
   const int total_xl = ((a.M + GX_M - 1) / GX_M) * (a.N / GX_N);
   if (XF == XF_NONE && g_gemm_big == 3 && a.M >= GEMM_BIG_M && a.N % GX_N == 0 && a.K % 32 == 0 &&
       (total_xl >= GEMM_BIG_TILES || g_gemm_big_any)) {
-    static bool attr = false;
-    if (!attr) {
-      if (hipFuncSetAttribute((const void*)k_gemm_xl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GX_LDS) !=
-          hipSuccess)
-        return 2;
-      attr = true;
-    }
+    static const bool attr = hipFuncSetAttribute((const void*)k_gemm_xl, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)GX_LDS) == hipSuccess;   // once (thread-safe static init)
+    if (!attr) return 2;
     hipLaunchKernelGGL(k_gemm_xl, dim3(total_xl), dim3(512), GX_LDS, st, a);
     return 0;
   }
@@ -1820,10 +1606,10 @@ static int launch_gemm_xf(const GemmArgs& a, hipStream_t st) {
     else hipLaunchKernelGGL(k_gemm_big<2>, dim3(((total + 7) >> 3) * 8), dim3(256), 0, st, a);
     return 0;
   }
-  // 64-wide tiles unless that leaves fewer than VV_GEMM_BN32 workgroups (the
+  // 64-wide tiles unless that leaves fewer than GEMM_BN32 workgroups (the
   // codec's 200-row stage: fc2 N = 256 is 16 workgroups of K = 1,024)
   const int wg64 = ((a.M + 63) / 64) * (a.N / 64);
-  if (a.N % 64 == 0 && wg64 >= VV_GEMM_BN32) {
+  if (a.N % 64 == 0 && wg64 >= GEMM_BN32) {
     dim3 grid((a.M + 63) / 64, a.N / 64);
     hipLaunchKernelGGL((k_gemm<64, XF>), grid, dim3(256), 0, st, a);
   } else if (a.N % 32 == 0) {
@@ -1887,7 +1673,8 @@ static GemmPlan gemv_resolve(GemmArgs& a) {
       if (!g_tune_u) p.u = 4;
     }
   }
-  a.handoff = g_tune_handoff >= 0 ? g_tune_handoff : 1;
+  const int ho = g_tune_handoff;
+  a.handoff = ho >= 0 ? ho : 1;
   a.tpw = 1;
   if (mrep == 1 && a.ksplit == 1 && a.xf.kind != XF_MIX && (p.tpw == 2 || p.tpw == 4 || p.tpw == 8) && p.nw % p.tpw == 0 && gemv1_fits(a))
     a.tpw = p.tpw;
@@ -1953,17 +1740,15 @@ int launch_gemm(GemmArgs a, hipStream_t st) {
       const int mt = (p.tpw == 2 || p.tpw == 4) && p.nw % p.tpw == 0 ? p.tpw : 1;
       a.tpw = mt;
       grid.x = (a.N / 16 + mt - 1) / mt;
-      static bool attr = false;   // > 64 KB of dynamic LDS needs the opt-in (one workgroup may hold 160 KiB)
-      if (!attr) {
-        if (hipFuncSetAttribute((const void*)k_gemv1<4, XF_MIX>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                98304) != hipSuccess ||
-            hipFuncSetAttribute((const void*)k_gemv1<4, XF_MIX, false, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                98304) != hipSuccess ||
-            hipFuncSetAttribute((const void*)k_gemv1<4, XF_MIX, false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                98304) != hipSuccess)
-          return 2;
-        attr = true;
-      }
+      // > 64 KB of dynamic LDS needs the opt-in (one workgroup may hold 160 KiB); once, thread-safe
+      static const bool attr =
+          hipFuncSetAttribute((const void*)k_gemv1<4, XF_MIX>, hipFuncAttributeMaxDynamicSharedMemorySize, 98304) ==
+              hipSuccess &&
+          hipFuncSetAttribute((const void*)k_gemv1<4, XF_MIX, false, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              98304) == hipSuccess &&
+          hipFuncSetAttribute((const void*)k_gemv1<4, XF_MIX, false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              98304) == hipSuccess;
+      if (!attr) return 2;
       if (mt == 4) hipLaunchKernelGGL((k_gemv1<4, XF_MIX, false, 4>), grid, block, lds, st, a);
       else if (mt == 2) hipLaunchKernelGGL((k_gemv1<4, XF_MIX, false, 2>), grid, block, lds, st, a);
       else hipLaunchKernelGGL((k_gemv1<4, XF_MIX>), grid, block, lds, st, a);

@@ -46,18 +46,13 @@ struct MemWT {
 
 // Weight-stream load.  Decode weights are read once per step (GBs against a
 // 256 MB Infinity Cache), so they go out non-temporal (MI355X_MICROARCH.md
-// "nt-weights"); VV_W_NT=0 builds the default-policy variant for A/B runs.
+// "nt-weights"; -2.2 % step time against the default policy).
 // KEEP (GemmArgs::keep): weights re-read soon — the diffusion head's 170 MB per
 // step is read S times per token and stays in the Infinity Cache with the
 // default policy (tools/head_mall.py: -7 % per head step).
-#ifndef VV_W_NT
-#define VV_W_NT 1
-#endif
 template <bool KEEP = false>
 DEV bf16x8 ldw(const bf16* p) {
-#if VV_W_NT
   if (!KEEP) return __builtin_nontemporal_load((const bf16x8*)p);
-#endif
   return *(const bf16x8*)p;
 }
 
@@ -229,28 +224,6 @@ DEV void epi_dpm(const GemmArgs& a, const DpmEpi& P, int n0, int lane, const flo
   MP::st8(P.m1 + off, mo);
 }
 
-// Epilogue operands a GEMV can load at kernel start instead of after its weight
-// stream (one dependent memory round trip less at the tail): bias, the
-// residual row and its per-column / per-row scale (EPI_STORE / GELU / RES / F32).
-struct EpiPre {
-  bf16x4 bias, res, scale;
-};
-template <class MP = MemPlain>
-DEV EpiPre epi_prefetch(const GemmArgs& a, int m, int n0, int lane) {
-  const EpiArgs& e = a.epi;
-  EpiPre p;
-  const bool plain = e.kind == EPI_STORE || e.kind == EPI_GELU || e.kind == EPI_RES || e.kind == EPI_F32;
-  if (!plain || m >= a.M) return p;
-  const int n = n0 + 4 * (lane >> 4);
-  if (e.bias) p.bias = *(const bf16x4*)(e.bias + n);
-  if (e.kind == EPI_RES) {
-    p.res = MP::ld8(rm_bf(e.res, m) + n);
-    if (e.gamma) p.scale = *(const bf16x4*)(e.gamma + n);
-    else if (e.gate.base) p.scale = MP::ld8(rm_bf(e.gate, m) + n);
-  }
-  return p;
-}
-
 // Row-contiguous epilogue forms for tiles staged through LDS (k_gemm_xl): 8
 // consecutive output columns n .. n+7 of row m per lane, so the stores are 16
 // bytes and a wave instruction covers whole 128-byte row segments (epi_tile's
@@ -408,7 +381,7 @@ DEV void rope_v8(const GemmArgs& a, int m0, int n, const float vin[8]) {
 }
 
 template <class MP = MemPlain>
-DEV void epi_tile(const GemmArgs& a, int m, int n0, int lane, const float v_in[4], const EpiPre* pre = nullptr) {
+DEV void epi_tile(const GemmArgs& a, int m, int n0, int lane, const float v_in[4]) {
   const EpiArgs& e = a.epi;
   float v[4];
 #pragma unroll
@@ -439,7 +412,7 @@ DEV void epi_tile(const GemmArgs& a, int m, int n0, int lane, const float v_in[4
   if (m >= a.M) return;
   const int n = n0 + 4 * g;
   if (e.bias) {
-    bf16x4 b = pre ? pre->bias : *(const bf16x4*)(e.bias + n);
+    const bf16x4 b = *(const bf16x4*)(e.bias + n);
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] += bf(b[i]);
   }
@@ -457,16 +430,16 @@ DEV void epi_tile(const GemmArgs& a, int m, int n0, int lane, const float v_in[4
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] = tobf(gelu_f(rb(v[i])));
   } else {  // EPI_RES
-    bf16x4 r = pre ? pre->res : MP::ld8(rm_bf(e.res, m) + n);
+    const bf16x4 r = MP::ld8(rm_bf(e.res, m) + n);
     float s[4] = {1.f, 1.f, 1.f, 1.f};
     bool scaled = false;
     if (e.gamma) {
-      bf16x4 gm = pre ? pre->scale : *(const bf16x4*)(e.gamma + n);
+      const bf16x4 gm = *(const bf16x4*)(e.gamma + n);
 #pragma unroll
       for (int i = 0; i < 4; ++i) s[i] = bf(gm[i]);
       scaled = true;
     } else if (e.gate.base) {
-      bf16x4 gm = pre ? pre->scale : MP::ld8(rm_bf(e.gate, m) + n);
+      const bf16x4 gm = MP::ld8(rm_bf(e.gate, m) + n);
 #pragma unroll
       for (int i = 0; i < 4; ++i) s[i] = bf(gm[i]);
       scaled = true;

@@ -187,11 +187,6 @@ class Engine:
         _lib.check(_lib.lib().vv_kv_copy(self.h, slots.shape[0], _ptr(slots), _ptr(src), _ptr(dst), _stream(stream)),
                    "kv_copy")
 
-    def kv_synthetic(self, slots, p0, p1, seed=0, stream=None):
-        """Benchmarks only: deterministic pseudo-random K/V at positions [p0, p1)."""
-        _lib.check(_lib.lib().vv_kv_synthetic(self.h, slots.shape[0], _ptr(slots), int(p0), int(p1), int(seed) & 0xffffffff,
-                                              _stream(stream)), "kv_synthetic")
-
     def embed(self, ids, out=None, stream=None):
         if out is None:
             out = torch.empty(ids.shape[0], self.hidden, dtype=torch.bfloat16, device=self.device)
