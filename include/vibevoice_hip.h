@@ -156,6 +156,12 @@ int vv_codec_reset_net(vv_ctx* ctx, int net, int n, const int* slots, vv_stream 
  * padded): audio [nv, L] bf16 -> mean_out [nv, ceil(L/hop), latent] bf16. */
 int vv_acoustic_encode(vv_ctx* ctx, int nv, int L, const void* audio, void* mean_out, vv_stream st);
 
+/* Non-streaming semantic encoder (semantic_tokenizer.encode(audio) without a
+ * cache, modular_vibevoice_tokenizer.py:1171-1175; each strided conv right-pads
+ * its input to whole strides, :127-133 / :393-408): audio [nv, L] bf16 ->
+ * mean_out [nv, ceil(L/hop), semantic_dim] bf16; L need not be whole frames. */
+int vv_semantic_encode(vv_ctx* ctx, int nv, int L, const void* audio, void* mean_out, vv_stream st);
+
 /* z = mean + std[v]*noise; feat = (z + bias) * scale   (rows = nv * frames) */
 int vv_vae_features(vv_ctx* ctx, int nv, int frames, const void* mean, const void* stdv, const void* noise,
                     void* feat_out, vv_stream st);

@@ -227,6 +227,32 @@ def g4_g5_codec():
     save("g4_codec.npz", **out)
 
 
+# ------------------------------------------------- G5 semantic encoder (partial frames)
+def g5_semantic():
+    """The semantic tokenizer's own model (VibeVoiceSemanticTokenizerModel,
+    modular_vibevoice_tokenizer.py:1118-1186): non-streaming encode of clips
+    whose length is NOT a multiple of the hop, so every strided conv gets the
+    reference's per-layer extra right padding (:127-133, :393-408); plus a
+    whole-frame clip streamed frame by frame vs its non-streaming encode."""
+    out = {}
+    C = R["cfg"]
+    kw = dict(encoder_n_filters=2, encoder_ratios=[8, 5, 5, 4, 2, 2], encoder_depths="1-1-1-1-1-1-1", vae_dim=16)
+    scfg = C.VibeVoiceSemanticTokenizerConfig(**kw)
+    m = R["tok"].VibeVoiceSemanticTokenizerModel(scfg).eval()
+    randomize(m, seed=5, std=0.2)
+    out.update(sd_arrays(m))
+    hop = int(np.prod(kw["encoder_ratios"]))
+    g = torch.Generator().manual_seed(12)
+    for dt, tag in ((torch.float32, "f32"), (torch.bfloat16, "bf16")):
+        mm = m.to(dt)
+        for L in (hop // 3, 2 * hop + hop // 2 + 3, 3 * hop - 1):   # < 1 frame, 2.5 frames, just short of 3
+            a = (0.3 * torch.randn(2, 1, L, generator=g)).to(dt)
+            with torch.no_grad():
+                out[f"ns_mean_{L}_{tag}"] = f32(mm.encode(a).mean)
+            out[f"ns_audio_{L}_{tag}"] = f32(a)
+    save("g5_semantic.npz", **out)
+
+
 # -------------------------------------------------------------- G6 connectors
 def g6_connector():
     out = {}
@@ -516,6 +542,7 @@ if __name__ == "__main__":
     g1_sde_scheduler()
     g2_g3_head()
     g4_g5_codec()
+    g5_semantic()
     g6_connector()
     g7_qwen2()
     g8_loop()

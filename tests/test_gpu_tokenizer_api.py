@@ -135,3 +135,29 @@ def test_tokenizer_views_on_a_tp_shard():
     a_1 = model.model.acoustic_tokenizer.decode(z)
     assert torch.equal(a_tp, a_1)
     assert torch.equal(sc.encode(a_tp).mean, model.model.semantic_tokenizer.encode(a_1).mean)
+
+
+@pytest.mark.parametrize("L", [1066, 8003, 9599, 9600])
+def test_semantic_encode_partial_frame_nonstreaming(setup, L):
+    """semantic_tokenizer.encode(audio) without a cache for clips ending in a
+    partial frame (modular_vibevoice_tokenizer.py:127-133, 393-408: every
+    strided conv right-pads its input to whole strides): ceil(L / hop) frames,
+    vs the oracle's non-streaming encoder (pinned to the reference's
+    VibeVoiceSemanticTokenizerModel by golden G5) at the real encoder shapes.
+    L = 9600 (whole frames) streams from zero state and must match too."""
+    cfg, sd, model = setup
+    ed = ocodec.codec_dims(cfg.semantic_tokenizer_config, "encoder")
+    sd_s = _sub(sd, "model.semantic_tokenizer.")
+    g = torch.Generator().manual_seed(L)
+    audio = (0.3 * torch.randn(2, 1, L, generator=g)).bfloat16()
+    got = model.model.semantic_tokenizer.encode(audio.to(dev)).mean
+    ref = ocodec.encode(sd_s, ed, audio, None, None, streaming=False)
+    assert got.shape == ref.shape == (2, -(-L // cfg.hop), 128), (got.shape, ref.shape)
+    for i in range(2):
+        e, c = rel_err(got[i], ref[i]), cos(got[i], ref[i])
+        print(f"semantic encode L={L} clip {i}: rel {e:.3e} cos {c:.6f}")
+        assert e < 3e-2 and c > 0.999
+    with pytest.raises(ValueError):
+        from vibevoice.modular.modular_vibevoice_tokenizer import VibeVoiceTokenizerStreamingCache as Cache
+        model.model.semantic_tokenizer.encode(audio[:, :, :L - 1 if L % cfg.hop == 0 else L].to(dev), cache=Cache(),
+                                              sample_indices=torch.arange(2), use_cache=True)

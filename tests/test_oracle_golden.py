@@ -138,6 +138,25 @@ def test_codec_encode(name, tag):
     close(m, t(z, f"{name}/enc_ns_mean_{tag}"), *TOL[tag])
 
 
+G5_CFG = CODEC["hop3200"]   # the same encoder shape, semantic model
+
+
+@pytest.mark.parametrize("L", [1066, 8003, 9599])
+@pytest.mark.parametrize("tag", ["f32", "bf16"])
+def test_semantic_encode_partial_frames(L, tag):
+    """G5: the reference's VibeVoiceSemanticTokenizerModel, non-streaming encode
+    of clips that end in a partial frame (each strided conv right-pads its input
+    to whole strides, modular_vibevoice_tokenizer.py:127-133, 393-408) ->
+    ceil(L / hop) frames; the oracle's non-streaming encoder."""
+    z = load("g5_semantic.npz")
+    sd = weights(z, prefix="w:", dtype=DT[tag])
+    dims = codec.codec_dims(G5_CFG, "encoder")
+    ref = t(z, f"ns_mean_{L}_{tag}")
+    assert ref.shape[1] == -(-L // 3200)
+    m = codec.encode(sd, dims, t(z, f"ns_audio_{L}_{tag}", DT[tag]), None, None, streaming=False)
+    close(m, ref, *TOL[tag])
+
+
 @pytest.mark.parametrize("din", [64, 128])
 @pytest.mark.parametrize("tag", ["f32", "bf16"])
 def test_connector(din, tag):

@@ -53,6 +53,7 @@ EXPORTS = [
     ("vv_codec_encode", I, [P, I, P, P, P, P]),
     ("vv_codec_reset_net", I, [P, I, I, P, P]),
     ("vv_acoustic_encode", I, [P, I, I, P, P, P]),
+    ("vv_semantic_encode", I, [P, I, I, P, P, P]),
     ("vv_vae_features", I, [P, I, I, P, P, P, P, P]),
     ("vv_connector", I, [P, I, I, P, P, P]),
     ("vv_scatter_rows", I, [P, I, I, P, I64, P, P, I64, P]),

@@ -143,6 +143,7 @@ struct vv_ctx {
   DevBuf head_ws;
   // codec
   ConvNet dec, sem, aenc;
+  ConvNet senc;     // the semantic encoder laid out for one non-streaming call (vv_semantic_encode)
   DevBuf codec_ws;  // connectors
   DevBuf slot_scratch;
   DevBuf unit_sb;   // bf16 {1, 0}: identity scaling / bias for vv_codec_decode
@@ -628,7 +629,7 @@ void vv_destroy(vv_ctx* c) {
                     &c->chain_sync, &c->chain_slabs, &c->chain_err, &c->coef_dev, &c->rope_tab};
   for (DevBuf* b : bufs) b->release();
   for (auto& kv : c->head_chain) kv.second.ops.release();
-  ConvNet* nets[] = {&c->dec, &c->sem, &c->aenc};
+  ConvNet* nets[] = {&c->dec, &c->sem, &c->aenc, &c->senc};
   for (ConvNet* n : nets) {
     n->state.release();
     n->work.release();
@@ -1439,15 +1440,16 @@ int vv_codec_reset_net(vv_ctx* c, int net, int n, const int* slots, vv_stream vs
   return 0;
 }
 
-int vv_acoustic_encode(vv_ctx* c, int nv, int L, const void* audio, void* mean_out, vv_stream vst) {
-  hipStream_t st = (hipStream_t)vst;
-  if (!c->w.count("aenc.stem_w")) FAIL("acoustic encoder weights not bound");
-  if (nv <= 0 || L <= 0) return 0;
-  ConvNet& net = c->aenc;
-  // (re)layout for this call: nv slots, T0 = L; per-layer right zero padding of
-  // strided-conv inputs reproduces the non-streaming extra padding (:127-133, :398-403)
-  if (net.slots != nv || net.T0 != L) {
-    convnet_shape(c, net, false, "aenc", c->cfg.ac_enc_n_filters, 1, c->cfg.latent_dim, L, nv);
+// Non-streaming encode of nv clips of L samples (zero-padded to a common L) by
+// one of the σ-VAE encoders, laid out for this call: nv slots, T0 = L.  The
+// per-layer right zero padding of the strided-conv inputs (ConvBuf rows past
+// the input, zeroed per call) is the reference's non-streaming extra padding
+// (modular_vibevoice_tokenizer.py:127-133, :393-408), so a clip that ends in a
+// partial frame gives ceil(L / hop) frames as the reference does.
+static int encode_nonstreaming(vv_ctx* c, ConvNet& net, const char* wp, int nf, int out_ch, int nv, int L,
+                               const void* audio, void* out, hipStream_t st) {
+  if (net.slots != nv || net.T0 != L || net.wp != wp) {
+    convnet_shape(c, net, false, wp, nf, 1, out_ch, L, nv);
     CHK(convnet_alloc(net, 7));
   } else {
     HIPCHK(hipMemsetAsync(net.state.p, 0, net.state.bytes, st));
@@ -1460,10 +1462,23 @@ int vv_acoustic_encode(vv_ctx* c, int nv, int L, const void* audio, void* mean_o
   HIPCHK(hipMemcpy2DAsync(net.stem.base + net.stem.ctx, net.stem.sB * sizeof(bf16), audio, (size_t)L * sizeof(bf16),
                           (size_t)L * sizeof(bf16), nv, hipMemcpyDeviceToDevice, st));
   const int Tl = net.T[net.nst - 1];
-  CHK(convnet_run(c, net, nv, d_ids, rowmap(mean_out, c->cfg.latent_dim, Tl, (long long)Tl * c->cfg.latent_dim),
-                  RowMap{}, st));
+  CHK(convnet_run(c, net, nv, d_ids, rowmap(out, out_ch, Tl, (long long)Tl * out_ch), RowMap{}, st));
   HIPCHK(hipStreamSynchronize(st));  // d_ids scratch is reused by the next call
   return 0;
+}
+
+int vv_acoustic_encode(vv_ctx* c, int nv, int L, const void* audio, void* mean_out, vv_stream vst) {
+  if (!c->w.count("aenc.stem_w")) FAIL("acoustic encoder weights not bound");
+  if (nv <= 0 || L <= 0) return 0;
+  return encode_nonstreaming(c, c->aenc, "aenc", c->cfg.ac_enc_n_filters, c->cfg.latent_dim, nv, L, audio, mean_out,
+                             (hipStream_t)vst);
+}
+
+int vv_semantic_encode(vv_ctx* c, int nv, int L, const void* audio, void* mean_out, vv_stream vst) {
+  if (!c->finalized) FAIL("vv_semantic_encode before vv_finalize");
+  if (nv <= 0 || L <= 0) return 0;
+  return encode_nonstreaming(c, c->senc, "sem", c->cfg.sem_n_filters, c->cfg.semantic_dim, nv, L, audio, mean_out,
+                             (hipStream_t)vst);
 }
 
 int vv_vae_features(vv_ctx* c, int nv, int frames, const void* mean, const void* stdv, const void* noise, void* feat,

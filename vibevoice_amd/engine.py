@@ -234,6 +234,17 @@ class Engine:
                                                  _stream(stream)), "acoustic_encode")
         return mean
 
+    def semantic_encode(self, audio_bf16, stream=None):
+        """Non-streaming semantic encode of nv clips [nv, L] (L need not be whole
+        frames) -> [nv, ceil(L / hop), semantic_dim]."""
+        nv, L = audio_bf16.shape
+        frames = -(-L // self.hop)
+        S = self.cfg.semantic_vae_dim
+        mean = torch.empty(nv, frames, S, dtype=torch.bfloat16, device=self.device)
+        _lib.check(_lib.lib().vv_semantic_encode(self.h, nv, L, _ptr(audio_bf16.contiguous()), _ptr(mean),
+                                                 _stream(stream)), "semantic_encode")
+        return mean
+
     def vae_features(self, mean, stdv, noise, stream=None):
         nv, frames, D = mean.shape
         out = torch.empty_like(mean)

@@ -201,6 +201,10 @@ class VibeVoiceForConditionalGenerationInference:
         self._bufs = {}
         self._graph_cache, self._graph_seen = {}, set()
         self._graph_epoch = None        # engine workspace epoch the cached graphs were captured at
+        # this model's own capture stream: torch.cuda.graph() shares one side stream
+        # process-wide and synchronizes the whole device, so two models generating
+        # on two host threads would capture into each other's graphs
+        self._capture_stream = None
 
     def _step_buffers(self, B):
         """Static device operands of the loop body for batch B (shared by every
@@ -326,9 +330,13 @@ class VibeVoiceForConditionalGenerationInference:
                  speech_masks=None, speech_input_mask=None, return_speech=True, cfg_scale=1.0,
                  stop_check_fn=None, **kwargs):
         """The reference's generate() (modeling_vibevoice_inference.py:327-710), same
-        arguments and return type.  Extra keyword (bench / tests only):
-        `forced_tokens` = per-sample token schedule that replaces the constrained
-        argmax (the argmax is still computed and read back every step)."""
+        arguments and return type.  Extra keywords: `forced_tokens` (bench /
+        tests) = per-sample token schedule that replaces the constrained argmax
+        (the argmax is still computed and read back every step); `generator` = a
+        CPU torch.Generator for the per-step diffusion noise (default: the global
+        RNG, as the reference's torch.randn at :716) — with one per call,
+        generate() calls on several host threads draw independently of each
+        other's interleaving (the Gradio demo serves from worker threads)."""
         verbose = kwargs.get("verbose", False)
         sess = self.generate_session(inputs, generation_config, audio_streamer, speech_tensors, speech_masks,
                                      speech_input_mask, cfg_scale, stop_check_fn, **kwargs)
@@ -392,6 +400,7 @@ class GenerateSession:
         self.max_length_times = kwargs.pop("max_length_times", 2)
         self.refresh_negative = kwargs.get("refresh_negative", True)
         self.forced = kwargs.get("forced_tokens", None)
+        self.gen = kwargs.get("generator", None)          # CPU generator of the diffusion noise (None: global RNG)
         self.cfg_scale = cfg_scale
         self.stop_check_fn = stop_check_fn
         self.audio_streamer = audio_streamer
@@ -506,8 +515,20 @@ class GenerateSession:
                 self.seen.add(full)
                 return fn()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                fn()
+            cur = torch.cuda.current_stream()
+            if self.m._capture_stream is None:
+                self.m._capture_stream = torch.cuda.Stream(self.dev)
+            cs = self.m._capture_stream
+            cs.wait_stream(cur)
+            with torch.cuda.stream(cs):
+                # thread-local capture mode: another host thread's engine calls
+                # (their own streams) stay legal while this one captures
+                g.capture_begin(capture_error_mode="thread_local")
+                try:
+                    fn()
+                finally:
+                    g.capture_end()
+            cur.wait_stream(cs)
             self.graphs[full] = g
         g.replay()
 
@@ -572,7 +593,7 @@ class GenerateSession:
         n = didx.numel()
         dp, npin = self.didx_pins[buf], self.noise_pins[buf]
         dp[:n].copy_(didx)
-        noise = torch.randn(2 * n, self.m.config.acoustic_vae_dim)
+        noise = torch.randn(2 * n, self.m.config.acoustic_vae_dim, generator=self.gen)
         npin[:n].copy_(noise[:n])
         self.dn_dev.copy_(self.dn_pins[buf], non_blocking=True)      # rows + noise in one copy
 
@@ -591,10 +612,16 @@ class GenerateSession:
         rows = torch.nonzero(~self.finished & ((last == self.diff_id) | (last == self.start_id))).reshape(-1)
         if rows.numel() == 0:
             return None
-        state = torch.get_rng_state()
+        state = self.gen.get_state() if self.gen is not None else torch.get_rng_state()
         self._stage_diffusion(rows, self.step_idx & 1)
         self._diff_phase(rows.numel())
         return rows, state
+
+    def _restore_rng(self, state):
+        if self.gen is not None:
+            self.gen.set_state(state)
+        else:
+            torch.set_rng_state(state)
 
     # ---------------------------------------------------------------- one iteration
     def step(self):
@@ -693,7 +720,7 @@ class GenerateSession:
             if spec is None or not torch.equal(spec[0], didx):
                 if spec is not None:   # mispredicted: the speculative copies may still be queued
                     torch.cuda.current_stream().synchronize()
-                    torch.set_rng_state(spec[1])
+                    self._restore_rng(spec[1])
                     self.spec_miss += 1
                 self._stage_diffusion(didx, self.step_idx & 1)
                 self._diff_phase(n)
@@ -705,7 +732,7 @@ class GenerateSession:
                 st.put(audio[:, None, :], didx)
         else:
             if spec is not None:
-                torch.set_rng_state(spec[1])
+                self._restore_rng(spec[1])
                 self.spec_miss += 1
             self._push_controls(nxt)
             self._post_phase(0)

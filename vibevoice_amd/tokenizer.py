@@ -209,17 +209,23 @@ class SemanticTokenizer(_TokenizerView):
 
     @torch.no_grad()
     def encode(self, audio, cache=None, sample_indices=None, use_cache=False, debug=False):
-        """audio [n, 1, L], L a multiple of the hop (whole frames, as generate()
-        feeds it, :673-679) -> output with mean [n, L / hop, semantic_dim].
-        A partial last frame raises: the reference pads it per conv layer
-        (extra right padding of each strided conv, :127-133), which no fixture
-        pins; INTEGRATION.md lists this difference."""
+        """audio [n, 1, L] -> output with mean [n, ceil(L / hop), semantic_dim].
+        Whole frames (as generate() feeds them, :673-679) stream frame by frame
+        through the per-slot state (from zero state without a cache) — the same
+        kernels as the fused loop step.  Without a cache, a clip that ends in a
+        partial frame takes the non-streaming encoder (vv_semantic_encode), which
+        right-pads every strided conv's input to whole strides as the reference's
+        non-streaming path does (:127-133, :393-408; golden G5).  A partial frame
+        WITH a streaming cache raises (the reference's streaming convs carry the
+        remainder in their cache; generate() never feeds one)."""
         eng = self._pool.eng
         a = audio.reshape(audio.shape[0], -1).to(self.device, torch.bfloat16)
         n, L = a.shape
         hop = self._m.engine.hop
         if L % hop:
-            raise ValueError(f"semantic encode takes whole {hop}-sample frames (got {L} samples)")
+            if use_cache and cache is not None:
+                raise ValueError(f"streaming semantic encode takes whole {hop}-sample frames (got {L} samples)")
+            return VibeVoiceTokenizerEncoderOutput(mean=self._m.engine.semantic_encode(a.contiguous()))
         slots, tmp = self._slots(1, n, cache, sample_indices, use_cache)
         S = self._m.config.semantic_vae_dim
         mean = torch.empty(n, L // hop, S, dtype=torch.bfloat16, device=self.device)
