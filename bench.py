@@ -226,6 +226,28 @@ def measure_tp_collective(make_pass, n_layers, world, dev, iters=20, reps=3):
                      "max over ranks of graph-replayed LM passes with / without the collectives")
 
 
+def head_pass_maker(model, sess):
+    """make_pass for the sharded diffusion head (tp_head): one diffusion call of
+    the loop (all B rows, S steps) with its S x head_layers all-reduces."""
+    from vibevoice_amd import _lib
+    eng, B = model.engine, sess.B
+    L = _lib.lib()
+    pos, neg = sess.hid[:B], sess.hid[B:]
+    x = sess.noise_dev[:B]
+
+    def make(null):
+        L.vv_tp_null_collective(1 if null else 0)
+        try:
+            eng.diffusion_sample(pos, neg, x, 1.3)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                eng.diffusion_sample(pos, neg, x, 1.3)
+        finally:
+            L.vv_tp_null_collective(0)
+        return g.replay
+    return make
+
+
 def lm_pass_maker(model, sess):
     """make_pass for measure_tp_collective: the loop's LM phase body on the
     session's static buffers, captured into a hipGraph per switch setting."""
@@ -265,20 +287,47 @@ def cpu_baseline(cfg, tokens, S):
     tk = tokenizer_ids()
     ids = dict(eos=tk.eos_token_id, start=tk.speech_start_id, end=tk.speech_end_id, diffusion=tk.speech_diffusion_id)
 
+    # per-stage clocks: the oracle functions the loop calls for
+    # each stage, wrapped for the duration of the CPU leg
+    stages = dict(lm_positive=(oloop.lm, "forward_rows"), lm_negative=(oloop.lm, "forward_rows_masked"),
+                  diffusion=(oloop.head, "sample_speech_tokens"), acoustic_decode=(oloop.codec, "decode"),
+                  semantic_encode=(oloop.codec, "encode"))
+    clock = {k: 0.0 for k in stages}
+
+    def timed(name, fn):
+        def w(*a, **kw):
+            t0 = time.perf_counter()
+            try:
+                return fn(*a, **kw)
+            finally:
+                clock[name] += time.perf_counter() - t0
+        return w
+
     def run(k):
         forced = [[tk.speech_diffusion_id] * k + [tk.eos_token_id]]
+        for n in clock:
+            clock[n] = 0.0
         t0 = time.perf_counter()
         with torch.no_grad():
             oloop.generate(sd, cfg, inp["input_ids"], inp["attention_mask"], ids, ddpm_steps=S, cfg_scale=1.3,
                            forced=forced, dtype=torch.float32)
-        return time.perf_counter() - t0
-    run(1)                                   # warm-up (allocator, thread pool)
-    t1 = run(1)
-    tk_ = run(1 + tokens)
+        return time.perf_counter() - t0, dict(clock)
+    saved = {n: getattr(mod, attr) for n, (mod, attr) in stages.items()}
+    for n, (mod, attr) in stages.items():
+        setattr(mod, attr, timed(n, saved[n]))
+    try:
+        run(1)                                   # warm-up (allocator, thread pool)
+        t1, c1 = run(1)
+        tk_, ck = run(1 + tokens)
+    finally:
+        for n, (mod, attr) in stages.items():
+            setattr(mod, attr, saved[n])
     per = (tk_ - t1) / tokens
     tps = 1.0 / per
+    stage_ms = {n: round((ck[n] - c1[n]) / tokens * 1e3, 2) for n in stages}
+    stage_ms["other"] = round(per * 1e3 - sum(stage_ms.values()), 2)
     return dict(value=round(tps * HOP / SR, 4), unit="audio-sec/wall-sec", tokens_per_s=round(tps, 3),
-                cores=torch.get_num_threads(), kind="port",
+                cores=torch.get_num_threads(), kind="port", stage_ms_per_token=stage_ms,
                 sample=f"oracle/loop.py fp32 eager on CPU, VibeVoice-1.5B shapes (seeded random weights), "
                        f"B=1, S={S}, {tokens} timed diffusion tokens after a 1-token run (difference of two runs)")
 
@@ -395,6 +444,15 @@ def main():
     if T > 1:   # after the timed loop: the null-collective passes corrupt the session's state
         tp_coll = measure_tp_collective(lm_pass_maker(model, sess), model.config.decoder_config.num_hidden_layers,
                                         world, dev)
+        if model.tp_head:   # the sharded diffusion head's S x head_layers all-reduces per token
+            hl = model.config.diffusion_head_config.head_layers
+            hc = measure_tp_collective(head_pass_maker(model, sess), hl * S / 2, world, dev)
+            tp_coll["head"] = dict(diffusion_call_us=hc["lm_pass_us"],
+                                   diffusion_call_us_null_collective=hc["lm_pass_us_null_collective"],
+                                   allreduce_us_per_call=hc["allreduce_us_per_pass"],
+                                   allreduce_calls_per_call=int(hl * S), allreduce_share=hc["allreduce_share"],
+                                   note="RCCL all-reduce of the [2B, H] head state after each head layer's "
+                                        "row-parallel down_proj (sharded head, tp_head)")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:   # bounded CPU sample, N=1 only

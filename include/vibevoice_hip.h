@@ -119,6 +119,21 @@ int vv_tp_init(vv_ctx* ctx, int rank, int size, const void* unique_id);
 int vv_lm_forward_group(int n, vv_ctx* const* ctxs, int ntok, const void* embeds, int embed_rows, const int* slot,
                         const int* pos, int max_pos_p1, int nout, const int* out_idx, void* hidden_out,
                         float* logits_out, vv_stream st);
+/* The diffusion head split over the same ranks (SURVEY.md §8e's option for
+ * VibeVoice-Large, whose 925 MB of per-step head weights would otherwise be
+ * streamed by every rank): the engine was created with head_ffn = this rank's
+ * 1/size of the FFN width and bound to its shard (gate|up rows of its hidden
+ * columns, column-parallel; the matching down_proj input columns,
+ * row-parallel); after each head layer the [2n, H] state is all-reduced
+ * (RCCL, sum, bf16, in place; S x head_layers collectives per token), rank 0
+ * alone carrying the residual.  adaLN, noisy / cond / final projections and the
+ * DPM update stay replicated.
+ *   vv_tp_shard_head: mark the engine's head as sharded (after vv_tp_init)
+ *   vv_diffusion_sample_group: the group's ranks on ONE device, a device-side
+ *                    sum as the all-reduce (tests / single-GPU emulation). */
+int vv_tp_shard_head(vv_ctx* ctx, int on);
+int vv_diffusion_sample_group(int n_ranks, vv_ctx* const* ctxs, int n, const void* pos_h, const void* neg_h,
+                              void* x_io, float cfg_scale, const float* sde_noise, vv_stream st);
 /* Copy the K/V cache entry src[i] -> dst[i] of slot slots[i] (all layers). */
 int vv_kv_copy(vv_ctx* ctx, int n, const int* slots, const int* src, const int* dst, vv_stream st);
 /* embeds_out[i] = embed_tokens[ids[i]] */
@@ -130,6 +145,14 @@ int vv_embed(vv_ctx* ctx, int n, const int* ids, void* embeds_out, vv_stream st)
  * per-step draws [steps][2n][latent] (step()'s randn, dpm_solver.py:985-987). */
 int vv_diffusion_sample(vv_ctx* ctx, int n, const void* pos_h, const void* neg_h, void* x_io, float cfg_scale,
                         const float* sde_noise, vv_stream st);
+/* At 2n <= 4 rows each head layer is ONE launch when the engine has the fused
+ * layer's weight streams bound (head.<l>.gu_rows / head.<l>.dn_rows): its
+ * workgroups wait for each other inside the launch (bounded, ~200 ms).  If a
+ * wait ever gave up (workgroups not co-resident, e.g. more than two such
+ * launches from other contexts on the device at once), every output since is
+ * invalid: vv_sync_error returns 1 (and resets), else 0; it synchronises the
+ * device.  GenerateSession checks it once per generate(). */
+int vv_sync_error(vv_ctx* ctx);
 
 /* One streaming codec step for n samples in codec slots slots[n]:
  * latent [n, latent] -> audio_out [n, hop]; semantic features -> sem_out

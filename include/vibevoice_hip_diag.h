@@ -126,6 +126,9 @@ int vv_gemm_tune_apack(int on);
 /* Tuning hook (benchmarks only): override the GEMV plan (waves, K splits, chunks
  * in flight, tiles per workgroup) for one weight shape N x K at M <= mmax rows;
  * up to 8 overrides; N <= 0 clears them. */
+/* Test / A-B switch: 1 (default) = the fused head FFN layer (head_ffn.hip)
+ * where it applies; 0 = gate|up + down GEMV launches per layer. */
+int vv_head_fused(int on);
 int vv_gemv_tune_shape(int N, int K, int mmax, int nw, int ks, int u, int tpw);
 /* Test switch: 1 (default) = the q|k|v RoPE epilogue reads the engine's
  * per-position bf16 cos / sin table; 0 = computes cosf / sinf inline
@@ -137,6 +140,11 @@ int vv_rope_table(int on);
  * (bit-identical to the same splits merged in the attention kernel); on = n >= 2:
  * passes of <= n rows (n <= 16); 0 = the attn_plan splits everywhere. */
 int vv_attn_defer(int on, int chunk);
+/* Test switch: 1 (default) = decode passes of <= 16 rows over more than 8,192
+ * keys run up to 128 splits of >= 256 keys merged in <= 8 groups by each
+ * group's last-arriving workgroup, o_proj merging the groups; 0 = 1,024-key
+ * splits merged by k_attn_merge. */
+int vv_attn_group(int on);
 /* Test switch: 1 (default) = the A rows of the prefill's 256 x 256-tile GEMMs
  * are written MFMA-fragment-packed by their producers (RMSNorm rows for q|k|v
  * and gate|up, gate|up's SiLU*up rows for down); 0 = row-major.  Both give the

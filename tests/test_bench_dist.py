@@ -99,8 +99,8 @@ class _FakeEngine:
     model wires its TP rank into the engine."""
     made = []
 
-    def __init__(self, cfg, sd, device, max_batch, max_ctx, tp_rank=0, tp_size=1, tp_unique_id=None):
-        self.args = dict(tp_rank=tp_rank, tp_size=tp_size, uid=tp_unique_id)
+    def __init__(self, cfg, sd, device, max_batch, max_ctx, tp_rank=0, tp_size=1, tp_unique_id=None, tp_head=False):
+        self.args = dict(tp_rank=tp_rank, tp_size=tp_size, uid=tp_unique_id, tp_head=tp_head)
         self.schedule = None
         self.max_batch = max_batch
 
@@ -119,7 +119,7 @@ def _tp_worker(rank, world, T, port, out):
     group, replica, replicas = bench.tp_groups(w, r, T)
     m = mvi.VibeVoiceForConditionalGenerationInference(tiny_config(), {}, "cpu", tp_group=group)
     out[rank] = (replica, replicas, m.tp_rank, m.tp_size, m.engine.args["tp_rank"], m.engine.args["tp_size"],
-                 m.engine.args["uid"])
+                 m.engine.args["uid"], m.engine.args["tp_head"])
     torch.distributed.destroy_process_group()
 
 
@@ -134,7 +134,8 @@ def test_model_tp_wiring_world4_tp2():
         mp.spawn(_tp_worker, args=(4, 2, port, out), nprocs=4, join=True)
         res = dict(out)
     for r in range(4):
-        replica, replicas, tr, ts, etr, ets, uid = res[r]
+        replica, replicas, tr, ts, etr, ets, uid, th = res[r]
+        assert th is False      # tiny_config's head is cache-resident: replicated (head_tp_default)
         assert (replica, replicas) == (r // 2, 2)
         assert tr == etr == r % 2 and ts == ets == 2
         assert uid == f"uid-of-global-rank-{2 * (r // 2)}".encode()

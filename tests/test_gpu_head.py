@@ -100,9 +100,14 @@ def test_head_sde_vs_oracle(n):
     assert err < 2e-2 and c > 0.999
 
 
-@pytest.mark.parametrize("n", [1, 3])
-def test_head_real_shape_vs_oracle(n):
+@pytest.mark.parametrize("fused", [1, 0])
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_head_real_shape_vs_oracle(n, fused):
+    """n = 1, 2 (2n <= 4 rows) run the fused FFN layer (head_ffn.hip) by
+    default; fused=0 forces gate|up + down launches for every n."""
+    from vibevoice_amd import _lib
     from vibevoice_amd.config import VibeVoiceConfig
+    _lib.lib().vv_head_fused(fused)
     cfg = VibeVoiceConfig.builtin("1.5B")
     hc = cfg.diffusion_head_config
     g = torch.Generator().manual_seed(11)
@@ -133,9 +138,55 @@ def test_head_real_shape_vs_oracle(n):
     neg = r(n, H, std=1.0)
     noise = torch.randn(2 * n, 64, generator=g).bfloat16()
     x = noise[:n].to(dev).contiguous()
-    eng.diffusion_sample(pos.to(dev), neg.to(dev), x, 1.3)
-    torch.cuda.synchronize()
+    try:
+        eng.diffusion_sample(pos.to(dev), neg.to(dev), x, 1.3)
+        torch.cuda.synchronize()
+    finally:
+        _lib.lib().vv_head_fused(1)
+    eng.check_sync()
     ref = ohead.sample_speech_tokens(sd, pos, neg, noise, S, 1.3, hc.head_layers)
     err, c = rel_err(x, ref), cos(x, ref)
-    print(f"n={n} rel_err={err:.3e} cos={c:.6f}")
+    print(f"n={n} fused={fused} rel_err={err:.3e} cos={c:.6f}")
     assert err < 2e-2 and c > 0.999
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_head_fused_deterministic_and_close(n):
+    """The fused layer's split-K reduction is fixed-order: repeated calls give
+    identical bits (also inside a graph replay); it stays within bf16 noise of
+    the two-launch form (different summation order, same rounding points)."""
+    from vibevoice_amd import _lib
+    g = torch.Generator().manual_seed(21)
+    sd, hc, H = real_head_sd(g)
+    tiny = tiny_config(hidden=H, layers=1, heads=12, kv_heads=2, inter=256)
+    eng, _ = engine_with_head(tiny, sd)
+    eng.set_steps(10)
+    pos = torch.randn(n, H, generator=g).bfloat16().to(dev)
+    neg = torch.randn(n, H, generator=g).bfloat16().to(dev)
+    x0 = torch.randn(n, 64, generator=g).bfloat16().to(dev)
+    outs = []
+    for fused in (1, 1, 0):
+        _lib.lib().vv_head_fused(fused)
+        x = x0.clone()
+        eng.diffusion_sample(pos, neg, x, 1.3)
+        torch.cuda.synchronize()
+        outs.append(x.float().cpu())
+    _lib.lib().vv_head_fused(1)
+    # graph replay of the fused form, twice
+    s = torch.cuda.Stream()
+    xg = x0.clone()
+    with torch.cuda.stream(s):
+        gr = torch.cuda.CUDAGraph()
+        gr.capture_begin(capture_error_mode="thread_local")
+        eng.diffusion_sample(pos, neg, xg, 1.3, stream=s)
+        gr.capture_end()
+    for _ in range(2):
+        xg.copy_(x0)
+        gr.replay()
+        torch.cuda.synchronize()
+        outs.append(xg.float().cpu())
+    eng.check_sync()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[3]) and torch.equal(outs[3], outs[4])
+    err = rel_err(outs[0], outs[2])
+    print(f"n={n} fused vs two-launch rel {err:.3e}")
+    assert err < 1e-2

@@ -339,3 +339,86 @@ def test_28_layer_32k_prefill_graph_decode_vs_oracle():
               f"rel {e:.3e} cos {cos(hr, ref):.6f}")
         assert same
         assert e < 3e-2 and cos(hr, ref) > 0.999
+
+
+def test_long_context_grouped_split_merge_ragged_rows():
+    """Decode over contexts past 8,192 keys with rows of very different lengths
+    (20,000 / 9,001 / 300 keys, max_ctx 32K): up to 128 splits of >= 256 keys,
+    each group of consecutive splits merged by its last-arriving workgroup and
+    the groups merged by o_proj (XF_ATTN_MERGE) — vs oracle/lm.py, and vs the
+    1,024-key plan with k_attn_merge (vv_attn_group(0)) within bf16."""
+    from vibevoice_amd import _lib
+    cfg = tiny_config(hidden=1536, layers=2, heads=12, kv_heads=2, inter=8960)
+    cfg.decoder_config["max_position_embeddings"] = 65536
+    sd = synthetic_state_dict(cfg, seed=28, device="cpu", mode="test", with_acoustic_encoder=False)
+    eng = Engine(cfg, sd, dev, max_batch=3, max_ctx=32768, valid_ids=VALID)
+    osd, lcfg = oracle_sd(sd, dev), dict(cfg.decoder_config)
+    g = torch.Generator(device=dev).manual_seed(9)
+    lens = [20000, 9001, 300]
+    kvs = []
+    for r, n in enumerate(lens):   # one slot at a time (k_attn_pf prefill of each row)
+        x = torch.randn(n, 1536, device=dev, generator=g).bfloat16()
+        eng.lm_forward(x, torch.full((n,), r, **I32), torch.arange(n).to(**I32), torch.tensor([n - 1]).to(**I32))
+        kv = olm.RowKV(2)
+        with torch.no_grad():
+            _oracle_prefill_gpu(osd, lcfg, x, kv)
+        kvs.append(kv)
+    L = torch.tensor(lens)
+    rows = torch.arange(3).to(**I32)
+    for s in range(2):
+        step = torch.randn(3, 1536, device=dev, generator=g).bfloat16()
+        outs = {}
+        for mode in (1, 0):
+            _lib.lib().vv_attn_group(mode)
+            try:
+                outs[mode], _ = eng.lm_forward(step, rows, (L + s).to(**I32), rows, max_pos=32767)
+            finally:
+                _lib.lib().vv_attn_group(1)
+        with torch.no_grad():
+            ref = olm.forward_rows(osd, lcfg, step[:, None], kvs)[:, -1]
+        torch.cuda.synchronize()
+        for r in range(3):
+            e, e0 = rel_err(outs[1][r], ref[r]), rel_err(outs[1][r], outs[0][r])
+            print(f"grouped merge step {s} row {r} ({lens[r] + s + 1} keys): rel {e:.3e} vs oracle, "
+                  f"{e0:.3e} vs the k_attn_merge plan")
+            assert e < 2e-2 and cos(outs[1][r], ref[r]) > 0.999
+            assert e0 < 1e-2
+
+
+@pytest.mark.parametrize("tp,n", [(4, 1), (4, 4), (2, 4)])
+def test_large_head_tp_group_matches_single_engine(tp, n):
+    """configs[3]: the VibeVoice-Large diffusion head (H 3,584, FFN 10,752,
+    4 layers, S = 10, CFG 1.3) sharded over `tp` ranks (gate|up
+    column-parallel, down row-parallel, one all-reduce of [2n, H] per head
+    layer; adaLN / noisy / final / DPM replicated) — the ranks' shards
+    interleaved on one GPU with an on-device sum as the all-reduce
+    (vv_diffusion_sample_group) — vs the TP = 1 engine and vs oracle/head.py,
+    within bf16."""
+    cfg = VibeVoiceConfig.builtin("Large")
+    hc = cfg.diffusion_head_config
+    lm_cfg = tiny_config(layers=1, **LARGE)
+    sd = synthetic_state_dict(lm_cfg, seed=22, device="cpu", mode="test", with_acoustic_encoder=False)
+    hsd = {k[len("model.prediction_head."):]: v for k, v in sd.items() if k.startswith("model.prediction_head.")}
+    full = Engine(lm_cfg, sd, dev, max_batch=4, max_ctx=64)
+    group = [Engine(lm_cfg, sd, dev, max_batch=4, max_ctx=64, tp_rank=r, tp_size=tp, tp_head=True) for r in range(tp)]
+    assert group[1].w["head.0.down_w"].shape == (3584, 10752 // tp)
+    S = 10
+    full.set_steps(S)
+    group[0].set_steps(S)
+    g = torch.Generator().manual_seed(10 + n)
+    pos = torch.randn(n, 3584, generator=g).bfloat16()
+    neg = torch.randn(n, 3584, generator=g).bfloat16()
+    noise = torch.randn(2 * n, 64, generator=g).bfloat16()
+    x1 = noise[:n].to(dev).contiguous()
+    xg = x1.clone()
+    full.diffusion_sample(pos.to(dev), neg.to(dev), x1, 1.3)
+    group[0].diffusion_sample_group(group[1:], pos.to(dev), neg.to(dev), xg, 1.3)
+    torch.cuda.synchronize()
+    ref = ohead.sample_speech_tokens(hsd, pos, neg, noise, S, 1.3, hc.head_layers)
+    e1, eg = rel_err(xg, x1), rel_err(xg, ref)
+    print(f"Large head TP={tp} n={n}: rel {e1:.3e} vs TP=1, {eg:.3e} vs oracle (TP=1 vs oracle {rel_err(x1, ref):.3e})")
+    assert e1 < 2e-2 and cos(xg, x1) > 0.999
+    assert eg < 2e-2 and cos(xg, ref) > 0.999
+    # a sharded engine refuses the single-engine call without a communicator
+    with pytest.raises(RuntimeError):
+        group[1].diffusion_sample(pos.to(dev), neg.to(dev), xg.clone(), 1.3)

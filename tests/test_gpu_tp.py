@@ -86,3 +86,37 @@ def test_rccl_allreduce_path_single_rank():
     gph.replay()
     torch.cuda.synchronize()
     assert torch.equal(hc, hd) and torch.equal(lc, ld)
+
+
+def test_rccl_head_allreduce_path_single_rank():
+    """The sharded diffusion head's RCCL path (one all-reduce of [2n, H] per
+    head layer) with a single-rank communicator: bit-exact against the
+    communicator-free engine, eagerly and inside a captured hipGraph."""
+    from vibevoice_amd import _lib
+    cfg = tiny_config(hidden=256, layers=2, heads=2, kv_heads=1, inter=512)
+    sd = synthetic_state_dict(cfg, seed=13, device="cpu", mode="test", with_acoustic_encoder=False)
+    plain = Engine(cfg, sd, dev, max_batch=2, max_ctx=128, valid_ids=VALID)
+    rccl = Engine(cfg, sd, dev, max_batch=2, max_ctx=128, valid_ids=VALID, tp_rank=0, tp_size=1,
+                  tp_unique_id=Engine.tp_unique_id())
+    _lib.check(_lib.lib().vv_tp_shard_head(rccl.h, 1), "tp_shard_head")
+    for e in (plain, rccl):
+        e.set_steps(10)
+    g = torch.Generator().manual_seed(4)
+    pos = torch.randn(2, 256, generator=g).bfloat16().to(dev)
+    neg = torch.randn(2, 256, generator=g).bfloat16().to(dev)
+    x0 = torch.randn(2, 64, generator=g).bfloat16().to(dev)
+    xa, xb = x0.clone(), x0.clone()
+    plain.diffusion_sample(pos, neg, xa, 1.3)
+    rccl.diffusion_sample(pos, neg, xb, 1.3)
+    torch.cuda.synchronize()
+    assert torch.equal(xa, xb)
+    xc = x0.clone()
+    rccl.diffusion_sample(pos, neg, xc, 1.3)   # warm
+    xc.copy_(x0)
+    gph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gph):
+        rccl.diffusion_sample(pos, neg, xc, 1.3)
+    xc.copy_(x0)
+    gph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(xa, xc)

@@ -45,6 +45,8 @@ EXPORTS = [
     ("vv_tp_init", I, [P, I, I, P]),
     ("vv_tp_null_collective", I, [I]),
     ("vv_lm_forward_group", I, [I, ctypes.POINTER(P), I, P, I, P, P, I, I, P, P, P, P]),
+    ("vv_tp_shard_head", I, [P, I]),
+    ("vv_diffusion_sample_group", I, [I, ctypes.POINTER(P), I, P, P, P, F, P, P]),
     ("vv_embed", I, [P, I, P, P, P]),
     ("vv_diffusion_sample", I, [P, I, P, P, P, F, P, P]),
     ("vv_codec_step", I, [P, I, P, P, P, P, P, P, P]),
@@ -83,6 +85,9 @@ EXPORTS = [
     ("vv_gemv_tune_shape", I, [I, I, I, I, I, I, I]),
     ("vv_rope_table", I, [I]),
     ("vv_attn_defer", I, [I, I]),
+    ("vv_attn_group", I, [I]),
+    ("vv_head_fused", I, [I]),
+    ("vv_sync_error", I, [P]),
     ("vv_norm_pack", I, [I]),
 ]
 

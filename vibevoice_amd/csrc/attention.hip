@@ -94,8 +94,34 @@ __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int r = lane & 15, g = lane >> 4;
   astamp(a, 0);
-  const int qi = blockIdx.x / a.nkv, kh = blockIdx.x - qi * a.nkv, split = blockIdx.y;
-  const int len = a.pos[qi] + 1;
+  // grid (split, row x kv head): consecutive workgroup ids -- which the
+  // dispatcher deals round-robin over the 8 XCDs -- are consecutive splits of
+  // one (row, kv head), so every XCD gets an equal share of each row's keys.
+  // (With (row x kv head, split) a row's splits fell on id % 8 = the same 2
+  // of 8 XCDs per kv head: at 65K keys B = 1 the long row's work ran on half
+  // the chip while the short negative row's splits held the other half.)
+  const int rk = blockIdx.y, split = blockIdx.x;
+  const int qi = rk / a.nkv, kh = rk - qi * a.nkv;
+  // the row's length, its KV slot and the Q fragments: all issued before any
+  // is used, one memory round trip (the compiler sank the slot and Q loads
+  // behind the early exit below, each a round trip of its own); the empty asm
+  // makes len / slot live here, so their wait leaves the Q loads in flight
+  const int pos_q = a.pos[qi];
+  const int slot = a.slots[qi];
+  // Q fragments (A operand): row = head r (zero past G), k = dims 32c + 8g .. +7;
+  // the fp32 scores are scaled by 1/sqrt(d) after the MFMA
+  bf16x8 qf[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if (r < G) {
+      const bf16x8 q8 = *(const bf16x8*)(a.q + (long long)qi * a.nh * 128 + (kh * G + r) * 128 + 32 * c + 8 * g);
+      qf[c] = q8;
+    } else {
+      qf[c] = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  asm volatile("" ::"v"(pos_q), "v"(slot));
+  const int len = pos_q + 1;
   // this row's split size: >= a.chunk, all nsplit splits cover len; splits past
   // the row's last key exit at once
   const int chunk = row_chunk(a, len);
@@ -107,24 +133,12 @@ __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
   const int per = ((k1 - k0 + NW - 1) / NW + 31) / 32 * 32;
   const int w0 = k0 + wave * per;
   const int w1 = min(k1, w0 + per);
-  const long long cbase = (long long)a.layer * a.kv.s_layer + (long long)a.slots[qi] * a.kv.s_slot +
+  const long long cbase = (long long)a.layer * a.kv.s_layer + (long long)slot * a.kv.s_slot +
                           (long long)kh * a.kv.s_head;
   const bf16* K = a.kv.k + cbase;             // [ctx][128]
   const bf16* VB = a.kv.v + cbase;            // 32-position blocks of [128][32] (v_off)
   const bf16x8 z8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
 
-  // Q fragments (A operand): row = head r (zero past G), k = dims 32c + 8g .. +7;
-  // the fp32 scores are scaled by 1/sqrt(d) after the MFMA
-  bf16x8 qf[4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    if (r < G) {
-      const bf16x8 q8 = *(const bf16x8*)(a.q + (long long)qi * a.nh * d + (kh * G + r) * d + 32 * c + 8 * g);
-      qf[c] = q8;
-    } else {
-      qf[c] = z8;
-    }
-  }
   f32x4 o[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) o[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -134,41 +148,41 @@ __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
     m[i] = -INFINITY;
     l[i] = 0.f;
   }
-  bf16x8 kf[2][4], vf[8];
-  auto load = [&](int c0) {
+  // K / V fragments of two 32-key steps in flight per wave (two register sets,
+  // both issued before the first step computes): a 512-key split (65K context)
+  // is 64 keys per wave, so all of a workgroup's K / V is requested at once
+  bf16x8 kA[2][4], vA[8], kB[2][4], vB[8];
+  // Loads are unconditional, from positions clamped into [0, w1): no branch
+  // and no per-load wait.  (Guarded V loads followed by the tail mask compiled
+  // to a branch + s_waitcnt vmcnt(0) after EACH of a step's 8 V loads -- eight
+  // serialized memory round trips per step.)  Keys past w1 are masked where
+  // their values are used: S to -inf (so P = 0) and V to 0 on the tail step
+  // (the clamped rows hold other keys' values, and 0 x NaN would not vanish).
+  auto load = [&](int c0, bf16x8 (&kf)[2][4], bf16x8 (&vf)[8]) {
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt) {
-      const int key = c0 + 16 * tt + r;       // B operand of S: col = key
-      const bool ok = key < w1;
+      const int key = min(c0 + 16 * tt + r, w1 - 1);   // B operand of S: col = key
 #pragma unroll
-      for (int c = 0; c < 4; ++c) kf[tt][c] = ok ? *(const bf16x8*)(K + (long long)key * d + 32 * c + 8 * g) : z8;
+      for (int c = 0; c < 4; ++c) kf[tt][c] = *(const bf16x8*)(K + (long long)key * d + 32 * c + 8 * g);
     }
-    const int kb = c0 + 8 * g;                 // B operand of O: k = keys kb .. kb+7, col = dim
+    const int kb = min(c0 + 8 * g, (w1 - 1) & ~7);      // B operand of O: k = keys kb .. kb+7, col = dim
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      bf16x8 v = kb < w1 ? *(const bf16x8*)(VB + v_off(16 * j + r, kb)) : z8;
-      if (kb + 8 > w1) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (kb + e >= w1) v[e] = (bf16)0.f;
-      }
-      vf[j] = v;
-    }
+    for (int j = 0; j < 8; ++j) vf[j] = *(const bf16x8*)(VB + v_off(16 * j + r, kb));
   };
-  if (w0 < w1) load(w0);
+  if (w0 < w1) load(w0, kA, vA);
+  if (w0 + 32 < w1) load(w0 + 32, kB, vB);
   if (a.stamps) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     astamp(a, 1);
   }
-  for (int c0 = w0; c0 < w1; c0 += 32) {
-    bf16x8 kc[2][4], vc[8];
+  auto step = [&](int c0, const bf16x8 (&kc)[2][4], bf16x8 (&vc)[8]) {   // vc is masked in place
+    if (c0 + 32 > w1) {   // the wave's tail step (uniform): keys kb + e >= w1 contribute nothing
+      const int kb = c0 + 8 * g;
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
+      for (int j = 0; j < 8; ++j)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) kc[tt][c] = kf[tt][c];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) vc[j] = vf[j];
-    if (c0 + 32 < w1) load(c0 + 32);
+        for (int e = 0; e < 8; ++e) vc[j][e] = kb + e < w1 ? vc[j][e] : (bf16)0.f;
+    }
     // S tiles: lane holds S[head 4g+i][key c0 + 16tt + r]
     f32x4 sacc[2];
 #pragma unroll
@@ -205,6 +219,14 @@ __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = amfma(pa, vc[j], o[j]);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  for (int c0 = w0; c0 < w1; c0 += 64) {
+    step(c0, kA, vA);
+    if (c0 + 64 < w1) load(c0 + 64, kA, vA);
+    if (c0 + 32 < w1) {
+      step(c0 + 32, kB, vB);
+      if (c0 + 96 < w1) load(c0 + 96, kB, vB);
+    }
   }
   // this wave's (m, l, O): lane holds O[head 4g+i][dim 16j + r]
 #pragma unroll
@@ -244,7 +266,7 @@ __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
     }
     res[q] = sum;
   }
-  if (nact == 1 && !a.defer) {
+  if (nact == 1 && !a.defer && !a.group) {
 #pragma unroll
     for (int q = 0; q < NE; ++q) {
       const int e = t + q * 64 * NW;
@@ -265,7 +287,7 @@ __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
   // reads them with sc1 loads.  No release / acquire fence: an agent fence
   // writes back the XCD's whole L2 (MI355X_MICROARCH.md "publish-large", the
   // hand-off table's first row).
-  const bool wt = !a.merge && !a.defer;
+  const bool wt = !a.merge && !a.defer;   // group mode: write-through too (its last arriver reads them)
 #pragma unroll
   for (int q = 0; q < NE; ++q) {
     const int e = t + q * 64 * NW;
@@ -290,14 +312,58 @@ __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
   if (!wt) return;    // k_attn_merge or the consumer's merge (defer) runs next
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  // group mode: splits [gs0, gs1) of this row's active ones form the group; its
+  // last arriver merges them into the group partial
+  const int gi = a.group ? split / a.group : 0;
+  const int gs0 = a.group ? gi * a.group : 0, gs1 = a.group ? min(nact, gs0 + a.group) : nact;
   if (t == 0) {
-    unsigned* ctr = a.counters + blockIdx.x;
+    unsigned* ctr = a.counters + (a.group ? rk * a.ngroups + gi : rk);
     const unsigned tk = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last_flag = tk == (unsigned)(nact - 1);
+    last_flag = tk == (unsigned)(gs1 - gs0 - 1);
     if (last_flag) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   if (!last_flag) return;
+  if (a.group) {
+    // out = the group's (M, L, O): M = max m_s, L = sum e^{m_s - M} l_s, O = sum
+    // e^{m_s - M} o_s in split order (the consumer divides by the merged L)
+    auto ldg = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    constexpr int GMAX = 16;
+    const int ng = gs1 - gs0;
+    for (int e = t; e < G * d; e += 64 * NW) {
+      const int h = e / d, j = e - h * d;
+      const long long p0 = ((long long)qi * a.nh + kh * G + h) * a.nsplit + gs0;
+      float mv[GMAX], lv[GMAX], ov[GMAX];
+#pragma unroll
+      for (int s2 = 0; s2 < GMAX; ++s2) {
+        if (s2 < ng) {
+          mv[s2] = ldg(a.part_ml + (p0 + s2) * 2);
+          lv[s2] = ldg(a.part_ml + (p0 + s2) * 2 + 1);
+          ov[s2] = ldg(a.part_o + (p0 + s2) * d + j);
+        }
+      }
+      float M = -INFINITY;
+#pragma unroll
+      for (int s2 = 0; s2 < GMAX; ++s2)
+        if (s2 < ng) M = fmaxf(M, mv[s2]);
+      float num = 0.f, den = 0.f;
+#pragma unroll
+      for (int s2 = 0; s2 < GMAX; ++s2) {
+        if (s2 < ng) {
+          const float w = __expf(mv[s2] - M);
+          num += w * ov[s2];
+          den += w * lv[s2];
+        }
+      }
+      const long long q0 = ((long long)qi * a.nh + kh * G + h) * a.ngroups + gi;
+      a.part_o2[q0 * d + j] = num;
+      if (j == 0) {
+        a.part_ml2[q0 * 2] = M;
+        a.part_ml2[q0 * 2 + 1] = den;
+      }
+    }
+    return;
+  }
   // merge the splits: out = sum_s e^{m_s - M} o_s / sum_s e^{m_s - M} l_s
   auto ld = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   for (int e = t; e < G * d; e += 64 * NW) {
@@ -880,9 +946,12 @@ int launch_attn(AttnArgs a, hipStream_t st) {
   if (a.chunk % ATT_KC || a.nsplit > ATT_SPLITS_MAX) return 1;
   if ((a.nsplit > 1 || a.defer) && (!a.part_o || !a.part_ml || !a.counters)) return 1;
   if (a.defer && a.nsplit > ATT_MERGE_IN) return 1;
+  if (a.group && (a.defer || a.group > 16 || a.ngroups > ATT_MERGE_IN || a.ngroups * a.group < a.nsplit ||
+                  !a.part_o2 || !a.part_ml2 || (long long)a.nq * a.nkv * a.ngroups > 65536))
+    return 1;
   const int mi = g_att_merge_in;
-  a.merge = !a.defer && a.nsplit > (mi >= 0 ? mi : ATT_MERGE_IN) ? 1 : 0;
-  dim3 grid(a.nq * a.nkv, a.nsplit);
+  a.merge = !a.defer && !a.group && a.nsplit > (mi >= 0 ? mi : ATT_MERGE_IN) ? 1 : 0;
+  dim3 grid(a.nsplit, a.nq * a.nkv);
   const int nw = a.chunk >= 256 ? 8 : a.chunk >= 128 ? 4 : 2;   // 32 keys per wave step
   if (nw == 8) launch_attn_nw<8>(a, grid, st);
   else if (nw == 4) launch_attn_nw<4>(a, grid, st);

@@ -104,12 +104,18 @@ struct RowMap {
 };
 
 DEV long long rm_off(const RowMap& r, int m) {
+  if (r.T == (1 << 30) && !r.idx) return (long long)m * r.sT;   // a plain row-major map (no division)
   int g = m / r.T;
   int t = m - g * r.T;
   long long s = r.idx ? (long long)r.idx[g] : (long long)g;
   return s * r.sB + (long long)t * r.sT;
 }
 DEV const bf16* rm_bf(const RowMap& r, int m) { return (const bf16*)r.base + rm_off(r, m); }
+// a map known to have no slot table (r.idx == nullptr): no conditional load
+DEV const bf16* rm_bf_plain(const RowMap& r, int m) {
+  const int g = m / r.T;
+  return (const bf16*)r.base + (long long)g * r.sB + (long long)(m - g * r.T) * r.sT;
+}
 DEV bf16* rm_bfw(const RowMap& r, int m) { return (bf16*)r.base + rm_off(r, m); }
 
 // Epilogues (what a GEMM does with acc = sum_k A[m,k] W[n,k]):

@@ -151,7 +151,9 @@ struct vv_ctx {
   // this engine holds rank tp_rank's shard; the residual stream is all-reduced
   // after o_proj and down_proj
   int tp_rank = 0, tp_size = 1;
+  int head_tp = 0;      // 1: the diffusion head's FFN is sharded too (vv_tp_shard_head; head_ffn is local)
   ncclComm_t comm = nullptr;
+  DevBuf zero_rows;     // [2 * max_batch][H] zeros: the residual of a sharded head's rank > 0
   // persistent chains (chain.hip): op tables per diffusing-row count n for the
   // current schedule; sync words (zeroed per launch), split slabs, error word
   struct Chain {
@@ -161,6 +163,9 @@ struct vv_ctx {
   };
   std::unordered_map<int, Chain> head_chain;
   DevBuf chain_sync, chain_slabs, chain_err, coef_dev;
+  // fused head FFN layer (head_ffn.hip): partial-sum slabs, grid-wait words + error word
+  DevBuf hf_slab, hf_sync;
+  bool hf_ready = false;   // its weights are bound (head.<l>.gu_rows / dn_rows) and the shape fits
   DevBuf rope_tab;   // [max_ctx][cos 64 | sin 64] bf16 (k_rope_table)
 };
 
@@ -626,7 +631,8 @@ void vv_destroy(vv_ctx* c) {
   (void)hipDeviceSynchronize();
   DevBuf* bufs[] = {&c->norm_ws, &c->kv_k, &c->kv_v, &c->lm_ws, &c->attn_part, &c->attn_cnt, &c->valid_ids, &c->splitk_ws, &c->splitk_cnt,
                     &c->temb, &c->tfreq_tmp, &c->head_ws, &c->codec_ws, &c->slot_scratch, &c->unit_sb,
-                    &c->chain_sync, &c->chain_slabs, &c->chain_err, &c->coef_dev, &c->rope_tab};
+                    &c->chain_sync, &c->chain_slabs, &c->chain_err, &c->coef_dev, &c->rope_tab, &c->zero_rows,
+                    &c->hf_slab, &c->hf_sync};
   for (DevBuf* b : bufs) b->release();
   for (auto& kv : c->head_chain) kv.second.ops.release();
   ConvNet* nets[] = {&c->dec, &c->sem, &c->aenc, &c->senc};
@@ -690,6 +696,19 @@ int vv_finalize(vv_ctx* c) {
     CHK(need(c, p + ".down_w", {H, F}));
   }
   CHK(need(c, "head.final_w", {D, H}));
+  // the fused FFN layer's streams (optional: without them every layer runs gate|up + down)
+  c->hf_ready = false;
+  if (head_ffn_fits(H, F, 2) && c->w.count("head.0.gu_rows")) {
+    for (int l = 0; l < L; ++l) {
+      const std::string p = "head." + std::to_string(l);
+      CHK(need(c, p + ".gu_rows", {2LL * F, H}));
+      CHK(need(c, p + ".dn_rows", {F, H}));
+    }
+    CHK(c->hf_slab.ensure((size_t)head_ffn_grid() * 4 * H * sizeof(float)));
+    CHK(c->hf_sync.ensure(11 * 128));
+    HIPCHK(hipMemset(c->hf_sync.p, 0, 11 * 128));
+    c->hf_ready = true;
+  }
   // ---- connectors + latent scaling
   CHK(need(c, "conn.ac.fc1_w", {H, D}));
   CHK(need(c, "conn.se.fc1_w", {H, k.semantic_dim}));
@@ -756,6 +775,8 @@ int vv_finalize(vv_ctx* c) {
     CHK(c->head_ws.ensure(elems * sizeof(bf16)));
   }
   CHK(c->codec_ws.ensure((size_t)k.max_batch * (4 * H + 2 * 256) * sizeof(bf16) + 4096));
+  CHK(c->zero_rows.ensure((size_t)2 * k.max_batch * H * sizeof(bf16)));
+  HIPCHK(hipMemset(c->zero_rows.p, 0, (size_t)2 * k.max_batch * H * sizeof(bf16)));
   CHK(c->slot_scratch.ensure(4096));
   {
     const uint16_t one_zero[2] = {0x3F80, 0x0000};
@@ -848,8 +869,18 @@ extern "C" int vv_attn_defer(int on, int chunk) {
   g_defer_chunk = chunk;
   return 0;
 }
+// Long contexts (> 8 splits of 1,024 keys, i.e. > 8,192 keys) with <= 16 rows:
+// up to 128 splits of >= 256 keys (65K: 128 x 512, so the one long row's 2 kv
+// heads fill all 256 CUs where 1,024-key splits busied 128), merged in <= 8
+// groups of <= 16 consecutive splits by each group's last-arriving workgroup;
+// o_proj merges the group partials (XF_ATTN_MERGE) -- no k_attn_merge launch.
+static std::atomic<int> g_attn_group{1};   // diagnostic (vv_attn_group): 0 = the 1,024-key plan + k_attn_merge
+extern "C" int vv_attn_group(int on) {
+  g_attn_group = on ? 1 : 0;
+  return 0;
+}
 struct LmPass {
-  int ntok = 0, nsplit = 1, chunk = 64, prefill = 0, defer = 0;
+  int ntok = 0, nsplit = 1, chunk = 64, prefill = 0, defer = 0, group = 0, ngroups = 0;
   bf16 *h = nullptr, *q = nullptr, *att = nullptr, *act = nullptr;
   RowMap in_m, hm;
   const int *slot = nullptr, *pos = nullptr;
@@ -892,9 +923,22 @@ static int lm_begin(vv_ctx* c, LmPass& P, int ntok, const void* embeds, int embe
       P.chunk = ch;
     }
   }
+  P.group = P.ngroups = 0;
+  if (!P.prefill && !P.defer && g_attn_group && P.nsplit > 8 && ntok <= 16 && k.head_dim == 128) {
+    int ns = std::min(128, (max_pos_p1 + 255) / 256);
+    const int ch = ((max_pos_p1 + ns - 1) / ns + 31) / 32 * 32;
+    ns = (max_pos_p1 + ch - 1) / ch;
+    const int gs = (ns + 7) / 8;
+    if (gs <= 16) {
+      P.nsplit = ns;
+      P.chunk = ch;
+      P.group = gs;
+      P.ngroups = (ns + gs - 1) / gs;
+    }
+  }
   if (P.nsplit > 1) {
-    if ((size_t)ntok * k.n_kv_heads > 65536) FAIL("attention split tickets exhausted");
-    CHK(c->attn_part.ensure((size_t)ntok * k.n_heads * P.nsplit * (d + 2) * sizeof(float)));
+    if ((size_t)ntok * k.n_kv_heads * std::max(1, P.ngroups) > 65536) FAIL("attention split tickets exhausted");
+    CHK(c->attn_part.ensure((size_t)ntok * k.n_heads * (P.nsplit + P.ngroups) * (d + 2) * sizeof(float)));
   }
   // token row m reads embeds row m % embed_rows (the negative CFG rows consume the
   // positive rows' embeddings, :594-596); layer 0's attention residual writes h
@@ -959,6 +1003,12 @@ static int lm_attn_half(vv_ctx* c, LmPass& P, int l, hipStream_t st) {
   at.kv = c->kv;
   at.part_o = (float*)c->attn_part.p;
   at.part_ml = at.part_o ? at.part_o + (size_t)P.ntok * k.n_heads * P.nsplit * d : nullptr;
+  at.group = P.group;
+  at.ngroups = P.ngroups;
+  if (P.group) {
+    at.part_o2 = at.part_ml + (size_t)P.ntok * k.n_heads * P.nsplit * 2;
+    at.part_ml2 = at.part_o2 + (size_t)P.ntok * k.n_heads * P.ngroups * d;
+  }
   KCHK(launch_attn(at, st));
   GemmArgs g = gemm_args(c, P.ntok, H, nhd, rowmap(P.att, nhd), W(c, p + ".o_w"), EPI_RES, P.hm);
   if (P.defer) {
@@ -968,6 +1018,13 @@ static int lm_attn_half(vv_ctx* c, LmPass& P, int l, hipStream_t st) {
     g.xf.qpos = P.pos;
     g.xf.nsplit = P.nsplit;
     g.xf.chunk = P.chunk;
+  } else if (P.group) {   // the groups' partials: group g spans keys [g, g + 1) x group x chunk
+    g.xf.kind = XF_ATTN_MERGE;
+    g.xf.part_o = at.part_o2;
+    g.xf.part_ml = at.part_ml2;
+    g.xf.qpos = P.pos;
+    g.xf.nsplit = P.ngroups;
+    g.xf.chunk = P.group * P.chunk;
   }
   tp_residual(c, g, l == 0 ? P.in_m : P.hm);
   CHK(gemm(c, g, st));
@@ -1114,6 +1171,25 @@ extern "C" int vv_chain_error(vv_ctx* c) {
   return (int)v;
 }
 
+// Fused head FFN layer (head_ffn.hip) where its weights are bound and the shape
+// fits; 0 = gate|up + down launches (diagnostic vv_head_fused, A/B and tests)
+static std::atomic<int> g_head_fused{1};
+extern "C" int vv_head_fused(int on) {
+  g_head_fused = on ? 1 : 0;
+  return 0;
+}
+// A grid wait of the fused head layer gave up (workgroups not co-resident):
+// every output since the last call is invalid.  Reset on read.
+int vv_sync_error(vv_ctx* c) {
+  unsigned v = 0;
+  if (c->hf_sync.p) {
+    if (hipMemcpy(&v, (unsigned*)c->hf_sync.p + 10 * 32, 4, hipMemcpyDeviceToHost) != hipSuccess)
+      FAIL("vv_sync_error: reading the error word failed (hipMemcpy)");
+    if (v) HIPCHK(hipMemset((unsigned*)c->hf_sync.p + 10 * 32, 0, 4));
+  }
+  return v ? 1 : 0;
+}
+
 // Plan every op of `ops` (chain.hip), lay out slabs and tickets, upload.
 static int chain_upload(vv_ctx* c, std::vector<ChainOp>& ops, vv_ctx::Chain& T) {
   const int G = chain_grid();
@@ -1168,11 +1244,163 @@ static int chain_launch(vv_ctx* c, const vv_ctx::Chain& T, ChainArgs A, hipStrea
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   HIPCHK(hipStreamIsCapturing(st, &cap));
   if (cap == hipStreamCaptureStatusNone) {
+    // (a host sync per eager chain launch: the chain is an opt-in diagnostic switch)
     HIPCHK(hipStreamSynchronize(st));
     const int e = vv_chain_error(c);
+    if (e < 0) FAIL("persistent chain: reading the error word failed (hipMemcpy)");
     if (e) FAIL("persistent chain: a dependency wait gave up at op " + std::to_string(e - 1) +
                 " (workgroups not co-resident); outputs are invalid");
   }
+  return 0;
+}
+
+// ------------------------------------------------------------------ diffusion head
+// One rank's buffers and operands of a vv_diffusion_sample call.
+struct HeadRun {
+  int n = 0, R = 0;
+  long long MODW = 0;
+  bf16 *cat = nullptr, *condp = nullptr, *xh = nullptr, *mods = nullptr, *sa = nullptr, *act = nullptr, *v = nullptr,
+       *m1 = nullptr;
+  const bf16* cond = nullptr;
+  RowMap xh_m;
+  bool keep = false;
+};
+
+// layout, condition rows and cond_proj (step-invariant: once per token)
+static int head_begin(vv_ctx* c, int n, const void* pos_h, const void* neg_h, HeadRun& h, hipStream_t st) {
+  const vv_config& k = c->cfg;
+  const int H = k.hidden, F = k.head_ffn, D = k.latent_dim, L = k.head_layers;
+  h.n = n;
+  h.R = 2 * n;
+  h.MODW = (3LL * L + 2) * H;
+  const int R = h.R;
+  h.cat = (bf16*)c->head_ws.p;
+  h.condp = h.cat + (size_t)R * H;
+  bf16* sc = h.condp + (size_t)R * H;
+  h.xh = sc + (size_t)R * H;
+  bf16* a = h.xh + (size_t)R * H;
+  h.mods = a + (size_t)R * H;                             // [HEAD_SC steps][R][MODW]
+  h.sa = h.mods + (size_t)HEAD_SC * R * h.MODW;           // [HEAD_SC steps][R][H] adaLN inputs
+  h.act = h.sa + (size_t)HEAD_SC * R * H;
+  h.v = h.act + (size_t)R * F;
+  h.m1 = h.v + (size_t)R * D;
+  h.xh_m = rowmap(h.xh, H);
+  // condition rows cat[pos_h, neg_h]: used in place when the caller's rows are adjacent
+  h.cond = (const bf16*)pos_h;
+  if ((const bf16*)neg_h != (const bf16*)pos_h + (size_t)n * H) {
+    HIPCHK(hipMemcpyAsync(h.cat, pos_h, (size_t)n * H * sizeof(bf16), hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(h.cat + (size_t)n * H, neg_h, (size_t)n * H * sizeof(bf16), hipMemcpyDeviceToDevice, st));
+    h.cond = h.cat;
+  }
+  // the per-step head weights (noisy, gate|up, down, final: 170 MB at 1.5B) are
+  // re-read by every diffusion step: default cache policy keeps them in the
+  // Infinity Cache (256 MB) across the S steps.  VibeVoice-Large's (925 MB per
+  // step; 231 MB per rank at TP = 4) stream non-temporal like the LM's
+  h.keep = (size_t)L * 3 * F * H * sizeof(bf16) <= (192ull << 20) && !(c->head_tp && c->tp_size > 1);
+  CHK(gemm(c, gemm_args(c, R, H, H, rowmap(h.cond, H), W(c, "head.cond_w"), EPI_STORE, rowmap(h.condp, H)), st));
+  return 0;
+}
+
+static int head_gemm(vv_ctx* c, const HeadRun& h, GemmArgs g, hipStream_t st) {
+  g.keep = h.keep ? 1 : 0;
+  return gemm(c, g, st);
+}
+
+// all adaLN modulations ([shift|scale|gate] x L, [shift|scale] final) of up to
+// HEAD_SC steps in ONE GEMM: the condition is step-invariant and the timesteps
+// are the schedule's, so silu(cond_proj(c) + t_emb[s]) is known for every step
+// up front -- the 3LH+2H x H adaLN matrix is read once per chunk, not per step
+static int head_mods(vv_ctx* c, const HeadRun& h, int s, hipStream_t st) {
+  if (s % HEAD_SC) return 0;
+  const int H = c->cfg.hidden, sc = std::min(HEAD_SC, c->steps - s);
+  KCHK(launch_head_cond(sc, h.R, H, h.condp, (const bf16*)c->temb.p + (size_t)s * H, h.sa, st));
+  CHK(gemm(c, gemm_args(c, sc * h.R, (int)h.MODW, H, rowmap(h.sa, H), W(c, "head.ada_w"), EPI_STORE,
+                        rowmap(h.mods, h.MODW)), st));
+  return 0;
+}
+
+// x = noisy_images_proj(cat[x, x])  -- both halves read the same n latent rows
+static int head_noisy(vv_ctx* c, const HeadRun& h, const void* x_io, hipStream_t st) {
+  const int H = c->cfg.hidden, D = c->cfg.latent_dim;
+  return head_gemm(c, h, gemm_args(c, h.R, H, D, rowmap(x_io, D, h.n, 0), W(c, "head.noisy_w"), EPI_STORE, h.xh_m),
+                   st);
+}
+
+// layer l of step s: modulate(norm(x)) -> gate|up -> SiLU*up -> down -> x += gate * (.)
+// With the FFN sharded (vv_tp_shard_head) this rank holds head_ffn / tp_size of
+// the hidden columns: gate|up column-parallel, down row-parallel; rank 0 adds
+// the residual, the others contribute gate * partial only (onto zero rows), and
+// the caller sums x over the ranks (all-reduce).
+static int head_layer(vv_ctx* c, const HeadRun& h, int s, int l, hipStream_t st) {
+  const vv_config& k = c->cfg;
+  const int H = k.hidden, F = k.head_ffn;
+  const std::string p = "head." + std::to_string(l);
+  const bf16* mod = h.mods + (size_t)(s % HEAD_SC) * h.R * h.MODW;
+  const int o = 3 * H * l;
+  // modulate(norm(x), shift, scale) fused into gate|up's A load
+  GemmArgs g = gemm_args(c, h.R, 2 * F, H, h.xh_m, W(c, p + ".gu_w"), EPI_SILU_MUL, rowmap(h.act, F));
+  g.xf = xf_norm(W(c, p + ".norm"), k.head_eps, mod, h.MODW, o, o + H);
+  const bool partial = c->head_tp && c->tp_size > 1 && c->tp_rank > 0;
+  if (c->hf_ready && g_head_fused && head_ffn_fits(H, F, h.R)) {   // one launch: head_ffn.hip
+    HeadFfnArgs a;
+    memset(&a, 0, sizeof(a));
+    a.x = h.xh;
+    a.out = h.xh;
+    a.res = partial ? (const bf16*)c->zero_rows.p : h.xh;
+    a.ldx = a.ldres = H;
+    a.nw = W(c, p + ".norm");
+    a.mod = mod;
+    a.ldmod = h.MODW;
+    a.shift_off = o;
+    a.scale_off = o + H;
+    a.gate_off = o + 2 * H;
+    a.R = h.R;
+    a.eps = k.head_eps;
+    a.gu = W(c, p + ".gu_rows");
+    a.dn = W(c, p + ".dn_rows");
+    a.slab = (float*)c->hf_slab.p;
+    a.sync = (unsigned*)c->hf_sync.p;
+    a.err = (unsigned*)c->hf_sync.p + 10 * 32;
+    KCHK(launch_head_ffn(a, st));
+    return 0;
+  }
+  CHK(head_gemm(c, h, g, st));
+  g = gemm_args(c, h.R, H, F, rowmap(h.act, F), W(c, p + ".down_w"), EPI_RES, h.xh_m);
+  g.epi.res = partial ? rowmap(c->zero_rows.p, H) : h.xh_m;
+  g.epi.gate = rowmap(mod + o + 2 * H, h.MODW);
+  return head_gemm(c, h, g, st);
+}
+
+// final layer: modulate(norm_final(x)) -> linear -> CFG + DPM-Solver++ step on x
+static int head_final(vv_ctx* c, const HeadRun& h, int s, void* x_io, float cfg_scale, const float* sde_noise,
+                      hipStream_t st) {
+  const vv_config& k = c->cfg;
+  const int H = k.hidden, D = k.latent_dim, L = k.head_layers;
+  const bf16* mod = h.mods + (size_t)(s % HEAD_SC) * h.R * h.MODW;
+  DpmCoef e = c->coef[s];
+  e.cfg = cfg_scale;
+  // sde-dpmsolver++: this step's [2n, D] fp32 draw; rows [0, n) update the live latents
+  const float* zs = sde_noise ? sde_noise + (size_t)s * h.R * D : nullptr;
+  GemmArgs g = gemm_args(c, h.R, D, H, h.xh_m, W(c, "head.final_w"), EPI_STORE, rowmap(h.v, D));
+  g.xf = xf_norm(nullptr, k.head_eps, mod, h.MODW, 3 * H * L, 3 * H * L + H);
+  if (h.R <= 16) {
+    g.epi.kind = EPI_CFG_DPM;
+    g.dpm.n = h.n;
+    g.dpm.k = e;
+    g.dpm.x = (bf16*)x_io;
+    g.dpm.m1 = h.m1;
+    g.dpm.noise = zs;
+    CHK(head_gemm(c, h, g, st));
+  } else {
+    CHK(head_gemm(c, h, g, st));
+    KCHK(launch_cfg_dpm(h.n, D, e, h.v, (bf16*)x_io, h.m1, zs, st));
+  }
+  return 0;
+}
+
+int vv_tp_shard_head(vv_ctx* c, int on) {
+  if (on && c->tp_size > 1 && c->cfg.head_ffn % 32) FAIL("vv_tp_shard_head: the local head FFN width must be a multiple of 32");
+  c->head_tp = on ? 1 : 0;
   return 0;
 }
 
@@ -1183,39 +1411,18 @@ int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, 
   if (n <= 0) return 0;
   const vv_config& k = c->cfg;
   if (n > k.max_batch) FAIL("vv_diffusion_sample: n > max_batch");
-  const int H = k.hidden, F = k.head_ffn, D = k.latent_dim, L = k.head_layers;
-  const int R = 2 * n;
-  const long long MODW = (3LL * L + 2) * H;
-  bf16* cat = (bf16*)c->head_ws.p;
-  bf16* condp = cat + (size_t)R * H;
-  bf16* sc = condp + (size_t)R * H;
-  bf16* xh = sc + (size_t)R * H;
-  bf16* a = xh + (size_t)R * H;
-  bf16* mods = a + (size_t)R * H;                         // [HEAD_SC steps][R][MODW]
-  bf16* sa = mods + (size_t)HEAD_SC * R * MODW;            // [HEAD_SC steps][R][H] adaLN inputs
-  bf16* act = sa + (size_t)HEAD_SC * R * H;
-  bf16* v = act + (size_t)R * F;
-  bf16* m1 = v + (size_t)R * D;
-  // condition rows cat[pos_h, neg_h]: used in place when the caller's rows are adjacent
-  const bf16* cond = (const bf16*)pos_h;
-  if ((const bf16*)neg_h != (const bf16*)pos_h + (size_t)n * H) {
-    HIPCHK(hipMemcpyAsync(cat, pos_h, (size_t)n * H * sizeof(bf16), hipMemcpyDeviceToDevice, st));
-    HIPCHK(hipMemcpyAsync(cat + (size_t)n * H, neg_h, (size_t)n * H * sizeof(bf16), hipMemcpyDeviceToDevice, st));
-    cond = cat;
-  }
-  // the per-step head weights (noisy, gate|up, down, final: 170 MB at 1.5B) are
-  // re-read by every diffusion step: default cache policy keeps them in the
-  // Infinity Cache (256 MB) across the S steps.  VibeVoice-Large's (925 MB per
-  // step) cannot stay there: they stream non-temporal like the LM's
-  const bool head_keep = (size_t)L * 3 * F * H * sizeof(bf16) <= (192ull << 20);
-  auto hgemm = [&](GemmArgs g) {
-    g.keep = head_keep ? 1 : 0;
-    return gemm(c, g, st);
-  };
-  // cond_proj is step-invariant: computed once per token (bit-identical to per step)
-  CHK(gemm(c, gemm_args(c, R, H, H, rowmap(cond, H), W(c, "head.cond_w"), EPI_STORE, rowmap(condp, H)), st));
-  RowMap xh_m = rowmap(xh, H), a_m = rowmap(a, H);
-  if (g_chain && R <= 16 && c->steps <= HEAD_SC) {
+  const bool sharded = c->head_tp && (c->tp_size > 1 || c->comm);   // (a 1-rank communicator: tests)
+  if (sharded && !c->comm) FAIL("sharded diffusion head without a communicator (vv_tp_init; one process: "
+                                "vv_diffusion_sample_group)");
+  const int H = k.hidden, D = k.latent_dim, L = k.head_layers;
+  HeadRun h;
+  CHK(head_begin(c, n, pos_h, neg_h, h, st));
+  const int R = h.R;
+  const long long MODW = h.MODW;
+  bf16 *mods = h.mods, *act = h.act, *v = h.v, *m1 = h.m1, *sa = h.sa;
+  const int F = k.head_ffn;
+  RowMap xh_m = h.xh_m;
+  if (g_chain && R <= 16 && c->steps <= HEAD_SC && !sharded) {
     // all S steps (noisy, L x [gate|up, down], final + CFG + DPM) in one persistent launch
     auto it = c->head_chain.find(n);
     if (it == c->head_chain.end() || it->second.mode != g_chain) {
@@ -1264,7 +1471,7 @@ int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, 
       }
     }
     if (it != c->head_chain.end() && it->second.nops > 0) {
-      KCHK(launch_head_cond(c->steps, R, H, condp, (const bf16*)c->temb.p, sa, st));
+      KCHK(launch_head_cond(c->steps, R, H, h.condp, (const bf16*)c->temb.p, sa, st));
       CHK(gemm(c, gemm_args(c, c->steps * R, (int)MODW, H, rowmap(sa, H), W(c, "head.ada_w"), EPI_STORE,
                             rowmap(mods, MODW)), st));
       ChainArgs A;
@@ -1278,50 +1485,50 @@ int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, 
     }
   }
   for (int s = 0; s < c->steps; ++s) {
-    // all adaLN modulations ([shift|scale|gate] x L, [shift|scale] final) of up to
-    // HEAD_SC steps in ONE GEMM: the condition is step-invariant and the timesteps
-    // are the schedule's, so silu(cond_proj(c) + t_emb[s]) is known for every step
-    // up front — the 3LH+2H x H adaLN matrix is read once per chunk, not per step
-    if (s % HEAD_SC == 0) {
-      const int sc = std::min(HEAD_SC, c->steps - s);
-      KCHK(launch_head_cond(sc, R, H, condp, (const bf16*)c->temb.p + (size_t)s * H, sa, st));
-      CHK(gemm(c, gemm_args(c, sc * R, (int)MODW, H, rowmap(sa, H), W(c, "head.ada_w"), EPI_STORE,
-                            rowmap(mods, MODW)), st));
-    }
-    const bf16* mod = mods + (size_t)(s % HEAD_SC) * R * MODW;
-    // x = noisy_images_proj(cat[x, x])  -- both halves read the same n latent rows
-    CHK(hgemm(gemm_args(c, R, H, D, rowmap(x_io, D, n, 0), W(c, "head.noisy_w"), EPI_STORE, xh_m)));
+    CHK(head_mods(c, h, s, st));
+    CHK(head_noisy(c, h, x_io, st));
     for (int l = 0; l < L; ++l) {
-      const std::string p = "head." + std::to_string(l);
-      const int o = 3 * H * l;
-      // modulate(norm(x), shift, scale) fused into gate|up's A load
-      GemmArgs g = gemm_args(c, R, 2 * F, H, xh_m, W(c, p + ".gu_w"), EPI_SILU_MUL, rowmap(act, F));
-      g.xf = xf_norm(W(c, p + ".norm"), k.head_eps, mod, MODW, o, o + H);
-      CHK(hgemm(g));
-      g = gemm_args(c, R, H, F, rowmap(act, F), W(c, p + ".down_w"), EPI_RES, xh_m);
-      g.epi.res = xh_m;
-      g.epi.gate = rowmap(mod + o + 2 * H, MODW);
-      CHK(hgemm(g));
+      CHK(head_layer(c, h, s, l, st));
+      if (sharded && !g_tp_null) {   // x = sum over the ranks (rank 0 carried the residual)
+        const ncclResult_t r = ncclAllReduce(h.xh, h.xh, (size_t)R * H, ncclBfloat16, ncclSum, c->comm, st);
+        if (r != ncclSuccess) FAIL(std::string("ncclAllReduce (head): ") + ncclGetErrorString(r));
+      }
     }
-    // final layer: modulate(norm_final(x)) -> linear -> CFG + DPM-Solver++ step on x
-    DpmCoef e = c->coef[s];
-    e.cfg = cfg_scale;
-    // sde-dpmsolver++: this step's [2n, D] fp32 draw; rows [0, n) update the live latents
-    const float* zs = sde_noise ? sde_noise + (size_t)s * R * D : nullptr;
-    GemmArgs g = gemm_args(c, R, D, H, xh_m, W(c, "head.final_w"), EPI_STORE, rowmap(v, D));
-    g.xf = xf_norm(nullptr, k.head_eps, mod, MODW, 3 * H * L, 3 * H * L + H);
-    if (R <= 16) {
-      g.epi.kind = EPI_CFG_DPM;
-      g.dpm.n = n;
-      g.dpm.k = e;
-      g.dpm.x = (bf16*)x_io;
-      g.dpm.m1 = m1;
-      g.dpm.noise = zs;
-      CHK(hgemm(g));
-    } else {
-      CHK(hgemm(g));
-      KCHK(launch_cfg_dpm(n, D, e, v, (bf16*)x_io, m1, zs, st));
+    CHK(head_final(c, h, s, x_io, cfg_scale, sde_noise, st));
+  }
+  return 0;
+}
+
+int vv_diffusion_sample_group(int nr, vv_ctx* const* ctxs, int n, const void* pos_h, const void* neg_h, void* x_io,
+                              float cfg_scale, const float* sde_noise, vv_stream vst) {
+  hipStream_t st = (hipStream_t)vst;
+  if (nr < 1 || nr > 8) FAIL("vv_diffusion_sample_group: 1..8 ranks");
+  if (n <= 0) return 0;
+  HeadRun h[8];
+  SumRows sr;
+  sr.n = nr;
+  for (int r = 0; r < nr; ++r) {
+    vv_ctx* c = ctxs[r];
+    if (c->tp_rank != r || c->tp_size != nr || !c->head_tp)
+      FAIL("vv_diffusion_sample_group: engine r must be TP rank r of n with a sharded head (vv_tp_shard_head)");
+    if (!c->finalized || c->steps != ctxs[0]->steps) FAIL("vv_diffusion_sample_group: engines not finalized alike");
+    if (n > c->cfg.max_batch) FAIL("vv_diffusion_sample_group: n > max_batch");
+    CHK(head_begin(c, n, pos_h, neg_h, h[r], st));
+    sr.p[r] = h[r].xh;
+  }
+  const vv_config& k = ctxs[0]->cfg;
+  const long long count = (long long)h[0].R * k.hidden;
+  for (int s = 0; s < ctxs[0]->steps; ++s) {
+    for (int r = 0; r < nr; ++r) {
+      CHK(head_mods(ctxs[r], h[r], s, st));
+      CHK(head_noisy(ctxs[r], h[r], x_io, st));
     }
+    for (int l = 0; l < k.head_layers; ++l) {
+      for (int r = 0; r < nr; ++r) CHK(head_layer(ctxs[r], h[r], s, l, st));
+      KCHK(launch_sum_rows(sr, count, st));
+    }
+    // the latent update once (every rank would compute the same; rank 0's x is the sum)
+    CHK(head_final(ctxs[0], h[0], s, x_io, cfg_scale, sde_noise, st));
   }
   return 0;
 }

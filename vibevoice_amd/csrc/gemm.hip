@@ -52,6 +52,14 @@ DEV void stamp(const GemmArgs& a, int which) {
 }
 
 // ------------------------------------------------------------------ GEMV
+// Index math of the prologues.  blockDim.x is a 16-bit implicit kernel
+// argument; gfx950 has no 16-bit scalar load, so a read of it that the
+// compiler cannot prove unclobbered (any global store earlier in the kernel,
+// e.g. a timing stamp) becomes a VECTOR load + s_waitcnt vmcnt(0): a whole
+// memory round trip before the first A / weight load was issued.  Kernels read
+// it once, first (a scalar load), and the K ranges use 32-bit arithmetic (the
+// 64-bit divisions were ~300 VALU instructions ahead of the first load).
+DEV int part_of(int len, int i, int n) { return (int)((unsigned)(len * i) / (unsigned)n); }
 // Split-K hand-off of the 16 x (16*MREP) fp32 tile between the workgroups of one
 // tile column: every split stores its slab, takes a ticket, the last arriver
 // sums the slabs in split order (deterministic) and runs the epilogue.
@@ -60,13 +68,13 @@ DEV void stamp(const GemmArgs& a, int which) {
 //              one agent atomic per workgroup, sc1 loads by the last arriver
 //              (MI355X_MICROARCH.md "Valid forms", first table row)
 // Returns true in the workgroup that must run the epilogue (red[] = sums).
-DEV bool splitk_handoff(const GemmArgs& a, float* red, int TILE, unsigned* last_flag) {
+DEV bool splitk_handoff(const GemmArgs& a, float* red, int TILE, unsigned* last_flag, int NT) {
   float* slab = a.ws + ((long long)blockIdx.x * a.ksplit + blockIdx.y) * TILE;
   const int t = threadIdx.x;
   if (a.handoff == 1) {
-    for (int e = t; e < TILE; e += blockDim.x) __hip_atomic_store(slab + e, red[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int e = t; e < TILE; e += NT) __hip_atomic_store(slab + e, red[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
-    for (int e = t; e < TILE; e += blockDim.x) slab[e] = red[e];
+    for (int e = t; e < TILE; e += NT) slab[e] = red[e];
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -88,7 +96,7 @@ DEV bool splitk_handoff(const GemmArgs& a, float* red, int TILE, unsigned* last_
   __syncthreads();
   if (!*last_flag) return false;
   const float* slabs = a.ws + (long long)blockIdx.x * a.ksplit * TILE;
-  for (int e = t; e < TILE; e += blockDim.x) {
+  for (int e = t; e < TILE; e += NT) {
     float s = 0.f;
     if (a.handoff == 1) {
       for (int k = 0; k < a.ksplit; ++k) s += __hip_atomic_load(slabs + k * TILE + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -120,8 +128,18 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   __shared__ float inv_s[16];
   __shared__ float red[8 * 256];
   __shared__ unsigned last_flag;
+  const int NT = blockDim.x, NW = NT >> 6;   // first: a scalar load (see part_of)
+  // XF_MIX: the (<= 4) samples' conv-buffer slot bases, read before any store
+  // so they are scalar loads issued together (as guarded per-slot vector loads
+  // each took a round trip of its own)
+  long long sbase[4] = {0, 0, 0, 0};
+  if constexpr (XF == XF_MIX) {
+    const int nsl = a.M / a.xf.T;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sbase[q] = (long long)a.xf.slots[min(q, nsl - 1)] * a.xf.buf_sB;
+  }
   stamp(a, 0);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, NW = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   // The workgroup owns TPW consecutive 16-row weight tiles and stages the A
   // rows once for all of them (at M = 16 one tile per workgroup re-read the
@@ -135,10 +153,10 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   const bool tile_ok = TPW == 1 || tile < ntile;
   const int nchunk = a.K >> 5;
   // this workgroup's chunk range, then each wave's
-  const int b0 = (int)((long long)nchunk * blockIdx.y / a.ksplit);
-  const int b1 = (int)((long long)nchunk * (blockIdx.y + 1) / a.ksplit);
-  const int c0 = b0 + (int)((long long)(b1 - b0) * kwv / KW);
-  const int c1 = tile_ok ? b0 + (int)((long long)(b1 - b0) * (kwv + 1) / KW) : c0;
+  const int b0 = a.ksplit == 1 ? 0 : part_of(nchunk, blockIdx.y, a.ksplit);
+  const int b1 = a.ksplit == 1 ? nchunk : part_of(nchunk, blockIdx.y + 1, a.ksplit);
+  const int c0 = b0 + part_of(b1 - b0, kwv, KW);
+  const int c1 = tile_ok ? b0 + part_of(b1 - b0, kwv + 1, KW) : c0;
   // MFMA-packed W (a wave past the last tile streams nothing; its clamped
   // prologue loads read tile 0)
   const bf16* wrow = a.w + (long long)(tile_ok ? tile : 0) * a.K * 16 + lane * 8;
@@ -156,7 +174,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   float* part = (float*)(smem + (((size_t)a.M * lds_ld * 2 + 15) & ~(size_t)15));
   bf16x8 wa[U], wb[U];
   constexpr int Q = 4;   // A items per thread on the fast path
-  const bool fast = a.M * n8 <= Q * (int)blockDim.x;
+  const bool fast = a.M * n8 <= Q * NT;
   // row-per-wave norm prologue: items per lane per row (IPR) x rows per wave (RPW)
   // (RW instantiations only; the host picks them for eligible shapes, gemv1_rw)
   const int ipr = n8 >> 6, rpw = (a.M + NW - 1) / NW;
@@ -207,6 +225,8 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
       ss = wave_sum(ss);
       const float inv = rsqrtf(ss / (float)a.K + a.xf.eps);
       const int m = wave * RPW + r;
+      // (the uniform has_w / has_mod tests stay per element: hoisting them into
+      // specialised copies raised the kernel to 180 VGPRs, 3 -> 2 waves / SIMD)
       if (m < a.M) {
 #pragma unroll
         for (int i = 0; i < IPR; ++i) {
@@ -243,6 +263,10 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
       for (int i = 0; i < IPR; ++i)
         __builtin_amdgcn_global_load_lds((const void*)(xr + (lane + 64 * i) * 8),
                                          (__attribute__((address_space(3))) void*)(xrow_l + 64 * i * 8), 16, 0, 0);
+      // the counted wait below needs exactly these loads younger than the DMA,
+      // in this order: sched_barrier fences keep the scheduler from moving any
+      // of them across
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < IPR; ++i) {
         const int k = (lane + 64 * i) * 8;
@@ -251,8 +275,10 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
         sc[i] = *(const bf16x8*)(md + a.xf.scale_off + k);
       }
     }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
+    __builtin_amdgcn_sched_barrier(0);
     if (wave < a.M) {
       // the DMA is older than 3 * IPR operand loads and the weight loads
       constexpr int after = 3 * IPR + U;
@@ -303,8 +329,12 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     // term for term (bit-identical), one round trip of partial loads here instead
     // of a ticket + merge at the attention's tail.  Item (m, 8 dims of head hq).
     const int nsp = a.xf.nsplit;
+    // the weight stream first: the merge's two dependent round trips (query
+    // length, then the partials) then overlap it instead of preceding it
+#pragma unroll
+    for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
 #pragma unroll 1
-    for (int e = threadIdx.x; e < a.M * n8; e += blockDim.x) {
+    for (int e = threadIdx.x; e < a.M * n8; e += NT) {
       const int m = e / n8, k = (e - m * n8) * 8;
       const int hq = k >> 7, j0 = k & 127;
       const int len = a.xf.qpos[m] + 1;
@@ -349,8 +379,6 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
       for (int jj = 0; jj < 8; ++jj) o8[jj] = tobf(num[jj] / den);
       *(bf16x8*)(xs + m * lds_ld + k) = o8;
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
   } else if (XF == XF_MIX) {
     // Codec Block1D front half for the M = ns * T rows (k_mix's math and
     // summation order, elementwise.hip): every workgroup recomputes it (a few
@@ -359,7 +387,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     // x rows and history rows are issued together ahead of the weight stream
     // (the slot ids come through the scalar cache), the raw x rows stay in LDS
     // (xs) and are overwritten by y, then by fc1's normalised input.
-    const int C = a.K, T = a.xf.T, ctx = a.xf.ctx, ns = a.M / T, NT = blockDim.x;
+    const int C = a.K, T = a.xf.T, ctx = a.xf.ctx, ns = a.M / T;
     bf16* nrm = (bf16*)part;                                 // [ns][ctx + T][C] conv input rows
     float* ssp = (float*)(nrm + (size_t)ns * (ctx + T) * C); // [M][n8] partial sums of squares
     const bool writer = blockIdx.x == 0;
@@ -371,25 +399,30 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     gv = *(const bf16x8*)(a.xf.gamma + c2 * 8);
     wf = *(const bf16x8*)(a.xf.ffn_w + c2 * 8);
     wn = *(const bf16x8*)(a.xf.w + c2 * 8);
-    long long sbase[4];                                      // ns <= 4 (host check)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) sbase[q] = q < ns ? (long long)a.xf.slots[q] * a.xf.buf_sB : 0;
-    // items [0, M*n8): x row m; [M*n8, (M + ns*ctx)*n8): history row h of sample s
-    const int nx = a.M * n8, nitem = (a.M + ns * ctx) * n8;
-    for (int e0 = threadIdx.x, first = 1; e0 < nitem; e0 += 8 * NT, first = 0) {
+    // items [0, M*n8): x row m; [M*n8, (M + ns*ctx)*n8): history row h of sample s.
+    // Every load is unconditional from an address chosen by selects (items past
+    // the end re-read the last one): guarded loads, and rm_off's optional slot
+    // lookup, compiled to a branch + s_waitcnt vmcnt(0) per item -- eight
+    // serialized round trips per pass.  (x rows: host-checked plain map, no idx.)
+    // Rows, not items: the n8 consecutive threads of a row share it, so thread t
+    // takes rows t / n8 + j * (NT / n8) -- no per-item division (the item form
+    // spent ~100 VALU per item on index math ahead of the weight stream).
+    constexpr int CTX = 6;                                    // host-checked (k = 7)
+    const int nrow = a.M + ns * CTX, rpt = NT / n8, rt = threadIdx.x / n8, nx = a.M * n8;
+    const bf16* xbase = (const bf16*)a.a.base;
+    for (int r0 = 0, first = 1; r0 < nrow; r0 += 8 * rpt, first = 0) {
       bf16x8 v[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const int e = e0 + q * NT;
-        if (e < nx) {
-          v[q] = *(const bf16x8*)(rm_bf(a.a, e / n8) + c2 * 8);
-        } else if (e < nitem) {
-          const int hr = (e - nx) / n8, s_ = hr / ctx;
-          long long sb = sbase[0];
+        const int R = min(r0 + rt + q * rpt, nrow - 1);
+        const int mx = min(R, a.M - 1), gx = mx / a.a.T;
+        const bf16* px = xbase + gx * a.a.sB + (long long)(mx - gx * a.a.T) * a.a.sT;
+        const int hr = max(R - a.M, 0), s_ = hr / CTX;
+        long long sb = sbase[0];
 #pragma unroll
-          for (int q2 = 1; q2 < 4; ++q2) sb = s_ == q2 ? sbase[q2] : sb;
-          v[q] = *(const bf16x8*)(a.xf.buf + sb + (long long)(hr - s_ * ctx) * C + c2 * 8);
-        }
+        for (int q2 = 1; q2 < 4; ++q2) sb = s_ == q2 ? sbase[q2] : sb;
+        const bf16* ph = a.xf.buf + sb + (long long)(hr - s_ * CTX) * C;
+        v[q] = *(const bf16x8*)((R < a.M ? px : ph) + c2 * 8);
       }
       if (first) {
 #pragma unroll
@@ -397,17 +430,16 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
       }
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const int e = e0 + q * NT;
-        if (e < nx) {
-          const int m = e / n8;
-          *(bf16x8*)(xs + m * lds_ld + c2 * 8) = v[q];
+        const int R = r0 + rt + q * rpt;
+        if (R < a.M) {
+          *(bf16x8*)(xs + R * lds_ld + c2 * 8) = v[q];
           float ss = 0.f;
 #pragma unroll
           for (int j = 0; j < 8; ++j) ss += bf(v[q][j]) * bf(v[q][j]);
-          ssp[e] = ss;
-        } else if (e < nitem) {
-          const int hr = (e - nx) / n8, s_ = hr / ctx;
-          *(bf16x8*)(nrm + ((size_t)s_ * (ctx + T) + (hr - s_ * ctx)) * C + c2 * 8) = v[q];
+          ssp[R * n8 + c2] = ss;
+        } else if (R < nrow) {
+          const int hr = R - a.M, s_ = hr / CTX;
+          *(bf16x8*)(nrm + ((size_t)s_ * (CTX + T) + (hr - s_ * CTX)) * C + c2 * 8) = v[q];
         }
       }
     }
@@ -482,31 +514,42 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     }
   } else if (fast) {
     bf16x8 xv[Q], wv[Q], sh[Q], sc[Q];
+    // every A-side load unconditional (items past the end re-read the last;
+    // absent operands re-read the row) and, for a plain row map, no slot
+    // lookup: a guarded load compiled to a branch + s_waitcnt vmcnt(0) at its
+    // join, so each item waited for the one before it and the weight stream
+    // behind them was issued several round trips late
+    const int ne = a.M * n8;
+    const bool has_w = XF == XF_NORM ? a.xf.w != nullptr : XF == XF_SILU_ADD;
+    const bool has_mod = XF == XF_NORM && a.xf.mod != nullptr;
+    auto fast_loads = [&](auto plain_c) {
+      constexpr bool PLAIN = decltype(plain_c)::value;
 #pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const int e = threadIdx.x + q * blockDim.x;
-      if (e < a.M * n8) {
+      for (int q = 0; q < Q; ++q) {
+        const int e = min(threadIdx.x + q * NT, ne - 1);
         const int m = e / n8, k = b0 * 32 + (e - m * n8) * 8;
-        xv[q] = *(const bf16x8*)(rm_bf(a.a, m) + k);
+        const bf16* xr = PLAIN ? rm_bf_plain(a.a, m) : rm_bf(a.a, m);
+        xv[q] = *(const bf16x8*)(xr + k);
+        if (XF == XF_NORM || XF == XF_SILU_ADD) {
+          const bf16* wp = has_w ? (XF == XF_NORM ? a.xf.w : a.xf.vec) : xr;
+          wv[q] = *(const bf16x8*)(wp + k);
+        }
         if (XF == XF_NORM) {
-          if (a.xf.w) wv[q] = *(const bf16x8*)(a.xf.w + k);
-          if (a.xf.mod) {
-            const bf16* md = a.xf.mod + (long long)m * a.xf.mod_ld;
-            sh[q] = *(const bf16x8*)(md + a.xf.shift_off + k);
-            sc[q] = *(const bf16x8*)(md + a.xf.scale_off + k);
-          }
-        } else if (XF == XF_SILU_ADD) {
-          wv[q] = *(const bf16x8*)(a.xf.vec + k);
+          const bf16* md = has_mod ? a.xf.mod + (long long)m * a.xf.mod_ld : xr;
+          sh[q] = *(const bf16x8*)(md + (has_mod ? a.xf.shift_off : 0) + k);
+          sc[q] = *(const bf16x8*)(md + (has_mod ? a.xf.scale_off : 0) + k);
         }
       }
-    }
+    };
+    if (a.a.idx) fast_loads(std::false_type());
+    else fast_loads(std::true_type());
 #pragma unroll
     for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
     if (XF == XF_NORM) {
       // per-item sums of squares -> LDS, rows reduced in a fixed order
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
-        const int e = threadIdx.x + q * blockDim.x;
+        const int e = threadIdx.x + q * NT;
         if (e < a.M * n8) {
           float ss = 0.f;
 #pragma unroll
@@ -529,7 +572,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     }
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-      const int e = threadIdx.x + q * blockDim.x;
+      const int e = threadIdx.x + q * NT;
       if (e < a.M * n8) {
         const int m = e / n8, k8 = (e - m * n8) * 8;
         bf16x8 o = xv[q];
@@ -553,19 +596,19 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     // many rows (B >= 8 batches): weights first, then the A rows in batches
 #pragma unroll
     for (int u = 0; u < U; ++u) wa[u] = ldw<KEEP>(wrow + min(c0 + u, max(c1 - 1, 0)) * 512);
-    for (int e0 = threadIdx.x; e0 < a.M * n8; e0 += 4 * blockDim.x) {
+    const int ne = a.M * n8;
+    const bool plain = !a.a.idx;
+    for (int e0 = threadIdx.x; e0 < ne; e0 += 4 * NT) {
       bf16x8 xv[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int e = e0 + q * blockDim.x;
-        if (e < a.M * n8) {
-          const int m = e / n8, k8 = (e - m * n8) * 8;
-          xv[q] = *(const bf16x8*)(rm_bf(a.a, m) + b0 * 32 + k8);
-        }
+      for (int q = 0; q < 4; ++q) {   // unconditional loads (see the fast path)
+        const int e = min(e0 + q * NT, ne - 1);
+        const int m = e / n8, k8 = (e - m * n8) * 8;
+        xv[q] = *(const bf16x8*)((plain ? rm_bf_plain(a.a, m) : rm_bf(a.a, m)) + b0 * 32 + k8);
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int e = e0 + q * blockDim.x;
+        const int e = e0 + q * NT;
         if (e < a.M * n8) {
           const int m = e / n8, k8 = (e - m * n8) * 8;
           *(bf16x8*)(xs + m * lds_ld + k8) = xv[q];
@@ -591,7 +634,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         }
-      for (int e = threadIdx.x; e < a.M * n8; e += blockDim.x) {
+      for (int e = threadIdx.x; e < a.M * n8; e += NT) {
         const int m = e / n8, k8 = (e - m * n8) * 8;
         bf16x8* px = (bf16x8*)(xs + m * lds_ld + k8);
         *px = xform<XF>(a, *px, m, b0 * 32 + k8, XF == XF_NORM ? inv_s[m] : 0.f);
@@ -634,7 +677,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   for (int i = 0; i < 4; ++i) red[(wave * 4 + i) * 64 + lane] = acc[i];
   __syncthreads();
   if (KW > 1) {
-    for (int e = threadIdx.x; e < TPW * 256; e += blockDim.x) {
+    for (int e = threadIdx.x; e < TPW * 256; e += NT) {
       const int base = (e >> 8) * KW * 256 + (e & 255);
       float s = 0.f;
       for (int w = 1; w < KW; ++w) s += red[base + w * 256];
@@ -642,7 +685,7 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     }
     __syncthreads();
   }
-  if (a.ksplit > 1 && !splitk_handoff(a, red, 256, &last_flag)) return;   // host: ksplit > 1 => TPW == 1
+  if (a.ksplit > 1 && !splitk_handoff(a, red, 256, &last_flag, NT)) return;   // host: ksplit > 1 => TPW == 1
   if (wave < TPW && (TPW == 1 || blockIdx.x * TPW + wave < ntile)) {
     float v[4];
 #pragma unroll
@@ -662,14 +705,15 @@ __global__ void __launch_bounds__(512) k_gemv(GemmArgs a) {
   __shared__ float red[8 * MREP * 256];
   __shared__ float inv_s[64];
   __shared__ unsigned last_flag;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, NW = blockDim.x >> 6;
+  const int NT = blockDim.x, NW = NT >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int n0 = blockIdx.x * 16;
   const int nchunk = a.K >> 5;
-  const int b0 = (int)((long long)nchunk * blockIdx.y / a.ksplit);
-  const int b1 = (int)((long long)nchunk * (blockIdx.y + 1) / a.ksplit);
-  const int c0 = b0 + (int)((long long)(b1 - b0) * wave / NW);
-  const int c1 = b0 + (int)((long long)(b1 - b0) * (wave + 1) / NW);
+  const int b0 = a.ksplit == 1 ? 0 : part_of(nchunk, blockIdx.y, a.ksplit);
+  const int b1 = a.ksplit == 1 ? nchunk : part_of(nchunk, blockIdx.y + 1, a.ksplit);
+  const int c0 = b0 + part_of(b1 - b0, wave, NW);
+  const int c1 = b0 + part_of(b1 - b0, wave + 1, NW);
   const bf16* wrow = a.w + (long long)(n0 >> 4) * a.K * 16 + lane * 8;  // MFMA-packed W
   const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
   if (XF == XF_NORM) {
@@ -729,14 +773,14 @@ __global__ void __launch_bounds__(512) k_gemv(GemmArgs a) {
     for (int i = 0; i < 4; ++i) red[(wave * MREP * 4 + mr * 4 + i) * 64 + lane] = acc[mr][i];
   __syncthreads();
   if (NW > 1) {
-    for (int e = threadIdx.x; e < TILE; e += blockDim.x) {
+    for (int e = threadIdx.x; e < TILE; e += NT) {
       float s = 0.f;
       for (int w = 1; w < NW; ++w) s += red[w * TILE + e];
       red[e] += s;
     }
     __syncthreads();
   }
-  if (a.ksplit > 1 && !splitk_handoff(a, red, TILE, &last_flag)) return;
+  if (a.ksplit > 1 && !splitk_handoff(a, red, TILE, &last_flag, NT)) return;
   for (int mr = wave; mr < MREP; mr += NW) {
     float v[4];
 #pragma unroll
@@ -1326,6 +1370,12 @@ constexpr unsigned WC_VM12 = 0x0F7C, WC_VM8_LGKM0 = 0x0078, WC_LGKM0 = 0xC07F, W
 // v_mfma_f32_32x32x16_bf16 -- 0.305 vs 0.443 of peak on gate|up -- and the
 // ablation builds that located the ceiling; neither is built any more.)
 constexpr int GX_M = 256, GX_N = 256, GX_NS = 4;
+// fewest 256 x 256 tiles that take k_gemm_xl: 3/4 of the 256 CUs.  One round of
+// 192 tiles (the diffusion head's down projection at M = 8,192: 32 x 6) runs
+// at the per-tile rate of k_gemm_xl's multi-round launches (~1,000 TF/s at
+// 384 tiles, DESIGN.md "MFMA utilisation") where k_gemm_big's 768 128² tiles
+// reached 665 TF/s
+constexpr int GX_MIN_TILES = 192;
 constexpr int GX_STAGE = 32 * 512;                       // elements per stage
 constexpr size_t GX_LDS = (size_t)GX_NS * GX_STAGE * 2;   // 128 KB
 
@@ -1578,7 +1628,7 @@ bool gemm_uses_xl(const GemmArgs& a) {
   const int total_xl = ((a.M + GX_M - 1) / GX_M) * (a.N / GX_N);
   return !(a.M <= 64 && (a.M <= 16 || a.M <= g_gemv_max_m || a.epi.kind == EPI_CFG_DPM)) && a.epi.kind != EPI_CFG_DPM &&
          g_gemm_big == 3 && a.M >= GEMM_BIG_M && a.N % GX_N == 0 && a.K % 32 == 0 &&
-         (total_xl >= GEMM_BIG_TILES || g_gemm_big_any);
+         (total_xl >= GX_MIN_TILES || g_gemm_big_any);
 }
 
 constexpr int GEMM_BN32 = 128;   // fewer 64-wide-tile workgroups than this: 32-wide tiles
@@ -1589,10 +1639,10 @@ static int launch_gemm_xf(const GemmArgs& a, hipStream_t st) {
   // x K <= 1,024: 24 - 104 such tiles) are faster as k_gemm's 4x more 64 x 64
   // workgroups (B = 8 step 5.53 ms vs 5.83), a 1K-token prompt's o / down /
   // q|k|v projections (108 - 144 tiles, K >= 1,536) on k_gemm_big (14.5 -> 13.4 ms)
-  // k_gemm_xl with >= one 256 x 256 tile per CU (16K-token prefill: 384 - 4,480 tiles)
+  // k_gemm_xl with >= GX_MIN_TILES 256 x 256 tiles (16K-token prefill: 384 - 4,480 tiles)
   const int total_xl = ((a.M + GX_M - 1) / GX_M) * (a.N / GX_N);
   if (XF == XF_NONE && g_gemm_big == 3 && a.M >= GEMM_BIG_M && a.N % GX_N == 0 && a.K % 32 == 0 &&
-      (total_xl >= GEMM_BIG_TILES || g_gemm_big_any)) {
+      (total_xl >= GX_MIN_TILES || g_gemm_big_any)) {
     static const bool attr = hipFuncSetAttribute((const void*)k_gemm_xl, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                  (int)GX_LDS) == hipSuccess;   // once (thread-safe static init)
     if (!attr) return 2;
@@ -1632,25 +1682,6 @@ size_t gemv_mix_lds(int M, int T, int C) {
   return lds <= 98304 ? lds : 0;
 }
 
-// The plan launch_gemm would run for a decode GEMV on k_gemv1 (chain.hip's
-// mirror mode reproduces it bit for bit).  Returns 1 if the shape takes another kernel.
-int gemv_plan_query(const GemmArgs& a0, int* nw, int* ksplit, int* tpw, int* fast) {
-  GemmArgs a = a0;
-  if (a.M <= 0 || a.M > 16 || a.K % 32 || a.N % 16 || a.xf.kind == XF_MIX) return 1;
-  GemmPlan p = gemv_plan(a.N, a.K, a.M);
-  if (p.nw > max_waves(1)) p.nw = max_waves(1);
-  a.ksplit = p.ksplit;
-  if (a.ksplit > 1 && (!a.ws || !a.counters || a.N / 16 > 65536)) a.ksplit = 1;
-  if (!gemv1_fits(a)) return 1;
-  int t = 1;
-  if (a.ksplit == 1 && (p.tpw == 2 || p.tpw == 4 || p.tpw == 8) && p.nw % p.tpw == 0) t = p.tpw;
-  *nw = p.nw;
-  *ksplit = a.ksplit;
-  *tpw = t;
-  *fast = 64 * p.nw;   // k_gemv1's fast staging: M * n8 <= 4 * blockDim.x
-  return 0;
-}
-
 // The decode-GEMV launch plan for a (M <= 64): waves, K split, tiles per
 // workgroup; sets a.ksplit / a.handoff / a.tpw (launch_gemm, vv_gemv_plan).
 static GemmPlan gemv_resolve(GemmArgs& a) {
@@ -1679,6 +1710,21 @@ static GemmPlan gemv_resolve(GemmArgs& a) {
   if (mrep == 1 && a.ksplit == 1 && a.xf.kind != XF_MIX && (p.tpw == 2 || p.tpw == 4 || p.tpw == 8) && p.nw % p.tpw == 0 && gemv1_fits(a))
     a.tpw = p.tpw;
   return p;
+}
+
+// The plan launch_gemm would run for a decode GEMV on k_gemv1 (chain.hip's
+// mirror mode reproduces it bit for bit): gemv_resolve's, so one function owns
+// the plan.  Returns 1 if the shape takes another kernel.
+int gemv_plan_query(const GemmArgs& a0, int* nw, int* ksplit, int* tpw, int* fast) {
+  GemmArgs a = a0;
+  if (a.M <= 0 || a.M > 16 || a.K % 32 || a.N % 16 || a.xf.kind == XF_MIX || a.xf.kind == XF_ATTN_MERGE) return 1;
+  const GemmPlan p = gemv_resolve(a);
+  if (!gemv1_fits(a)) return 1;
+  *nw = p.nw;
+  *ksplit = a.ksplit;
+  *tpw = a.tpw;
+  *fast = 64 * p.nw;   // k_gemv1's fast staging: M * n8 <= 4 * blockDim.x
+  return 0;
 }
 
 // Host-only plan query (no device work; tests and tools): the kernel form and
@@ -1734,7 +1780,7 @@ int launch_gemm(GemmArgs a, hipStream_t st) {
     dim3 grid((a.N / 16 + a.tpw - 1) / a.tpw, a.ksplit), block(64 * p.nw);
     if (a.xf.kind == XF_MIX) {
       const size_t lds = gemv_mix_lds(a.M, a.xf.T, a.K);
-      if (mrep != 1 || a.ksplit != 1 || !lds || (64 * p.nw) % (a.K / 8) || a.xf.ctx != 6) return 1;
+      if (mrep != 1 || a.ksplit != 1 || !lds || (64 * p.nw) % (a.K / 8) || a.xf.ctx != 6 || a.a.idx) return 1;
       // tiles per workgroup (diagnostic plans only so far): the Block1D front half is
       // recomputed once per workgroup, so fewer, wider workgroups recompute it less
       const int mt = (p.tpw == 2 || p.tpw == 4) && p.nw % p.tpw == 0 ? p.tpw : 1;

@@ -175,6 +175,12 @@ struct AttnArgs {
   unsigned long long* stamps;   // diagnostics only (tools/attn_stamps.py): 4 stamps per workgroup
   int prefill;          // 1: k_attn_pf (query rows in runs sharing a slot; no splits), see attn_use_prefill
   int defer;            // 1: every active split writes its partial, the consumer (o_proj, XF_ATTN_MERGE) merges
+  int group;            // > 0 (long contexts): splits merge in groups of `group` consecutive splits -- the
+                        // last-arriving workgroup of a group merges its partials into part_o2 / part_ml2
+                        // ([nq][nh][ngroups][d] / [..][2]), which the consumer merges (XF_ATTN_MERGE)
+  int ngroups;
+  float* part_o2;
+  float* part_ml2;
 };
 
 // out_r = sum_r in_r for every r (single-process tensor-parallel group)
@@ -221,6 +227,28 @@ int launch_chain(const ChainArgs& A, size_t lds, hipStream_t st);
 // the per-op kernel's plan for a decode GEMV (gemm.hip): 0 and the plan when it runs k_gemv1
 // (*fast = its workgroup's threads)
 int gemv_plan_query(const GemmArgs& a, int* nw, int* ksplit, int* tpw, int* fast);
+
+// ---- fused diffusion-head FFN layer (head_ffn.hip): modulate(norm(x)) -> gate|up
+// -> SiLU*up -> down -> x += gate * (.), one launch per layer at 2n <= 4 rows
+struct HeadFfnArgs {
+  const bf16* x;            // [R][H] rows (ld ldx), read for the norm
+  bf16* out;                // [R][H] rows (ld ldx): x + gate * ffn (in place: out == x)
+  const bf16* res;          // residual rows (ld ldres): x, or zero rows on a sharded rank > 0
+  const bf16* nw;           // RMSNorm weight [H]
+  const bf16* mod;          // adaLN rows [R][ldmod]: shift / scale / gate at the offsets
+  long long ldx, ldres, ldmod;
+  int shift_off, scale_off, gate_off, R;
+  float eps;
+  int pad_;
+  const bf16* gu;           // gate / up rows in the kernel's stream order (weights.py: head_ffn_pack)
+  const bf16* dn;           // down_proj transposed: [F][H]
+  float* slab;              // [G][R][H] fp32 partial sums of down, one per workgroup
+  unsigned* sync;           // 10 lines of 32 words: 8 shard counters, top counter, generation
+  unsigned* err;            // set to 1 when the grid wait gave up
+};
+bool head_ffn_fits(int H, int F, int R);
+int head_ffn_grid();
+int launch_head_ffn(const HeadFfnArgs& a, hipStream_t st);
 
 size_t gemv_mix_lds(int M, int T, int C);
 int launch_gemm(GemmArgs a, hipStream_t st);

@@ -10,7 +10,7 @@ import torch
 from . import _lib
 from .config import VibeVoiceConfig
 from .schedule import Schedule
-from .weights import codec_channels, pack
+from .weights import codec_channels, head_tp_check, pack
 
 _VALID_IDS_DEFAULT = None
 
@@ -24,9 +24,10 @@ def _stream(stream=None):
     return ctypes.c_void_p(s.cuda_stream)
 
 
-def engine_config(cfg: VibeVoiceConfig, max_batch, max_ctx, tp_size=1):
+def engine_config(cfg: VibeVoiceConfig, max_batch, max_ctx, tp_size=1, tp_head=False):
     """vv_config of one engine; with tensor parallelism the LM head and
-    intermediate counts are this rank's local ones."""
+    intermediate counts are this rank's local ones (and the head FFN width,
+    with tp_head)."""
     lm = cfg.decoder_config
     hc = cfg.diffusion_head_config
     c = _lib.VVConfig()
@@ -39,7 +40,7 @@ def engine_config(cfg: VibeVoiceConfig, max_batch, max_ctx, tp_size=1):
     c.rms_eps = lm.rms_norm_eps
     c.rope_theta = lm.rope_theta
     c.head_layers = hc.head_layers
-    c.head_ffn = int(hc.hidden_size * hc.head_ffn_ratio)
+    c.head_ffn = int(hc.hidden_size * hc.head_ffn_ratio) // (tp_size if tp_head else 1)
     c.latent_dim = hc.latent_size
     c.head_eps = hc.rms_norm_eps
     c.n_stages = len(cfg.dec_depths)
@@ -63,13 +64,15 @@ class Engine:
     """One device-resident VibeVoice model instance."""
 
     def __init__(self, cfg: VibeVoiceConfig, state_dict, device="cuda", max_batch=1, max_ctx=4096,
-                 valid_ids=None, tp_rank=0, tp_size=1, tp_unique_id=None, packed=None):
+                 valid_ids=None, tp_rank=0, tp_size=1, tp_unique_id=None, packed=None, tp_head=False):
         """tp_size > 1: rank tp_rank's shard of the LM; tp_unique_id (bytes of
         vv_tp_unique_id, shared by the group) creates its RCCL communicator, None
         leaves it for a single-process group (lm_forward_group).
         packed: another engine's packed weights (`Engine.w`) to bind instead of
         packing `state_dict` again — a second context over the same device
-        weights (the standalone tokenizer API's own codec slots)."""
+        weights (the standalone tokenizer API's own codec slots).
+        tp_head: shard the diffusion head's FFN over the TP group as well
+        (vv_tp_shard_head)."""
         L = _lib.lib()
         self.cfg = cfg
         self.device = torch.device(device)
@@ -81,17 +84,22 @@ class Engine:
         self.latent = cfg.diffusion_head_config.latent_size
         self.hop = cfg.hop
         self.tp_rank, self.tp_size = tp_rank, tp_size
+        self.tp_head = bool(tp_head and tp_size > 1)
+        if self.tp_head:
+            head_tp_check(cfg, tp_size)
         with torch.cuda.device(self.device):
             self.w = packed if packed is not None else pack(state_dict, cfg, self.device, tp_rank=tp_rank,
-                                                            tp_size=tp_size)
+                                                            tp_size=tp_size, tp_head=self.tp_head)
             h = ctypes.c_void_p()
-            self._ecfg = engine_config(cfg, max_batch, max_ctx, tp_size)
+            self._ecfg = engine_config(cfg, max_batch, max_ctx, tp_size, self.tp_head)
             _lib.check(L.vv_create(ctypes.byref(self._ecfg), self.device.index or 0, ctypes.byref(h)), "create")
             self.h = h
             if tp_size > 1 or tp_unique_id is not None:
                 uid = None if tp_unique_id is None else ctypes.create_string_buffer(bytes(tp_unique_id),
                                                                                    len(tp_unique_id))
                 _lib.check(L.vv_tp_init(h, tp_rank, tp_size, uid), "tp_init")
+                if self.tp_head:
+                    _lib.check(L.vv_tp_shard_head(h, 1), "tp_shard_head")
             for name, t in self.w.items():
                 shape = (ctypes.c_int64 * max(1, t.dim()))(*t.shape)
                 _lib.check(L.vv_bind_weight(h, name.encode(), _ptr(t), shape, t.dim()), f"bind {name}")
@@ -118,6 +126,16 @@ class Engine:
         arr = (ctypes.c_int * len(ids))(*ids)
         _lib.check(_lib.lib().vv_set_valid_ids(self.h, len(ids), arr), "set_valid_ids")
         self.n_valid = len(ids)
+
+    def check_sync(self):
+        """Raise if a fused head layer's in-launch grid wait gave up since the
+        last check (its outputs are then invalid; vv_sync_error).  Synchronises."""
+        r = _lib.lib().vv_sync_error(self.h)
+        if r < 0:
+            _lib.check(r, "sync_error")
+        if r:
+            raise RuntimeError("fused diffusion-head layer: an in-launch grid wait gave up (workgroups not "
+                               "co-resident); the outputs since the last check are invalid")
 
     def set_schedule(self, schedule):
         """Replace the solver (model.model.noise_scheduler = ...); coefficients are
@@ -200,6 +218,20 @@ class Engine:
         _lib.check(_lib.lib().vv_diffusion_sample(self.h, pos_h.shape[0], _ptr(pos_h), _ptr(neg_h), _ptr(x_io),
                                                   float(cfg_scale), _ptr(sde_noise), _stream(stream)),
                    "diffusion_sample")
+        return x_io
+
+    def diffusion_sample_group(self, peers, pos_h, neg_h, x_io, cfg_scale, sde_noise=None, stream=None):
+        """The sharded diffusion head of the TP group [self] + peers (ranks
+        0..n-1 with tp_head, same device), ranks interleaved layer by layer with
+        an on-device sum as the all-reduce; x_io updated once."""
+        if self.schedule.sde != (sde_noise is not None):
+            raise ValueError("sde_noise must be given exactly when the schedule is sde-dpmsolver++")
+        for p in peers:
+            p.set_steps(self.steps)
+        ctxs = (ctypes.c_void_p * (1 + len(peers)))(self.h, *[p.h for p in peers])
+        _lib.check(_lib.lib().vv_diffusion_sample_group(1 + len(peers), ctxs, pos_h.shape[0], _ptr(pos_h), _ptr(neg_h),
+                                                        _ptr(x_io), float(cfg_scale), _ptr(sde_noise),
+                                                        _stream(stream)), "diffusion_sample_group")
         return x_io
 
     def codec_step(self, slots, latent, audio_out, sem_out=None, embeds_out=None, embed_rows=None, stream=None):

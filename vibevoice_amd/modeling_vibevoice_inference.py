@@ -30,7 +30,7 @@ import torch
 from . import _lib
 from .config import VibeVoiceConfig
 from .engine import Engine
-from .weights import synthetic_state_dict
+from .weights import head_tp_default, synthetic_state_dict
 
 
 @dataclass
@@ -173,11 +173,13 @@ class VibeVoiceTokenConstraintProcessor:
 
 class VibeVoiceForConditionalGenerationInference:
     def __init__(self, config: VibeVoiceConfig, state_dict, device="cuda", attn_implementation="hip",
-                 max_batch=8, max_ctx=8192, tp_group=None):
+                 max_batch=8, max_ctx=8192, tp_group=None, tp_head=None):
         """tp_group: a torch.distributed process group whose ranks (one per GPU)
         tensor-parallel-shard the Qwen2 backbone over RCCL; every
         rank then runs generate() on the same inputs (SPMD) and gets the same
-        result.  None: the whole model on this GPU."""
+        result.  None: the whole model on this GPU.  tp_head: shard the
+        diffusion head's FFN over the group too (None: when its per-step
+        weights exceed the Infinity Cache, i.e. VibeVoice-Large)."""
         self.config = config
         self.attn_implementation = attn_implementation
         self.device = torch.device(device)
@@ -192,7 +194,8 @@ class VibeVoiceForConditionalGenerationInference:
                 dist.broadcast_object_list(box, src=dist.get_global_rank(tp_group, 0), group=tp_group)
                 uid = box[0]
         self.tp_rank, self.tp_size = tp_rank, tp_size
-        self.engine = Engine(config, state_dict, self.device, max_batch=max_batch,
+        self.tp_head = head_tp_default(config, tp_size) if tp_head is None else bool(tp_head and tp_size > 1)
+        self.engine = Engine(config, state_dict, self.device, max_batch=max_batch, tp_head=self.tp_head,
                              max_ctx=min(max_ctx, config.decoder_config.max_position_embeddings),
                              tp_rank=tp_rank, tp_size=tp_size, tp_unique_id=uid)
         self.ddpm_inference_steps = config.diffusion_head_config.ddpm_num_inference_steps
@@ -740,6 +743,7 @@ class GenerateSession:
         return True
 
     def result(self, return_speech=True):
+        self.eng.check_sync()
         if self.audio_streamer is not None:
             self.audio_streamer.end()
         outs = [torch.cat(c, dim=-1) if c else None for c in self.audio_chunks]

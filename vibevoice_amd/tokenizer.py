@@ -97,7 +97,7 @@ class _SlotPool:
             # same TP coordinates as the owner: its packed LM weights are this rank's shards
             # (no communicator: the views only run the replicated codec / connectors)
             self._eng = Engine(self.model.config, None, m.device, max_batch=self.n, max_ctx=64, packed=m.w,
-                               tp_rank=m.tp_rank, tp_size=m.tp_size)
+                               tp_rank=m.tp_rank, tp_size=m.tp_size, tp_head=m.tp_head)
         return self._eng
 
     def _i32(self, xs):

@@ -186,6 +186,31 @@ def _gu(gate, up):
     return torch.stack([gate.reshape(I // 8, 8, H), up.reshape(I // 8, 8, H)], dim=1).reshape(2 * I, H)
 
 
+# The fused head FFN layer (csrc/head_ffn.hip) at its one instantiated shape:
+# G = 256 workgroups, each owning F / G hidden units, 16 lanes per gate / up row.
+HEAD_FFN_SHAPE = (1536, 4608)   # (hidden, head FFN width)
+
+
+def head_ffn_pack(gate, up, G=256, KS=16):
+    """gate / up [F, H] -> head_ffn.hip's stream order, returned as [2F, H]:
+    workgroup w's block [CPT][NT][8] holds, at (i, t = rho * KS + kap), the
+    8 columns of chunk i * KS + kap of row rho (rho = 2u: gate of hidden unit
+    w * F / G + u, 2u + 1: its up)."""
+    F, H = gate.shape
+    HPW, CPT = F // G, H // 8 // KS
+    x = torch.stack([gate.reshape(G, HPW, CPT, KS, 8), up.reshape(G, HPW, CPT, KS, 8)], dim=2)
+    return x.permute(0, 3, 1, 2, 4, 5).contiguous().reshape(2 * F, H)
+
+
+def head_ffn_unpack(p, G=256, KS=16):
+    """Inverse of head_ffn_pack: -> (gate, up)."""
+    F2, H = p.shape
+    F = F2 // 2
+    HPW, CPT = F // G, H // 8 // KS
+    x = p.reshape(G, CPT, HPW, 2, KS, 8).permute(0, 2, 3, 1, 4, 5)
+    return x[:, :, 0].reshape(F, H), x[:, :, 1].reshape(F, H)
+
+
 def mfma_pack(w):
     """[N, K] -> the same shape in MFMA-fragment order (csrc/gemm.hip header):
     block (tile t, chunk c) of 16 rows x 32 columns is 1 KB contiguous, lane l
@@ -245,14 +270,35 @@ def tp_check(cfg: VibeVoiceConfig, tp_size):
         raise ValueError(f"TP={tp_size} does not shard {nh} q / {nkv} kv heads / intermediate {inter} cleanly")
 
 
-def pack(sd, cfg: VibeVoiceConfig, device, with_acoustic_encoder=True, tp_rank=0, tp_size=1):
+def head_tp_check(cfg: VibeVoiceConfig, tp_size):
+    """The diffusion head's FFN splits into whole 32-column chunks per rank
+    (the row-parallel down projection's K; Large: 10,752 / 4 = 2,688 = 84 x 32)."""
+    hc = cfg.diffusion_head_config
+    F = int(hc.hidden_size * hc.head_ffn_ratio)
+    if F % (32 * tp_size):
+        raise ValueError(f"TP={tp_size} does not shard the diffusion head FFN ({F}) into 32-column chunks")
+
+
+def head_tp_default(cfg: VibeVoiceConfig, tp_size):
+    """Shard the head when its per-step weights cannot stay in the 256 MB
+    Infinity Cache (VibeVoice-Large: 925 MB per step, streamed by every
+    replicated rank); the 1.5B head (170 MB, cache-resident) stays replicated."""
+    hc = cfg.diffusion_head_config
+    F = int(hc.hidden_size * hc.head_ffn_ratio)
+    return tp_size > 1 and hc.head_layers * 3 * F * hc.hidden_size * 2 > (192 << 20)
+
+
+def pack(sd, cfg: VibeVoiceConfig, device, with_acoustic_encoder=True, tp_rank=0, tp_size=1, tp_head=False):
     """Reference state dict -> {engine name: contiguous device tensor}.
 
     tp_size > 1: this rank's Megatron shard of the Qwen2 layers
     (configuration_vibevoice.py:175-183): q/k/v rows of its heads and
     gate/up rows of its intermediate slice (column-parallel), the matching
     o_proj / down_proj input columns (row-parallel).  Embedding, norms,
-    lm_head, diffusion head, codec and connectors are replicated."""
+    lm_head, diffusion head, codec and connectors are replicated, except with
+    tp_head: the diffusion head's FFN then splits the same way (gate|up rows of
+    the rank's hidden columns, the matching down_proj input columns; SURVEY.md
+    §8e)."""
     dt = torch.bfloat16
     tp_check(cfg, tp_size)
 
@@ -293,11 +339,22 @@ def pack(sd, cfg: VibeVoiceConfig, device, with_acoustic_encoder=True, tp_rank=0
     ada = [sd[f"{HEAD}layers.{i}.adaLN_modulation.1.weight"] for i in range(hc.head_layers)]
     ada.append(sd[HEAD + "final_layer.adaLN_modulation.1.weight"])
     out["head.ada_w"] = t(torch.cat(ada, 0))
+    hF = int(hc.hidden_size * hc.head_ffn_ratio)
+    if tp_head and tp_size > 1:
+        head_tp_check(cfg, tp_size)
+        hl = hF // tp_size
+        hs = slice(tp_rank * hl, (tp_rank + 1) * hl)
+    else:
+        hs = slice(0, hF)
     for i in range(hc.head_layers):
         p = f"{HEAD}layers.{i}."
         out[f"head.{i}.norm"] = t(sd[p + "norm.weight"])
-        out[f"head.{i}.gu_w"] = t(_gu(sd[p + "ffn.gate_proj.weight"], sd[p + "ffn.up_proj.weight"]))
-        out[f"head.{i}.down_w"] = t(sd[p + "ffn.down_proj.weight"])
+        out[f"head.{i}.gu_w"] = t(_gu(sd[p + "ffn.gate_proj.weight"][hs], sd[p + "ffn.up_proj.weight"][hs]))
+        out[f"head.{i}.down_w"] = t(sd[p + "ffn.down_proj.weight"][:, hs])
+        if (hc.hidden_size, hs.stop - hs.start) == HEAD_FFN_SHAPE:   # the fused layer's streams
+            out[f"head.{i}.gu_rows"] = t(head_ffn_pack(sd[p + "ffn.gate_proj.weight"][hs],
+                                                       sd[p + "ffn.up_proj.weight"][hs]))
+            out[f"head.{i}.dn_rows"] = t(sd[p + "ffn.down_proj.weight"][:, hs].t())
     out["head.final_w"] = t(sd[HEAD + "final_layer.linear.weight"])
 
     for src, dst in (("acoustic", "ac"), ("semantic", "se")):
