@@ -129,6 +129,12 @@ int vv_gemm_tune_apack(int on);
 /* Test / A-B switch: 1 (default) = the fused head FFN layer (head_ffn.hip)
  * where it applies; 0 = gate|up + down GEMV launches per layer. */
 int vv_head_fused(int on);
+/* Diagnostic: per-workgroup s_memrealtime stamps of every fused head layer
+ * launch into buf ([256][8] u64, overwritten per launch; NULL = off). */
+int vv_head_ffn_stamps(void* buf);
+/* A/B switch: 1 (default) = the balanced many-tile GEMV plan at M >= 8 (one
+ * workgroup per CU, 4-5 weight tiles each); 0 = ntile / 8 workgroups. */
+int vv_gemv_tune_bal(int on);
 int vv_gemv_tune_shape(int N, int K, int mmax, int nw, int ks, int u, int tpw);
 /* Test switch: 1 (default) = the q|k|v RoPE epilogue reads the engine's
  * per-position bf16 cos / sin table; 0 = computes cosf / sinf inline

@@ -6,6 +6,8 @@
   * the balanced plan (mode 1) re-splits K, so it differs from the per-op path
     by summation order only: deterministic run to run, rel L2 < 1e-2 against it;
   * no dependency wait gave up (vv_chain_error == 0).
+The per-op reference runs with the fused head FFN layer switched off (it sums in
+a different order; tests/test_gpu_head.py pins it).
 Real VibeVoice-1.5B head shapes (H = 1536, FFN 4608, 4 layers), S = 10, CFG 1.3.
 """
 import pytest
@@ -32,8 +34,12 @@ def head_engine():
         sd["model.prediction_head." + k] = v
     eng = Engine(cfg, sd, dev, max_batch=8, max_ctx=64)
     eng.set_steps(10)
+    # the chain mirrors the per-op GEMV launches (gate|up, down); the fused FFN
+    # layer (head_ffn.hip, the default at n <= 2) is a different summation order
+    _lib.lib().vv_head_fused(0)
     yield eng, H, g
     _lib.lib().vv_chain_tune(0)
+    _lib.lib().vv_head_fused(1)
 
 
 def run(eng, mode, pos, neg, noise, n, sde=None):

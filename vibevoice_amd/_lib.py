@@ -87,6 +87,8 @@ EXPORTS = [
     ("vv_attn_defer", I, [I, I]),
     ("vv_attn_group", I, [I]),
     ("vv_head_fused", I, [I]),
+    ("vv_gemv_tune_bal", I, [I]),
+    ("vv_head_ffn_stamps", I, [P]),
     ("vv_sync_error", I, [P]),
     ("vv_norm_pack", I, [I]),
 ]

@@ -79,8 +79,15 @@ DEV float row16_sum(float v) {
 }
 
 DEV void astamp(const AttnArgs& a, int which) {
-  if (a.stamps && threadIdx.x == 0)
-    a.stamps[((long long)blockIdx.y * gridDim.x + blockIdx.x) * 4 + which] = __builtin_amdgcn_s_memrealtime();
+  if (a.stamps && threadIdx.x == 0) {
+    unsigned long long* p = a.stamps + ((long long)blockIdx.y * gridDim.x + blockIdx.x) * 4;
+    p[which] = __builtin_amdgcn_s_memrealtime();
+    // at entry, slot 3 also records where the workgroup runs (bit 62 marks it; a
+    // storing workgroup overwrites it): XCC_ID << 32 | HW_ID (cu / sh / se fields)
+    if (which == 0)
+      p[3] = (1ull << 62) | ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+             __builtin_amdgcn_s_getreg((31 << 11) | 4);
+  }
 }
 
 template <int G, int NW>

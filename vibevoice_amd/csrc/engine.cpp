@@ -1178,6 +1178,11 @@ extern "C" int vv_head_fused(int on) {
   g_head_fused = on ? 1 : 0;
   return 0;
 }
+static std::atomic<unsigned long long*> g_head_ffn_stamps{nullptr};
+extern "C" int vv_head_ffn_stamps(void* buf) {   // diagnostic: [256][8] per-workgroup stamps of each launch
+  g_head_ffn_stamps = (unsigned long long*)buf;
+  return 0;
+}
 // A grid wait of the fused head layer gave up (workgroups not co-resident):
 // every output since the last call is invalid.  Reset on read.
 int vv_sync_error(vv_ctx* c) {
@@ -1361,6 +1366,7 @@ static int head_layer(vv_ctx* c, const HeadRun& h, int s, int l, hipStream_t st)
     a.slab = (float*)c->hf_slab.p;
     a.sync = (unsigned*)c->hf_sync.p;
     a.err = (unsigned*)c->hf_sync.p + 10 * 32;
+    a.stamps = g_head_ffn_stamps;
     KCHK(launch_head_ffn(a, st));
     return 0;
   }

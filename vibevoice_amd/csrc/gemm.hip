@@ -122,11 +122,14 @@ DEV bool splitk_handoff(const GemmArgs& a, float* red, int TILE, unsigned* last_
 // (Rejected variants -- weights issued twice as deep before the prologue, a
 // one-round-trip M = 16 prologue, epilogue operands prefetched at kernel start --
 // are recorded with their measurements in DESIGN.md and no longer built.)
+// TPW = 5: the balanced many-tile form (gemv_resolve): one workgroup per CU, 4 or
+// 5 tiles each, 2 waves per tile (10 waves)
+constexpr int gemv1_max_waves(int tpw) { return tpw == 5 ? 10 : 8; }
 template <int U, int XF, bool KEEP = false, int TPW = 1, int RW = 0>
-__global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
+__global__ void __launch_bounds__(64 * gemv1_max_waves(TPW)) k_gemv1(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ float inv_s[16];
-  __shared__ float red[8 * 256];
+  __shared__ float red[gemv1_max_waves(TPW) * 256];
   __shared__ unsigned last_flag;
   const int NT = blockDim.x, NW = NT >> 6;   // first: a scalar load (see part_of)
   // XF_MIX: the (<= 4) samples' conv-buffer slot bases, read before any store
@@ -149,8 +152,12 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
   const int KW = TPW == 1 ? NW : NW / TPW;
   const int tw = TPW == 1 ? 0 : wave / KW, kwv = TPW == 1 ? wave : wave - tw * KW;
   const int ntile = a.N >> 4;
-  const int tile = blockIdx.x * TPW + tw;
-  const bool tile_ok = TPW == 1 || tile < ntile;
+  // tiles [T0, T0 + ntl) of this workgroup: an even share of the grid's (<= TPW
+  // each; = TPW * blockIdx.x .. when the grid is ntile / TPW workgroups)
+  const int T0 = TPW == 1 ? blockIdx.x : part_of(ntile, blockIdx.x, gridDim.x);
+  const int ntl = TPW == 1 ? 1 : part_of(ntile, blockIdx.x + 1, gridDim.x) - T0;
+  const int tile = T0 + tw;
+  const bool tile_ok = TPW == 1 || tw < ntl;
   const int nchunk = a.K >> 5;
   // this workgroup's chunk range, then each wave's
   const int b0 = a.ksplit == 1 ? 0 : part_of(nchunk, blockIdx.y, a.ksplit);
@@ -686,11 +693,11 @@ __global__ void __launch_bounds__(512) k_gemv1(GemmArgs a) {
     __syncthreads();
   }
   if (a.ksplit > 1 && !splitk_handoff(a, red, 256, &last_flag, NT)) return;   // host: ksplit > 1 => TPW == 1
-  if (wave < TPW && (TPW == 1 || blockIdx.x * TPW + wave < ntile)) {
+  if (wave < TPW && (TPW == 1 || wave < ntl)) {
     float v[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = red[wave * KW * 256 + i * 64 + lane];
-    epi_tile(a, r, (blockIdx.x * TPW + wave) * 16, lane, v);
+    epi_tile(a, r, (T0 + wave) * 16, lane, v);
     if (a.stamps) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       stamp(a, 3);
@@ -1088,6 +1095,11 @@ __global__ void __launch_bounds__(256) k_gemm_big(GemmArgs a) {
 
 // ------------------------------------------------------------------ host launch
 static std::atomic<int> g_tune_nw{0}, g_tune_ks{0}, g_tune_handoff{-1}, g_tune_waves{0}, g_tune_u{0}, g_tune_tpw{0};
+static std::atomic<int> g_gemv_bal{1};   // diagnostic (vv_gemv_tune_bal): 0 = ntile / 8 workgroups at M >= 8
+extern "C" int vv_gemv_tune_bal(int on) {
+  g_gemv_bal = on ? 1 : 0;
+  return 0;
+}
 static std::atomic<int> g_gemv_max_m{64};   // more rows than this: the tiled k_gemm (vv_gemv_tune_maxm)
 extern "C" int vv_gemv_tune_maxm(int m) {
   g_gemv_max_m = m > 0 ? m : 64;
@@ -1117,7 +1129,7 @@ extern "C" int vv_gemv_tune_tpw(int tpw) {
   return 0;
 }
 
-struct GemmPlan { int nw, ksplit, u, tpw; };
+struct GemmPlan { int nw, ksplit, u, tpw, grid = 0; };   // grid: workgroups when not ntile / tpw
 
 // Measured on MI355X (tools/gemv_sweep.py two-pass min, profiles/r01_gemv_sweep*.txt).
 // Cross-workgroup split-K only for few-tile, long-row shapes (the M >= 8 down
@@ -1331,6 +1343,7 @@ static void launch_gemv_xf(const GemmArgs& a, int mrep, int u, dim3 grid, dim3 b
     if (a.tpw == 1) launch_gemv1<XF, 1>(a, u, grid, block, lds, st);
     else if (a.tpw == 2) launch_gemv1<XF, 2>(a, u, grid, block, lds, st);
     else if (a.tpw == 4) launch_gemv1<XF, 4>(a, u, grid, block, lds, st);
+    else if (a.tpw == 5) launch_gemv1<XF, 5>(a, u, grid, block, lds, st);
     else launch_gemv1<XF, 8>(a, u, grid, block, lds, st);
     return;
   }
@@ -1709,6 +1722,18 @@ static GemmPlan gemv_resolve(GemmArgs& a) {
   a.tpw = 1;
   if (mrep == 1 && a.ksplit == 1 && a.xf.kind != XF_MIX && (p.tpw == 2 || p.tpw == 4 || p.tpw == 8) && p.nw % p.tpw == 0 && gemv1_fits(a))
     a.tpw = p.tpw;
+  // Many tiles at M >= 8 (B = 8 LM gate|up: 1,120 tiles): ntile / 8 = 140
+  // workgroups streamed from 140 of the 256 CUs (tools/gemv_stamps.py: 8.2 us of
+  // stream per workgroup).  Balanced form: one workgroup per CU, an even share of
+  // 4 or 5 tiles each, 2 waves per tile (k_gemv1<.., 5, ..>).
+  if (g_gemv_bal && a.tpw == 8 && a.M >= 8 && a.xf.kind != XF_ATTN_MERGE) {
+    const int ncu = head_ffn_grid(), tiles = a.N / 16;
+    if (ncu > 0 && (tiles + ncu - 1) / ncu == 5) {
+      a.tpw = 5;
+      p.nw = 10;
+      p.grid = ncu;
+    }
+  }
   return p;
 }
 
@@ -1719,7 +1744,7 @@ int gemv_plan_query(const GemmArgs& a0, int* nw, int* ksplit, int* tpw, int* fas
   GemmArgs a = a0;
   if (a.M <= 0 || a.M > 16 || a.K % 32 || a.N % 16 || a.xf.kind == XF_MIX || a.xf.kind == XF_ATTN_MERGE) return 1;
   const GemmPlan p = gemv_resolve(a);
-  if (!gemv1_fits(a)) return 1;
+  if (!gemv1_fits(a) || p.grid) return 1;   // (the chain has no balanced many-tile form)
   *nw = p.nw;
   *ksplit = a.ksplit;
   *tpw = a.tpw;
@@ -1777,7 +1802,7 @@ int launch_gemm(GemmArgs a, hipStream_t st) {
     if (launch_gemvw(a, st)) return hipGetLastError() == hipSuccess ? 0 : 2;
     const int mrep = (a.M + 15) / 16;
     const GemmPlan p = gemv_resolve(a);
-    dim3 grid((a.N / 16 + a.tpw - 1) / a.tpw, a.ksplit), block(64 * p.nw);
+    dim3 grid(p.grid ? p.grid : (a.N / 16 + a.tpw - 1) / a.tpw, a.ksplit), block(64 * p.nw);
     if (a.xf.kind == XF_MIX) {
       const size_t lds = gemv_mix_lds(a.M, a.xf.T, a.K);
       if (mrep != 1 || a.ksplit != 1 || !lds || (64 * p.nw) % (a.K / 8) || a.xf.ctx != 6 || a.a.idx) return 1;

@@ -8,15 +8,18 @@
 // the A rows' dependent round trip and an epilogue tail.  Here the down
 // projection is a split-K over each workgroup's own SwiGLU hidden slice:
 //   * workgroup w owns hidden units [18w, 18w + 18) of F = 4,608 (G = 256
-//     workgroups, one per CU); it streams their 36 gate / up rows (110 KB,
-//     issued at entry) and the matching 18 rows of down_proj^T (55 KB, issued
-//     as the first half of the gate / up registers frees up), so the layer's
-//     42.5 MB stream never waits on an input;
+//     workgroups, one per CU); it streams their 36 gate / up rows (110 KB into
+//     registers) and the matching 18 rows of down_proj^T (55 KB by LDS DMA),
+//     all issued at entry, so the layer's 42.5 MB stream never waits on an input;
 //   * it writes its [R][H] fp32 partial of down to its own slab (write-through),
 //     arrives on an XCD-sharded counter, and waits for the grid (bounded);
 //   * then every workgroup reduces 12 (R = 2) of the R x H outputs over the 256
 //     slabs in a FIXED order (slab-major 16 x 16 tree), so results are
 //     deterministic, and applies the gated residual.
+// (A barrier-free form -- partials tagged with the launch generation, each
+// reducer polling its slabs' tags -- measured 22 us per layer against 15 us:
+// write-through stores took ~4 us to become visible and the polls flooded the
+// memory system; tools/head_ffn_stamps.py, DESIGN.md "Fused head FFN".)
 // Arithmetic: the A transform is k_gemv1's term for term (row_inv's summation
 // order, xform's rounding points), SiLU*up and the gated residual round as
 // epi_silu8 / epi_row8; the dot products run on v_dot2c_f32_bf16 (fp32
@@ -24,7 +27,7 @@
 // MFMA path -- within the head's parity bounds, not bit-identical to it.
 //
 // Grid wait: every workgroup must be resident at once.  G = 256 <= the CU
-// count, and a workgroup (9 waves, <= 96 VGPRs, ~27 KB LDS) leaves room for a
+// count, and a workgroup (9 waves, <= 96 VGPRs, <= 68 KB LDS) leaves room for a
 // second one per CU, so two such launches from two engines also fit together.
 // The wait gives up after ~200 ms (error word; vv_sync_error), never hangs.
 // Counters are monotonic (no per-launch memset): shard s counts arrivals of the
@@ -32,6 +35,10 @@
 // top counter, whose 8th bumps the generation word the waiters poll; all
 // periods divide 2^32, so wrap-around keeps the counts aligned.
 #include "gemv_dev.h"
+
+// the LDS DMA below sets m0 in inline asm: listed as clobbered for the reader,
+// though hipcc reserves m0 (no other instruction of these kernels uses it)
+#pragma clang diagnostic ignored "-Winline-asm"
 
 namespace hf {
 constexpr int H = 1536, F = 4608, G = 256;
@@ -63,19 +70,37 @@ DEV float dot8(bf16x8 w, bf16x8 x, float acc) {
   return acc;
 }
 
-template <int R>
+// ST: the stamped diagnostic instantiation (its own copy, so the stores do not
+// perturb the product kernel's wait counts)
+template <int R, bool ST>
 __global__ void __launch_bounds__(hf::NT) __attribute__((amdgpu_waves_per_eu(5))) k_head_ffn(HeadFfnArgs a) {
   using namespace hf;
   constexpr int E = R * H / G;                 // outputs reduced per workgroup (12 at R = 2)
   constexpr int APT = (R * NCH + NT - 1) / NT; // A chunks per thread
   static_assert(E % 2 == 0 && E * 16 <= NT, "head_ffn reduce geometry");
   __shared__ __attribute__((aligned(16))) bf16 xs[R * H];               // x rows, then the transformed rows
-  __shared__ __attribute__((aligned(16))) float p2[2 * NCH * R * 8];    // down subsets 1, 2; then the reduce
+  // this workgroup's down_proj^T rows (LDS DMA, [UPS][NT][8]: lane t's 16 bytes
+  // of row s at (s * NT + t) * 8); once read into registers, the same bytes hold
+  // the down subsets 1, 2 (p2) and then the reduce scratch
+  __shared__ __attribute__((aligned(16))) bf16 dn_s[UPS * NT * 8];
   __shared__ float inv_s[R], gu_s[ROWS * R], h_s[HPW * R];
   __shared__ unsigned ok_s;
-  static_assert(G * (E + 1) + E * 16 <= 2 * NCH * R * 8, "reduce scratch fits in p2");
+  float* p2 = (float*)dn_s;
+  static_assert(2 * NCH * R * 8 * 4 <= UPS * NT * 16 && (G * (E + 1) + E * 16) * 4 <= UPS * NT * 16,
+                "p2 / reduce scratch fit in the down rows' LDS");
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int w = blockIdx.x;
+  auto stamp = [&](int k) {
+    if constexpr (ST) {
+      if (t == 0) a.stamps[w * 8 + k] = __builtin_amdgcn_s_memrealtime();
+    }
+  };
+  stamp(0);
+  if constexpr (ST) {   // placement: XCC_ID << 32 | HW_ID (cu / sh / se fields)
+    if (t == 0)
+      a.stamps[w * 8 + 6] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                            __builtin_amdgcn_s_getreg((31 << 11) | 4);
+  }
   unsigned* gen = a.sync + 9 * LINE;
   // the generation at entry (before this workgroup arrives); read by every lane,
   // unconditionally, so no branch join waits for it ahead of the streams below
@@ -94,16 +119,38 @@ __global__ void __launch_bounds__(hf::NT) __attribute__((amdgpu_waves_per_eu(5))
     sha[k] = hf_ld(md + a.shift_off + 8 * c);
     sca[k] = hf_ld(md + a.scale_off + 8 * c);
   }
-  // (2) the weight stream: this lane's gate / up row chunks now; its down_proj^T
-  // rows are issued in phase (4) into the registers of the first chunks consumed
-  // (<= 96 VGPRs: two workgroups per CU; head weights stay in the Infinity
-  // Cache: default policy)
+  // the epilogue's gate and residual values of this workgroup's outputs, now (the
+  // residual rows are this launch's x: nobody writes them before the grid wait)
+  const int f0 = w * E;
+  bf16 gate_pre, res_pre;
+  {
+    const int f = f0 + min(t, E - 1), r = f / H, col = f - r * H;
+    gate_pre = *(const __attribute__((address_space(1))) bf16*)(a.mod + r * a.ldmod + a.gate_off + col);
+    res_pre = *(const __attribute__((address_space(1))) bf16*)(a.res + r * a.ldres + col);
+  }
+  // (2) the whole weight stream at once: this lane's gate / up row chunks into
+  // registers, then its down_proj^T rows by LDS DMA (no registers: <= 96 VGPRs
+  // keeps two workgroups per CU; head weights stay in the Infinity Cache:
+  // default policy)
+  // The DMA goes first: hipcc cannot tell its LDS target from xs, so the first
+  // LDS store below waits for it -- which, issued ahead of the gate / up loads,
+  // is a wait for the A side's round trip only, not for the register stream.
   bf16x8 wg[CPT], wd[UPS];
+  const int q2 = t / NCH, c2 = t - q2 * NCH;
+  const bf16* dp = a.dn + (long long)(w * HPW + q2 * UPS) * H + 8 * c2;
+  // (inline asm: the builtin makes hipcc drain every load, vmcnt(0), before the
+  // first LDS access that follows, as it cannot tell dn_s from xs; its own wait
+  // counts stay exact for the register loads issued after these)
+#pragma unroll
+  for (int s = 0; s < UPS; ++s) {
+    const unsigned lds = __builtin_amdgcn_readfirstlane(
+        (unsigned)(unsigned long long)(__attribute__((address_space(3))) bf16*)(dn_s + (s * NT + 64 * wave) * 8));
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(dp + (long long)s * H)
+                 : "memory", "m0");
+  }
   const bf16* gp = a.gu + ((long long)w * CPT * NT + t) * 8;
 #pragma unroll
   for (int i = 0; i < CPT; ++i) wg[i] = hf_ld(gp + (long long)i * NT * 8);
-  const int q2 = t / NCH, c2 = t - q2 * NCH;
-  const bf16* dp = a.dn + (long long)(w * HPW + q2 * UPS) * H + 8 * c2;
 
   // (3) x rows to LDS; inverse RMS in row_inv's order (lane l: chunks l, l + 64, ...)
 #pragma unroll
@@ -139,6 +186,7 @@ __global__ void __launch_bounds__(hf::NT) __attribute__((amdgpu_waves_per_eu(5))
     }
   }
   __syncthreads();
+  stamp(1);
 
   // (4) gate / up: row rho = t / KS of this workgroup's 36 (2u = gate of unit u,
   // 2u + 1 = its up), chunks i * KS + kap; the 16 lanes of a row reduce by DPP
@@ -152,9 +200,6 @@ __global__ void __launch_bounds__(hf::NT) __attribute__((amdgpu_waves_per_eu(5))
       const int c = i * KS + kap;
 #pragma unroll
       for (int r = 0; r < R; ++r) acc[r] = dot8(wg[i], *(const bf16x8*)(xs + r * H + 8 * c), acc[r]);
-      if (i == UPS - 1)
-#pragma unroll
-        for (int s = 0; s < UPS; ++s) wd[s] = hf_ld(dp + (long long)s * H);
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = group_sum<16>(acc[r]);
@@ -163,6 +208,7 @@ __global__ void __launch_bounds__(hf::NT) __attribute__((amdgpu_waves_per_eu(5))
       for (int r = 0; r < R; ++r) gu_s[rho * R + r] = acc[r];
   }
   __syncthreads();
+  stamp(2);
   if (t < HPW * R) {   // SiLU(gate) * up, rounded to the bf16 activation (epi_silu8)
     const int u = t / R, r = t - u * R;
     const float g = gu_s[2 * u * R + r], up = gu_s[(2 * u + 1) * R + r];
@@ -172,6 +218,12 @@ __global__ void __launch_bounds__(hf::NT) __attribute__((amdgpu_waves_per_eu(5))
 
   // (5) down: subset q2 of 6 hidden units x columns [8 c2, 8 c2 + 8); subsets
   // summed 0 + 1 + 2 in that order; the workgroup's partial to its slab
+  // this lane's own DMA'd down rows (the DMA is older than every load still
+  // counted), then the barrier before the region is reused as p2
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int s = 0; s < UPS; ++s) wd[s] = *(const bf16x8*)(dn_s + (s * NT + t) * 8);
+  __syncthreads();
   float y[R][8];
 #pragma unroll
   for (int r = 0; r < R; ++r)
@@ -197,7 +249,7 @@ __global__ void __launch_bounds__(hf::NT) __attribute__((amdgpu_waves_per_eu(5))
       for (int e = 0; e < 8; e += 4) *(f32x4*)(d + r * 8 + e) = (f32x4){y[r][e], y[r][e + 1], y[r][e + 2], y[r][e + 3]};
   }
   __syncthreads();
-  if (q2 == 0) {
+  if (q2 == 0) {   // the workgroup's partial, written through (sc1), then the arrival
     const float* d1 = p2 + c2 * R * 8;
     const float* d2 = p2 + (NCH + c2) * R * 8;
 #pragma unroll
@@ -215,6 +267,7 @@ __global__ void __launch_bounds__(hf::NT) __attribute__((amdgpu_waves_per_eu(5))
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slab is written through before the arrival
   }
   __syncthreads();
+  stamp(3);
 
   // (6) arrival and the bounded grid wait
   if (t == 0) {
@@ -242,19 +295,21 @@ __global__ void __launch_bounds__(hf::NT) __attribute__((amdgpu_waves_per_eu(5))
 
   // (7) outputs [f0, f0 + E) of the flat [R][H] block: slab p's values to LDS
   // (thread p), then 16 x 16 fixed-order partial sums, then the gated residual
-  const int f0 = w * E;
   float* red = p2;
   float* s4 = p2 + G * (E + 1);
-  if (t < G) {
+  if (t < G) {   // all of this lane's slab loads in flight, then the LDS stores
     const float* sl = a.slab + (long long)t * R * H + f0;
+    unsigned long long b[E / 2];
+#pragma unroll
+    for (int k = 0; k < E / 2; ++k) b[k] = MemWT::l64(sl + 2 * k);
 #pragma unroll
     for (int k = 0; k < E / 2; ++k) {
-      const unsigned long long b = MemWT::l64(sl + 2 * k);
-      red[t * (E + 1) + 2 * k] = __uint_as_float((unsigned)b);
-      red[t * (E + 1) + 2 * k + 1] = __uint_as_float((unsigned)(b >> 32));
+      red[t * (E + 1) + 2 * k] = __uint_as_float((unsigned)b[k]);
+      red[t * (E + 1) + 2 * k + 1] = __uint_as_float((unsigned)(b[k] >> 32));
     }
   }
   __syncthreads();
+  stamp(4);
   if (t < E * 16) {
     const int e = t >> 4, qq = t & 15;
     float s = 0.f;
@@ -269,9 +324,10 @@ __global__ void __launch_bounds__(hf::NT) __attribute__((amdgpu_waves_per_eu(5))
     for (int qq = 0; qq < 16; ++qq) s += s4[t * 16 + qq];
     const int f = f0 + t, r = f / H, col = f - r * H;
     float v = rb(s);
-    v = rb(bf(a.mod[r * a.ldmod + a.gate_off + col]) * v);
-    a.out[r * a.ldx + col] = tobf(bf(a.res[r * a.ldres + col]) + v);
+    v = rb(bf(gate_pre) * v);
+    a.out[r * a.ldx + col] = tobf(bf(res_pre) + v);
   }
+  stamp(5);
 }
 
 bool head_ffn_fits(int H, int F, int R) {
@@ -291,7 +347,13 @@ int head_ffn_grid() {
 
 int launch_head_ffn(const HeadFfnArgs& a, hipStream_t st) {
   if (!head_ffn_fits(hf::H, hf::F, a.R)) return 1;
-  if (a.R == 2) hipLaunchKernelGGL(k_head_ffn<2>, dim3(hf::G), dim3(hf::NT), 0, st, a);
-  else hipLaunchKernelGGL(k_head_ffn<4>, dim3(hf::G), dim3(hf::NT), 0, st, a);
+  if (a.stamps) {
+    if (a.R == 2) hipLaunchKernelGGL((k_head_ffn<2, true>), dim3(hf::G), dim3(hf::NT), 0, st, a);
+    else hipLaunchKernelGGL((k_head_ffn<4, true>), dim3(hf::G), dim3(hf::NT), 0, st, a);
+  } else if (a.R == 2) {
+    hipLaunchKernelGGL((k_head_ffn<2, false>), dim3(hf::G), dim3(hf::NT), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((k_head_ffn<4, false>), dim3(hf::G), dim3(hf::NT), 0, st, a);
+  }
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

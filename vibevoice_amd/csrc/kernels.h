@@ -245,6 +245,7 @@ struct HeadFfnArgs {
   float* slab;              // [G][R][H] fp32 partial sums of down, one per workgroup
   unsigned* sync;           // 10 lines of 32 words: 8 shard counters, top counter, generation
   unsigned* err;            // set to 1 when the grid wait gave up
+  unsigned long long* stamps;   // diagnostics (tools/head_ffn_stamps.py): [G][8] s_memrealtime, or nullptr
 };
 bool head_ffn_fits(int H, int F, int R);
 int head_ffn_grid();
