@@ -123,15 +123,20 @@ def bytes_per_token(wb, cfg, B, S, ctx_pos, ctx_neg):
 
 
 # ------------------------------------------------------------------ dominant kernel, live
-# U = 4 chunks in flight, XF_NORM, non-temporal weights, tiles per workgroup (gemm.hip gemv_plan: 1 at M < 8,
-# 8 at 8 <= M <= 16), row-per-wave norm prologue (RW = 1); HBM traffic per launch from tools/pmc_traffic.py
-# (rocprofv3 PMC, committed per M)
+# U = 4 chunks in flight, XF_NORM, non-temporal weights, tiles per workgroup (gemm.hip gemv_resolve: 1 at
+# M < 8; at 8 <= M <= 16 the balanced form, 4-5 of the 1,120 tiles on each of the 256 CUs: TPW = 5),
+# row-per-wave norm prologue (RW = 1); HBM traffic per launch from tools/pmc_traffic.py (rocprofv3 PMC,
+# committed per M)
 def roof_kernel(M):
-    return f"k_gemv1<4, 1, false, {8 if M >= 8 else 1}, 1>"
+    return f"k_gemv1<4, 1, false, {5 if M >= 8 else 1}, 1>"
 
 
 def pmc_file(M):
-    return os.path.join(ROOT, "profiles", f"r03_pmc_traffic_m{M}.json")
+    for r in ("r04", "r03"):
+        p = os.path.join(ROOT, "profiles", f"{r}_pmc_traffic_m{M}.json")
+        if os.path.exists(p):
+            return p
+    return os.path.join(ROOT, "profiles", f"r04_pmc_traffic_m{M}.json")
 
 
 def measure_gemv(model, B, iters=6):

@@ -147,9 +147,9 @@ int vv_rope_table(int on);
  * passes of <= n rows (n <= 16); 0 = the attn_plan splits everywhere. */
 int vv_attn_defer(int on, int chunk);
 /* Test switch: 1 (default) = decode passes of <= 16 rows over more than 8,192
- * keys run up to 128 splits of >= 256 keys merged in <= 8 groups by each
- * group's last-arriving workgroup, o_proj merging the groups; 0 = 1,024-key
- * splits merged by k_attn_merge. */
+ * keys run up to 120 splits of >= 256 keys merged in <= 8 groups by each
+ * group's last-arriving workgroup, o_proj merging the groups; n >= 2: at most
+ * n (<= 128) such splits; 0 = 1,024-key splits merged by k_attn_merge. */
 int vv_attn_group(int on);
 /* Test switch: 1 (default) = the A rows of the prefill's 256 x 256-tile GEMMs
  * are written MFMA-fragment-packed by their producers (RMSNorm rows for q|k|v

@@ -5,7 +5,7 @@ context.  Per-workgroup s_memrealtime stamps (10 ns ticks) of the last layer's
 attention launch: start -> this workgroup's K/V/Q landed -> its waves done ->
 (group / split merge) stored.
 
-usage: python tools/attn_long_stamps.py [ctx ...]"""
+usage: python tools/attn_long_stamps.py [--group N] [ctx ...]"""
 import ctypes
 import os
 import sys
@@ -24,12 +24,20 @@ I32 = dict(dtype=torch.int32, device="cuda")
 
 
 def main():
-    ctxs = [int(x) for x in sys.argv[1:]] or [65000, 32000, 16000]
+    args = sys.argv[1:]
+    group = None
+    if "--group" in args:   # vv_attn_group cap (diagnostic): at most this many splits per (row, kv head)
+        i = args.index("--group")
+        group = int(args[i + 1])
+        args = args[:i] + args[i + 2:]
+    ctxs = [int(x) for x in args] or [65000, 32000, 16000]
     cfg = tiny_config(hidden=1536, layers=2, heads=12, kv_heads=2, inter=8960)
     cfg.decoder_config["max_position_embeddings"] = 65536
     sd = synthetic_state_dict(cfg, seed=3, device="cpu", mode="test", with_acoustic_encoder=False)
     eng = Engine(cfg, sd, "cuda", max_batch=1, max_ctx=65040, valid_ids=[1, 2, 3, 4])
     L = _lib.lib()
+    if group is not None:
+        L.vv_attn_group(group)
     x = torch.randn(2, 1536, device="cuda").bfloat16()
     slots = torch.tensor([0, 1], **I32)
     oi = torch.zeros(1, **I32)

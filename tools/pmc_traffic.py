@@ -7,8 +7,8 @@ doubled on gfx950 (it tallies 128-B streaming requests at 64 B), per dispatch.
 usage (GPU box):
   python tools/pmc_traffic.py run [M]         # the workload alone (what rocprofv3 wraps)
   python tools/pmc_traffic.py collect [M]     # both rocprofv3 passes + summary ->
-                                              # profiles/r03_pmc_traffic_m<M>.json
-M = 2 (B = 1, one tile per workgroup) or 16 (B = 8: 8 tiles per workgroup).
+                                              # profiles/r04_pmc_traffic_m<M>.json
+M = 2 (B = 1, one tile per workgroup) or 16 (B = 8: the balanced form, 4-5 tiles per workgroup).
 """
 import csv
 import ctypes
@@ -22,7 +22,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 M = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 N, K, NL = 17920, 1536, 28
-KERNEL = f"k_gemv1<4, 1, false, {8 if M >= 8 else 1}, 1>"  # U, XF_NORM, non-temporal, tiles per workgroup, RW form
+KERNEL = f"k_gemv1<4, 1, false, {5 if M >= 8 else 1}, 1>"  # U, XF_NORM, non-temporal, tiles per workgroup, RW form
 
 
 def run():
@@ -62,7 +62,7 @@ def collect():
         d = os.path.join(out, counter.lower())
         cmd = ["rocprofv3", "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
                sys.executable, os.path.abspath(__file__), "run", str(M)]
-        subprocess.run(cmd, check=True, timeout=600)
+        subprocess.run(cmd, check=True, timeout=120)
         files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
         with open(files[0]) as f:
             print(counter, "header:", f.readline().strip()[:300])
@@ -81,7 +81,7 @@ def collect():
                    alg_bytes_per_launch=alg, traffic_over_alg=round((fetch + write) / alg, 4),
                    method="rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, tools/pmc_traffic.py run; "
                           "FETCH_SIZE x 2 (gfx950), KiB -> bytes")
-    for path in (os.path.join(ROOT, "profiles", f"r03_pmc_traffic_m{M}.json"), os.path.join(out, "pmc_traffic.json")):
+    for path in (os.path.join(ROOT, "profiles", f"r04_pmc_traffic_m{M}.json"), os.path.join(out, "pmc_traffic.json")):
         with open(path, "w") as f:
             json.dump(summary, f, indent=1)
     print(json.dumps(summary))

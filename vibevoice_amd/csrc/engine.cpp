@@ -870,13 +870,18 @@ extern "C" int vv_attn_defer(int on, int chunk) {
   return 0;
 }
 // Long contexts (> 8 splits of 1,024 keys, i.e. > 8,192 keys) with <= 16 rows:
-// up to 128 splits of >= 256 keys (65K: 128 x 512, so the one long row's 2 kv
-// heads fill all 256 CUs where 1,024-key splits busied 128), merged in <= 8
+// up to 120 splits of >= 256 keys (65K: 120 x 544, so the one long row's 2 kv
+// heads fill 240 CUs where 1,024-key splits busied 128), merged in <= 8
 // groups of <= 16 consecutive splits by each group's last-arriving workgroup;
 // o_proj merges the group partials (XF_ATTN_MERGE) -- no k_attn_merge launch.
-static std::atomic<int> g_attn_group{1};   // diagnostic (vv_attn_group): 0 = the 1,024-key plan + k_attn_merge
-extern "C" int vv_attn_group(int on) {
-  g_attn_group = on ? 1 : 0;
+// 120, not 128: k_attn takes one CU per workgroup (234 VGPRs), and the
+// dispatcher does not deal workgroups to the 8 XCDs strictly round-robin
+// (tools/attn_long_stamps.py: 256 workgroups landed 30 / 34 on two XCDs), so
+// with 256 keyed workgroups two CUs ran two in turn and the launch took twice
+// as long as its median workgroup.
+static std::atomic<int> g_attn_group{120};   // diagnostic (vv_attn_group): 0 = the 1,024-key plan + k_attn_merge
+extern "C" int vv_attn_group(int on) {      // 1 = default; n >= 2: at most n splits (<= 128)
+  g_attn_group = on == 1 ? 120 : on <= 0 ? 0 : std::min(on, 128);
   return 0;
 }
 struct LmPass {
@@ -925,7 +930,7 @@ static int lm_begin(vv_ctx* c, LmPass& P, int ntok, const void* embeds, int embe
   }
   P.group = P.ngroups = 0;
   if (!P.prefill && !P.defer && g_attn_group && P.nsplit > 8 && ntok <= 16 && k.head_dim == 128) {
-    int ns = std::min(128, (max_pos_p1 + 255) / 256);
+    int ns = std::min((int)g_attn_group, (max_pos_p1 + 255) / 256);
     const int ch = ((max_pos_p1 + ns - 1) / ns + 31) / 32 * 32;
     ns = (max_pos_p1 + ch - 1) / ch;
     const int gs = (ns + 7) / 8;
