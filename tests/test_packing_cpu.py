@@ -1,0 +1,44 @@
+"""Weight layouts the fused diffusion-head FFN layer streams (csrc/head_ffn.hip),
+host side only: weights.py's head_ffn_pack order is the one the kernel indexes
+(workgroup w, chunk step i, thread t = rho * 16 + kap, 8 columns), it inverts,
+and pack() emits the fused layer's streams exactly for the shape the kernel is
+instantiated for (unsharded 1.5B head: H 1,536, F 4,608)."""
+import torch
+
+from tiny import tiny_config
+from vibevoice_amd.weights import HEAD_FFN_SHAPE, head_ffn_pack, head_ffn_unpack, pack, synthetic_state_dict
+
+
+def test_head_ffn_pack_order_and_inverse():
+    g = torch.Generator().manual_seed(3)
+    H, F = HEAD_FFN_SHAPE
+    gate = torch.randn(F, H, generator=g)
+    up = torch.randn(F, H, generator=g)
+    p = head_ffn_pack(gate, up)
+    assert p.shape == (2 * F, H)
+    G, HPW, KS, CPT, NT = 256, F // 256, 16, H // 8 // 16, 2 * (F // 256) * 16
+    flat = p.reshape(-1)
+    for (w, i, t, e) in [(0, 0, 0, 0), (5, 7, 123, 3), (255, 11, 575, 7), (100, 3, 17, 1)]:
+        rho, kap = divmod(t, KS)
+        u, which = divmod(rho, 2)
+        src = gate if which == 0 else up
+        assert flat[((w * CPT + i) * NT + t) * 8 + e] == src[w * HPW + u, (i * KS + kap) * 8 + e]
+    g2, u2 = head_ffn_unpack(p)
+    assert torch.equal(g2, gate) and torch.equal(u2, up)
+
+
+def test_pack_emits_fused_streams_for_the_instantiated_shape():
+    cfg = tiny_config(hidden=1536, layers=1, heads=12, kv_heads=2, inter=256)
+    sd = synthetic_state_dict(cfg, seed=1, device="cpu", mode="test", with_acoustic_encoder=False)
+    w = pack(sd, cfg, "cpu", with_acoustic_encoder=False)
+    P = "model.prediction_head.layers.0.ffn."
+    assert torch.equal(w["head.0.dn_rows"], sd[P + "down_proj.weight"].t().contiguous().bfloat16())
+    gate, up = head_ffn_unpack(w["head.0.gu_rows"])
+    assert torch.equal(gate, sd[P + "gate_proj.weight"].bfloat16()) and torch.equal(up, sd[P + "up_proj.weight"].bfloat16())
+    # a sharded head (F / 2 per rank) or another width has no fused streams
+    w2 = pack(sd, cfg, "cpu", with_acoustic_encoder=False, tp_rank=0, tp_size=2, tp_head=True)
+    assert "head.0.gu_rows" not in w2 and "head.0.dn_rows" not in w2
+    small = tiny_config()
+    ws = pack(synthetic_state_dict(small, seed=1, device="cpu", mode="test", with_acoustic_encoder=False), small, "cpu",
+              with_acoustic_encoder=False)
+    assert not any(k.endswith(("gu_rows", "dn_rows")) for k in ws)
