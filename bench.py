@@ -199,6 +199,68 @@ def measure_gemv(model, B, iters=6):
                 avg_us=round(avg_s * 1e6, 2), alg_bytes_per_launch=alg)
 
 
+def measure_head_layers(model, B, reps=10, iters=4):
+    """The diffusion head's FFN layers as the loop runs them at this batch
+    (vv_head_layers_replay: at 2B <= 4 rows the fused layer k_head_ffn, one
+    launch per layer -- the largest kernel of the B = 1 step by time; else the
+    gate|up + down GEMVs), S x head_layers of them per token.  Two graphs (1 and
+    1 + reps passes over the layers, each after the same condition / adaLN set-up)
+    are replayed on one stream between HIP events; their difference over reps x
+    head_layers is the time per layer.  Algorithmic bytes per layer: the layer's
+    gate|up and down weights + its rows."""
+    from vibevoice_amd import _lib
+    eng = model.engine
+    hc = model.config.diffusion_head_config
+    H, L = hc.hidden_size, hc.head_layers
+    F = int(H * hc.head_ffn_ratio) // (eng.tp_size if eng.tp_head else 1)
+    if eng.tp_head:
+        return None
+    R = 2 * B
+    cond = torch.randn(R, H, device=model.device).bfloat16()
+    lib = _lib.lib()
+    stream = torch.cuda.Stream(model.device)
+
+    def graph(passes):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(stream):
+            g.capture_begin(capture_error_mode="thread_local")
+            _lib.check(lib.vv_head_layers_replay(eng.h, B, ctypes.c_void_p(cond.data_ptr()),
+                                                 ctypes.c_void_p(cond[B:].data_ptr()), passes,
+                                                 ctypes.c_void_p(stream.cuda_stream)), "head_layers_replay")
+            g.capture_end()
+        return g
+
+    with torch.cuda.stream(stream):   # eager warm-up (plans, workspaces)
+        _lib.check(lib.vv_head_layers_replay(eng.h, B, ctypes.c_void_p(cond.data_ptr()),
+                                             ctypes.c_void_p(cond[B:].data_ptr()), 1,
+                                             ctypes.c_void_p(stream.cuda_stream)), "head_layers_replay")
+    stream.synchronize()
+    g1, gn = graph(1), graph(1 + reps)
+    times = []
+    for g in (g1, gn):
+        g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(iters):
+            g.replay()
+        e1.record(stream)
+        e1.synchronize()
+        times.append(e0.elapsed_time(e1) / 1e3 / iters)
+    eng.check_sync()
+    per_layer = (times[1] - times[0]) / (reps * L)
+    alg = 3 * F * H * 2 + R * H * 2 * 2
+    fused = R <= 4 and H == 1536 and F == 4608
+    ach = alg / per_layer / 1e9
+    return dict(kernel=(f"k_head_ffn<{R}, false> (fused head FFN layer: norm + adaLN, gate|up, SiLU*up, down, gated "
+                        f"residual in one launch)" if fused else
+                        "k_gemv1 gate|up + down GEMV launches (one head FFN layer)"),
+                shape=f"rows={R} H={H} F={F}", bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS,
+                unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4), avg_us=round(per_layer * 1e6, 2),
+                alg_bytes_per_launch=alg, launches_per_token=int(model.ddpm_inference_steps * L),
+                traffic=None, note="weights kept in the Infinity Cache across the S steps (default cache policy); "
+                                   "the 8 TB/s HBM figure is the stated peak")
+
+
 # ------------------------------------------------------------------ TP collective share
 def measure_tp_collective(make_pass, n_layers, world, dev, iters=20, reps=3):
     """Time of one LM pass with its 2 x n_layers RCCL all-reduces and with
@@ -445,6 +507,7 @@ def main():
     bpt = bytes_per_token(wb, model.config, B, S, ctx_avg, (ctx0 + ctx1) / 2 - L)
     step_ach = bpt * B / (dt / K) / 1e9
     roof = measure_gemv(model, B)
+    roof_head = measure_head_layers(model, B) if world == 1 or T == 1 else None
     tp_coll = None
     if T > 1:   # after the timed loop: the null-collective passes corrupt the session's state
         tp_coll = measure_tp_collective(lm_pass_maker(model, sess), model.config.decoder_config.num_hidden_layers,
@@ -488,6 +551,7 @@ def main():
                        "diffusion_steps": S, "parallelism": f"dp{replicas} (independent replicas), tp{T}",
                        "context_start": ctx0, "context_end": ctx1},
             "roofline": roof,
+            "roofline_head": roof_head,
             "step_roofline": {"bound": "hbm", "achieved": round(step_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(step_ach / HBM_PEAK_GBS, 4),
                               "alg_bytes_per_token": int(bpt), "note": "whole loop iteration, SURVEY.md §8d bytes"},

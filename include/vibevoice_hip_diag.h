@@ -132,6 +132,10 @@ int vv_head_fused(int on);
 /* Diagnostic: per-workgroup s_memrealtime stamps of every fused head layer
  * launch into buf ([256][8] u64, overwritten per launch; NULL = off). */
 int vv_head_ffn_stamps(void* buf);
+/* Diagnostic (bench.py): the head's condition rows and step-0 modulations for
+ * n samples, then `reps` passes over its FFN layers alone (the kernels the loop
+ * runs for them at this n), asynchronously on st. */
+int vv_head_layers_replay(vv_ctx* ctx, int n, const void* pos_h, const void* neg_h, int reps, vv_stream st);
 /* A/B switch: 1 (default) = the balanced many-tile GEMV plan at M >= 8 (one
  * workgroup per CU, 4-5 weight tiles each); 0 = ntile / 8 workgroups. */
 int vv_gemv_tune_bal(int on);

@@ -89,6 +89,7 @@ EXPORTS = [
     ("vv_head_fused", I, [I]),
     ("vv_gemv_tune_bal", I, [I]),
     ("vv_head_ffn_stamps", I, [P]),
+    ("vv_head_layers_replay", I, [P, I, P, P, I, P]),
     ("vv_sync_error", I, [P]),
     ("vv_norm_pack", I, [I]),
 ]

@@ -1409,6 +1409,24 @@ static int head_final(vv_ctx* c, const HeadRun& h, int s, void* x_io, float cfg_
   return 0;
 }
 
+// Diagnostic (bench.py's roofline of the head FFN layer): the condition rows
+// and step 0's modulations as vv_diffusion_sample sets them up, then `reps`
+// passes over the head_layers FFN layers alone (the kernels the loop launches
+// for them at this n: the fused layer, or gate|up + down), on stream st.
+extern "C" int vv_head_layers_replay(vv_ctx* c, int n, const void* pos_h, const void* neg_h, int reps,
+                                     vv_stream vst) {
+  hipStream_t st = (hipStream_t)vst;
+  if (!c->finalized || c->steps == 0) FAIL("vv_head_layers_replay: engine not finalized or no schedule");
+  if (n <= 0 || n > c->cfg.max_batch) FAIL("vv_head_layers_replay: bad n");
+  if (c->head_tp && (c->tp_size > 1 || c->comm)) FAIL("vv_head_layers_replay: sharded head");
+  HeadRun h;
+  CHK(head_begin(c, n, pos_h, neg_h, h, st));
+  CHK(head_mods(c, h, 0, st));
+  for (int r = 0; r < reps; ++r)
+    for (int l = 0; l < c->cfg.head_layers; ++l) CHK(head_layer(c, h, 0, l, st));
+  return 0;
+}
+
 int vv_tp_shard_head(vv_ctx* c, int on) {
   if (on && c->tp_size > 1 && c->cfg.head_ffn % 32) FAIL("vv_tp_shard_head: the local head FFN width must be a multiple of 32");
   c->head_tp = on ? 1 : 0;
