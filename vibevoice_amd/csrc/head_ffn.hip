@@ -55,7 +55,6 @@ static_assert(ROWS * KS == NT && KS * CPT == NCH && PS * NCH == NT && PS * UPS =
 static_assert(KS == 16, "the gate / up row reduction is one 16-lane DPP row");
 }  // namespace hf
 
-typedef __bf16 hf_bf16x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(1))) const bf16x8 hf_gbf16x8;
 typedef __attribute__((address_space(1))) unsigned hf_gu32;
 // global (not flat) loads: a flat load also counts in lgkmcnt, so the LDS waits
