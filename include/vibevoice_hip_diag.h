@@ -155,6 +155,10 @@ int vv_attn_defer(int on, int chunk);
  * group's last-arriving workgroup, o_proj merging the groups; n >= 2: at most
  * n (<= 128) such splits; 0 = 1,024-key splits merged by k_attn_merge. */
 int vv_attn_group(int on);
+/* The decode attention's plan for a pass of ntok rows over max_pos_p1 keys,
+ * host logic only (CPU tests): out = {prefill, nsplit, chunk, defer, group,
+ * ngroups}. */
+int vv_attn_pass_plan(int ntok, int lm_slots, int head_dim, int n_kv, int max_pos_p1, int* out);
 /* Test switch: 1 (default) = the A rows of the prefill's 256 x 256-tile GEMMs
  * are written MFMA-fragment-packed by their producers (RMSNorm rows for q|k|v
  * and gate|up, gate|up's SiLU*up rows for down); 0 = row-major.  Both give the

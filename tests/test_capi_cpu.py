@@ -102,3 +102,38 @@ def test_gemv_plan_rules():
     finally:
         L.vv_gemv_tune_rw(0)
     assert _plan(2, 17920, 1536, NORM, w=True)["rw"] == 1
+
+
+def _attn(ntok, max_pos_p1, lm_slots=2):
+    out = (ctypes.c_int * 6)()
+    assert _lib.lib().vv_attn_pass_plan(ntok, lm_slots, 128, 2, max_pos_p1, out) == 0
+    return dict(zip(("prefill", "nsplit", "chunk", "defer", "group", "ngroups"), list(out)))
+
+
+def test_attention_pass_plan_rules():
+    """The decode attention plans DESIGN.md §3 documents (host logic only)."""
+    L = _lib.lib()
+    # B = 1 short context: 2..8 deferred splits of >= 128 keys, merged by o_proj
+    p = _attn(2, 900)
+    assert (p["prefill"], p["defer"], p["nsplit"], p["chunk"], p["group"]) == (0, 1, 8, 128, 0)
+    # B = 8 (16 rows) does not defer: one 1,024-key split per (row, kv head) at this length
+    p = _attn(16, 900, lm_slots=16)
+    assert (p["defer"], p["nsplit"], p["group"]) == (0, 1, 0)
+    # 64K: at most 120 splits of >= 256 keys in <= 8 groups of <= 16 (one CU per keyed workgroup)
+    p = _attn(2, 65040)
+    assert (p["nsplit"], p["chunk"], p["group"], p["ngroups"]) == (120, 544, 15, 8)
+    p = _attn(2, 20000)
+    assert (p["nsplit"], p["chunk"], p["group"], p["ngroups"]) == (79, 256, 10, 8)
+    # the switch: 0 = 1,024-key splits merged by k_attn_merge; n = at most n splits
+    L.vv_attn_group(0)
+    try:
+        p = _attn(2, 65040)
+        assert (p["nsplit"], p["chunk"], p["group"]) == (64, 1024, 0)
+        L.vv_attn_group(128)
+        assert _attn(2, 65040)["nsplit"] == 128
+    finally:
+        L.vv_attn_group(1)
+    assert _attn(2, 65040)["nsplit"] == 120
+    # a prompt: the prefill kernel (>= 256 rows and >= 32 rows per slot), no splits
+    p = _attn(512, 512)
+    assert (p["prefill"], p["nsplit"]) == (1, 1)

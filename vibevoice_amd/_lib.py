@@ -86,6 +86,7 @@ EXPORTS = [
     ("vv_rope_table", I, [I]),
     ("vv_attn_defer", I, [I, I]),
     ("vv_attn_group", I, [I]),
+    ("vv_attn_pass_plan", I, [I, I, I, I, I, ctypes.POINTER(I)]),
     ("vv_head_fused", I, [I]),
     ("vv_gemv_tune_bal", I, [I]),
     ("vv_head_ffn_stamps", I, [P]),

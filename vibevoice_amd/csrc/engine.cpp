@@ -892,6 +892,53 @@ struct LmPass {
   const float* inv_freq = nullptr;
 };
 
+// The decode attention's plan for a pass of ntok rows over max_pos_p1 keys
+// (lm_begin; vv_attn_pass_plan reports it to the CPU tests): prefill kernel or
+// not, key splits, deferred merge (o_proj merges), grouped merge.
+struct AttnPassPlan {
+  int prefill = 0, nsplit = 1, chunk = 64, defer = 0, group = 0, ngroups = 0;
+};
+static AttnPassPlan attn_pass_plan(int ntok, int lm_slots, int head_dim, int n_kv, int max_pos_p1) {
+  AttnPassPlan P;
+  P.prefill = attn_use_prefill(ntok, lm_slots) ? 1 : 0;
+  P.nsplit = P.prefill ? 1 : attn_plan(ntok, n_kv, max_pos_p1, &P.chunk);
+  if (!P.prefill && g_attn_defer && ntok <= g_attn_defer && ntok <= 16 && head_dim == 128) {
+    // 2..8 splits of >= g_defer_chunk keys, up to 8 x 1,024 keys (longer contexts
+    // keep attn_plan's many 1,024-key splits: the merge input grows with them)
+    int ch = g_defer_chunk, ns = (max_pos_p1 + ch - 1) / ch;
+    if (ns > 8) {
+      ch = ((max_pos_p1 + 7) / 8 + 31) / 32 * 32;
+      ns = (max_pos_p1 + ch - 1) / ch;
+    }
+    if (ns >= 2 && ns <= 8 && ch <= 1024) {
+      P.defer = 1;
+      P.nsplit = ns;
+      P.chunk = ch;
+    }
+  }
+  if (!P.prefill && !P.defer && g_attn_group && P.nsplit > 8 && ntok <= 16 && head_dim == 128) {
+    int ns = std::min((int)g_attn_group, (max_pos_p1 + 255) / 256);
+    const int ch = ((max_pos_p1 + ns - 1) / ns + 31) / 32 * 32;
+    ns = (max_pos_p1 + ch - 1) / ch;
+    const int gs = (ns + 7) / 8;
+    if (gs <= 16) {
+      P.nsplit = ns;
+      P.chunk = ch;
+      P.group = gs;
+      P.ngroups = (ns + gs - 1) / gs;
+    }
+  }
+  return P;
+}
+// diagnostic: out = {prefill, nsplit, chunk, defer, group, ngroups}
+extern "C" int vv_attn_pass_plan(int ntok, int lm_slots, int head_dim, int n_kv, int max_pos_p1, int* out) {
+  if (!out || ntok <= 0 || max_pos_p1 <= 0) return 1;
+  const AttnPassPlan P = attn_pass_plan(ntok, lm_slots, head_dim, n_kv, max_pos_p1);
+  const int v[6] = {P.prefill, P.nsplit, P.chunk, P.defer, P.group, P.ngroups};
+  for (int i = 0; i < 6; ++i) out[i] = v[i];
+  return 0;
+}
+
 static int lm_begin(vv_ctx* c, LmPass& P, int ntok, const void* embeds, int embed_rows, const int* slot,
                     const int* pos, int max_pos_p1) {
   if (!c->finalized) FAIL("vv_lm_forward before vv_finalize");
@@ -911,36 +958,13 @@ static int lm_begin(vv_ctx* c, LmPass& P, int ntok, const void* embeds, int embe
   P.q = qkv + (size_t)ntok * c->qkv_n;
   P.att = P.q + (size_t)ntok * nhd;
   P.act = P.att + (size_t)ntok * nhd;
-  P.prefill = attn_use_prefill(ntok, c->lm_slots) ? 1 : 0;
-  P.nsplit = P.prefill ? 1 : attn_plan(ntok, k.n_kv_heads, max_pos_p1, &P.chunk);
-  P.defer = 0;
-  if (!P.prefill && g_attn_defer && ntok <= g_attn_defer && ntok <= 16 && k.head_dim == 128) {
-    // 2..8 splits of >= g_defer_chunk keys, up to 8 x 1,024 keys (longer contexts
-    // keep attn_plan's many 1,024-key splits: the merge input grows with them)
-    int ch = g_defer_chunk, ns = (max_pos_p1 + ch - 1) / ch;
-    if (ns > 8) {
-      ch = ((max_pos_p1 + 7) / 8 + 31) / 32 * 32;
-      ns = (max_pos_p1 + ch - 1) / ch;
-    }
-    if (ns >= 2 && ns <= 8 && ch <= 1024) {
-      P.defer = 1;
-      P.nsplit = ns;
-      P.chunk = ch;
-    }
-  }
-  P.group = P.ngroups = 0;
-  if (!P.prefill && !P.defer && g_attn_group && P.nsplit > 8 && ntok <= 16 && k.head_dim == 128) {
-    int ns = std::min((int)g_attn_group, (max_pos_p1 + 255) / 256);
-    const int ch = ((max_pos_p1 + ns - 1) / ns + 31) / 32 * 32;
-    ns = (max_pos_p1 + ch - 1) / ch;
-    const int gs = (ns + 7) / 8;
-    if (gs <= 16) {
-      P.nsplit = ns;
-      P.chunk = ch;
-      P.group = gs;
-      P.ngroups = (ns + gs - 1) / gs;
-    }
-  }
+  const AttnPassPlan ap = attn_pass_plan(ntok, c->lm_slots, k.head_dim, k.n_kv_heads, max_pos_p1);
+  P.prefill = ap.prefill;
+  P.nsplit = ap.nsplit;
+  P.chunk = ap.chunk;
+  P.defer = ap.defer;
+  P.group = ap.group;
+  P.ngroups = ap.ngroups;
   if (P.nsplit > 1) {
     if ((size_t)ntok * k.n_kv_heads * std::max(1, P.ngroups) > 65536) FAIL("attention split tickets exhausted");
     CHK(c->attn_part.ensure((size_t)ntok * k.n_heads * (P.nsplit + P.ngroups) * (d + 2) * sizeof(float)));
