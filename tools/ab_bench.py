@@ -1,6 +1,6 @@
 """A/B a library switch on one box: python tools/ab_bench.py <switch> <value> [bench args]
 (switch: codec_mix_fusion; or "lib" <path> to load another build of the
-library, e.g. a -DVV_W_NT=0 variant).  Runs bench.py's main with it set first."""
+library, e.g. an older commit's build kept under tools/lib_*.so).  Runs bench.py's main with it set first."""
 import os
 import sys
 
