@@ -99,18 +99,43 @@ def tp_groups(world, rank, T):
 
 
 # ------------------------------------------------------------------ algorithmic bytes
-def weight_bytes(w):
-    """Bytes of the packed device weights by role (SURVEY.md §8d conventions)."""
+HEAD_SC = 16   # engine.cpp: the adaLN modulations of up to 16 diffusion steps come from ONE batched GEMM
+
+
+def head_fused_layout(w, B):
+    """True when the loop's head FFN layers at this batch read the fused layer's
+    weight streams (head.<l>.gu_rows / dn_rows: 2B <= 4 rows and the streams
+    packed), else the GEMV layout (head.<l>.gu_w / down_w).  Each role is
+    counted once, in the layout the loop actually reads."""
+    return 2 * B <= 4 and "head.0.gu_rows" in w
+
+
+def weight_bytes(w, B=1, S=10):
+    """Bytes of the packed device weights the loop reads, by role (SURVEY.md §8d
+    conventions).  head_step: read by EVERY diffusion step (noisy / final
+    projections, the per-layer norms and FFN weights in the layout the loop
+    reads at this batch); head_token: read once per token (cond_proj, and the
+    stacked adaLN matrix once per HEAD_SC steps -- its GEMM covers the steps'
+    modulations at once)."""
     def sz(pred):
         return sum(t.numel() * t.element_size() for k, t in w.items() if pred(k))
     H = w["lm.norm"].numel()
+    fused = head_fused_layout(w, B)
+    ffn = (".gu_rows", ".dn_rows") if fused else (".gu_w", ".down_w")
+
+    def per_step(k):
+        if k in ("head.noisy_w", "head.final_w"):
+            return True
+        parts = k.split(".")
+        return len(parts) == 3 and parts[1].isdigit() and (parts[2] == "norm" or k.endswith(ffn))
     return dict(
         lm=sz(lambda k: k.startswith("lm.") and k.split(".")[1].isdigit()) + sz(lambda k: k == "lm.norm"),
         lm_head4=4 * H * 2,
-        head_step=sz(lambda k: k.startswith("head.") and k not in ("head.cond_w", "head.t0_w", "head.t2_w")),
-        head_token=sz(lambda k: k == "head.cond_w"),
+        head_step=sz(lambda k: k.startswith("head.") and per_step(k)),
+        head_token=sz(lambda k: k == "head.cond_w") + -(-S // HEAD_SC) * sz(lambda k: k == "head.ada_w"),
         codec=sz(lambda k: k.startswith("dec.") or k.startswith("sem.")),
         conn=sz(lambda k: k.startswith("conn.")),
+        head_layout="fused layer streams (gu_rows / dn_rows)" if fused else "GEMV layout (gu_w / down_w)",
     )
 
 
@@ -120,6 +145,23 @@ def bytes_per_token(wb, cfg, B, S, ctx_pos, ctx_neg):
     kv_pos = lmc.num_hidden_layers * 2 * lmc.num_key_value_heads * d * 2      # 28,672 B at 1.5B
     shared = wb["lm"] + wb["lm_head4"] + S * wb["head_step"] + wb["head_token"] + wb["codec"] + wb["conn"]
     return shared / B + kv_pos * (ctx_pos + ctx_neg + 2)
+
+
+def roof(kernel, shape, alg_bytes, seconds, traffic=None, **extra):
+    """A roofline object against the 8 TB/s HBM peak.  A fraction above 1 is a
+    measurement error (e.g. events on an idle stream), never a result: it is
+    reported as an `error` field with no `frac`."""
+    ach = alg_bytes / seconds / 1e9 if seconds > 0 else float("inf")
+    d = dict(kernel=kernel, shape=shape, bound="hbm", peak=HBM_PEAK_GBS, unit="GB/s", avg_us=round(seconds * 1e6, 2),
+             alg_bytes_per_launch=int(alg_bytes), traffic=traffic,
+             traffic_unit="HBM bytes per launch (rocprofv3 PMC)" if traffic else None)
+    if not (ach / HBM_PEAK_GBS <= 1.0):
+        d.update(achieved=None, frac=None,
+                 error=f"implausible: {alg_bytes} B in {seconds * 1e6:.2f} us = {ach:.0f} GB/s exceeds the peak")
+    else:
+        d.update(achieved=round(ach, 1), frac=round(ach / HBM_PEAK_GBS, 4))
+    d.update(extra)
+    return d
 
 
 # ------------------------------------------------------------------ dominant kernel, live
@@ -132,7 +174,7 @@ def roof_kernel(M):
 
 
 def pmc_file(M):
-    for r in ("r04", "r03"):
+    for r in ("r05", "r04", "r03"):
         p = os.path.join(ROOT, "profiles", f"{r}_pmc_traffic_m{M}.json")
         if os.path.exists(p):
             return p
@@ -182,7 +224,6 @@ def measure_gemv(model, B, iters=6):
     e1.synchronize()
     avg_s = e0.elapsed_time(e1) / 1e3 / (iters * nl)
     alg = 2 * I * H * 2 + M * H * 2 + M * I * 2
-    ach = alg / avg_s / 1e9
     shape = f"M={M} N={2 * I} K={H}"
     traffic = None
     if os.path.exists(pmc_file(M)):
@@ -193,10 +234,7 @@ def measure_gemv(model, B, iters=6):
     kernel = (f"{roof_kernel(M)} (LM post-norm + gate|up + SiLU*up, graph-replayed)" if M <= 16 else
               "k_rmsnorm + k_gemv/k_gemvw (the engine's M > 16 dispatch: post-norm once, then gate|up + SiLU*up; "
               "graph-replayed, both launches timed)")
-    return dict(kernel=kernel, shape=shape,
-                bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
-                traffic=traffic, traffic_unit="bytes per launch" if traffic else None,
-                avg_us=round(avg_s * 1e6, 2), alg_bytes_per_launch=alg)
+    return roof(kernel, shape, alg, avg_s, traffic, launches_per_token=nl)
 
 
 def measure_head_layers(model, B, reps=10, iters=4):
@@ -240,28 +278,37 @@ def measure_head_layers(model, B, reps=10, iters=4):
     stream.synchronize()
     g1, gn = graph(1), graph(1 + reps)
     times = []
-    for g in (g1, gn):
-        g.replay()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(iters):
+    # graph replays launch on the CURRENT stream: replay and record the events on
+    # the same one (round 4 recorded them on an idle stream: frac 29.4)
+    with torch.cuda.stream(stream):
+        for g in (g1, gn):
             g.replay()
-        e1.record(stream)
-        e1.synchronize()
-        times.append(e0.elapsed_time(e1) / 1e3 / iters)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(iters):
+                g.replay()
+            e1.record(stream)
+            e1.synchronize()
+            times.append(e0.elapsed_time(e1) / 1e3 / iters)
     eng.check_sync()
     per_layer = (times[1] - times[0]) / (reps * L)
     alg = 3 * F * H * 2 + R * H * 2 * 2
-    fused = R <= 4 and H == 1536 and F == 4608
-    ach = alg / per_layer / 1e9
-    return dict(kernel=(f"k_head_ffn<{R}, false> (fused head FFN layer: norm + adaLN, gate|up, SiLU*up, down, gated "
-                        f"residual in one launch)" if fused else
-                        "k_gemv1 gate|up + down GEMV launches (one head FFN layer)"),
-                shape=f"rows={R} H={H} F={F}", bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS,
-                unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4), avg_us=round(per_layer * 1e6, 2),
-                alg_bytes_per_launch=alg, launches_per_token=int(model.ddpm_inference_steps * L),
-                traffic=None, note="weights kept in the Infinity Cache across the S steps (default cache policy); "
-                                   "the 8 TB/s HBM figure is the stated peak")
+    fused = R <= 4 and head_fused_layout(eng.w, B)
+    kernel = (f"k_head_ffn<{R}, false> (fused head FFN layer: norm + adaLN, gate|up, SiLU*up, down, gated "
+              f"residual in one launch)" if fused else
+              "k_gemv1 gate|up + k_gemv/k_gemv1 down (one head FFN layer = two GEMV launches, timed together)")
+    traffic = None
+    pf = os.path.join(ROOT, "profiles", f"r05_pmc_head_r{R}.json")
+    if os.path.exists(pf):
+        with open(pf) as f:
+            pmc = json.load(f)
+        if pmc.get("kernel") == kernel.split(" (")[0] and pmc.get("shape") == f"rows={R} H={H} F={F}":
+            traffic = pmc["hbm_bytes_per_launch"]
+    return roof(kernel, f"rows={R} H={H} F={F}", alg, per_layer, traffic,
+                launches_per_token=int(model.ddpm_inference_steps * L),
+                note="graph-replayed head FFN layers (vv_head_layers_replay), HIP events on the replay stream; "
+                     "weights kept in the Infinity Cache across the S steps (default cache policy), the 8 TB/s "
+                     "HBM figure is the stated peak")
 
 
 # ------------------------------------------------------------------ TP collective share
@@ -505,18 +552,23 @@ def main():
     dt = max_over_ranks(dt, world, dev)
     ctx1 = int(sess.pos_len.float().mean())
     tps, audio_per_s = throughput(dt, B, K, replicas)
-    wb = weight_bytes(model.engine.w)
+    wb = weight_bytes(model.engine.w, B, S)
     ctx_avg = (ctx0 + ctx1) / 2
     bpt = bytes_per_token(wb, model.config, B, S, ctx_avg, (ctx0 + ctx1) / 2 - L)
-    step_ach = bpt * B / (dt / K) / 1e9
-    roof = measure_gemv(model, B)
+    # `roofline`: the head FFN layer, the largest unit of the step by time at B = 1 and B = 8
+    # (profiles/r04_steps_b1_headffn.txt, r04_steps_b8_v.txt); `roofline_lm`: the LM gate|up GEMV
+    roof_lm = measure_gemv(model, B)
     roof_head = None
     if world == 1 or T == 1:
-        try:   # a diagnostic next to `roofline`: never let it cost the bench line
+        try:
             roof_head = measure_head_layers(model, B)
         except Exception as e:   # noqa: BLE001
-            print(f"bench: roofline_head not measured: {e}", file=sys.stderr, flush=True)
+            print(f"bench: head roofline not measured: {e}", file=sys.stderr, flush=True)
             roof_head = {"error": str(e)[:200]}
+    if roof_head is None or "error" in roof_head:   # sharded head (TP) or a failed measurement
+        roofline, roofline_2 = roof_lm, roof_head
+    else:
+        roofline, roofline_2 = roof_head, roof_lm
     tp_coll = None
     if T > 1:   # after the timed loop: the null-collective passes corrupt the session's state
         tp_coll = measure_tp_collective(lm_pass_maker(model, sess), model.config.decoder_config.num_hidden_layers,
@@ -559,11 +611,12 @@ def main():
                        "model": f"VibeVoice-{args.model}", "global_batch": B * replicas, "seq_len": L,
                        "diffusion_steps": S, "parallelism": f"dp{replicas} (independent replicas), tp{T}",
                        "context_start": ctx0, "context_end": ctx1},
-            "roofline": roof,
-            "roofline_head": roof_head,
-            "step_roofline": {"bound": "hbm", "achieved": round(step_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                              "frac": round(step_ach / HBM_PEAK_GBS, 4),
-                              "alg_bytes_per_token": int(bpt), "note": "whole loop iteration, SURVEY.md §8d bytes"},
+            "roofline": roofline,
+            "roofline_2": roofline_2,
+            "step_roofline": dict(roof("whole loop iteration", f"B={B} S={S}", bpt * B, dt / K),
+                                  alg_bytes_per_token=int(bpt), head_layout=wb["head_layout"],
+                                  note="SURVEY.md §8d bytes, each weight role counted once in the layout the loop "
+                                       "reads (bench.py weight_bytes); avg_us = ms_per_step"),
             "cpu_baseline": cpu,
         }
         if tp_coll is not None:

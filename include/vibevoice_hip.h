@@ -151,8 +151,14 @@ int vv_diffusion_sample(vv_ctx* ctx, int n, const void* pos_h, const void* neg_h
  * wait ever gave up (workgroups not co-resident, e.g. more than two such
  * launches from other contexts on the device at once), every output since is
  * invalid: vv_sync_error returns 1 (and resets), else 0; it synchronises the
- * device.  GenerateSession checks it once per generate(). */
+ * device.  vv_sync_error_async is its stream-ordered form: it enqueues on st
+ * a copy of the error word into dst (4 bytes of pinned host or device memory)
+ * and the word's reset, so a host that reads dst after an event recorded
+ * behind it sees every launch queued before the call.  GenerateSession reads
+ * it with every step's logits read-back and, when a streamer is attached,
+ * before the step's audio leaves (step() raises; no invalid chunk is put). */
 int vv_sync_error(vv_ctx* ctx);
+int vv_sync_error_async(vv_ctx* ctx, void* dst, vv_stream st);
 
 /* One streaming codec step for n samples in codec slots slots[n]:
  * latent [n, latent] -> audio_out [n, hop]; semantic features -> sem_out

@@ -136,6 +136,9 @@ int vv_head_ffn_stamps(void* buf);
  * n samples, then `reps` passes over its FFN layers alone (the kernels the loop
  * runs for them at this n), asynchronously on st. */
 int vv_head_layers_replay(vv_ctx* ctx, int n, const void* pos_h, const void* neg_h, int reps, vv_stream st);
+/* Test hook: raise the engine's grid-wait error word as a wait that gave up
+ * would (synchronises the device first). */
+int vv_diag_raise_sync_error(vv_ctx* ctx);
 /* A/B switch: 1 (default) = the balanced many-tile GEMV plan at M >= 8 (one
  * workgroup per CU, 4-5 weight tiles each); 0 = ntile / 8 workgroups. */
 int vv_gemv_tune_bal(int on);

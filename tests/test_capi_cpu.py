@@ -134,6 +134,17 @@ def test_attention_pass_plan_rules():
     finally:
         L.vv_attn_group(1)
     assert _attn(2, 65040)["nsplit"] == 120
+    # grouped merge, ragged rows in one pass (the plan is sized by the longest row):
+    # the producer's active groups for a row of n keys, ceil(ceil(n / chunk) / group),
+    # equal the consumer's ceil(n / (group * chunk)) and never exceed ngroups
+    for max_len in (8193, 20000, 32768, 65040, 65536):
+        p = _attn(2, max_len)
+        ch, gs, ng = p["chunk"], p["group"], p["ngroups"]
+        assert gs > 0 and ng * gs * ch >= max_len
+        for n in (1, 200, ch - 1, ch, ch + 1, gs * ch, gs * ch + 1, max_len // 3, max_len - 1, max_len):
+            prod = -(-(-(-n // ch)) // gs)
+            cons = min(-(-n // (gs * ch)), ng)
+            assert prod == cons <= ng, (max_len, n, prod, cons)
     # a prompt: the prefill kernel (>= 256 rows and >= 32 rows per slot), no splits
     p = _attn(512, 512)
     assert (p["prefill"], p["nsplit"]) == (1, 1)

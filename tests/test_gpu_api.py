@@ -122,6 +122,39 @@ def test_streamer_and_stop_check():
     assert out2.speech_outputs[0].shape[-1] == 4 * m.engine.hop
 
 
+def test_grid_wait_error_raises_before_audio_is_streamed():
+    """A grid wait of a fused head layer that gave up (raised here by the
+    diagnostic hook, as the kernel's bounded wait would) invalidates that step's
+    latents: the error word is read back behind every diffusion step
+    (vv_sync_error_async), and step() raises before that step's audio reaches
+    the streamer -- chunks before it were streamed, none from it on."""
+    from vibevoice_amd import _lib
+    cfg = tiny_config(hidden=256, layers=2, heads=2, kv_heads=1, inter=512)
+    sd = synthetic_state_dict(cfg, seed=10, device="cpu", mode="test", with_acoustic_encoder=False)
+    m = _model(sd, cfg)
+    ids, mask = _inputs()
+    for end_with_result in (False, True):
+        st = RecordingStreamer(2)
+        torch.manual_seed(6)
+        sess = m.generate_session(input_ids=ids, attention_mask=mask, tokenizer=TOK, cfg_scale=1.3,
+                                  forced_tokens=[[D] * 8 + [X]] * 2, audio_streamer=st)
+        assert sess.step() and sess.step() and sess.step()
+        clean = [len(c) for c in st.chunks]
+        assert clean == [2, 2]                    # steps 0, 1 streamed; step 2's chunk waits for its check
+        _lib.check(_lib.lib().vv_diag_raise_sync_error(m.engine.h), "raise")
+        assert sess.step()                        # step 3 diffuses behind the raised word; step 2's chunk goes out
+        assert [len(c) for c in st.chunks] == [3, 3]
+        with pytest.raises(RuntimeError, match="grid wait gave up"):
+            sess.result() if end_with_result else sess.step()
+        assert [len(c) for c in st.chunks] == [3, 3]          # step 3's chunk never reached the streamer
+        assert not sess.step()                                # the session is over
+        # the word was reset by its read-back: a fresh session runs clean
+        st2 = RecordingStreamer(2)
+        out = m.generate(input_ids=ids, attention_mask=mask, tokenizer=TOK, cfg_scale=1.3,
+                         forced_tokens=[[D, D, X]] * 2, audio_streamer=st2, show_progress_bar=False)
+        assert [len(c) for c in st2.chunks] == [2, 2] and out.speech_outputs[0].shape[-1] == 2 * m.engine.hop
+
+
 def test_noise_scheduler_swap_sde():
     """gradio_demo.py:114-119: model.model.noise_scheduler replaced through
     from_config(config, algorithm_type="sde-dpmsolver++",

@@ -92,6 +92,8 @@ EXPORTS = [
     ("vv_head_ffn_stamps", I, [P]),
     ("vv_head_layers_replay", I, [P, I, P, P, I, P]),
     ("vv_sync_error", I, [P]),
+    ("vv_sync_error_async", I, [P, P, P]),
+    ("vv_diag_raise_sync_error", I, [P]),
     ("vv_norm_pack", I, [I]),
 ]
 

@@ -698,6 +698,9 @@ int vv_finalize(vv_ctx* c) {
   CHK(need(c, "head.final_w", {D, H}));
   // the fused FFN layer's streams (optional: without them every layer runs gate|up + down)
   c->hf_ready = false;
+  // grid-wait words + the error word (always present: vv_sync_error_async reads it)
+  CHK(c->hf_sync.ensure(11 * 128));
+  HIPCHK(hipMemset(c->hf_sync.p, 0, 11 * 128));
   if (head_ffn_fits(H, F, 2) && c->w.count("head.0.gu_rows")) {
     for (int l = 0; l < L; ++l) {
       const std::string p = "head." + std::to_string(l);
@@ -705,8 +708,6 @@ int vv_finalize(vv_ctx* c) {
       CHK(need(c, p + ".dn_rows", {F, H}));
     }
     CHK(c->hf_slab.ensure((size_t)head_ffn_grid() * 4 * H * sizeof(float)));
-    CHK(c->hf_sync.ensure(11 * 128));
-    HIPCHK(hipMemset(c->hf_sync.p, 0, 11 * 128));
     c->hf_ready = true;
   }
   // ---- connectors + latent scaling
@@ -921,7 +922,9 @@ static AttnPassPlan attn_pass_plan(int ntok, int lm_slots, int head_dim, int n_k
     const int ch = ((max_pos_p1 + ns - 1) / ns + 31) / 32 * 32;
     ns = (max_pos_p1 + ch - 1) / ch;
     const int gs = (ns + 7) / 8;
-    if (gs <= 16) {
+    // the consumer (o_proj's XF_ATTN_MERGE) takes groups of gs * ch keys, at most
+    // ngroups of them: every key of the longest row must fall in one
+    if (gs <= 16 && (long long)((ns + gs - 1) / gs) * gs * ch >= max_pos_p1) {
       P.nsplit = ns;
       P.chunk = ch;
       P.group = gs;
@@ -1214,14 +1217,39 @@ extern "C" int vv_head_ffn_stamps(void* buf) {   // diagnostic: [256][8] per-wor
 }
 // A grid wait of the fused head layer gave up (workgroups not co-resident):
 // every output since the last call is invalid.  Reset on read.
+// (hipMemcpy on the null stream does not wait for non-blocking streams, where
+// the host's generate() runs: synchronise the device first)
 int vv_sync_error(vv_ctx* c) {
   unsigned v = 0;
   if (c->hf_sync.p) {
+    HIPCHK(hipDeviceSynchronize());
     if (hipMemcpy(&v, (unsigned*)c->hf_sync.p + 10 * 32, 4, hipMemcpyDeviceToHost) != hipSuccess)
       FAIL("vv_sync_error: reading the error word failed (hipMemcpy)");
     if (v) HIPCHK(hipMemset((unsigned*)c->hf_sync.p + 10 * 32, 0, 4));
   }
   return v ? 1 : 0;
+}
+// Stream-ordered form: enqueue on st a copy of the error word to dst (4 bytes of
+// pinned host or device memory) and its reset, behind everything queued before.
+// The host reads dst once an event recorded after this call has completed
+// (GenerateSession: with each step's logits read-back, and before audio leaves
+// for a streamer).
+int vv_sync_error_async(vv_ctx* c, void* dst, vv_stream vst) {
+  hipStream_t st = (hipStream_t)vst;
+  if (!dst) FAIL("vv_sync_error_async: dst is NULL");
+  if (!c->finalized) FAIL("vv_sync_error_async before vv_finalize");
+  unsigned* word = (unsigned*)c->hf_sync.p + 10 * 32;
+  HIPCHK(hipMemcpyAsync(dst, word, 4, hipMemcpyDefault, st));
+  HIPCHK(hipMemsetAsync(word, 0, 4, st));
+  return 0;
+}
+// Diagnostic (tests): raise the error word as a grid wait that gave up would.
+extern "C" int vv_diag_raise_sync_error(vv_ctx* c) {
+  if (!c->finalized) FAIL("vv_diag_raise_sync_error before vv_finalize");
+  HIPCHK(hipDeviceSynchronize());
+  const unsigned one = 1;
+  HIPCHK(hipMemcpy((unsigned*)c->hf_sync.p + 10 * 32, &one, 4, hipMemcpyHostToDevice));
+  return 0;
 }
 
 // Plan every op of `ops` (chain.hip), lay out slabs and tickets, upload.

@@ -137,6 +137,12 @@ class Engine:
             raise RuntimeError("fused diffusion-head layer: an in-launch grid wait gave up (workgroups not "
                                "co-resident); the outputs since the last check are invalid")
 
+    def sync_error_async(self, dst, stream=None):
+        """Queue on the stream a copy of the grid-wait error word into dst (a
+        1-element int32 pinned host or device tensor) and its reset; dst is valid
+        once work queued after this call has been waited for."""
+        _lib.check(_lib.lib().vv_sync_error_async(self.h, _ptr(dst), _stream(stream)), "sync_error_async")
+
     def set_schedule(self, schedule):
         """Replace the solver (model.model.noise_scheduler = ...); coefficients are
         rebuilt at the next set_steps."""

@@ -480,6 +480,12 @@ class GenerateSession:
         self.spec_miss = 0
         self.pos_pushed = False
         self.logits_ready = torch.cuda.Event()
+        # the engine's grid-wait error word, read back stream-ordered after every
+        # diffusion step (vv_sync_error_async): a step's audio goes to the streamer
+        # only once the word covering its diffusion has been read as clear
+        self.err_pin = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self.err_ready = torch.cuda.Event()
+        self.pending_put = None
         self.graphs = model._graph_cache
         self.seen = model._graph_seen
 
@@ -620,6 +626,28 @@ class GenerateSession:
         self._diff_phase(rows.numel())
         return rows, state
 
+    def _check_err(self):
+        """Raise if the error word read back last (err_pin) is set: a fused head
+        layer's in-launch grid wait gave up, the latents of that step are invalid."""
+        if int(self.err_pin[0]):
+            self.pending_put = None
+            self.done = True
+            raise RuntimeError("fused diffusion-head layer: an in-launch grid wait gave up (workgroups not "
+                               "co-resident); this step's latents and audio are invalid and were not streamed")
+
+    def _flush_audio(self, sync):
+        """Put the previous diffusion step's audio into the streamer once the
+        error word covering it has been read (sync=False: it already has, by the
+        logits read-back that follows it on the stream)."""
+        if self.pending_put is None:
+            return
+        if sync:
+            self.err_ready.synchronize()
+            self._check_err()
+        audio, didx = self.pending_put
+        self.pending_put = None
+        self.audio_streamer.put(audio[:, None, :], didx)
+
     def _restore_rng(self, state):
         if self.gen is not None:
             self.gen.set_state(state)
@@ -637,6 +665,7 @@ class GenerateSession:
         st = self.audio_streamer
         if self.stop_check_fn is not None and self.stop_check_fn():       # :434-440
             if st is not None:
+                self._flush_audio(sync=True)
                 st.end()
             self.done = True
             return False
@@ -666,6 +695,9 @@ class GenerateSession:
         self.logits_ready.record()
         spec = self._speculate()
         self.logits_ready.synchronize()
+        self._check_err()            # err_pin: copied behind the previous step's diffusion + codec
+        if st is not None:
+            self._flush_audio(sync=False)
         lg = self.logits_pin.clone()
         if self.do_sample:
             r = torch.softmax(lg, -1) / self.q_pin                            # ties -> lowest id, as over the vocab
@@ -729,10 +761,12 @@ class GenerateSession:
                 self._diff_phase(n)
             self._post_phase(n)
             audio = self.audio_dev[:n].clone()
+            self.eng.sync_error_async(self.err_pin)
+            self.err_ready.record()
             for i, b in enumerate(didx.tolist()):
                 self.audio_chunks[b].append(audio[i:i + 1])
-            if st is not None:
-                st.put(audio[:, None, :], didx)
+            if st is not None:      # streamed once the next read-back shows the error word clear
+                self.pending_put = (audio, didx)
         else:
             if spec is not None:
                 self._restore_rng(spec[1])
@@ -743,6 +777,8 @@ class GenerateSession:
         return True
 
     def result(self, return_speech=True):
+        if self.pending_put is not None:
+            self._flush_audio(sync=True)
         self.eng.check_sync()
         if self.audio_streamer is not None:
             self.audio_streamer.end()

@@ -75,11 +75,14 @@ def synthetic_state_dict(cfg: VibeVoiceConfig, seed=0, device="cpu", dtype=torch
     untrained model.  mode="test": larger, fan-in-scaled weights, random
     norms / gammas / biases so every term of every kernel is exercised.
     """
-    g = torch.Generator(device=device).manual_seed(seed)
+    meta = torch.device(device).type == "meta"     # shapes only (no data: byte accounting, layout tests)
+    g = None if meta else torch.Generator(device=device).manual_seed(seed)
     sd = {}
     test = mode == "test"
 
     def rnd(shape, std):
+        if meta:
+            return torch.empty(shape, device=device, dtype=dtype)
         return (torch.randn(shape, generator=g, device=device, dtype=torch.float32) * std).to(dtype)
 
     def lin(name, shape, bias=None):
