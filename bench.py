@@ -237,6 +237,81 @@ def measure_gemv(model, B, iters=6):
     return roof(kernel, shape, alg, avg_s, traffic, launches_per_token=nl)
 
 
+def measure_head_loop(model, B, reps=4, iters=4):
+    """The persistent diffusion head (head_loop.hip: every step of a token's
+    diffusion -- noisy projection, 4 FFN layers, final layer, CFG + DPM update --
+    in ONE launch at 2B <= 4 rows; the largest kernel of the B = 1 step).
+    vv_head_loop_replay sets up the condition rows and modulations, then 1 or
+    1 + reps launches inside two captured graphs; the difference of their replay
+    times (HIP events on the replay stream) over reps is the time per launch.
+    Algorithmic bytes per launch: S x the per-step head weights (bench.py
+    weight_bytes head_step, read once per step) + each FFN layer's rows in / out."""
+    from vibevoice_amd import _lib
+    eng = model.engine
+    hc = model.config.diffusion_head_config
+    H, L = hc.hidden_size, hc.head_layers
+    S = min(model.ddpm_inference_steps, HEAD_SC)
+    R = 2 * B
+    if eng.tp_head or not head_fused_layout(eng.w, B):
+        return None
+    cond = torch.randn(R, H, device=model.device).bfloat16()
+    x = torch.randn(B, hc.latent_size, device=model.device).bfloat16()
+    lib = _lib.lib()
+    stream = torch.cuda.Stream(model.device)
+
+    def call(n_rep):
+        return lib.vv_head_loop_replay(eng.h, B, ctypes.c_void_p(cond.data_ptr()),
+                                       ctypes.c_void_p(cond[B:].data_ptr()), ctypes.c_void_p(x.data_ptr()), 1.3,
+                                       n_rep, ctypes.c_void_p(stream.cuda_stream))
+
+    with torch.cuda.stream(stream):   # eager warm-up (plans, workspaces); "not applicable" -> None
+        if call(1) != 0:
+            return None
+    stream.synchronize()
+
+    def graph(n_rep):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(stream):
+            g.capture_begin(capture_error_mode="thread_local")
+            try:
+                rc = call(n_rep)
+            finally:
+                g.capture_end()
+        _lib.check(rc, "head_loop_replay")
+        return g
+    g1, gn = graph(1), graph(1 + reps)
+    times = []
+    with torch.cuda.stream(stream):   # replays launch on the current stream: time them there
+        for g in (g1, gn):
+            g.replay()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(iters):
+                g.replay()
+            e1.record(stream)
+            e1.synchronize()
+            times.append(e0.elapsed_time(e1) / 1e3 / iters)
+    eng.check_sync()
+    per_launch = (times[1] - times[0]) / reps
+    wb = weight_bytes(eng.w, B, S)
+    alg = S * (wb["head_step"] + L * R * H * 2 * 2)
+    kernel = f"k_head_loop<{R}, false>"
+    traffic = None
+    pf = os.path.join(ROOT, "profiles", f"r05_pmc_head_loop_r{R}.json")
+    if os.path.exists(pf):
+        with open(pf) as f:
+            pmc = json.load(f)
+        if pmc.get("kernel") == kernel and pmc.get("shape") == f"rows={R} H={H} S={S}":
+            traffic = pmc["hbm_bytes_per_launch"]
+    return roof(kernel + " (persistent diffusion head: S x [noisy, 4 FFN layers, final + CFG + DPM] in one launch)",
+                f"rows={R} H={H} S={S}", alg, per_launch, traffic, launches_per_token=-(-model.ddpm_inference_steps //
+                                                                                      HEAD_SC),
+                per_step_us=round(per_launch / S * 1e6, 2),
+                note="graph-replayed persistent launches (vv_head_loop_replay), HIP events on the replay stream; "
+                     "head weights kept in the Infinity Cache across the S steps (default cache policy), the 8 TB/s "
+                     "HBM figure is the stated peak")
+
+
 def measure_head_layers(model, B, reps=10, iters=4):
     """The diffusion head's FFN layers as the loop runs them at this batch
     (vv_head_layers_replay: at 2B <= 4 rows the fused layer k_head_ffn, one
@@ -561,7 +636,7 @@ def main():
     roof_head = None
     if world == 1 or T == 1:
         try:
-            roof_head = measure_head_layers(model, B)
+            roof_head = measure_head_loop(model, B) or measure_head_layers(model, B)
         except Exception as e:   # noqa: BLE001
             print(f"bench: head roofline not measured: {e}", file=sys.stderr, flush=True)
             roof_head = {"error": str(e)[:200]}

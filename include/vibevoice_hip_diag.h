@@ -129,6 +129,18 @@ int vv_gemm_tune_apack(int on);
 /* Test / A-B switch: 1 (default) = the fused head FFN layer (head_ffn.hip)
  * where it applies; 0 = gate|up + down GEMV launches per layer. */
 int vv_head_fused(int on);
+/* Test / A-B switch: 1 (default) = at 2n <= 4 rows the whole diffusion of a
+ * token runs as one persistent launch per 16 steps (head_loop.hip); 0 = one
+ * fused-layer launch per FFN layer + the noisy / final GEMVs. */
+int vv_head_loop(int on);
+/* Diagnostic: per-workgroup phase stamps of the persistent head launch into buf
+ * ([256][64] u64, the last step's phases; NULL = off). */
+int vv_head_loop_stamps(void* buf);
+/* Diagnostic (bench.py): the head's condition rows and the first 16 steps'
+ * modulations for n samples, then `reps` persistent head launches over those
+ * steps (x_io updated by each), asynchronously on st. */
+int vv_head_loop_replay(vv_ctx* ctx, int n, const void* pos_h, const void* neg_h, void* x_io, float cfg_scale,
+                        int reps, vv_stream st);
 /* Diagnostic: per-workgroup s_memrealtime stamps of every fused head layer
  * launch into buf ([256][8] u64, overwritten per launch; NULL = off). */
 int vv_head_ffn_stamps(void* buf);

@@ -190,3 +190,48 @@ def test_head_fused_deterministic_and_close(n):
     err = rel_err(outs[0], outs[2])
     print(f"n={n} fused vs two-launch rel {err:.3e}")
     assert err < 1e-2
+
+
+@pytest.mark.parametrize("n,S,sde", [(1, 10, False), (2, 10, False), (1, 5, False), (2, 20, False), (1, 10, True),
+                                     (2, 10, True)])
+def test_head_loop_vs_oracle_and_layer_launches(n, S, sde):
+    """2n <= 4 rows: the whole diffusion runs as ONE persistent launch per 16
+    steps (head_loop.hip; S = 20 takes two, the DPM history crossing the launch
+    boundary through global memory).  Checked against the oracle (real 1.5B head
+    shapes, bound 2e-2 as every head path), against the per-layer launches
+    (vv_head_loop(0): the same FFN layer arithmetic, noisy / final projections by
+    the MFMA GEMV -- a different summation order), and for determinism."""
+    from vibevoice_amd import _lib
+    from vibevoice_amd.schedule import Schedule
+    L = _lib.lib()
+    g = torch.Generator().manual_seed(31 + n + S)
+    sd, hc, H = real_head_sd(g)
+    tiny = tiny_config(hidden=H, layers=1, heads=12, kv_heads=2, inter=256)
+    eng, _ = engine_with_head(tiny, sd)
+    if sde:
+        eng.set_schedule(Schedule.from_config(eng.schedule.config, algorithm_type="sde-dpmsolver++",
+                                              beta_schedule="squaredcos_cap_v2"))
+    eng.set_steps(S)
+    pos = torch.randn(n, H, generator=g).bfloat16()
+    neg = torch.randn(n, H, generator=g).bfloat16()
+    noise = torch.randn(2 * n, 64, generator=g).bfloat16()
+    z = torch.randn(S, 2 * n, 64, generator=g) if sde else None
+    outs = []
+    try:
+        for loop in (1, 1, 0):
+            L.vv_head_loop(loop)
+            x = noise[:n].to(dev).contiguous()
+            eng.diffusion_sample(pos.to(dev), neg.to(dev), x, 1.3, sde_noise=None if z is None else z.to(dev))
+            torch.cuda.synchronize()
+            outs.append(x.float().cpu())
+    finally:
+        L.vv_head_loop(1)
+    eng.check_sync()
+    ref = ohead.sample_speech_tokens(sd, pos, neg, noise, S, 1.3, hc.head_layers, sde_noise=z)
+    err, c = rel_err(outs[0], ref), cos(outs[0], ref)
+    e_layer = rel_err(outs[0], outs[2])
+    print(f"head loop n={n} S={S} sde={sde}: vs oracle rel {err:.3e} cos {c:.6f} (per-layer launches "
+          f"{rel_err(outs[2], ref):.3e}); loop vs per-layer rel {e_layer:.3e}")
+    assert torch.equal(outs[0], outs[1])
+    assert err < 2e-2 and c > 0.999
+    assert e_layer < 1e-2

@@ -88,6 +88,9 @@ EXPORTS = [
     ("vv_attn_group", I, [I]),
     ("vv_attn_pass_plan", I, [I, I, I, I, I, ctypes.POINTER(I)]),
     ("vv_head_fused", I, [I]),
+    ("vv_head_loop", I, [I]),
+    ("vv_head_loop_stamps", I, [P]),
+    ("vv_head_loop_replay", I, [P, I, P, P, P, F, I, P]),
     ("vv_gemv_tune_bal", I, [I]),
     ("vv_head_ffn_stamps", I, [P]),
     ("vv_head_layers_replay", I, [P, I, P, P, I, P]),

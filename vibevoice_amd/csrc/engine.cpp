@@ -165,6 +165,7 @@ struct vv_ctx {
   DevBuf chain_sync, chain_slabs, chain_err, coef_dev;
   // fused head FFN layer (head_ffn.hip): partial-sum slabs, grid-wait words + error word
   DevBuf hf_slab, hf_sync;
+  DevBuf hl_lat;           // persistent head (head_loop.hip): [D][2] latent hand-off
   bool hf_ready = false;   // its weights are bound (head.<l>.gu_rows / dn_rows) and the shape fits
   DevBuf rope_tab;   // [max_ctx][cos 64 | sin 64] bf16 (k_rope_table)
 };
@@ -632,7 +633,7 @@ void vv_destroy(vv_ctx* c) {
   DevBuf* bufs[] = {&c->norm_ws, &c->kv_k, &c->kv_v, &c->lm_ws, &c->attn_part, &c->attn_cnt, &c->valid_ids, &c->splitk_ws, &c->splitk_cnt,
                     &c->temb, &c->tfreq_tmp, &c->head_ws, &c->codec_ws, &c->slot_scratch, &c->unit_sb,
                     &c->chain_sync, &c->chain_slabs, &c->chain_err, &c->coef_dev, &c->rope_tab, &c->zero_rows,
-                    &c->hf_slab, &c->hf_sync};
+                    &c->hf_slab, &c->hf_sync, &c->hl_lat};
   for (DevBuf* b : bufs) b->release();
   for (auto& kv : c->head_chain) kv.second.ops.release();
   ConvNet* nets[] = {&c->dec, &c->sem, &c->aenc, &c->senc};
@@ -708,6 +709,7 @@ int vv_finalize(vv_ctx* c) {
       CHK(need(c, p + ".dn_rows", {F, H}));
     }
     CHK(c->hf_slab.ensure((size_t)head_ffn_grid() * 4 * H * sizeof(float)));
+    CHK(c->hl_lat.ensure((size_t)D * 2 * sizeof(bf16) + 256));
     c->hf_ready = true;
   }
   // ---- connectors + latent scaling
@@ -1210,6 +1212,19 @@ extern "C" int vv_head_fused(int on) {
   g_head_fused = on ? 1 : 0;
   return 0;
 }
+// The whole diffusion in one persistent launch (head_loop.hip) where the fused
+// layer's streams are bound and the shape fits; 0 = one k_head_ffn launch per
+// layer (A/B and tests)
+static std::atomic<int> g_head_loop{1};
+extern "C" int vv_head_loop(int on) {
+  g_head_loop = on ? 1 : 0;
+  return 0;
+}
+static std::atomic<unsigned long long*> g_head_loop_stamps{nullptr};
+extern "C" int vv_head_loop_stamps(void* buf) {   // diagnostic: [256][64] per-workgroup phase stamps
+  g_head_loop_stamps = (unsigned long long*)buf;
+  return 0;
+}
 static std::atomic<unsigned long long*> g_head_ffn_stamps{nullptr};
 extern "C" int vv_head_ffn_stamps(void* buf) {   // diagnostic: [256][8] per-workgroup stamps of each launch
   g_head_ffn_stamps = (unsigned long long*)buf;
@@ -1479,6 +1494,69 @@ extern "C" int vv_head_layers_replay(vv_ctx* c, int n, const void* pos_h, const 
   return 0;
 }
 
+// The persistent head (head_loop.hip) applies: fused streams bound, 2n <= 4 rows,
+// unsharded, the switches on.
+static bool head_loop_on(vv_ctx* c, int R, bool sharded) {
+  return c->hf_ready && g_head_fused && g_head_loop && !sharded && !g_chain &&
+         head_loop_fits(c->cfg.hidden, c->cfg.head_ffn, R, c->cfg.head_layers);
+}
+// One persistent launch over steps [s0, min(steps, s0 + HEAD_SC)); head_mods(s0)
+// must have run on the stream before it.
+static int head_loop_launch(vv_ctx* c, const HeadRun& h, int s0, void* x_io, float cfg_scale, const float* sde_noise,
+                            hipStream_t st) {
+  const vv_config& k = c->cfg;
+  const int L = k.head_layers;
+  HeadLoopArgs A;
+  memset(&A, 0, sizeof(A));
+  A.n = h.n;
+  A.R = h.R;
+  A.s0 = s0;
+  A.s1 = std::min(c->steps, s0 + HEAD_SC);
+  A.L = L;
+  A.eps = k.head_eps;
+  A.cfg = cfg_scale;
+  A.x = (bf16*)x_io;
+  A.m1 = h.m1;
+  A.noise = sde_noise;
+  A.coef = (const DpmCoef*)c->coef_dev.p;
+  A.mods = h.mods;
+  A.modw = h.MODW;
+  A.noisy_w = W(c, "head.noisy_w");
+  A.final_w = W(c, "head.final_w");
+  for (int l = 0; l < L; ++l) {
+    const std::string p = "head." + std::to_string(l);
+    A.nw[l] = W(c, p + ".norm");
+    A.gu[l] = W(c, p + ".gu_rows");
+    A.dn[l] = W(c, p + ".dn_rows");
+  }
+  A.xh = h.xh;
+  A.lat = (bf16*)c->hl_lat.p;
+  A.slab = (float*)c->hf_slab.p;
+  A.sync = (unsigned*)c->hf_sync.p;
+  A.err = (unsigned*)c->hf_sync.p + 10 * 32;
+  A.stamps = g_head_loop_stamps;
+  const int rc = launch_head_loop(A, st);
+  if (rc) FAIL("persistent diffusion head: launch failed (" + std::to_string(rc) + ": " +
+               hipGetErrorString(hipGetLastError()) + ")");
+  return 0;
+}
+
+// Diagnostic (bench.py's roofline of the persistent head): the condition rows and
+// the first HEAD_SC steps' modulations as vv_diffusion_sample sets them up, then
+// `reps` persistent launches over those steps (x_io updated by each).
+extern "C" int vv_head_loop_replay(vv_ctx* c, int n, const void* pos_h, const void* neg_h, void* x_io, float cfg_scale,
+                                   int reps, vv_stream vst) {
+  hipStream_t st = (hipStream_t)vst;
+  if (!c->finalized || c->steps == 0) FAIL("vv_head_loop_replay: engine not finalized or no schedule");
+  if (n <= 0 || n > c->cfg.max_batch) FAIL("vv_head_loop_replay: bad n");
+  if (!head_loop_on(c, 2 * n, c->head_tp && (c->tp_size > 1 || c->comm))) FAIL("vv_head_loop_replay: not applicable");
+  HeadRun h;
+  CHK(head_begin(c, n, pos_h, neg_h, h, st));
+  CHK(head_mods(c, h, 0, st));
+  for (int r = 0; r < reps; ++r) CHK(head_loop_launch(c, h, 0, x_io, cfg_scale, nullptr, st));
+  return 0;
+}
+
 int vv_tp_shard_head(vv_ctx* c, int on) {
   if (on && c->tp_size > 1 && c->cfg.head_ffn % 32) FAIL("vv_tp_shard_head: the local head FFN width must be a multiple of 32");
   c->head_tp = on ? 1 : 0;
@@ -1500,6 +1578,15 @@ int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, 
   CHK(head_begin(c, n, pos_h, neg_h, h, st));
   const int R = h.R;
   const long long MODW = h.MODW;
+  if (head_loop_on(c, R, sharded)) {
+    // every step of the diffusion in one persistent launch per HEAD_SC steps (the
+    // adaLN GEMM before it covers exactly those steps' modulations)
+    for (int s0 = 0; s0 < c->steps; s0 += HEAD_SC) {
+      CHK(head_mods(c, h, s0, st));
+      CHK(head_loop_launch(c, h, s0, x_io, cfg_scale, sde_noise, st));
+    }
+    return 0;
+  }
   bf16 *mods = h.mods, *act = h.act, *v = h.v, *m1 = h.m1, *sa = h.sa;
   const int F = k.head_ffn;
   RowMap xh_m = h.xh_m;

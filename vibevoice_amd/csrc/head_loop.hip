@@ -1,0 +1,585 @@
+// The whole diffusion of one token in ONE launch at decode batch (2n <= 4 rows):
+// for every DPM-Solver++ step s, noisy_images_proj -> L x HeadLayer -> FinalLayer
+// -> CFG -> solver update (sample_speech_tokens, modeling_vibevoice_inference.py:
+// 712-725; VibeVoiceDiffusionHead.forward, modular_vibevoice_diffusion_head.py:
+// 254-280; HeadLayer / FeedForwardNetwork :96-161; FinalLayer :164-190;
+// DPMSolverMultistepScheduler.step, dpm_solver.py:935-1022).
+//
+// Why (DESIGN.md "Persistent head"): round 4 ran each FFN layer as one launch
+// with a grid wait inside (k_head_ffn, 15.8 us per layer): its 42.5 MB weight
+// slice was streamed only once the launch began, and the boundary, the A rows'
+// round trip and the reduce tail were paid 40 times per token.  Here the grid of
+// 256 workgroups (one per CU) stays resident for all S x L layers and streams
+// layer l+1's slice while layer l's waits and reduce run.
+//
+// Decomposition per workgroup w (H = 1,536, F = 4,608, G = 256):
+//   * FFN layer: w owns hidden units [18w, 18w + 18): gate / up rows in registers
+//     (weights.py head_ffn_pack stream order), down_proj^T rows in LDS (DMA);
+//     its fp32 partial of down goes to slab w; after a grid wait w reduces the
+//     E = R*H/G outputs [E w, E w + E) of the flat [R][H] state over the 256
+//     slabs in a fixed order and applies the gated residual;
+//   * noisy projection: w computes the same E outputs of x = noisy(cat[lat, lat]);
+//   * final layer + CFG + solver: workgroup d < 64 owns latent dim d (its value
+//     and the 2nd-order history stay in its LDS across the steps).
+// Each hand-off (state slices, slabs, latents) is a grid-wide wait: 2L + 2 per
+// step.  Roles inside a workgroup: 9 compute waves hold the weight stream (their
+// vmcnt queue carries nothing else, so a wait never sits behind a weight load);
+// the control wave (wave 9) does every other global access -- state rows, slabs,
+// latents, stores -- and the arrival / poll.
+// Hand-offs follow MI355X_MICROARCH.md's table, first row: write-through (sc1)
+// stores of 4 / 8 bytes, the control wave's s_waitcnt vmcnt(0), ONE arrival per
+// workgroup on an XCD-sharded counter (its 32nd arrival bumps a top counter,
+// whose 8th bumps the generation word), sc1 loads after the poll and a
+// workgroup barrier.  Waits are bounded (~200 ms, error word; vv_sync_error*).
+// Residency: one workgroup per CU (<= 160 KB LDS), launched cooperatively, so
+// the launch fails with a HIP error instead of waiting on an unplaced grid.
+//
+// Arithmetic: the FFN layer is k_gemv1 / k_head_ffn's term for term (row_inv
+// order, xform / epi_silu8 / epi_row8 rounding points; v_dot2c fp32 products);
+// noisy / final projections are fp32 dot products (fp32 accumulation of exact
+// bf16 products, a different summation order than the MFMA GEMV); the CFG and
+// solver update are epi_dpm's term for term.  Deterministic: fixed orders
+// everywhere, bit-identical run to run and under graph replay.
+#include "gemv_dev.h"
+
+#pragma clang diagnostic ignored "-Winline-asm"
+
+namespace hl {
+constexpr int H = 1536, F = 4608, G = 256, D = 64, LMAX = 4;
+constexpr int HPW = F / G;          // hidden units per workgroup (18)
+constexpr int ROWS = 2 * HPW;       // gate / up rows per workgroup (36)
+constexpr int NTC = 576;            // compute threads (9 waves)
+constexpr int NT = NTC + 64;        // + the control wave
+constexpr int NCH = H / 8;          // 16-byte chunks per row (192)
+constexpr int KS = NTC / ROWS;      // lanes per gate / up row (16)
+constexpr int CPT = NCH / KS;       // chunks per lane per row (12)
+constexpr int PS = NTC / NCH;       // down_proj subsets (3)
+constexpr int UPS = HPW / PS;       // down rows per subset (6)
+constexpr int LINE = 32;            // words per counter line
+static_assert(ROWS * KS == NTC && KS * CPT == NCH && PS * NCH == NTC && PS * UPS == HPW, "head_loop geometry");
+
+// LDS carve-up (bytes), one dynamic array: [xs | dn | p2 (also the reduce scratch) | part | fw | small]
+template <int R>
+struct Lds {
+  static constexpr int E = R * H / G;                       // state outputs per workgroup (12 / 24)
+  static constexpr int XS = 0, XS_B = R * H * 2;
+  static constexpr int DN = XS + XS_B, DN_B = UPS * NTC * 16;
+  static constexpr int P2 = DN + DN_B, P2_B = 2 * NCH * R * 8 * 4;
+  static constexpr int PART = P2 + P2_B, PART_B = R * H * 4;
+  static constexpr int FW = PART + PART_B, FW_B = H * 2;
+  static constexpr int SM = FW + FW_B;                      // small scalars below
+  static constexpr int SM_B = (8 + ROWS * R + HPW * R + 4 * E + 3 * R * 2 + 16) * 4;
+  static constexpr int TOTAL = SM + SM_B;
+  static_assert((G * E + E * 16) * 4 <= P2_B && E % 4 == 0, "reduce scratch fits p2");
+  static_assert(TOTAL <= 160 * 1024, "one workgroup per CU");
+};
+}  // namespace hl
+
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) const bf16x8 hl_gbf16x8;
+typedef __attribute__((address_space(1))) unsigned hl_gu32;
+DEV bf16x8 hl_ld(const bf16* p) { return *(hl_gbf16x8*)p; }
+
+DEV float hl_dot8(bf16x8 w, bf16x8 x, float acc) {
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(w, w, 0, 1), __builtin_shufflevector(x, x, 0, 1), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(w, w, 2, 3), __builtin_shufflevector(x, x, 2, 3), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(w, w, 4, 5), __builtin_shufflevector(x, x, 4, 5), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(w, w, 6, 7), __builtin_shufflevector(x, x, 6, 7), acc, false);
+  return acc;
+}
+
+// 16-byte LDS DMA (global_load_lds_dwordx4): lane l's 16 bytes from gptr land at
+// lds_base + 16 l (lds_base wave-uniform).  Inline asm, so hipcc neither drains
+// the queue before the first LDS access nor counts it: the issuing wave waits
+// with an explicit s_waitcnt vmcnt.  SC1: the bytes were written in this launch
+// (write-through stores, MI355X_MICROARCH.md's hand-off table: sc1 loads).
+template <bool SC1>
+DEV void hl_dma16(const void* lds_base, const void* gptr) {
+  const unsigned lds = __builtin_amdgcn_readfirstlane(
+      (unsigned)(unsigned long long)(__attribute__((address_space(3))) const unsigned char*)lds_base);
+  if (SC1)
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off sc1" ::"s"(lds), "v"(gptr) : "memory", "m0");
+  else
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(gptr) : "memory", "m0");
+}
+
+// A kernel-argument pointer re-read inside a loop: hipcc would otherwise hoist
+// every per-lane address derived from it out of the step / layer loops and keep
+// dozens of them live (VGPR spills); through this opaque copy they are recomputed
+// where used (a few VALU each).
+template <class T>
+DEV T* hl_opaque(T* p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+DEV int hl_vopaque(int v) {   // the same for a per-lane value
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// element (row j, column k) of an MFMA-packed [N][K] weight (weights.py mfma_pack):
+// the 16-byte chunk holding columns k .. k+7 (k % 8 == 0)
+DEV const bf16* hl_packed(const bf16* w, int K, int j, int k) {
+  return w + ((long long)((j >> 4) * (K >> 5) + (k >> 5)) * 64 + (j & 15) + 16 * ((k & 31) >> 3)) * 8;
+}
+
+// One grid-wide wait: arrival of this workgroup + poll until `k` waits of this
+// launch have completed.  Control wave, lane 0 only, behind the control wave's
+// own s_waitcnt vmcnt(0) (it made every store this workgroup publishes).
+DEV bool hl_grid_wait(unsigned* sync, unsigned g0, unsigned k, int w, unsigned* err) {
+  using namespace hl;
+  unsigned* gen = sync + 9 * LINE;
+  const unsigned v = __hip_atomic_fetch_add((hl_gu32*)(sync + (w & 7) * LINE), 1u, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+  if ((v + 1) % (G / 8) == 0) {
+    const unsigned v2 = __hip_atomic_fetch_add((hl_gu32*)(sync + 8 * LINE), 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+    if ((v2 + 1) % 8 == 0) __hip_atomic_fetch_add((hl_gu32*)gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while ((unsigned)(__hip_atomic_load((hl_gu32*)gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - g0) < k) {
+    __builtin_amdgcn_s_sleep(1);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {   // ~200 ms at 100 MHz
+      __hip_atomic_store((hl_gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  }
+  return true;
+}
+
+template <int R, bool ST>
+__global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
+  using namespace hl;
+  using LL = Lds<R>;
+  constexpr int E = LL::E;
+  constexpr int APT = (R * NCH + NTC - 1) / NTC;   // transform chunks per compute thread
+  static_assert((H + 2 * R * H) * 2 <= LL::P2_B, "A operands fit the p2 area");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16* xs = (bf16*)(smem + LL::XS);        // state rows, then their transform
+  bf16* dn_s = (bf16*)(smem + LL::DN);      // down_proj^T rows of this workgroup ([UPS][NTC][8], DMA)
+  float* p2 = (float*)(smem + LL::P2);      // A operands; down subsets 1, 2; the reduce scratch
+  float* part = (float*)(smem + LL::PART);  // the workgroup's [R][H] down partial
+  bf16* fw_s = (bf16*)(smem + LL::FW);      // final_layer.linear row d (w < 64)
+  float* sm = (float*)(smem + LL::SM);
+  float* inv_s = sm;                         // [R] (<= 4)
+  unsigned* ok_s = (unsigned*)(sm + 4);
+  float* lat_s = sm + 5;                     // [2] latent (dim d) of samples 0, 1
+  float* m1_s = sm + 7;                      // (8 words in all so far)
+  float* gu_s = sm + 8;                      // [ROWS][R]
+  float* h_s = gu_s + ROWS * R;              // [HPW][R]
+  float* res_s = h_s + HPW * R;              // [E] residual of this workgroup's outputs
+  float* gate_s = res_s + E;                 // [E]
+  float* out_s = gate_s + E;                 // [2E] outputs as bf16 pairs
+  float* fin_s = out_s + 2 * E;              // [3][R] wave partials of the final linear
+  bf16* nw_s = (bf16*)p2;                    // A operands in the p2 area: norm weight [H],
+  bf16* sh_s = nw_s + H;                     // shift rows [R][H]
+  bf16* sc_s = sh_s + R * H;                 // scale rows [R][H]
+  float* red = p2;                           // reduce: [G][E] slab values
+  float* s4 = p2 + G * E;                    //         [E][16] partial sums
+
+  // Per-thread values are re-derived in every phase from an opaque thread id:
+  // hoisted out of the step / layer loops, hipcc kept dozens of per-lane
+  // addresses live next to the 48-register weight slice and spilled.
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool ctl = wave == NTC / 64;
+  const int w = blockIdx.x, n = a.n;
+  const int f0 = w * E;                      // this workgroup's slice of the flat [R][H] state
+  unsigned g0 = 0, nwait = 0;
+  if (ctl) g0 = __hip_atomic_load((hl_gu32*)(a.sync + 9 * LINE), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  auto stamp = [&](int k) {
+    if constexpr (ST) {
+      if (threadIdx.x == NTC && a.stamps) a.stamps[w * 64 + k] = __builtin_amdgcn_s_memrealtime();
+    }
+  };
+  // grid wait by the control wave (behind its own vmcnt(0)); false: a wait gave up
+  auto grid_wait = [&]() -> bool {
+    ++nwait;
+    if (ctl) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if ((threadIdx.x & 63) == 0) ok_s[0] = hl_grid_wait(a.sync, g0, nwait, w, a.err) ? 1u : 0u;
+    }
+    __syncthreads();
+    return ok_s[0] != 0;
+  };
+
+  // ---- the weight stream: layer l's gate / up rows into registers, down rows by DMA
+  bf16x8 wg[CPT];
+  auto issue_gu = [&](int l, int t) {
+    const bf16* gp = a.gu[l] + ((long long)w * CPT * NTC + t) * 8;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) wg[i] = hl_ld(gp + (long long)i * NTC * 8);
+  };
+  auto issue_dn = [&](int l, int t) {
+    const int q2 = t / NCH, c2 = t - q2 * NCH;
+    const bf16* dp = a.dn[l] + (long long)(w * HPW + q2 * UPS) * H + 8 * c2;
+#pragma unroll
+    for (int s2 = 0; s2 < UPS; ++s2) hl_dma16<false>(dn_s + (s2 * NTC + 64 * wave) * 8, dp + (long long)s2 * H);
+  };
+  if (!ctl) {
+    const int t = threadIdx.x;
+    issue_dn(0, t);
+    issue_gu(0, t);
+  }
+  stamp(0);
+  if (ctl && w < D) {   // final_layer row d, latent / history of dim d (workgroup d < 64)
+    const int lane = threadIdx.x & 63;
+    for (int c = lane; c < NCH; c += 64) *(bf16x8*)(fw_s + 8 * c) = hl_ld(hl_packed(a.final_w, H, w, 8 * c));
+    if (lane < n) {
+      lat_s[lane] = bf(a.x[lane * D + w]);
+      m1_s[lane] = bf(a.m1[lane * D + w]);
+    }
+  }
+
+  for (int s = a.s0; s < a.s1; ++s) {
+    const bf16* mod = hl_opaque(a.mods) + (long long)(s - a.s0) * R * a.modw;
+    // ================= noisy_images_proj(cat[lat, lat]) -> this workgroup's state slice
+    if (ctl) {   // LPO lanes per output, each 64 / LPO latent dims
+      constexpr int LPO = E <= 16 ? 4 : 2, DPL = D / LPO, NCL = DPL / 8;
+      const int lane = hl_vopaque(threadIdx.x & 63);
+      const int no = lane / LPO, nk = lane - no * LPO;
+      const int nf = f0 + min(no, E - 1), nr = nf / H, ncol = nf - nr * H, xr = nr % n;
+      bf16x8 nwt[NCL], xv[NCL];
+#pragma unroll
+      for (int j = 0; j < NCL; ++j) {
+        const int d0 = nk * DPL + 8 * j;
+        nwt[j] = hl_ld(hl_packed(a.noisy_w, D, ncol, d0));
+        if (s == a.s0) {   // the launch's input latents
+          xv[j] = hl_ld(a.x + xr * D + d0);
+        } else {           // the previous step's latents, [D][2] (dims d0 .. d0+7, both samples): sc1
+          const bf16x8 p0 = MemWT::ld16(a.lat + 2 * d0), p1 = MemWT::ld16(a.lat + 2 * d0 + 8);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            xv[j][e] = xr ? p0[2 * e + 1] : p0[2 * e];
+            xv[j][4 + e] = xr ? p1[2 * e + 1] : p1[2 * e];
+          }
+        }
+      }
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < NCL; ++j) acc = hl_dot8(nwt[j], xv[j], acc);
+      acc = group_sum<LPO>(acc);
+      if (nk == 0 && no < E) ((bf16*)out_s)[no] = tobf(acc);   // EPI_STORE (no bias)
+      // (the control wave alone: LDS accesses of one wave are ordered)
+      if (lane < E / 4) MemWT::st8(a.xh + f0 + 4 * lane, *(const bf16x4*)((const bf16*)out_s + 4 * lane));
+    }
+    if (!grid_wait()) return;
+    stamp(1);
+    for (int l = 0; l < a.L; ++l) {
+      const bool has_next = l + 1 < a.L || s + 1 < a.s1;
+      const int ln = l + 1 < a.L ? l + 1 : 0;
+      const int o = 3 * H * l;
+      bf16* xh = hl_opaque(a.xh);
+      float* slab = hl_opaque(a.slab);
+      const int tl = hl_vopaque((int)threadIdx.x);   // this iteration's opaque thread id
+      // ================= A: modulate(norm(x)) -> gate|up -> SiLU*up -> down partial
+      if (ctl) {   // every operand by LDS DMA: the state rows (this launch's: sc1), the norm
+                   // weight and this step's shift / scale rows; this slice's residual and gate
+        const int lane = hl_vopaque(tl & 63);
+#pragma unroll
+        for (int j = 0; j < R * NCH / 64; ++j) {
+          const int q = 64 * j + lane, r = q / NCH, c = q - r * NCH;
+          hl_dma16<true>(xs + 512 * j, xh + 8 * q);
+          hl_dma16<false>(sh_s + 512 * j, mod + r * a.modw + o + 8 * c);
+          hl_dma16<false>(sc_s + 512 * j, mod + r * a.modw + o + H + 8 * c);
+        }
+#pragma unroll
+        for (int j = 0; j < NCH / 64; ++j) hl_dma16<false>(nw_s + 512 * j, a.nw[l] + 8 * (64 * j + lane));
+        bf16 gv = bf16(0.f);
+        if (lane < E) {
+          const int f = f0 + lane, r = f / H, col = f - r * H;
+          gv = mod[r * a.modw + o + 2 * H + col];
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane < E) {
+          res_s[lane] = bf(xs[f0 + lane]);
+          gate_s[lane] = bf(gv);
+        }
+      }
+      __syncthreads();
+      stamp(2 + 3 * l);
+      if (wave < R) {   // inverse RMS in row_inv's order
+        const int lane = tl & 63;
+        float ss = 0.f;
+        for (int c = lane; c < NCH; c += 64) {
+          const bf16x8 v = *(const bf16x8*)(xs + wave * H + 8 * c);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss += bf(v[j]) * bf(v[j]);
+        }
+        ss = wave_sum(ss);
+        if (lane == 0) inv_s[wave] = rsqrtf(ss / (float)H + a.eps);
+      }
+      __syncthreads();
+      if (!ctl) {   // xform<XF_NORM>'s rounding points
+        const int t = hl_vopaque(tl);
+#pragma unroll
+        for (int k = 0; k < APT; ++k) {
+          const int q = t + k * NTC;
+          if (q < R * NCH) {
+            const float inv = inv_s[q / NCH];
+            const bf16x8 xv = *(const bf16x8*)(xs + 8 * q);
+            const bf16x8 nwv = *(const bf16x8*)(nw_s + 8 * (q % NCH));
+            const bf16x8 shv = *(const bf16x8*)(sh_s + 8 * q), scv = *(const bf16x8*)(sc_s + 8 * q);
+            bf16x8 ov;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              float v = rb(bf(xv[j]) * inv);
+              v = rb(v * bf(nwv[j]));
+              v = rb(rb(v * rb(1.0f + bf(scv[j]))) + bf(shv[j]));
+              ov[j] = tobf(v);
+            }
+            *(bf16x8*)(xs + 8 * q) = ov;
+          }
+        }
+      }
+      __syncthreads();
+      if (!ctl) {   // gate / up rows (rho = t / KS: 2u gate, 2u + 1 up of unit u), 16 lanes per row
+        const int t = hl_vopaque(tl);
+        const int rho = t / KS, kap = t - rho * KS;
+        float acc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = 0.f;
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+          const int c = i * KS + kap;
+#pragma unroll
+          for (int r = 0; r < R; ++r) acc[r] = hl_dot8(wg[i], *(const bf16x8*)(xs + r * H + 8 * c), acc[r]);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = group_sum<16>(acc[r]);
+        if (kap == 0)
+#pragma unroll
+          for (int r = 0; r < R; ++r) gu_s[rho * R + r] = acc[r];
+        // (a compiler fence: the next slice's loads must not be hoisted above the
+        // dot products -- both slices would then hold registers at once)
+        asm volatile("" ::: "memory");
+        if (has_next) issue_gu(ln, t);   // the next layer's gate / up slice, streamed from here on
+      }
+      __syncthreads();
+      if (tl < HPW * R) {   // SiLU(gate) * up, rounded to the bf16 activation (epi_silu8)
+        const int u = tl / R, r = tl - u * R;
+        const float g = gu_s[2 * u * R + r], up = gu_s[(2 * u + 1) * R + r];
+        h_s[u * R + r] = bf(tobf(rb(silu_f(rb(g))) * rb(up)));
+      }
+      bf16x8 wd[UPS];
+      if (!ctl) {   // this layer's DMA'd down rows (older than the CPT gate / up loads just issued)
+        const int t = hl_vopaque(tl);
+        if (has_next) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int s2 = 0; s2 < UPS; ++s2) wd[s2] = *(const bf16x8*)(dn_s + (s2 * NTC + t) * 8);
+      }
+      __syncthreads();
+      float y[R][8];
+      if (!ctl) {   // down: subset q2 of 6 hidden units x columns [8 c2, 8 c2 + 8)
+        const int t = hl_vopaque(tl);
+        const int q2 = t / NCH, c2 = t - q2 * NCH;
+        if (has_next) issue_dn(ln, t);   // the next layer's down rows into the same LDS
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) y[r][e] = 0.f;
+#pragma unroll
+        for (int s2 = 0; s2 < UPS; ++s2) {
+          float wf[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) wf[e] = bf(wd[s2][e]);
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const float hv = h_s[(q2 * UPS + s2) * R + r];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) y[r][e] = fmaf(hv, wf[e], y[r][e]);
+          }
+        }
+        if (q2 > 0) {
+          float* d = p2 + ((q2 - 1) * NCH + c2) * R * 8;
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int e = 0; e < 8; e += 4) *(f32x4*)(d + r * 8 + e) = (f32x4){y[r][e], y[r][e + 1], y[r][e + 2], y[r][e + 3]};
+        }
+      }
+      __syncthreads();
+      if (!ctl) {   // subsets summed 0 + 1 + 2 in that order (k_head_ffn's order)
+        const int t = hl_vopaque(tl);
+        const int q2 = t / NCH, c2 = t - q2 * NCH;
+        if (q2 == 0) {
+          const float* d1 = p2 + c2 * R * 8;
+          const float* d2 = p2 + (NCH + c2) * R * 8;
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int e = 0; e < 8; e += 4)
+              *(f32x4*)(part + r * H + 8 * c2 + e) =
+                  (f32x4){(y[r][e] + d1[r * 8 + e]) + d2[r * 8 + e], (y[r][e + 1] + d1[r * 8 + e + 1]) + d2[r * 8 + e + 1],
+                          (y[r][e + 2] + d1[r * 8 + e + 2]) + d2[r * 8 + e + 2], (y[r][e + 3] + d1[r * 8 + e + 3]) + d2[r * 8 + e + 3]};
+        }
+      }
+      __syncthreads();
+      if (ctl) {   // the partial to slab w, written through
+        const int lane = hl_vopaque(tl & 63);
+        float* sl = slab + (long long)w * R * H;
+#pragma unroll 4
+        for (int q = lane; q < R * H / 2; q += 64) {
+          const unsigned long long b = *(const unsigned long long*)(part + 2 * q);
+          __hip_atomic_store((gu64*)(sl + 2 * q), b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      stamp(3 + 3 * l);
+      if (!grid_wait()) return;
+      // ================= B: outputs [f0, f0 + E) over the 256 slabs, fixed order; gated residual
+      if (ctl) {   // red[p][e] = slab p's value of output f0 + e: E / 4 16-byte pieces per slab, LDS DMA
+        constexpr int P = E / 4;
+        const int lane = hl_vopaque(tl & 63);
+#pragma unroll
+        for (int j = 0; j < G * P / 64; ++j) {
+          const int q = 64 * j + lane, p = q / P, k = q - p * P;
+          hl_dma16<true>(red + 256 * j, slab + (long long)p * R * H + f0 + 4 * k);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+      stamp(4 + 3 * l);
+      if (tl < E * 16) {
+        const int e = tl >> 4, qq = tl & 15;
+        float sacc = 0.f;
+#pragma unroll
+        for (int p = 0; p < 16; ++p) sacc += red[(qq * 16 + p) * E + e];
+        s4[e * 16 + qq] = sacc;
+      }
+      __syncthreads();
+      if (tl < E) {   // epi_row8's EPI_RES with the adaLN gate
+        const int e = tl;
+        float sacc = 0.f;
+#pragma unroll
+        for (int qq = 0; qq < 16; ++qq) sacc += s4[e * 16 + qq];
+        float v = rb(sacc);
+        v = rb(gate_s[e] * v);
+        ((bf16*)out_s)[e] = tobf(res_s[e] + v);
+      }
+      __syncthreads();
+      if (ctl && (tl & 63) < E / 4) {
+        const int lane = tl & 63;
+        MemWT::st8(xh + f0 + 4 * lane, *(const bf16x4*)((const bf16*)out_s + 4 * lane));
+      }
+      if (!grid_wait()) return;
+    }
+    // ================= FinalLayer (workgroup w = latent dim d < 64) + CFG + solver update
+    if (w < D) {
+      const int o = 3 * H * a.L;
+      bf16* xh = hl_opaque(a.xh);
+      const int tl = hl_vopaque((int)threadIdx.x);
+      if (ctl) {
+        const int lane = hl_vopaque(tl & 63);
+#pragma unroll
+        for (int j = 0; j < R * NCH / 64; ++j) {
+          const int q = 64 * j + lane, r = q / NCH, c = q - r * NCH;
+          hl_dma16<true>(xs + 512 * j, xh + 8 * q);
+          hl_dma16<false>(sh_s + 512 * j, mod + r * a.modw + o + 8 * c);
+          hl_dma16<false>(sc_s + 512 * j, mod + r * a.modw + o + H + 8 * c);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+      if (wave < R) {
+        const int lane = tl & 63;
+        float ss = 0.f;
+        for (int c = lane; c < NCH; c += 64) {
+          const bf16x8 v = *(const bf16x8*)(xs + wave * H + 8 * c);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss += bf(v[j]) * bf(v[j]);
+        }
+        ss = wave_sum(ss);
+        if (lane == 0) inv_s[wave] = rsqrtf(ss / (float)H + a.eps);
+      }
+      __syncthreads();
+      if (wave < NCH / 64) {   // chunk c = t of every row: modulate(norm(x)) (no norm weight) . final row d
+        const int t = tl;
+        const bf16x8 fwv = *(const bf16x8*)(fw_s + 8 * t);
+        float acc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const bf16x8 sh = *(const bf16x8*)(sh_s + r * H + 8 * t), sc = *(const bf16x8*)(sc_s + r * H + 8 * t);
+          const bf16x8 xv = *(const bf16x8*)(xs + r * H + 8 * t);
+          bf16x8 tv;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float v = rb(bf(xv[j]) * inv_s[r]);
+            v = rb(rb(v * rb(1.0f + bf(sc[j]))) + bf(sh[j]));
+            tv[j] = tobf(v);
+          }
+          acc[r] = wave_sum(hl_dot8(fwv, tv, 0.f));
+        }
+        if ((t & 63) == 0)
+#pragma unroll
+          for (int r = 0; r < R; ++r) fin_s[wave * R + r] = acc[r];
+      }
+      __syncthreads();
+      if (ctl && (tl & 63) < n) {   // epi_dpm: CFG combine + DPM-Solver++ step, dim d of sample i
+        const int i = tl & 63;
+        const DpmCoef k = a.coef[s];
+        const float c = rb((fin_s[i] + fin_s[R + i]) + fin_s[2 * R + i]);
+        const float un = rb((fin_s[n + i] + fin_s[R + n + i]) + fin_s[2 * R + n + i]);
+        const float vv = rb(un + rb(a.cfg * rb(c - un)));
+        const float xsv = lat_s[i];
+        const float x0 = rb(rb(k.alpha_s * xsv) - rb(k.sigma_s * vv));
+        float out = k.c_x * xsv - rb(k.c_d0 * x0);
+        if (k.order == 2) {
+          const float d1 = rb(k.inv_r0 * rb(x0 - m1_s[i]));
+          out = out - rb(k.c_d1 * d1);
+        }
+        if (a.noise) out = out + k.c_n * a.noise[(long long)s * R * D + i * D + w];
+        lat_s[i] = bf(tobf(out));
+        m1_s[i] = bf(tobf(x0));
+      }
+      if (ctl && (tl & 63) == 0 && s + 1 < a.s1) {   // [D][2] hand-off of dim d (one 4-byte store)
+        const bf16x2 pr = {tobf(lat_s[0]), tobf(n > 1 ? lat_s[1] : 0.f)};
+        __hip_atomic_store((hl_gu32*)(a.lat + 2 * w), __builtin_bit_cast(unsigned, pr), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (s + 1 < a.s1 && !grid_wait()) return;
+  }
+  // the launch's outputs (its end publishes them)
+  if (ctl && w < D && (threadIdx.x & 63) < n) {
+    const int i = threadIdx.x & 63;
+    a.x[i * D + w] = tobf(lat_s[i]);
+    a.m1[i * D + w] = tobf(m1_s[i]);
+  }
+  stamp(63);
+}
+
+bool head_loop_fits(int H, int F, int R, int L) {
+  return H == hl::H && F == hl::F && (R == 2 || R == 4) && L >= 1 && L <= hl::LMAX && head_loop_grid() >= hl::G;
+}
+
+int head_loop_grid() {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    return n;
+  }();
+  return cus;
+}
+
+template <int R, bool ST>
+static int launch_loop(const HeadLoopArgs& a, hipStream_t st) {
+  static const bool attr = hipFuncSetAttribute((const void*)k_head_loop<R, ST>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, hl::Lds<R>::TOTAL) ==
+                           hipSuccess;
+  if (!attr) return 3;
+  HeadLoopArgs args = a;
+  void* kp[] = {&args};
+  // cooperative: the grid is checked against the occupancy query at launch (one
+  // workgroup per CU by its LDS), so the in-launch waits never face an unplaced grid
+  if (hipLaunchCooperativeKernel((const void*)k_head_loop<R, ST>, dim3(hl::G), dim3(hl::NT), kp, hl::Lds<R>::TOTAL,
+                                 st) != hipSuccess)
+    return 2;
+  return 0;
+}
+
+int launch_head_loop(const HeadLoopArgs& a, hipStream_t st) {
+  if (!head_loop_fits(hl::H, hl::F, a.R, a.L) || a.n * 2 != a.R || a.s1 <= a.s0) return 1;
+  if (a.stamps) return a.R == 2 ? launch_loop<2, true>(a, st) : launch_loop<4, true>(a, st);
+  return a.R == 2 ? launch_loop<2, false>(a, st) : launch_loop<4, false>(a, st);
+}

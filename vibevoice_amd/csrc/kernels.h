@@ -251,6 +251,33 @@ bool head_ffn_fits(int H, int F, int R);
 int head_ffn_grid();
 int launch_head_ffn(const HeadFfnArgs& a, hipStream_t st);
 
+// ---- the whole diffusion of a token in one persistent launch (head_loop.hip):
+// steps [s0, s1) of noisy -> L FFN layers -> final + CFG + DPM-Solver++ at 2n <= 4 rows
+struct HeadLoopArgs {
+  int n, R, s0, s1, L, pad_;
+  float eps, cfg;
+  bf16* x;                  // [n][D] latents: in (noise / current), out (after step s1 - 1)
+  bf16* m1;                 // [n][D] previous x0 (2nd-order history), in / out
+  const float* noise;       // sde-dpmsolver++: step s's [2n][D] fp32 at noise + s*2n*D; nullptr (ODE)
+  const DpmCoef* coef;      // [steps] (cfg from `cfg`)
+  const bf16* mods;         // step s's adaLN rows [2n][modw] at mods + (s - s0) * 2n * modw
+  long long modw;
+  const bf16* noisy_w;      // [H][D] MFMA-packed
+  const bf16* final_w;      // [D][H] MFMA-packed
+  const bf16* nw[4];        // per-layer RMSNorm weights [H]
+  const bf16* gu[4];        // gate / up rows in head_ffn_pack's stream order
+  const bf16* dn[4];        // down_proj^T [F][H]
+  bf16* xh;                 // [2n][H] state (workspace)
+  bf16* lat;                // [D][2] latents of the previous step (workspace; hand-off)
+  float* slab;              // [G][2n][H] fp32 partials of down (workspace)
+  unsigned* sync;           // 10 lines of 32 words: 8 shard counters, top counter, generation
+  unsigned* err;            // set to 1 when a grid wait gave up
+  unsigned long long* stamps;   // diagnostics: [G][64] s_memrealtime per phase, or nullptr
+};
+bool head_loop_fits(int H, int F, int R, int L);
+int head_loop_grid();
+int launch_head_loop(const HeadLoopArgs& a, hipStream_t st);
+
 size_t gemv_mix_lds(int M, int T, int C);
 int launch_gemm(GemmArgs a, hipStream_t st);
 int launch_sum_rows(SumRows s, long long count, hipStream_t st);
