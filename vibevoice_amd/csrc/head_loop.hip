@@ -68,7 +68,7 @@ struct Lds {
   static constexpr int PART = P2 + P2_B, PART_B = R * H * 4;
   static constexpr int FW = PART + PART_B, FW_B = H * 2;
   static constexpr int SM = FW + FW_B;                      // small scalars below
-  static constexpr int SM_B = (8 + ROWS * R + HPW * R + 4 * E + 3 * R * 2 + 16) * 4;
+  static constexpr int SM_B = (12 + ROWS * R + HPW * R + 4 * E + 3 * R * 2 + 16) * 4;
   static constexpr int TOTAL = SM + SM_B;
   static_assert((G * E + E * 16) * 4 <= P2_B && E % 4 == 0, "reduce scratch fits p2");
   static_assert(TOTAL <= 160 * 1024, "one workgroup per CU");
@@ -164,8 +164,8 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
   float* inv_s = sm;                         // [R] (<= 4)
   unsigned* ok_s = (unsigned*)(sm + 4);
   float* lat_s = sm + 5;                     // [2] latent (dim d) of samples 0, 1
-  float* m1_s = sm + 7;                      // (8 words in all so far)
-  float* gu_s = sm + 8;                      // [ROWS][R]
+  float* m1_s = sm + 7;                      // [2] 2nd-order history of dim d (12 words reserved so far)
+  float* gu_s = sm + 12;                     // [ROWS][R]
   float* h_s = gu_s + ROWS * R;              // [HPW][R]
   float* res_s = h_s + HPW * R;              // [E] residual of this workgroup's outputs
   float* gate_s = res_s + E;                 // [E]
@@ -262,8 +262,9 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
       // (the control wave alone: LDS accesses of one wave are ordered)
       if (lane < E / 4) MemWT::st8(a.xh + f0 + 4 * lane, *(const bf16x4*)((const bf16*)out_s + 4 * lane));
     }
+    stamp(40);
     if (!grid_wait()) return;
-    stamp(1);
+    stamp(41);
     for (int l = 0; l < a.L; ++l) {
       const bool has_next = l + 1 < a.L || s + 1 < a.s1;
       const int ln = l + 1 < a.L ? l + 1 : 0;
@@ -296,7 +297,7 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
         }
       }
       __syncthreads();
-      stamp(2 + 3 * l);
+      stamp(8 * l + 0);
       if (wave < R) {   // inverse RMS in row_inv's order
         const int lane = tl & 63;
         float ss = 0.f;
@@ -332,6 +333,7 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
         }
       }
       __syncthreads();
+      stamp(8 * l + 1);
       if (!ctl) {   // gate / up rows (rho = t / KS: 2u gate, 2u + 1 up of unit u), 16 lanes per row
         const int t = hl_vopaque(tl);
         const int rho = t / KS, kap = t - rho * KS;
@@ -355,6 +357,7 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
         if (has_next) issue_gu(ln, t);   // the next layer's gate / up slice, streamed from here on
       }
       __syncthreads();
+      stamp(8 * l + 2);
       if (tl < HPW * R) {   // SiLU(gate) * up, rounded to the bf16 activation (epi_silu8)
         const int u = tl / R, r = tl - u * R;
         const float g = gu_s[2 * u * R + r], up = gu_s[(2 * u + 1) * R + r];
@@ -369,6 +372,7 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
         for (int s2 = 0; s2 < UPS; ++s2) wd[s2] = *(const bf16x8*)(dn_s + (s2 * NTC + t) * 8);
       }
       __syncthreads();
+      stamp(8 * l + 3);
       float y[R][8];
       if (!ctl) {   // down: subset q2 of 6 hidden units x columns [8 c2, 8 c2 + 8)
         const int t = hl_vopaque(tl);
@@ -415,6 +419,7 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
         }
       }
       __syncthreads();
+      stamp(8 * l + 4);
       if (ctl) {   // the partial to slab w, written through
         const int lane = hl_vopaque(tl & 63);
         float* sl = slab + (long long)w * R * H;
@@ -424,7 +429,7 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
           __hip_atomic_store((gu64*)(sl + 2 * q), b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
-      stamp(3 + 3 * l);
+      stamp(8 * l + 5);
       if (!grid_wait()) return;
       // ================= B: outputs [f0, f0 + E) over the 256 slabs, fixed order; gated residual
       if (ctl) {   // red[p][e] = slab p's value of output f0 + e: E / 4 16-byte pieces per slab, LDS DMA
@@ -438,7 +443,7 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __syncthreads();
-      stamp(4 + 3 * l);
+      stamp(8 * l + 6);
       if (tl < E * 16) {
         const int e = tl >> 4, qq = tl & 15;
         float sacc = 0.f;
@@ -461,6 +466,7 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
         const int lane = tl & 63;
         MemWT::st8(xh + f0 + 4 * lane, *(const bf16x4*)((const bf16*)out_s + 4 * lane));
       }
+      stamp(8 * l + 7);
       if (!grid_wait()) return;
     }
     // ================= FinalLayer (workgroup w = latent dim d < 64) + CFG + solver update
