@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
     issue_dn(0, t);
     issue_gu(0, t);
   }
-  stamp(0);
+  stamp(62);
   if (ctl && w < D) {   // final_layer row d, latent / history of dim d (workgroup d < 64)
     const int lane = threadIdx.x & 63;
     for (int c = lane; c < NCH; c += 64) *(bf16x8*)(fw_s + 8 * c) = hl_ld(hl_packed(a.final_w, H, w, 8 * c));
