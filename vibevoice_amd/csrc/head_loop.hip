@@ -351,10 +351,6 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
         if (kap == 0)
 #pragma unroll
           for (int r = 0; r < R; ++r) gu_s[rho * R + r] = acc[r];
-        // (a compiler fence: the next slice's loads must not be hoisted above the
-        // dot products -- both slices would then hold registers at once)
-        asm volatile("" ::: "memory");
-        if (has_next) issue_gu(ln, t);   // the next layer's gate / up slice, streamed from here on
       }
       __syncthreads();
       stamp(8 * l + 2);
@@ -364,10 +360,9 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
         h_s[u * R + r] = bf(tobf(rb(silu_f(rb(g))) * rb(up)));
       }
       bf16x8 wd[UPS];
-      if (!ctl) {   // this layer's DMA'd down rows (older than the CPT gate / up loads just issued)
+      if (!ctl) {   // this layer's DMA'd down rows (the prefetch: the only loads of the compute waves)
         const int t = hl_vopaque(tl);
-        if (has_next) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
         for (int s2 = 0; s2 < UPS; ++s2) wd[s2] = *(const bf16x8*)(dn_s + (s2 * NTC + t) * 8);
       }
@@ -377,7 +372,6 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
       if (!ctl) {   // down: subset q2 of 6 hidden units x columns [8 c2, 8 c2 + 8)
         const int t = hl_vopaque(tl);
         const int q2 = t / NCH, c2 = t - q2 * NCH;
-        if (has_next) issue_dn(ln, t);   // the next layer's down rows into the same LDS
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -420,6 +414,16 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
       }
       __syncthreads();
       stamp(8 * l + 4);
+      if (!ctl && has_next) {
+        // The next layer's slice (gate / up rows into registers, down rows into the
+        // same LDS, both dead since the dots / the down product): issuing ~166 KB
+        // per CU stalls the issuing waves for microseconds, so it is done here,
+        // while the control wave publishes the partial and waits for the grid.
+        const int t = hl_vopaque(tl);
+        asm volatile("" ::: "memory");
+        issue_gu(ln, t);
+        issue_dn(ln, t);
+      }
       if (ctl) {   // the partial to slab w, written through
         const int lane = hl_vopaque(tl & 63);
         float* sl = slab + (long long)w * R * H;
