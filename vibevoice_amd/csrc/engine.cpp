@@ -700,8 +700,9 @@ int vv_finalize(vv_ctx* c) {
   // the fused FFN layer's streams (optional: without them every layer runs gate|up + down)
   c->hf_ready = false;
   // grid-wait words + the error word (always present: vv_sync_error_async reads it)
-  CHK(c->hf_sync.ensure(11 * 128));
-  HIPCHK(hipMemset(c->hf_sync.p, 0, 11 * 128));
+  // (+ 256 arrival flags of the persistent head at word 12 * 32, head_loop.hip)
+  CHK(c->hf_sync.ensure(12 * 128 + 1024));
+  HIPCHK(hipMemset(c->hf_sync.p, 0, 12 * 128 + 1024));
   if (head_ffn_fits(H, F, 2) && c->w.count("head.0.gu_rows")) {
     for (int l = 0; l < L; ++l) {
       const std::string p = "head." + std::to_string(l);
