@@ -28,9 +28,10 @@
 // latents, stores -- and the arrival / poll.
 // Hand-offs follow MI355X_MICROARCH.md's table, first row: write-through (sc1)
 // stores of 4 / 8 bytes (and LDS DMA loads with sc1), the control wave's
-// s_waitcnt vmcnt(0), then ONE flag store per workgroup (its running wait count)
-// that every workgroup's control wave polls with sc1 loads (hl_grid_wait), then
-// a workgroup barrier.  Waits are bounded (~200 ms, error word; vv_sync_error*).
+// s_waitcnt vmcnt(0), ONE arrival per workgroup on an XCD-sharded counter whose
+// last arrival bumps the generation word every control wave polls
+// (hl_grid_wait), then a workgroup barrier.  Waits are bounded (~200 ms, error
+// word; vv_sync_error*).
 // Residency: one workgroup per CU (<= 160 KB LDS), launched cooperatively, so
 // the launch fails with a HIP error instead of waiting on an unplaced grid.
 //
@@ -123,30 +124,32 @@ DEV const bf16* hl_packed(const bf16* w, int K, int j, int k) {
   return w + ((long long)((j >> 4) * (K >> 5) + (k >> 5)) * 64 + (j & 15) + 16 * ((k & 31) >> 3)) * 8;
 }
 
-// One grid-wide wait, by the whole control wave (behind its own s_waitcnt
-// vmcnt(0): it made every store this workgroup publishes).  Arrival: lane 0
-// stores this workgroup's running wait count into its own flag (a 4-byte
-// write-through store, no read-modify-write to serialise on); then every lane
-// polls 4 of the 256 flags (one 16-byte sc1 load each) until all of them reach
-// the target.  One store and one load round trip, where the sharded counter
-// (shard -> top -> generation) chained three device-scope atomics before the
-// first poll could succeed.  Flags are monotonic across launches (each launch
-// makes every workgroup wait the same number of times), compared wrap-safe.
-DEV bool hl_grid_wait(unsigned* flags, unsigned target, int w, unsigned* err, int lane) {
-  if (lane == 0) __hip_atomic_store((hl_gu32*)(flags + w), target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// One grid-wide wait: arrival of this workgroup + poll until k waits of this
+// launch have completed.  Control wave, lane 0, behind the control wave's own
+// s_waitcnt vmcnt(0) (it made every store this workgroup publishes).  The
+// arrival adds to this workgroup's XCD shard counter (w % 8: 32 workgroups
+// each); a shard's 32nd arrival of a wait bumps the generation word, so one
+// wait completes when the generation has advanced by 8.  Two chained
+// device-scope atomics before the release (round 4's k_head_ffn chained three:
+// shard -> top -> generation); polling all 256 per-workgroup flags instead
+// (one store per arrival, a 1 KB sc1 sweep per poll) measured 2x slower: 256
+// pollers sweeping the same lines.  Counters are monotonic across launches and
+// compared wrap-safe.
+DEV bool hl_grid_wait(unsigned* sync, unsigned g0, unsigned k, int w, unsigned* err) {
+  using namespace hl;
+  unsigned* gen = sync + 9 * LINE;
+  const unsigned v = __hip_atomic_fetch_add((hl_gu32*)(sync + (w & 7) * LINE), 1u, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+  if ((v + 1) % (G / 8) == 0) __hip_atomic_fetch_add((hl_gu32*)gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  for (;;) {
-    const u64x2 v = {MemWT::l64(flags + 4 * lane), MemWT::l64(flags + 4 * lane + 2)};
-    const unsigned f0 = (unsigned)v[0], f1 = (unsigned)(v[0] >> 32), f2 = (unsigned)v[1], f3 = (unsigned)(v[1] >> 32);
-    const bool ok = (int)(f0 - target) >= 0 && (int)(f1 - target) >= 0 && (int)(f2 - target) >= 0 &&
-                    (int)(f3 - target) >= 0;
-    if (__builtin_amdgcn_ballot_w64(!ok) == 0) return true;
+  while ((unsigned)(__hip_atomic_load((hl_gu32*)gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - g0) < 8 * k) {
     __builtin_amdgcn_s_sleep(1);
     if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {   // ~200 ms at 100 MHz
-      if (lane == 0) __hip_atomic_store((hl_gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((hl_gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
     }
   }
+  return true;
 }
 
 template <int R, bool ST>
@@ -186,12 +189,11 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
   const bool ctl = wave == NTC / 64;
   const int w = blockIdx.x, n = a.n;
   const int f0 = w * E;                      // this workgroup's slice of the flat [R][H] state
-  unsigned* flags = a.sync + 12 * LINE;      // [G] arrival flags (hl_grid_wait)
   unsigned g0 = 0, nwait = 0;
   // the control wave's memory instructions (hand-offs, operand DMA) issue ahead of
   // the compute waves' weight stream when both are ready
   if (ctl) __builtin_amdgcn_s_setprio(3);
-  if (ctl) g0 = flags[w];                    // (written by an earlier launch: a kernel boundary published it)
+  if (ctl) g0 = __hip_atomic_load((hl_gu32*)(a.sync + 9 * LINE), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   auto stamp = [&](int k) {
     if constexpr (ST) {
       if (threadIdx.x == NTC && a.stamps) a.stamps[w * 64 + k] = __builtin_amdgcn_s_memrealtime();
@@ -202,8 +204,7 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
     ++nwait;
     if (ctl) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const bool ok = hl_grid_wait(flags, g0 + nwait, w, a.err, threadIdx.x & 63);
-      if ((threadIdx.x & 63) == 0) ok_s[0] = ok ? 1u : 0u;
+      if ((threadIdx.x & 63) == 0) ok_s[0] = hl_grid_wait(a.sync, g0, nwait, w, a.err) ? 1u : 0u;
     }
     __syncthreads();
     return ok_s[0] != 0;
