@@ -129,10 +129,16 @@ int vv_gemm_tune_apack(int on);
 /* Test / A-B switch: 1 (default) = the fused head FFN layer (head_ffn.hip)
  * where it applies; 0 = gate|up + down GEMV launches per layer. */
 int vv_head_fused(int on);
-/* Test / A-B switch: 1 (default) = at 2n <= 4 rows the whole diffusion of a
- * token runs as one persistent launch per 16 steps (head_loop.hip); 0 = one
- * fused-layer launch per FFN layer + the noisy / final GEMVs. */
+/* Test / A-B switch: 2 (default) = at 2n <= 4 rows the whole diffusion of a
+ * token runs as one persistent launch per 16 steps (head_loop.hip), plain
+ * launch; 1 = the same launched cooperatively (measured +0.35 ms per loop
+ * step); 0 = one fused-layer launch per FFN layer + the noisy / final GEMVs.
+ * The persistent head runs only while its context is the device's only one
+ * with it bound (two cannot be resident together). */
 int vv_head_loop(int on);
+/* Test query: 1 when vv_diffusion_sample of n samples on ctx would run the
+ * persistent head now. */
+int vv_head_loop_active(vv_ctx* ctx, int n);
 /* Diagnostic: per-workgroup phase stamps of the persistent head launch into buf
  * ([256][64] u64, the last step's phases; NULL = off). */
 int vv_head_loop_stamps(void* buf);

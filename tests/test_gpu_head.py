@@ -217,21 +217,53 @@ def test_head_loop_vs_oracle_and_layer_launches(n, S, sde):
     noise = torch.randn(2 * n, 64, generator=g).bfloat16()
     z = torch.randn(S, 2 * n, 64, generator=g) if sde else None
     outs = []
+    assert L.vv_head_loop_active(eng.h, n) == 1
     try:
-        for loop in (1, 1, 0):
+        for loop in (2, 2, 0, 1):   # plain launch (default) twice, per-layer launches, cooperative launch
             L.vv_head_loop(loop)
             x = noise[:n].to(dev).contiguous()
             eng.diffusion_sample(pos.to(dev), neg.to(dev), x, 1.3, sde_noise=None if z is None else z.to(dev))
             torch.cuda.synchronize()
             outs.append(x.float().cpu())
     finally:
-        L.vv_head_loop(1)
+        L.vv_head_loop(2)
     eng.check_sync()
     ref = ohead.sample_speech_tokens(sd, pos, neg, noise, S, 1.3, hc.head_layers, sde_noise=z)
     err, c = rel_err(outs[0], ref), cos(outs[0], ref)
     e_layer = rel_err(outs[0], outs[2])
     print(f"head loop n={n} S={S} sde={sde}: vs oracle rel {err:.3e} cos {c:.6f} (per-layer launches "
           f"{rel_err(outs[2], ref):.3e}); loop vs per-layer rel {e_layer:.3e}")
-    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[3])
     assert err < 2e-2 and c > 0.999
     assert e_layer < 1e-2
+
+
+def test_head_loop_only_for_the_devices_sole_context():
+    """Two persistent head launches cannot be resident together (one workgroup
+    per CU each): with a second context of the same head bound on the device,
+    both take the per-layer launches; the first goes back to the persistent
+    head when the second is destroyed (graphs re-captured: vv_ws_epoch)."""
+    from vibevoice_amd import _lib
+    L = _lib.lib()
+    g = torch.Generator().manual_seed(41)
+    sd, hc, H = real_head_sd(g)
+    tiny = tiny_config(hidden=H, layers=1, heads=12, kv_heads=2, inter=256)
+    a, _ = engine_with_head(tiny, sd)
+    assert L.vv_head_loop_active(a.h, 1) == 1
+    e0 = L.vv_ws_epoch()
+    b, _ = engine_with_head(tiny, sd)
+    assert L.vv_head_loop_active(a.h, 1) == 0 and L.vv_head_loop_active(b.h, 1) == 0
+    assert L.vv_ws_epoch() != e0
+    a.set_steps(10)
+    pos = torch.randn(1, H, generator=g).bfloat16()
+    neg = torch.randn(1, H, generator=g).bfloat16()
+    noise = torch.randn(2, 64, generator=g).bfloat16()
+    x = noise[:1].to(dev).contiguous()
+    a.diffusion_sample(pos.to(dev), neg.to(dev), x, 1.3)
+    torch.cuda.synchronize()
+    ref = ohead.sample_speech_tokens(sd, pos, neg, noise, 10, 1.3, hc.head_layers)
+    assert rel_err(x, ref) < 2e-2
+    e1 = L.vv_ws_epoch()
+    b.close()
+    assert L.vv_head_loop_active(a.h, 1) == 1 and L.vv_ws_epoch() != e1
+    a.close()

@@ -90,6 +90,7 @@ EXPORTS = [
     ("vv_head_fused", I, [I]),
     ("vv_head_loop", I, [I]),
     ("vv_head_loop_stamps", I, [P]),
+    ("vv_head_loop_active", I, [P, I]),
     ("vv_head_loop_replay", I, [P, I, P, P, P, F, I, P]),
     ("vv_gemv_tune_bal", I, [I]),
     ("vv_head_ffn_stamps", I, [P]),

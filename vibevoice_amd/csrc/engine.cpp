@@ -12,6 +12,8 @@
 #include <cmath>
 #include <cstring>
 #include <atomic>
+#include <map>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -64,6 +66,25 @@ struct ConvBuf {
 // Bumped whenever a workspace moves: a hipGraph captured earlier bakes the old
 // pointers in, so the host drops its graphs when this changes (vv_ws_epoch).
 static std::atomic<int> g_ws_epoch{0};
+// Contexts per device that could run the persistent diffusion head (head_loop.hip:
+// one workgroup per CU, grid-wide waits).  Two such launches from two contexts
+// cannot be resident together, so the persistent head runs only while ONE
+// finalized context of the device has it bound; a change of that count bumps the
+// epoch, so hosts re-capture graphs that baked in the other path.
+static std::mutex g_hl_mu;
+static std::map<int, int> g_hl_ctxs;
+static void hl_register(int device, int delta) {
+  std::lock_guard<std::mutex> lk(g_hl_mu);
+  const int before = g_hl_ctxs[device];
+  const int after = before + delta;
+  g_hl_ctxs[device] = after;
+  if ((before == 1) != (after == 1)) g_ws_epoch.fetch_add(1);
+}
+static bool hl_sole(int device) {
+  std::lock_guard<std::mutex> lk(g_hl_mu);
+  auto it = g_hl_ctxs.find(device);
+  return it != g_hl_ctxs.end() && it->second == 1;
+}
 
 struct DevBuf {
   void* p = nullptr;
@@ -166,6 +187,7 @@ struct vv_ctx {
   // fused head FFN layer (head_ffn.hip): partial-sum slabs, grid-wait words + error word
   DevBuf hf_slab, hf_sync;
   DevBuf hl_lat;           // persistent head (head_loop.hip): [D][2] latent hand-off
+  bool hl_registered = false;   // counted in g_hl_ctxs (its device's persistent-head contexts)
   bool hf_ready = false;   // its weights are bound (head.<l>.gu_rows / dn_rows) and the shape fits
   DevBuf rope_tab;   // [max_ctx][cos 64 | sin 64] bf16 (k_rope_table)
 };
@@ -630,6 +652,7 @@ void vv_destroy(vv_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
+  if (c->hl_registered) hl_register(c->device, -1);
   DevBuf* bufs[] = {&c->norm_ws, &c->kv_k, &c->kv_v, &c->lm_ws, &c->attn_part, &c->attn_cnt, &c->valid_ids, &c->splitk_ws, &c->splitk_cnt,
                     &c->temb, &c->tfreq_tmp, &c->head_ws, &c->codec_ws, &c->slot_scratch, &c->unit_sb,
                     &c->chain_sync, &c->chain_slabs, &c->chain_err, &c->coef_dev, &c->rope_tab, &c->zero_rows,
@@ -712,6 +735,10 @@ int vv_finalize(vv_ctx* c) {
     CHK(c->hf_slab.ensure((size_t)head_ffn_grid() * 4 * H * sizeof(float)));
     CHK(c->hl_lat.ensure((size_t)D * 2 * sizeof(bf16) + 256));
     c->hf_ready = true;
+    if (!c->hl_registered && head_loop_fits(H, F, 2, L)) {
+      c->hl_registered = true;
+      hl_register(c->device, +1);
+    }
   }
   // ---- connectors + latent scaling
   CHK(need(c, "conn.ac.fc1_w", {H, D}));
@@ -1216,9 +1243,9 @@ extern "C" int vv_head_fused(int on) {
 // The whole diffusion in one persistent launch (head_loop.hip) where the fused
 // layer's streams are bound and the shape fits; 0 = one k_head_ffn launch per
 // layer (A/B and tests)
-static std::atomic<int> g_head_loop{1};
-extern "C" int vv_head_loop(int on) {
-  g_head_loop = on ? 1 : 0;
+static std::atomic<int> g_head_loop{2};
+extern "C" int vv_head_loop(int on) {   // 2 (default): plain launch, 1: cooperative launch, 0: off
+  g_head_loop = on < 0 ? 0 : on > 2 ? 2 : on;
   return 0;
 }
 static std::atomic<unsigned long long*> g_head_loop_stamps{nullptr};
@@ -1499,7 +1526,7 @@ extern "C" int vv_head_layers_replay(vv_ctx* c, int n, const void* pos_h, const 
 // unsharded, the switches on.
 static bool head_loop_on(vv_ctx* c, int R, bool sharded) {
   return c->hf_ready && g_head_fused && g_head_loop && !sharded && !g_chain &&
-         head_loop_fits(c->cfg.hidden, c->cfg.head_ffn, R, c->cfg.head_layers);
+         head_loop_fits(c->cfg.hidden, c->cfg.head_ffn, R, c->cfg.head_layers) && hl_sole(c->device);
 }
 // One persistent launch over steps [s0, min(steps, s0 + HEAD_SC)); head_mods(s0)
 // must have run on the stream before it.
@@ -1536,10 +1563,16 @@ static int head_loop_launch(vv_ctx* c, const HeadRun& h, int s0, void* x_io, flo
   A.sync = (unsigned*)c->hf_sync.p;
   A.err = (unsigned*)c->hf_sync.p + 10 * 32;
   A.stamps = g_head_loop_stamps;
-  const int rc = launch_head_loop(A, st);
+  const int rc = launch_head_loop(A, g_head_loop != 2, st);
   if (rc) FAIL("persistent diffusion head: launch failed (" + std::to_string(rc) + ": " +
                hipGetErrorString(hipGetLastError()) + ")");
   return 0;
+}
+
+// Diagnostic (tests): 1 when vv_diffusion_sample(n) of this context would run the
+// persistent head now
+extern "C" int vv_head_loop_active(vv_ctx* c, int n) {
+  return head_loop_on(c, 2 * n, c->head_tp && (c->tp_size > 1 || c->comm)) ? 1 : 0;
 }
 
 // Diagnostic (bench.py's roofline of the persistent head): the condition rows and

@@ -32,8 +32,12 @@
 // last arrival bumps the generation word every control wave polls
 // (hl_grid_wait), then a workgroup barrier.  Waits are bounded (~200 ms, error
 // word; vv_sync_error*).
-// Residency: one workgroup per CU (<= 160 KB LDS), launched cooperatively, so
-// the launch fails with a HIP error instead of waiting on an unplaced grid.
+// Residency: one workgroup per CU (<= 160 KB LDS).  Plain launch: a cooperative
+// one (hipLaunchCooperativeKernel, which checks the grid against the occupancy
+// query) measured +0.35 ms per loop step inside the captured graphs (interleaved
+// same-box A/B, DESIGN.md "Persistent head"); the engine runs this kernel only
+// while its context is the device's only one with it bound (engine.cpp
+// hl_register), and a wait that still gives up is reported per step.
 //
 // Arithmetic: the FFN layer is k_gemv1 / k_head_ffn's term for term (row_inv
 // order, xform / epi_silu8 / epi_row8 rounding points; v_dot2c fp32 products);
@@ -429,7 +433,6 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
         // while the control wave publishes the partial and waits for the grid.
         const int t = hl_vopaque(tl);
         asm volatile("" ::: "memory");
-        issue_gu(ln, t);
         issue_dn(ln, t);
       }
       if (ctl) {   // the partial to slab w, written through
@@ -479,6 +482,11 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
         MemWT::st8(xh + f0 + 4 * lane, *(const bf16x4*)((const bf16*)out_s + 4 * lane));
       }
       stamp(8 * l + 7);
+      if (!ctl && has_next) {   // the next layer's gate / up slice (registers free since the dots)
+        const int t = hl_vopaque(tl);
+        asm volatile("" ::: "memory");
+        issue_gu(ln, t);
+      }
       if (!grid_wait()) return;
     }
     // ================= FinalLayer (workgroup w = latent dim d < 64) + CFG + solver update
@@ -581,11 +589,15 @@ int head_loop_grid() {
 }
 
 template <int R, bool ST>
-static int launch_loop(const HeadLoopArgs& a, hipStream_t st) {
+static int launch_loop(const HeadLoopArgs& a, bool coop, hipStream_t st) {
   static const bool attr = hipFuncSetAttribute((const void*)k_head_loop<R, ST>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, hl::Lds<R>::TOTAL) ==
                            hipSuccess;
   if (!attr) return 3;
+  if (!coop) {   // plain launch: the same residency (one workgroup per CU), no launch-time check
+    hipLaunchKernelGGL((k_head_loop<R, ST>), dim3(hl::G), dim3(hl::NT), hl::Lds<R>::TOTAL, st, a);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+  }
   HeadLoopArgs args = a;
   void* kp[] = {&args};
   // cooperative: the grid is checked against the occupancy query at launch (one
@@ -596,8 +608,8 @@ static int launch_loop(const HeadLoopArgs& a, hipStream_t st) {
   return 0;
 }
 
-int launch_head_loop(const HeadLoopArgs& a, hipStream_t st) {
+int launch_head_loop(const HeadLoopArgs& a, bool coop, hipStream_t st) {
   if (!head_loop_fits(hl::H, hl::F, a.R, a.L) || a.n * 2 != a.R || a.s1 <= a.s0) return 1;
-  if (a.stamps) return a.R == 2 ? launch_loop<2, true>(a, st) : launch_loop<4, true>(a, st);
-  return a.R == 2 ? launch_loop<2, false>(a, st) : launch_loop<4, false>(a, st);
+  if (a.stamps) return a.R == 2 ? launch_loop<2, true>(a, coop, st) : launch_loop<4, true>(a, coop, st);
+  return a.R == 2 ? launch_loop<2, false>(a, coop, st) : launch_loop<4, false>(a, coop, st);
 }

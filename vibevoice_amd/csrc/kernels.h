@@ -276,7 +276,7 @@ struct HeadLoopArgs {
 };
 bool head_loop_fits(int H, int F, int R, int L);
 int head_loop_grid();
-int launch_head_loop(const HeadLoopArgs& a, hipStream_t st);
+int launch_head_loop(const HeadLoopArgs& a, bool coop, hipStream_t st);
 
 size_t gemv_mix_lds(int M, int T, int C);
 int launch_gemm(GemmArgs a, hipStream_t st);
