@@ -27,7 +27,8 @@ def engine_with_head(cfg, head_sd, seed=0):
     sd = synthetic_state_dict(cfg, seed=seed, device="cpu", mode="test", with_acoustic_encoder=False)
     for k, v in head_sd.items():
         sd["model.prediction_head." + k] = v
-    return Engine(cfg, sd, dev, max_batch=4, max_ctx=256), sd
+    # both head layouts: these tests switch between the fused / persistent and the GEMV paths on one engine
+    return Engine(cfg, sd, dev, max_batch=4, max_ctx=256, head_layout="both"), sd
 
 
 @pytest.mark.parametrize("S", [5, 10])

@@ -6,7 +6,9 @@ instantiated for (unsharded 1.5B head: H 1,536, F 4,608)."""
 import torch
 
 from tiny import tiny_config
-from vibevoice_amd.weights import HEAD_FFN_SHAPE, head_ffn_pack, head_ffn_unpack, pack, synthetic_state_dict
+from vibevoice_amd.config import VibeVoiceConfig
+from vibevoice_amd.weights import (HEAD_FFN_SHAPE, head_ffn_pack, head_ffn_unpack, head_layout_for, pack,
+                                   synthetic_state_dict)
 
 
 def test_head_ffn_pack_order_and_inverse():
@@ -42,3 +44,25 @@ def test_pack_emits_fused_streams_for_the_instantiated_shape():
     ws = pack(synthetic_state_dict(small, seed=1, device="cpu", mode="test", with_acoustic_encoder=False), small, "cpu",
               with_acoustic_encoder=False)
     assert not any(k.endswith(("gu_rows", "dn_rows")) for k in ws)
+
+
+def test_one_head_layout_resident():
+    """an engine packs ONE copy of the head FFN -- the fused
+    streams where every call has 2n <= 4 rows (max_batch <= 2) at the shape the
+    fused kernels are built for, else the GEMV layout -- and "both" only when
+    asked (tests switching paths on one engine).  1.5B: 170 MB saved."""
+    cfg = VibeVoiceConfig.builtin("1.5B")
+    assert head_layout_for(cfg, 1) == "fused" and head_layout_for(cfg, 2) == "fused"
+    assert head_layout_for(cfg, 3) == "gemv" and head_layout_for(cfg, 8) == "gemv"
+    assert head_layout_for(cfg, 1, tp_size=2, tp_head=True) == "gemv"          # sharded width
+    assert head_layout_for(VibeVoiceConfig.builtin("Large"), 1) == "gemv"
+    sd = synthetic_state_dict(cfg, device="meta")
+    sizes = {}
+    for layout in ("fused", "gemv", "both"):
+        w = pack(sd, cfg, "meta", head_layout=layout)
+        has_f = all(f"head.{i}.gu_rows" in w and f"head.{i}.dn_rows" in w for i in range(4))
+        has_g = all(f"head.{i}.gu_w" in w and f"head.{i}.down_w" in w for i in range(4))
+        assert (has_f, has_g) == {"fused": (True, False), "gemv": (False, True), "both": (True, True)}[layout]
+        sizes[layout] = sum(t.numel() * t.element_size() for t in w.values())
+    ffn = 4 * 3 * 4608 * 1536 * 2
+    assert sizes["both"] - sizes["fused"] == ffn and sizes["both"] - sizes["gemv"] == ffn

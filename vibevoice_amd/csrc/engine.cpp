@@ -188,6 +188,7 @@ struct vv_ctx {
   DevBuf hf_slab, hf_sync;
   DevBuf hl_lat;           // persistent head (head_loop.hip): [D][2] latent hand-off
   bool hl_registered = false;   // counted in g_hl_ctxs (its device's persistent-head contexts)
+  bool head_gemv = true;        // the head FFN's GEMV layout is bound (head.<l>.gu_w / down_w)
   bool hf_ready = false;   // its weights are bound (head.<l>.gu_rows / dn_rows) and the shape fits
   DevBuf rope_tab;   // [max_ctx][cos 64 | sin 64] bf16 (k_rope_table)
 };
@@ -713,12 +714,20 @@ int vv_finalize(vv_ctx* c) {
   CHK(need(c, "head.t0_w", {H, 256}));
   CHK(need(c, "head.t2_w", {H, H}));
   CHK(need(c, "head.ada_w", {(3LL * L + 2) * H, H}));
+  // the FFN in either layout, or both (weights.py head_layout_for): the GEMV
+  // layout (any batch), the fused layer's streams (2n <= 4 rows)
+  c->head_gemv = c->w.count("head.0.gu_w") > 0;
   for (int l = 0; l < L; ++l) {
     const std::string p = "head." + std::to_string(l);
     CHK(need(c, p + ".norm", {H}));
-    CHK(need(c, p + ".gu_w", {2LL * F, H}));
-    CHK(need(c, p + ".down_w", {H, F}));
+    if (c->head_gemv) {
+      CHK(need(c, p + ".gu_w", {2LL * F, H}));
+      CHK(need(c, p + ".down_w", {H, F}));
+    }
   }
+  if (!c->head_gemv && !(head_ffn_fits(H, F, 2) && c->w.count("head.0.gu_rows")))
+    FAIL("diffusion head FFN: neither the GEMV layout (head.<l>.gu_w / down_w) nor the fused layer's streams "
+         "(head.<l>.gu_rows / dn_rows, this shape) are bound");
   CHK(need(c, "head.final_w", {D, H}));
   // the fused FFN layer's streams (optional: without them every layer runs gate|up + down)
   c->hf_ready = false;
@@ -1470,6 +1479,9 @@ static int head_layer(vv_ctx* c, const HeadRun& h, int s, int l, hipStream_t st)
     KCHK(launch_head_ffn(a, st));
     return 0;
   }
+  if (!c->head_gemv)
+    FAIL("diffusion head: " + std::to_string(h.R) + " rows need the GEMV layout (head.<l>.gu_w / down_w), which this "
+         "engine did not bind (packed for max_batch <= 2: weights.head_layout_for)");
   CHK(head_gemm(c, h, g, st));
   g = gemm_args(c, h.R, H, F, rowmap(h.act, F), W(c, p + ".down_w"), EPI_RES, h.xh_m);
   g.epi.res = partial ? rowmap(c->zero_rows.p, H) : h.xh_m;
@@ -1624,7 +1636,7 @@ int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, 
   bf16 *mods = h.mods, *act = h.act, *v = h.v, *m1 = h.m1, *sa = h.sa;
   const int F = k.head_ffn;
   RowMap xh_m = h.xh_m;
-  if (g_chain && R <= 16 && c->steps <= HEAD_SC && !sharded) {
+  if (g_chain && R <= 16 && c->steps <= HEAD_SC && !sharded && c->head_gemv) {
     // all S steps (noisy, L x [gate|up, down], final + CFG + DPM) in one persistent launch
     auto it = c->head_chain.find(n);
     if (it == c->head_chain.end() || it->second.mode != g_chain) {

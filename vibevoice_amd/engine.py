@@ -10,7 +10,7 @@ import torch
 from . import _lib
 from .config import VibeVoiceConfig
 from .schedule import Schedule
-from .weights import codec_channels, head_tp_check, pack
+from .weights import codec_channels, head_layout_for, head_tp_check, pack
 
 _VALID_IDS_DEFAULT = None
 
@@ -64,7 +64,8 @@ class Engine:
     """One device-resident VibeVoice model instance."""
 
     def __init__(self, cfg: VibeVoiceConfig, state_dict, device="cuda", max_batch=1, max_ctx=4096,
-                 valid_ids=None, tp_rank=0, tp_size=1, tp_unique_id=None, packed=None, tp_head=False):
+                 valid_ids=None, tp_rank=0, tp_size=1, tp_unique_id=None, packed=None, tp_head=False,
+                 head_layout=None):
         """tp_size > 1: rank tp_rank's shard of the LM; tp_unique_id (bytes of
         vv_tp_unique_id, shared by the group) creates its RCCL communicator, None
         leaves it for a single-process group (lm_forward_group).
@@ -72,7 +73,10 @@ class Engine:
         packing `state_dict` again — a second context over the same device
         weights (the standalone tokenizer API's own codec slots).
         tp_head: shard the diffusion head's FFN over the TP group as well
-        (vv_tp_shard_head)."""
+        (vv_tp_shard_head).
+        head_layout: the head FFN weights' layout (weights.head_layout_for by
+        default: one copy, the one this capacity runs; "both" for tests that
+        switch paths on one engine)."""
         L = _lib.lib()
         self.cfg = cfg
         self.device = torch.device(device)
@@ -88,8 +92,10 @@ class Engine:
         if self.tp_head:
             head_tp_check(cfg, tp_size)
         with torch.cuda.device(self.device):
+            layout = head_layout or head_layout_for(cfg, max_batch, tp_size, self.tp_head)
             self.w = packed if packed is not None else pack(state_dict, cfg, self.device, tp_rank=tp_rank,
-                                                            tp_size=tp_size, tp_head=self.tp_head)
+                                                            tp_size=tp_size, tp_head=self.tp_head,
+                                                            head_layout=layout)
             h = ctypes.c_void_p()
             self._ecfg = engine_config(cfg, max_batch, max_ctx, tp_size, self.tp_head)
             _lib.check(L.vv_create(ctypes.byref(self._ecfg), self.device.index or 0, ctypes.byref(h)), "create")

@@ -291,8 +291,24 @@ def head_tp_default(cfg: VibeVoiceConfig, tp_size):
     return tp_size > 1 and hc.head_layers * 3 * F * hc.hidden_size * 2 > (192 << 20)
 
 
-def pack(sd, cfg: VibeVoiceConfig, device, with_acoustic_encoder=True, tp_rank=0, tp_size=1, tp_head=False):
+def head_layout_for(cfg: VibeVoiceConfig, max_batch, tp_size=1, tp_head=False):
+    """The diffusion head FFN's weight layout an engine of this capacity packs
+    (ONE copy resident): "fused" -- the fused layer's /
+    persistent head's streams (head.<l>.gu_rows / dn_rows) -- where every
+    diffusion call has 2n <= 4 rows (max_batch <= 2) and the shape is the one
+    those kernels are built for; else "gemv" (head.<l>.gu_w / down_w, MFMA
+    packed), which every batch size can run."""
+    hc = cfg.diffusion_head_config
+    F = int(hc.hidden_size * hc.head_ffn_ratio) // (tp_size if tp_head and tp_size > 1 else 1)
+    return "fused" if max_batch <= 2 and (hc.hidden_size, F) == HEAD_FFN_SHAPE else "gemv"
+
+
+def pack(sd, cfg: VibeVoiceConfig, device, with_acoustic_encoder=True, tp_rank=0, tp_size=1, tp_head=False,
+         head_layout="both"):
     """Reference state dict -> {engine name: contiguous device tensor}.
+
+    head_layout: "gemv", "fused" (head_layout_for) or "both" (tests that switch
+    between the two paths on one engine; byte accounting).
 
     tp_size > 1: this rank's Megatron shard of the Qwen2 layers
     (configuration_vibevoice.py:175-183): q/k/v rows of its heads and
@@ -352,9 +368,11 @@ def pack(sd, cfg: VibeVoiceConfig, device, with_acoustic_encoder=True, tp_rank=0
     for i in range(hc.head_layers):
         p = f"{HEAD}layers.{i}."
         out[f"head.{i}.norm"] = t(sd[p + "norm.weight"])
-        out[f"head.{i}.gu_w"] = t(_gu(sd[p + "ffn.gate_proj.weight"][hs], sd[p + "ffn.up_proj.weight"][hs]))
-        out[f"head.{i}.down_w"] = t(sd[p + "ffn.down_proj.weight"][:, hs])
-        if (hc.hidden_size, hs.stop - hs.start) == HEAD_FFN_SHAPE:   # the fused layer's streams
+        fits = (hc.hidden_size, hs.stop - hs.start) == HEAD_FFN_SHAPE
+        if head_layout != "fused" or not fits:
+            out[f"head.{i}.gu_w"] = t(_gu(sd[p + "ffn.gate_proj.weight"][hs], sd[p + "ffn.up_proj.weight"][hs]))
+            out[f"head.{i}.down_w"] = t(sd[p + "ffn.down_proj.weight"][:, hs])
+        if head_layout != "gemv" and fits:   # the fused layer's streams
             out[f"head.{i}.gu_rows"] = t(head_ffn_pack(sd[p + "ffn.gate_proj.weight"][hs],
                                                        sd[p + "ffn.up_proj.weight"][hs]))
             out[f"head.{i}.dn_rows"] = t(sd[p + "ffn.down_proj.weight"][:, hs].t())
