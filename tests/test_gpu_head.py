@@ -23,6 +23,16 @@ pytestmark = pytest.mark.gpu
 dev = "cuda"
 
 
+@pytest.fixture(autouse=True)
+def _collect_engines():
+    """Engines of earlier tests / modules that are garbage but not yet collected
+    still count as live contexts with the persistent head bound (engine.cpp
+    hl_register: it runs only for a device's sole such context)."""
+    import gc
+    gc.collect()
+    yield
+
+
 def engine_with_head(cfg, head_sd, seed=0):
     sd = synthetic_state_dict(cfg, seed=seed, device="cpu", mode="test", with_acoustic_encoder=False)
     for k, v in head_sd.items():
