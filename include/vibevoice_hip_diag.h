@@ -176,10 +176,6 @@ int vv_attn_defer(int on, int chunk);
  * group's last-arriving workgroup, o_proj merging the groups; n >= 2: at most
  * n (<= 128) such splits; 0 = 1,024-key splits merged by k_attn_merge. */
 int vv_attn_group(int on);
-/* A/B switch: 1 (default) = the grouped long-context passes run one k_attn
- * workgroup per CU, each walking (split, row) units in row-major order; 0 = one
- * workgroup per unit (same arithmetic, bit-identical). */
-int vv_attn_units(int on);
 /* The decode attention's plan for a pass of ntok rows over max_pos_p1 keys,
  * host logic only (CPU tests): out = {prefill, nsplit, chunk, defer, group,
  * ngroups}. */

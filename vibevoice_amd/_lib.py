@@ -86,7 +86,6 @@ EXPORTS = [
     ("vv_rope_table", I, [I]),
     ("vv_attn_defer", I, [I, I]),
     ("vv_attn_group", I, [I]),
-    ("vv_attn_units", I, [I]),
     ("vv_attn_pass_plan", I, [I, I, I, I, I, ctypes.POINTER(I)]),
     ("vv_head_fused", I, [I]),
     ("vv_head_loop", I, [I]),

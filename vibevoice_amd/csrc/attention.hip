@@ -78,9 +78,9 @@ DEV float row16_sum(float v) {
   return v + dpp_f<0x140>(v);
 }
 
-DEV void astamp(const AttnArgs& a, int which, int split, int rk) {
+DEV void astamp(const AttnArgs& a, int which) {
   if (a.stamps && threadIdx.x == 0) {
-    unsigned long long* p = a.stamps + ((long long)rk * a.nsplit + split) * 4;
+    unsigned long long* p = a.stamps + ((long long)blockIdx.y * gridDim.x + blockIdx.x) * 4;
     p[which] = __builtin_amdgcn_s_memrealtime();
     // at entry, slot 3 also records where the workgroup runs (bit 62 marks it; a
     // storing workgroup overwrites it): XCC_ID << 32 | HW_ID (cu / sh / se fields)
@@ -90,7 +90,7 @@ DEV void astamp(const AttnArgs& a, int which, int split, int rk) {
   }
 }
 
-template <int G, int NW, bool UNITS = false>
+template <int G, int NW>
 __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
   __shared__ float wm[NW][G], wl[NW][G];
   __shared__ float wo[NW][G][128];
@@ -98,25 +98,16 @@ __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
   __shared__ float fm[G], fl[G];
   __shared__ unsigned last_flag;
   constexpr int d = 128;
-  // One (split, row x kv head) unit.  Grid (split, row x kv head): consecutive
-  // workgroup ids -- which the dispatcher deals round-robin over the 8 XCDs --
-  // are consecutive splits of one (row, kv head), so every XCD gets an equal
-  // share of each row's keys.  (With (row x kv head, split) a row's splits fell
-  // on id % 8 = the same 2 of 8 XCDs per kv head.)  Long contexts (a.units):
-  // ONE workgroup per CU, each walking units blockIdx.x, + gridDim.x, ... in
-  // row-major order (the long row's splits first): with one workgroup per
-  // (split, row) the grid outnumbered the CUs (k_attn holds a CU per workgroup),
-  // and a keyed workgroup dealt to an XCD whose CUs were all busy started a
-  // whole split late (64K: launch 17.9 us against a median workgroup done at
-  // 10.5, tools/attn_long_stamps.py).
-  auto unit = [&](const int split, const int rk) {
-  // the thread's indices re-derived per unit (opaque to hipcc: hoisted out of the
-  // unit walk they held registers across it and spilled)
-  int tid = threadIdx.x;
-  if constexpr (UNITS) asm volatile("" : "+v"(tid));
-  const int t = tid, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int r = lane & 15, g = lane >> 4;
-  astamp(a, 0, split, rk);
+  astamp(a, 0);
+  // grid (split, row x kv head): consecutive workgroup ids -- which the
+  // dispatcher deals round-robin over the 8 XCDs -- are consecutive splits of
+  // one (row, kv head), so every XCD gets an equal share of each row's keys.
+  // (With (row x kv head, split) a row's splits fell on id % 8 = the same 2
+  // of 8 XCDs per kv head: at 65K keys B = 1 the long row's work ran on half
+  // the chip while the short negative row's splits held the other half.)
+  const int rk = blockIdx.y, split = blockIdx.x;
   const int qi = rk / a.nkv, kh = rk - qi * a.nkv;
   // the row's length, its KV slot and the Q fragments: all issued before any
   // is used, one memory round trip (the compiler sank the slot and Q loads
@@ -189,7 +180,7 @@ __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
   if (w0 + 32 < w1) load(w0 + 32, kB, vB);
   if (a.stamps) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    astamp(a, 1, split, rk);
+    astamp(a, 1);
   }
   auto step = [&](int c0, const bf16x8 (&kc)[2][4], bf16x8 (&vc)[8]) {   // vc is masked in place
     if (c0 + 32 > w1) {   // the wave's tail step (uniform): keys kb + e >= w1 contribute nothing
@@ -258,7 +249,7 @@ __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
     }
   }
   __syncthreads();
-  astamp(a, 2, split, rk);
+  astamp(a, 2);
   // merge the waves: waves with no keys carry m = -inf, l = 0
   if (t < G) {
     float M = -INFINITY;
@@ -293,7 +284,7 @@ __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
     }
     if (a.stamps) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      astamp(a, 3, split, rk);
+      astamp(a, 3);
     }
     return;
   }
@@ -411,20 +402,7 @@ __global__ void __launch_bounds__(64 * NW) k_attn(AttnArgs a) {
   }
   if (a.stamps) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    astamp(a, 3, split, rk);
-  }
-  };
-  if constexpr (UNITS) {   // its own instantiation: the loop costs the one-unit form registers
-    const int nunits = a.nsplit * a.nq * a.nkv;
-#pragma nounroll
-    for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
-      __syncthreads();   // the previous unit's LDS readers are done
-      int uu = u;
-      asm volatile("" : "+s"(uu));   // opaque: nothing derived from the unit is hoisted out of the loop
-      unit(uu % a.nsplit, uu / a.nsplit);
-    }
-  } else {
-    unit(blockIdx.x, blockIdx.y);
+    astamp(a, 3);
   }
 }
 
@@ -931,12 +909,6 @@ static int launch_attn_pf(const AttnArgs& a, hipStream_t st) {
 // sizes its own splits from its length (row_chunk), so a plan made for
 // max_ctx serves every step of a captured graph.
 static std::atomic<int> g_att_chunk{0}, g_att_merge_in{-1};   // diagnostic overrides (vv_attn_tune)
-// A/B switch: 1 (default) = long-context passes as one workgroup per CU walking the units (k_attn)
-static std::atomic<int> g_attn_units{1};
-extern "C" int vv_attn_units(int on) {
-  g_attn_units = on ? 1 : 0;
-  return 0;
-}
 extern "C" int vv_attn_tune(int chunk, int merge_in) {
   if (chunk % ATT_KC) return 1;
   g_att_chunk = chunk;
@@ -962,17 +934,6 @@ int attn_plan(int nq, int nkv, int max_len, int* chunk) {
 template <int NW>
 static void launch_attn_nw(const AttnArgs& a, dim3 grid, hipStream_t st) {
   const dim3 blk(64 * NW);
-  if (a.units) {   // the grouped long-context plan (8 waves) at the GQA ratios of the 1.5B / Large models
-    switch (a.nh / a.nkv) {
-      case 6: hipLaunchKernelGGL((k_attn<6, NW, true>), grid, blk, 0, st, a); return;
-      case 7: hipLaunchKernelGGL((k_attn<7, NW, true>), grid, blk, 0, st, a); return;
-      default: break;
-    }
-    AttnArgs b = a;   // other ratios: one workgroup per unit
-    b.units = 0;
-    launch_attn_nw<NW>(b, dim3(a.nsplit, a.nq * a.nkv), st);
-    return;
-  }
   switch (a.nh / a.nkv) {
     case 1: hipLaunchKernelGGL((k_attn<1, NW>), grid, blk, 0, st, a); break;
     case 2: hipLaunchKernelGGL((k_attn<2, NW>), grid, blk, 0, st, a); break;
@@ -998,11 +959,7 @@ int launch_attn(AttnArgs a, hipStream_t st) {
   const int mi = g_att_merge_in;
   a.merge = !a.defer && !a.group && a.nsplit > (mi >= 0 ? mi : ATT_MERGE_IN) ? 1 : 0;
   dim3 grid(a.nsplit, a.nq * a.nkv);
-  // long contexts (the grouped plan): one workgroup per CU walking the units
-  const int ncu = head_ffn_grid();
   const int nw = a.chunk >= 256 ? 8 : a.chunk >= 128 ? 4 : 2;   // 32 keys per wave step
-  a.units = a.group && nw == 8 && g_attn_units && ncu > 0 && (long long)a.nsplit * a.nq * a.nkv > ncu ? 1 : 0;
-  if (a.units) grid = dim3(ncu, 1);
   if (nw == 8) launch_attn_nw<8>(a, grid, st);
   else if (nw == 4) launch_attn_nw<4>(a, grid, st);
   else launch_attn_nw<2>(a, grid, st);

@@ -250,25 +250,24 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
       const int lane = hl_vopaque(threadIdx.x & 63);
       const int no = lane / LPO, nk = lane - no * LPO;
       const int nf = f0 + min(no, E - 1), nr = nf / H, ncol = nf - nr * H, xr = nr % n;
-      bf16x8 nwt[NCL], xv[NCL];
+      bf16* lx = (bf16*)p2;   // the latents as [2][D] in LDS (p2 is free between the waits)
+      bf16x8 nwt[NCL];
 #pragma unroll
-      for (int j = 0; j < NCL; ++j) {
-        const int d0 = nk * DPL + 8 * j;
-        nwt[j] = hl_ld(hl_packed(a.noisy_w, D, ncol, d0));
-        if (s == a.s0) {   // the launch's input latents
-          xv[j] = hl_ld(a.x + xr * D + d0);
-        } else {           // the previous step's latents, [D][2] (dims d0 .. d0+7, both samples): sc1
-          const bf16x8 p0 = MemWT::ld16(a.lat + 2 * d0), p1 = MemWT::ld16(a.lat + 2 * d0 + 8);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            xv[j][e] = xr ? p0[2 * e + 1] : p0[2 * e];
-            xv[j][4 + e] = xr ? p1[2 * e + 1] : p1[2 * e];
-          }
+      for (int j = 0; j < NCL; ++j) nwt[j] = hl_ld(hl_packed(a.noisy_w, D, ncol, nk * DPL + 8 * j));
+      if (lane < 16) {
+        if (s == a.s0) {   // the launch's input latents, [n][D]
+          const int i = lane >> 3;
+          if (i < n) *(bf16x8*)(lx + 8 * lane) = hl_ld(a.x + 8 * lane);
+        } else {           // the previous step's latents, [D][2] (dims 4 lane .. 4 lane + 3, both samples): sc1
+          const bf16x8 p = MemWT::ld16(a.lat + 8 * lane);
+          *(bf16x4*)(lx + 4 * lane) = (bf16x4){p[0], p[2], p[4], p[6]};
+          *(bf16x4*)(lx + D + 4 * lane) = (bf16x4){p[1], p[3], p[5], p[7]};
         }
       }
+      // (one wave: its LDS stores precede its loads)
       float acc = 0.f;
 #pragma unroll
-      for (int j = 0; j < NCL; ++j) acc = hl_dot8(nwt[j], xv[j], acc);
+      for (int j = 0; j < NCL; ++j) acc = hl_dot8(nwt[j], *(const bf16x8*)(lx + xr * D + nk * DPL + 8 * j), acc);
       acc = group_sum<LPO>(acc);
       if (nk == 0 && no < E) ((bf16*)out_s)[no] = tobf(acc);   // EPI_STORE (no bias)
       // (the control wave alone: LDS accesses of one wave are ordered)
@@ -574,8 +573,28 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
   stamp(63);
 }
 
+// One workgroup per CU, every wave resident from the start: the plain launch
+// checks nothing, so the build is checked here.  A kernel with scratch (VGPR
+// spills) is refused: round 5 measured R = 4 with an 8-byte spill time out in its
+// first grid wait under the plain launch (its waves waited for scratch slots).
+template <int R>
+static bool loop_resident() {
+  static const bool ok = [] {
+    hipFuncAttributes fa{};
+    int nb = 0;
+    const void* k = (const void*)k_head_loop<R, false>;
+    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, hl::Lds<R>::TOTAL) != hipSuccess ||
+        hipFuncGetAttributes(&fa, k) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, hl::NT, hl::Lds<R>::TOTAL) != hipSuccess)
+      return false;
+    return fa.localSizeBytes == 0 && nb >= 1;
+  }();
+  return ok;
+}
+
 bool head_loop_fits(int H, int F, int R, int L) {
-  return H == hl::H && F == hl::F && (R == 2 || R == 4) && L >= 1 && L <= hl::LMAX && head_loop_grid() >= hl::G;
+  return H == hl::H && F == hl::F && (R == 2 || R == 4) && L >= 1 && L <= hl::LMAX && head_loop_grid() >= hl::G &&
+         (R == 2 ? loop_resident<2>() : loop_resident<4>());
 }
 
 int head_loop_grid() {

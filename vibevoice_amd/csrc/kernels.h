@@ -181,8 +181,6 @@ struct AttnArgs {
   int ngroups;
   float* part_o2;
   float* part_ml2;
-  int units;            // set by launch_attn: 1 = one workgroup per CU walking the (split, row) units
-  int pad_u;
 };
 
 // out_r = sum_r in_r for every r (single-process tensor-parallel group)
