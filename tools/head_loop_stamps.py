@@ -12,7 +12,8 @@ s_memrealtime stamps (10 ns ticks) of its LAST diffusion step's phases:
 plus stamp 62 (launch entry).  Prints per phase the median / max over the 256
 workgroups relative to the first entry, and the phase-to-phase medians.
 
-usage: python tools/head_loop_stamps.py [n]"""
+usage: python tools/head_loop_stamps.py [n] [mode]   (mode: vv_head_loop's value for the persistent
+launch, 2 = plain launch with shard-polled waits (default), 3 = generation-word waits, 1 = cooperative)"""
 import os
 import sys
 
@@ -39,13 +40,14 @@ def capture(eng, pos, neg, x, s):
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+    mode = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     g = torch.Generator().manual_seed(5)
     sdh, hc, H = real_head_sd(g)
     cfg = tiny_config(hidden=H, layers=1, heads=12, kv_heads=2, inter=256)
     sd = synthetic_state_dict(cfg, seed=0, device="cpu", mode="test", with_acoustic_encoder=False)
     for k, v in sdh.items():
         sd["model.prediction_head." + k] = v
-    eng = Engine(cfg, sd, "cuda", max_batch=4, max_ctx=64)
+    eng = Engine(cfg, sd, "cuda", max_batch=2, max_ctx=64, head_layout="both")
     eng.set_steps(10)
     pos = torch.randn(n, H, generator=g).bfloat16().cuda()
     neg = torch.randn(n, H, generator=g).bfloat16().cuda()
@@ -53,8 +55,9 @@ def main():
     x = x0.clone()
     L = _lib.lib()
     s = torch.cuda.Stream()
-    for loop in (0, 1):   # the per-layer launches, then the persistent launch
+    for loop in (0, mode):   # the per-layer launches, then the persistent launch
         L.vv_head_loop(loop)
+        assert L.vv_head_loop_active(eng.h, n) == (1 if loop else 0)
         eng.diffusion_sample(pos, neg, x, 1.3)
         gr = capture(eng, pos, neg, x, s)
         best = 1e9

@@ -1268,7 +1268,8 @@ extern "C" int vv_head_ffn_stamps(void* buf) {   // diagnostic: [256][8] per-wor
   return 0;
 }
 // A grid wait of the fused head layer gave up (workgroups not co-resident):
-// every output since the last call is invalid.  Reset on read.
+// every output since the last call is invalid.  Reset on read (with the wait
+// counters).
 // (hipMemcpy on the null stream does not wait for non-blocking streams, where
 // the host's generate() runs: synchronise the device first)
 int vv_sync_error(vv_ctx* c) {
@@ -1277,7 +1278,9 @@ int vv_sync_error(vv_ctx* c) {
     HIPCHK(hipDeviceSynchronize());
     if (hipMemcpy(&v, (unsigned*)c->hf_sync.p + 10 * 32, 4, hipMemcpyDeviceToHost) != hipSuccess)
       FAIL("vv_sync_error: reading the error word failed (hipMemcpy)");
-    if (v) HIPCHK(hipMemset((unsigned*)c->hf_sync.p + 10 * 32, 0, 4));
+    // a launch that gave up left the wait counters part-advanced: with nothing in
+    // flight (the device is synchronised) every counter restarts from 0
+    if (v) HIPCHK(hipMemset(c->hf_sync.p, 0, 12 * 128));
   }
   return v ? 1 : 0;
 }

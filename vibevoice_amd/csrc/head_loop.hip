@@ -132,16 +132,25 @@ DEV const bf16* hl_packed(const bf16* w, int K, int j, int k) {
 // launch have completed.  Control wave, lane 0, behind the control wave's own
 // s_waitcnt vmcnt(0) (it made every store this workgroup publishes).  The
 // arrival adds to this workgroup's XCD shard counter (w % 8: 32 workgroups
-// each); a shard's 32nd arrival of a wait bumps the generation word, so one
-// wait completes when the generation has advanced by 8.  Two chained
+// each); a shard's 32nd arrival of a wait bumps this kernel's generation word,
+// so one wait completes when the generation has advanced by 8.  Two chained
 // device-scope atomics before the release (round 4's k_head_ffn chained three:
-// shard -> top -> generation); polling all 256 per-workgroup flags instead
-// (one store per arrival, a 1 KB sc1 sweep per poll) measured 2x slower: 256
-// pollers sweeping the same lines.  Counters are monotonic across launches and
-// compared wrap-safe.
+// shard -> top -> generation).  Measured against (DESIGN.md "Persistent head"):
+// polling all 256 per-workgroup flags (2x slower: 256 pollers sweeping the same
+// lines) and polling the 8 shard counters without the generation word (one
+// atomic per wait, but 8 lines per poll: 755 -> 774 us per head sample).
+// Counters are monotonic across launches and compared wrap-safe.
+//
+// The launch's base generation: only this kernel bumps its word (line 11; the
+// shard counters are shared with k_head_ffn, 256 workgroups and 32 arrivals per
+// shard per wait in both), 8 per wait, so it is a multiple of 8 between
+// launches.  A workgroup reading it at entry may see up to 7 bumps of the first
+// wait (other shards complete it; its own cannot): base = word rounded down to 8.
+DEV unsigned* hl_gen(unsigned* sync) { return sync + 11 * hl::LINE; }
+
 DEV bool hl_grid_wait(unsigned* sync, unsigned g0, unsigned k, int w, unsigned* err) {
   using namespace hl;
-  unsigned* gen = sync + 9 * LINE;
+  unsigned* gen = hl_gen(sync);
   const unsigned v = __hip_atomic_fetch_add((hl_gu32*)(sync + (w & 7) * LINE), 1u, __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT);
   if ((v + 1) % (G / 8) == 0) __hip_atomic_fetch_add((hl_gu32*)gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -197,7 +206,7 @@ __global__ void __launch_bounds__(hl::NT) k_head_loop(HeadLoopArgs a) {
   // the control wave's memory instructions (hand-offs, operand DMA) issue ahead of
   // the compute waves' weight stream when both are ready
   if (ctl) __builtin_amdgcn_s_setprio(3);
-  if (ctl) g0 = __hip_atomic_load((hl_gu32*)(a.sync + 9 * LINE), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (ctl) g0 = __hip_atomic_load((hl_gu32*)hl_gen(a.sync), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~7u;
   auto stamp = [&](int k) {
     if constexpr (ST) {
       if (threadIdx.x == NTC && a.stamps) a.stamps[w * 64 + k] = __builtin_amdgcn_s_memrealtime();

@@ -270,7 +270,7 @@ struct HeadLoopArgs {
   bf16* xh;                 // [2n][H] state (workspace)
   bf16* lat;                // [D][2] latents of the previous step (workspace; hand-off)
   float* slab;              // [G][2n][H] fp32 partials of down (workspace)
-  unsigned* sync;           // 10 lines of 32 words: 8 shard counters, (unused), generation
+  unsigned* sync;           // 12 lines of 32 words: 8 shard counters, (k_head_ffn's two), error word, generation
   unsigned* err;            // set to 1 when a grid wait gave up
   unsigned long long* stamps;   // diagnostics: [G][64] s_memrealtime per phase, or nullptr
 };
