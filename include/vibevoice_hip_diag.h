@@ -191,6 +191,17 @@ int vv_norm_pack(int on);
  * one k_block launch.  0 = separate k_mix + GEMM launches everywhere.  Every
  * mask gives the same bits. */
 int vv_codec_mix_fusion(int mask);
+/* Test / A-B switch: 1 (default) = a codec stage of Block1Ds at T = 1 and one
+ * sample (the acoustic decoder's first, the semantic encoder's last) runs as
+ * one persistent launch (codec_stage.hip) while ctx is the device's only
+ * context registered for persistent kernels; 0 = one launch per GEMV. */
+int vv_codec_stage(int on);
+/* Test query: 1 when a one-sample codec step on ctx would run the acoustic
+ * decoder's first stage as the persistent launch now. */
+int vv_codec_stage_active(vv_ctx* ctx);
+/* Diagnostic: the acoustic decoder's stage launches record per-workgroup
+ * s_memrealtime stamps into buf ([256][64] u64; nullptr: off). */
+int vv_codec_stage_stamps(void* buf);
 int vv_rmsnorm_bf16(int M, int C, const void* x, int64_t ldx, const void* w, float eps, void* y, int64_t ldy,
                     vv_stream st);
 

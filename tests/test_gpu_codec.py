@@ -22,6 +22,15 @@ pytestmark = pytest.mark.gpu
 dev = "cuda"
 
 
+@pytest.fixture(autouse=True)
+def _collect_engines():
+    """The persistent codec stage runs only while its context is the device's
+    only one registered for persistent kernels: drop engines of earlier tests."""
+    import gc
+    gc.collect()
+    yield
+
+
 def sub(sd, prefix):
     return {k[len(prefix):]: v for k, v in sd.items() if k.startswith(prefix)}
 
@@ -91,6 +100,7 @@ def test_mix_fusion_bit_exact(n, mask):
     lats = [torch.randn(n, 64, generator=g).bfloat16().to(dev) for _ in range(4)]
     slots = torch.arange(n, dtype=torch.int32, device=dev)
     outs = {}
+    _lib.lib().vv_codec_stage(0)   # the stage kernel would replace the n = 1 T = 1 stages in both modes
     try:
         for fuse in (0, mask):
             _lib.lib().vv_codec_mix_fusion(fuse)
@@ -106,6 +116,7 @@ def test_mix_fusion_bit_exact(n, mask):
             outs[fuse] = res
     finally:
         _lib.lib().vv_codec_mix_fusion(3)
+        _lib.lib().vv_codec_stage(1)
     for i, (a, b) in enumerate(zip(outs[0], outs[mask])):
         assert torch.equal(a, b), (n, i, (a.float() - b.float()).abs().max().item())
 
@@ -144,3 +155,61 @@ def test_codec_stream_batch_sizes(n):
             if not (ea < 3e-2 and es < 3e-2):
                 bad.append((step, r, ea, es))
     assert not bad, bad
+
+
+def test_codec_stage_persistent_launch():
+    """The C = 2,048 T = 1 stages (acoustic decoder's first, semantic encoder's
+    last; 8 Block1Ds each) as ONE persistent launch (codec_stage.hip) vs the
+    launch-per-GEMV path (XF_MIX fc1 + fc2 GEMVs) and vs the oracle, one
+    sample over four streamed frames (the stage's conv buffers carry state from
+    frame to frame): the front half is XF_MIX's arithmetic, fc1 / fc2 sum in
+    another order, so within bf16 of both (the codec tolerance, rel L2 < 3e-2,
+    vs each: the audio runs through 60+ bf16 layers after the stage, and the two
+    paths differ by as much as each differs from the oracle, 1.4e-2 vs 1.6e-2
+    at frame 0), and bitwise equal run to run."""
+    from vibevoice_amd import _lib
+    L = _lib.lib()
+    cfg = tiny_config(ratios=(8, 5, 5, 4, 2, 2), depths="3-3-3-3-3-3-8", nf=32)
+    sd = synthetic_state_dict(cfg, seed=3, device="cpu", mode="test", with_acoustic_encoder=False)
+    eng = Engine(cfg, sd, dev, max_batch=2, max_ctx=64)
+    assert L.vv_codec_stage_active(eng.h) == 1
+    H = cfg.decoder_config.hidden_size
+    dd = ocodec.codec_dims(cfg.acoustic_tokenizer_config, "decoder")
+    ed = ocodec.codec_dims(cfg.semantic_tokenizer_config, "encoder")
+    sd_a, sd_s = sub(sd, "model.acoustic_tokenizer."), sub(sd, "model.semantic_tokenizer.")
+    s_f, b_f = sd["model.speech_scaling_factor"], sd["model.speech_bias_factor"]
+    g = torch.Generator().manual_seed(13)
+    lats = [torch.randn(1, 64, generator=g).bfloat16() for _ in range(4)]
+    slot = torch.tensor([1], dtype=torch.int32, device=dev)
+    outs = {}
+    try:
+        for mode in (1, 0, 1):
+            L.vv_codec_stage(mode)
+            assert L.vv_codec_stage_active(eng.h) == mode
+            eng.codec_reset(slot)
+            res = []
+            for lat in lats:
+                audio = torch.empty(1, cfg.hop, dtype=torch.bfloat16, device=dev)
+                sem = torch.empty(1, 128, dtype=torch.bfloat16, device=dev)
+                emb = torch.zeros(2, H, dtype=torch.bfloat16, device=dev)
+                eng.codec_step(slot, lat.to(dev), audio, sem, emb, slot)
+                res.append((audio, sem, emb[1:2]))
+            torch.cuda.synchronize()
+            outs.setdefault(mode, []).append(res)
+    finally:
+        L.vv_codec_stage(1)
+    eng.check_sync()
+    st_a, st_s = ocodec.StreamState(2), ocodec.StreamState(2)
+    idx = torch.tensor([1])
+    for f, lat in enumerate(lats):
+        a_ref = ocodec.decode(sd_a, dd, (lat / s_f - b_f).unsqueeze(-1), st_a, idx)
+        s_ref = ocodec.encode(sd_s, ed, a_ref, st_s, idx)[:, 0]
+        e_ref = connector(sd, "model.acoustic_connector.", lat) + connector(sd, "model.semantic_connector.", s_ref)
+        for k, (name, ref) in enumerate((("audio", a_ref[:, 0]), ("sem", s_ref), ("emb", e_ref))):
+            got, base, again = outs[1][0][f][k], outs[0][0][f][k], outs[1][1][f][k]
+            e_o, e_b = rel_err(got, ref), rel_err(got, base)
+            print(f"frame {f} {name}: rel {e_o:.3e} vs oracle ({rel_err(base, ref):.3e} GEMV path), "
+                  f"{e_b:.3e} vs the GEMV path")
+            assert torch.equal(got, again), (f, name)
+            assert e_o < 3e-2 and cos(got, ref) > 0.999, (f, name, e_o)
+            assert e_b < 3e-2 and cos(got, base) > 0.999, (f, name, e_b)

@@ -1,0 +1,350 @@
+// A whole codec stage of Block1Ds at T = 1, C = 2,048, one sample, in ONE
+// persistent launch: the acoustic decoder's first stage and the semantic
+// encoder's last (8 blocks each; modular_vibevoice_tokenizer.py:620-684
+// Block1D: x + gamma * dwconv(norm(x)), then + ffn_gamma * fc2(gelu(fc1(ffn_norm(.))))).
+//
+// Why (DESIGN.md "Codec stage"): as separate launches each block is a fused
+// XF_MIX fc1 GEMV (13.6 us for 33.5 MB) and an fc2 GEMV (11.2 us for 33.5 MB):
+// each stream starts only when its launch does, behind the A row's round trip.
+// Here the grid of 256 workgroups (one per CU) stays resident for the stage and
+// streams block j+1's 256 KB slice per CU while block j's hand-offs run.
+//
+// Decomposition per workgroup w (C = 2,048, F = 8,192, G = 256):
+//   * front half: the control wave recomputes norm / conv / residual / FFN norm
+//     for the whole row (k_mix's and XF_MIX's arithmetic and summation order),
+//     the conv's six history taps ahead of time (during the previous waits);
+//     workgroup 0 appends the new conv-input row to the block's buffer;
+//   * fc1: w owns hidden units [32w, 32w + 32) (MFMA tiles 2w, 2w + 1: one
+//     contiguous 128 KB slice, LDS DMA) -> GELU -> 64 B of the hidden row,
+//     written through; grid wait;
+//   * fc2: w owns output columns [8w, 8w + 8) (half of MFMA tile w / 2, 128 KB,
+//     in registers: 16 chunks per compute thread) over the whole hidden row (LDS
+//     DMA) -> gamma residual -> 16 B of the next block's input; grid wait.
+// Weight stream order per compute wave: block j+1's fc1 DMA, then its fc2
+// register loads, both issued right after block j's fc2 products; the fc1 dots
+// wait with an explicit vmcnt(16) (the fc2 loads may still fly), the fc2 dots
+// with hipcc's own waits (nothing is issued behind them).  The compute waves'
+// queues carry nothing but weights; the control wave does every other global
+// access.  Hand-offs: write-through stores + the grid wait of persist_dev.h.
+//
+// Arithmetic: the front half is XF_MIX's term for term (bit-identical); fc1 /
+// fc2 are fp32 sums of exact bf16 products (v_dot2c) in a fixed order --
+// a different order than the MFMA GEMVs', so not bit-identical to the
+// launch-per-GEMV path (tests: within bf16 of it and of the oracle, bitwise
+// run to run).  Epilogues are epi_row8's EPI_GELU / EPI_RES.
+#include "persist_dev.h"
+
+namespace cs {
+constexpr int C = 2048, F = 4 * C, G = pk::G, CTX = 6;
+constexpr int NTC = 512, NT = NTC + 64;     // 8 compute waves + the control wave
+constexpr int NCH = C / 8;                  // 16-byte chunks of a row (= G: chunk w holds workgroup w's columns)
+constexpr int CPT = 16;                     // weight chunks per compute thread per GEMV
+constexpr int ROWS1 = F / G;                // fc1 rows per workgroup (32: two MFMA tiles)
+constexpr int ROWS2 = C / G;                // fc2 rows per workgroup (8: half a tile)
+static_assert(ROWS1 * C / 8 == CPT * NTC && ROWS2 * F / 8 == CPT * NTC && NCH == G && NCH == 4 * 64,
+              "codec stage geometry");
+// LDS carve-up (bytes)
+constexpr int W1 = 0, W1_B = ROWS1 * C * 2;            // fc1 slice (DMA), 128 KB
+constexpr int HS = W1 + W1_B, HS_B = F * 2;            // hidden row (fc2 phase) / fc1 input row (fc1 phase)
+constexpr int PA = HS + HS_B, PA_B = C * 4;            // the conv's history taps summed (fp32)
+constexpr int W6 = PA + PA_B, W6_B = C * 2;            // the conv's tap on the new row
+constexpr int RED = W6 + W6_B, RED_B = 8 * ROWS1 * 4;  // compute-wave partials
+constexpr int SM = RED + RED_B, SM_B = 64;             // ok flag, this workgroup's 8 columns of y
+constexpr int TOTAL = SM + SM_B;
+static_assert(TOTAL <= 160 * 1024, "one workgroup per CU");
+}  // namespace cs
+
+// the four 16-lane rows of a wave summed per lane position (lanes l, l ^ 16, l ^ 32, l ^ 48)
+DEV float cs_rows_sum(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+__global__ void __launch_bounds__(cs::NT) k_codec_stage(CodecStageArgs a) {
+  using namespace cs;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16* w1_s = (bf16*)(smem + W1);
+  bf16* h_s = (bf16*)(smem + HS);     // fc2 phase: the hidden row
+  bf16* a_s = (bf16*)(smem + HS);     // fc1 phase: fc1's input row (same bytes)
+  float* pa_s = (float*)(smem + PA);  // [NCH][8]
+  bf16* w6_s = (bf16*)(smem + W6);    // [NCH][8]
+  float* red = (float*)(smem + RED);
+  unsigned* ok_s = (unsigned*)(smem + SM);
+  bf16* y_s = (bf16*)(smem + SM + 16);
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool ctl = wave == NTC / 64;
+  const int w = blockIdx.x;
+  const long long slot = a.slots[0];
+  unsigned g0 = 0, nwait = 0;
+  if (ctl) __builtin_amdgcn_s_setprio(3);
+  if (ctl) g0 = __hip_atomic_load((hl_gu32*)hl_gen(a.sync), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~7u;
+  // diagnostics (tools/codec_stage_stamps.py): per block j, slot 8j + k, k =
+  // 0 front half begins, 1 fc1 input in LDS, 2 (compute wave 0) fc1 slice landed,
+  // 3 fc1 partials in LDS, 4 hidden-row wait released, 5 hidden row in LDS,
+  // 6 fc2 partials in LDS, 7 next-input wait released
+  auto stamp = [&](int k, bool by_ctl) {
+    if (a.stamps && threadIdx.x == (by_ctl ? NTC : 0)) a.stamps[w * 64 + k] = __builtin_amdgcn_s_memrealtime();
+  };
+
+  // ---- the weight stream of block j (compute waves): fc1 slice by LDS DMA
+  // (chunk g = i * NTC + t of the contiguous slice -> LDS 16 g), then the fc2
+  // slice into registers (chunk g: k-block g >> 5, k-sub (g >> 3) & 3, row g & 7
+  // of the workgroup's half tile; a wave's load = eight full 128-byte runs)
+  bf16x8 w2[CPT];
+  auto issue = [&](int j, int t) {
+    const bf16* g1 = hl_opaque(a.b[j].fc1_w) + (long long)w * ROWS1 * C;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) hl_dma16<false>(w1_s + (i * NTC + 64 * wave) * 8, g1 + ((long long)i * NTC + t) * 8);
+    const bf16* g2 = hl_opaque(a.b[j].fc2_w) + (long long)(w >> 1) * F * 16 + (w & 1) * 64;
+    const int r = t & 7, s = (t >> 3) & 3;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int kc = (i * NTC + t) >> 5;
+      w2[i] = hl_ldnt(g2 + (long long)kc * 512 + (16 * s + r) * 8);
+    }
+  };
+
+  // ---- the conv's history taps of block jb for chunks c = lane + 64 q, q in
+  // {q0, q0 + 1} (control wave): XF_MIX's tap order, taps 0..5 summed; the
+  // sum and tap 6 parked in LDS for the front half
+  auto hist = [&](int jb, int q0) {
+    const int lane = hl_vopaque((int)threadIdx.x & 63);
+    const bf16* mb = hl_opaque(a.b[jb].mix) + slot * a.b[jb].mix_sB;
+    const bf16* dw = hl_opaque(a.b[jb].dw_w);
+    bf16x8 hv[2][CTX], wk[2][7];
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      const int c = lane + 64 * (q0 + qq);
+#pragma unroll
+      for (int r = 0; r < CTX; ++r) hv[qq][r] = hl_ld(mb + (long long)r * C + c * 8);
+#pragma unroll
+      for (int k = 0; k < 7; ++k) wk[qq][k] = hl_ld(dw + (long long)c * 56 + k * 8);
+    }
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      const int c = lane + 64 * (q0 + qq);
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < CTX; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int f = j * 7 + k;
+          acc[j] += bf(wk[qq][f >> 3][f & 7]) * bf(hv[qq][k][j]);
+        }
+      bf16x8 t6;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int f = j * 7 + 6;
+        t6[j] = wk[qq][f >> 3][f & 7];
+      }
+      *(f32x4*)(pa_s + c * 8) = (f32x4){acc[0], acc[1], acc[2], acc[3]};
+      *(f32x4*)(pa_s + c * 8 + 4) = (f32x4){acc[4], acc[5], acc[6], acc[7]};
+      *(bf16x8*)(w6_s + c * 8) = t6;
+    }
+  };
+
+  // ---- the front half of block j (control wave; chunks c = lane + 64 q):
+  // y = x + gamma * dwconv(norm(x)) (workgroup 0 appends norm(x) to the conv
+  // buffer), a = ffn_norm(y) -> LDS; this workgroup's 8 columns of y -> LDS
+  auto front = [&](int j) {
+    const int lane = hl_vopaque((int)threadIdx.x & 63);
+    const CodecStageBlock& B = a.b[j];
+    bf16x8 xv[4], nw[4], db[4], gm[4], fw[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = lane + 64 * q;
+      xv[q] = j == 0 ? hl_ld(a.x + c * 8) : MemWT::ld16(hl_opaque(a.xe) + c * 8);   // this launch's rows: sc1
+      nw[q] = hl_ld(B.norm + c * 8);
+      db[q] = hl_ld(B.dw_b + c * 8);
+      gm[q] = hl_ld(B.gamma + c * 8);
+      fw[q] = hl_ld(B.ffn_norm + c * 8);
+    }
+    float ss = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {   // per-chunk sums, then chunks in ascending order (XF_MIX's)
+      float s8 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s8 += bf(xv[q][e]) * bf(xv[q][e]);
+      ss += s8;
+    }
+    const float inv = rsqrtf(wave_sum(ss) / (float)C + a.eps);
+    bf16x8 yv[4];
+    float ss2 = 0.f;
+    bf16* nb = B.mix + slot * B.mix_sB + (long long)a.ctx * C;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = lane + 64 * q;
+      bf16x8 nr;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) nr[e] = tobf(rb(rb(bf(xv[q][e]) * inv) * bf(nw[q][e])));
+      if (w == 0) *(bf16x8*)(nb + c * 8) = nr;   // read by the next frame's launch
+      const f32x4 p0 = *(const f32x4*)(pa_s + c * 8), p1 = *(const f32x4*)(pa_s + c * 8 + 4);
+      const bf16x8 t6 = *(const bf16x8*)(w6_s + c * 8);
+      float acc[8] = {p0[0], p0[1], p0[2], p0[3], p1[0], p1[1], p1[2], p1[3]};
+      float s8 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        acc[e] += bf(t6[e]) * bf(nr[e]);
+        yv[q][e] = tobf(bf(xv[q][e]) + rb(rb(acc[e] + bf(db[q][e])) * bf(gm[q][e])));
+        s8 += bf(yv[q][e]) * bf(yv[q][e]);
+      }
+      ss2 += s8;
+      if (c == w) *(bf16x8*)y_s = yv[q];
+    }
+    const float inv2 = rsqrtf(wave_sum(ss2) / (float)C + a.eps);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = lane + 64 * q;
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = tobf(rb(rb(bf(yv[q][e]) * inv2) * bf(fw[q][e])));
+      *(bf16x8*)(a_s + c * 8) = o;
+    }
+  };
+
+  // The two roles run separate loops (so the compute waves' 64 weight registers
+  // are not live in the control wave's code) with the same barriers B1 .. B6.
+  if (ctl) {
+    const int lane = threadIdx.x & 63;
+    // arrival (behind this wave's own stores), `between` while the grid gathers,
+    // then the poll; false: a wait gave up
+    auto grid_wait = [&](auto between) -> bool {
+      ++nwait;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) hl_arrive(a.sync, w);
+      between();
+      if (lane == 0) ok_s[0] = hl_poll(a.sync, g0, nwait, a.err) ? 1u : 0u;
+      __syncthreads();
+      return ok_s[0] != 0;
+    };
+    hist(0, 0);
+    hist(0, 2);
+    for (int j = 0; j < a.depth; ++j) {
+      const bool last = j + 1 == a.depth;
+      stamp(8 * j + 0, true);
+      front(j);
+      __syncthreads();   // B1: fc1's input row in LDS
+      stamp(8 * j + 1, true);
+      __syncthreads();   // B2: the compute waves' fc1 partials in LDS
+      stamp(8 * j + 3, true);
+      if (lane < ROWS1 / 4) {   // 4 hidden units per lane, epi_row8's EPI_GELU
+        const bf16x4 b1 = *(const bf16x4*)(a.b[j].fc1_b + ROWS1 * w + 4 * lane);
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int u = 4 * lane + e;
+          float sacc = 0.f;
+#pragma unroll
+          for (int v = 0; v < NTC / 64; ++v) sacc += red[v * ROWS1 + u];
+          o[e] = tobf(gelu_f(rb(sacc + bf(b1[e]))));
+        }
+        MemWT::st8(hl_opaque(a.h) + ROWS1 * w + 4 * lane, o);
+      }
+      if (!grid_wait([&] { if (!last) hist(j + 1, 0); })) return;   // B3
+      stamp(8 * j + 4, true);
+      {
+        const bf16* hp = hl_opaque(a.h) + hl_vopaque(lane) * 8;   // (per-lane addresses not hoisted)
+#pragma unroll
+        for (int i = 0; i < F / 8 / 64; ++i) hl_dma16<true>(h_s + i * 512, hp + i * 512);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();   // B4: the hidden row in LDS
+      stamp(8 * j + 5, true);
+      __syncthreads();   // B5: the compute waves' fc2 partials in LDS
+      stamp(8 * j + 6, true);
+      if (lane < ROWS2) {   // epi_row8's EPI_RES with ffn_gamma
+        const int col = ROWS2 * w + lane;
+        float sacc = 0.f;
+#pragma unroll
+        for (int v = 0; v < NTC / 64; ++v) sacc += red[v * ROWS2 + lane];
+        const float yv = rb(bf(a.b[j].ffn_gamma[col]) * rb(sacc + bf(a.b[j].fc2_b[col])));
+        const bf16 o = tobf(bf(y_s[lane]) + yv);
+        if (last) rm_bfw(a.out, 0)[col] = o;   // the launch's end publishes it
+        else MemWT::st2(a.xe + col, o);
+      }
+      if (!last && !grid_wait([&] { hist(j + 1, 2); })) return;   // B6
+      stamp(8 * j + 7, true);
+    }
+  } else {
+    issue(0, threadIdx.x);
+    for (int j = 0; j < a.depth; ++j) {
+      const bool last = j + 1 == a.depth;
+      __syncthreads();   // B1
+      {   // fc1: row (t & 15) of tiles 2w / 2w + 1 over this thread's 16 chunks
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // this wave's fc1 DMA (the fc2 loads may fly)
+        stamp(8 * j + 2, false);
+        const int t = hl_vopaque((int)threadIdx.x), s = (t & 63) >> 4;
+        float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+          const int kc = (8 * i + wave) & 63;
+          const bf16x8 wv = *(const bf16x8*)(w1_s + (i * NTC + t) * 8);
+          const bf16x8 av = *(const bf16x8*)(a_s + kc * 32 + 8 * s);
+          if (i < CPT / 2) acc0 = hl_dot8(wv, av, acc0);
+          else acc1 = hl_dot8(wv, av, acc1);
+        }
+        acc0 = cs_rows_sum(acc0);
+        acc1 = cs_rows_sum(acc1);
+        if ((t & 63) < 16) {
+          red[wave * ROWS1 + (t & 15)] = acc0;
+          red[wave * ROWS1 + 16 + (t & 15)] = acc1;
+        }
+      }
+      __syncthreads();   // B2
+      __syncthreads();   // B3
+      if (!ok_s[0]) return;
+      __syncthreads();   // B4
+      {   // fc2: row (t & 7) of the half tile over this thread's 16 chunks
+        const int t = hl_vopaque((int)threadIdx.x), s = (t >> 3) & 3;
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+          const int kc = (i * NTC + t) >> 5;
+          acc = hl_dot8(w2[i], *(const bf16x8*)(h_s + kc * 32 + 8 * s), acc);
+        }
+        acc += __shfl_xor(acc, 8);
+        acc += __shfl_xor(acc, 16);
+        acc += __shfl_xor(acc, 32);
+        if ((t & 63) < ROWS2) red[wave * ROWS2 + (t & 63)] = acc;
+      }
+      __syncthreads();   // B5
+      if (!last) {
+        issue(j + 1, threadIdx.x);   // the next block's slices (fc1's LDS and the registers are free)
+        __syncthreads();   // B6
+        if (!ok_s[0]) return;
+      }
+    }
+  }
+}
+
+// One workgroup per CU, all resident from the start: the plain launch checks
+// nothing, so the build is checked here (no scratch, one workgroup fits a CU).
+static bool stage_resident() {
+  static const bool ok = [] {
+    hipFuncAttributes fa{};
+    int nb = 0;
+    const void* k = (const void*)k_codec_stage;
+    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, cs::TOTAL) != hipSuccess ||
+        hipFuncGetAttributes(&fa, k) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, cs::NT, cs::TOTAL) != hipSuccess)
+      return false;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return false;
+    return fa.localSizeBytes == 0 && nb >= 1 && cus >= cs::G;
+  }();
+  return ok;
+}
+
+bool codec_stage_fits(int C, int T, int n, int depth) {
+  return C == cs::C && T == 1 && n == 1 && depth >= 1 && depth <= 8 && stage_resident();
+}
+
+int launch_codec_stage(const CodecStageArgs& a, hipStream_t st) {
+  if (!stage_resident()) return 3;
+  hipLaunchKernelGGL(k_codec_stage, dim3(cs::G), dim3(cs::NT), cs::TOTAL, st, a);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

@@ -187,6 +187,7 @@ struct vv_ctx {
   // fused head FFN layer (head_ffn.hip): partial-sum slabs, grid-wait words + error word
   DevBuf hf_slab, hf_sync;
   DevBuf hl_lat;           // persistent head (head_loop.hip): [D][2] latent hand-off
+  DevBuf cs_sync;          // persistent codec stage (codec_stage.hip): its wait counters
   bool hl_registered = false;   // counted in g_hl_ctxs (its device's persistent-head contexts)
   bool head_gemv = true;        // the head FFN's GEMV layout is bound (head.<l>.gu_w / down_w)
   bool hf_ready = false;   // its weights are bound (head.<l>.gu_rows / dn_rows) and the shape fits
@@ -454,6 +455,32 @@ extern "C" int vv_codec_mix_fusion(int mask) {
   return 0;
 }
 
+// A codec stage of Block1Ds at T = 1, one sample, runs as ONE persistent launch
+// (codec_stage.hip) while the context is the device's only one registered for
+// persistent kernels (hl_sole); 0 = the launch-per-GEMV path (A/B and tests).
+static std::atomic<int> g_codec_stage{1};
+extern "C" int vv_codec_stage(int on) {
+  g_codec_stage = on ? 1 : 0;
+  return 0;
+}
+static bool codec_stage_any(const ConvNet& net) {
+  for (int i = 0; i < net.nst; ++i)
+    if (net.T[i] == 1 && codec_stage_fits(net.chans[i], 1, 1, net.depth[i])) return true;
+  return false;
+}
+static bool codec_stage_on(vv_ctx* c, const ConvNet& net, int i, int n) {
+  return g_codec_stage && c->cs_sync.p && net.T[i] == 1 && codec_stage_fits(net.chans[i], net.T[i], n, net.depth[i]) &&
+         hl_sole(c->device);
+}
+static std::atomic<unsigned long long*> g_codec_stage_stamps{nullptr};
+extern "C" int vv_codec_stage_stamps(void* buf) {   // diagnostic: [256][64] per-workgroup phase stamps
+  g_codec_stage_stamps = (unsigned long long*)buf;
+  return 0;
+}
+extern "C" int vv_codec_stage_active(vv_ctx* c) {
+  return c && c->finalized && codec_stage_on(c, c->dec, 0, 1) ? 1 : 0;
+}
+
 // diffusion steps whose adaLN modulations are computed in one GEMM
 static constexpr int HEAD_SC = 16;
 
@@ -503,6 +530,44 @@ static int convnet_run(vv_ctx* c, ConvNet& net, int n, const int* slots, RowMap 
         GemmArgs g = gemm_args(c, n * T, C, 2 * r * Ci, a, W(c, t + "_w"), EPI_STORE, X, W(c, t + "_b"));
         CHK(gemm(c, g, st));
       }
+    }
+    if (codec_stage_on(c, net, i, n)) {
+      // the whole stage (T = 1, one sample) in one persistent launch (codec_stage.hip)
+      CodecStageArgs A;
+      memset(&A, 0, sizeof(A));
+      A.depth = net.depth[i];
+      A.ctx = net.mix[i][0].ctx;
+      A.eps = eps;
+      A.slots = slots;
+      A.x = net.X[i];
+      A.xe = net.Y[i];
+      A.h = net.F;
+      const ConvBuf& nb = (i + 1 < net.nst) ? net.tr[i + 1] : net.head;
+      A.out = buf_in_rows(nb, T, slots);
+      for (int j = 0; j < net.depth[i]; ++j) {
+        const std::string b = p + ".s" + std::to_string(i) + ".b" + std::to_string(j);
+        CodecStageBlock& B = A.b[j];
+        B.norm = W(c, b + ".norm");
+        B.dw_w = W(c, b + ".dw_w");
+        B.dw_b = W(c, b + ".dw_b");
+        B.gamma = W(c, b + ".gamma");
+        B.ffn_norm = W(c, b + ".ffn_norm");
+        B.fc1_w = W(c, b + ".fc1_w");
+        B.fc1_b = W(c, b + ".fc1_b");
+        B.fc2_w = W(c, b + ".fc2_w");
+        B.fc2_b = W(c, b + ".fc2_b");
+        B.ffn_gamma = W(c, b + ".ffn_gamma");
+        B.mix = net.mix[i][j].base;
+        B.mix_sB = net.mix[i][j].sB;
+        if (net.mix[i][j].ctx != A.ctx) FAIL("codec stage: conv buffers of one stage differ in history length");
+      }
+      A.sync = (unsigned*)c->cs_sync.p;
+      A.err = (unsigned*)c->hf_sync.p + 10 * 32;
+      A.stamps = i == 0 ? g_codec_stage_stamps.load() : nullptr;   // (the first stage of the net: the decoder's)
+      const int rc = launch_codec_stage(A, st);
+      if (rc) FAIL("persistent codec stage: launch failed (" + std::to_string(rc) + ": " +
+                   hipGetErrorString(hipGetLastError()) + ")");
+      continue;
     }
     const int Rb = std::max(1, std::min(T, 2048 / C));
     if ((g_mix_fusion & 2) && block_lds(Rb, C)) {
@@ -657,7 +722,7 @@ void vv_destroy(vv_ctx* c) {
   DevBuf* bufs[] = {&c->norm_ws, &c->kv_k, &c->kv_v, &c->lm_ws, &c->attn_part, &c->attn_cnt, &c->valid_ids, &c->splitk_ws, &c->splitk_cnt,
                     &c->temb, &c->tfreq_tmp, &c->head_ws, &c->codec_ws, &c->slot_scratch, &c->unit_sb,
                     &c->chain_sync, &c->chain_slabs, &c->chain_err, &c->coef_dev, &c->rope_tab, &c->zero_rows,
-                    &c->hf_slab, &c->hf_sync, &c->hl_lat};
+                    &c->hf_slab, &c->hf_sync, &c->hl_lat, &c->cs_sync};
   for (DevBuf* b : bufs) b->release();
   for (auto& kv : c->head_chain) kv.second.ops.release();
   ConvNet* nets[] = {&c->dec, &c->sem, &c->aenc, &c->senc};
@@ -778,6 +843,14 @@ int vv_finalize(vv_ctx* c) {
   }
   CHK(convnet_alloc(c->dec, 7));
   CHK(convnet_alloc(c->sem, 7));
+  // the persistent codec stage's wait counters; a context that can run it (or
+  // the persistent head) counts in the device's registry (hl_register)
+  CHK(c->cs_sync.ensure(12 * 128));
+  HIPCHK(hipMemset(c->cs_sync.p, 0, 12 * 128));
+  if (!c->hl_registered && (codec_stage_any(c->dec) || codec_stage_any(c->sem))) {
+    c->hl_registered = true;
+    hl_register(c->device, +1);
+  }
   // ---- LM KV cache: [layer][slot][kv_head][ctx][d]
   c->lm_slots = 2 * k.max_batch;
   c->kv.d = d;
@@ -1281,6 +1354,7 @@ int vv_sync_error(vv_ctx* c) {
     // a launch that gave up left the wait counters part-advanced: with nothing in
     // flight (the device is synchronised) every counter restarts from 0
     if (v) HIPCHK(hipMemset(c->hf_sync.p, 0, 12 * 128));
+    if (v && c->cs_sync.p) HIPCHK(hipMemset(c->cs_sync.p, 0, 12 * 128));
   }
   return v ? 1 : 0;
 }

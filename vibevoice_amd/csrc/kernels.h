@@ -278,6 +278,30 @@ bool head_loop_fits(int H, int F, int R, int L);
 int head_loop_grid();
 int launch_head_loop(const HeadLoopArgs& a, bool coop, hipStream_t st);
 
+// A whole codec stage of Block1Ds at T = 1, C = 2,048, one sample, in ONE
+// persistent launch (codec_stage.hip).
+struct CodecStageBlock {
+  const bf16 *norm, *dw_w, *dw_b, *gamma, *ffn_norm;   // mixer norm, depthwise conv [C][7] + bias, layer scale, FFN norm
+  const bf16 *fc1_w, *fc1_b, *fc2_w, *fc2_b, *ffn_gamma;   // MFMA-packed fc1 [4C][C], fc2 [C][4C]
+  bf16* mix;                // the block's conv buffer (history rows 0 .. ctx-1, new row ctx)
+  long long mix_sB;         // elements per slot
+};
+struct CodecStageArgs {
+  int depth, ctx;
+  float eps;
+  const int* slots;         // [1]: the sample's slot
+  const bf16* x;            // [C] stage input row
+  bf16* xe;                 // [C] block outputs between blocks (written through)
+  bf16* h;                  // [4C] hidden row (written through)
+  RowMap out;               // the last block's output row
+  CodecStageBlock b[8];
+  unsigned* sync;           // 12 lines of 32 words (shards 0-7, generation 11)
+  unsigned* err;            // set to 1 when a grid wait gave up
+  unsigned long long* stamps;   // diagnostics: [G][64] s_memrealtime per phase, or nullptr
+};
+bool codec_stage_fits(int C, int T, int n, int depth);
+int launch_codec_stage(const CodecStageArgs& a, hipStream_t st);
+
 size_t gemv_mix_lds(int M, int T, int C);
 int launch_gemm(GemmArgs a, hipStream_t st);
 int launch_sum_rows(SumRows s, long long count, hipStream_t st);
