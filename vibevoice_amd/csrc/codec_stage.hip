@@ -12,7 +12,8 @@
 // Decomposition per workgroup w (C = 2,048, F = 8,192, G = 256):
 //   * front half: the control wave recomputes norm / conv / residual / FFN norm
 //     for the whole row (k_mix's and XF_MIX's arithmetic and summation order),
-//     the conv's six history taps ahead of time (during the previous waits);
+//     the conv's six history taps ahead of time (during the previous block's
+//     first wait);
 //     workgroup 0 appends the new conv-input row to the block's buffer;
 //   * fc1: w owns hidden units [32w, 32w + 32) (MFMA tiles 2w, 2w + 1: one
 //     contiguous 128 KB slice, LDS DMA) -> GELU -> 64 B of the hidden row,
@@ -21,9 +22,13 @@
 //     in registers: 16 chunks per compute thread) over the whole hidden row (LDS
 //     DMA) -> gamma residual -> 16 B of the next block's input; grid wait.
 // Weight stream order per compute wave: block j+1's fc1 DMA, then its fc2
-// register loads, both issued right after block j's fc2 products; the fc1 dots
-// wait with an explicit vmcnt(16) (the fc2 loads may still fly), the fc2 dots
-// with hipcc's own waits (nothing is issued behind them).  The compute waves'
+// register loads, both issued right after block j's fc2 products (each wave DMAs
+// and reads only its own LDS chunks); the fc1 dots wait with an explicit
+// vmcnt(16) (the fc2 loads may still fly), the fc2 dots with hipcc's own
+// vmcnt(0).  Measured per block (tools/codec_stage_stamps.py, DESIGN.md "Codec
+// stage"): ~18.5 us, the second wait running behind the 256 KB stream; issuing
+// the fc1 slice a wait earlier put 128 KB behind each wait instead and measured
+// the same (17.8 us per block, the codec step 14 us slower).  The compute waves'
 // queues carry nothing but weights; the control wave does every other global
 // access.  Hand-offs: write-through stores + the grid wait of persist_dev.h.
 //
@@ -94,10 +99,13 @@ __global__ void __launch_bounds__(cs::NT) k_codec_stage(CodecStageArgs a) {
   // slice into registers (chunk g: k-block g >> 5, k-sub (g >> 3) & 3, row g & 7
   // of the workgroup's half tile; a wave's load = eight full 128-byte runs)
   bf16x8 w2[CPT];
-  auto issue = [&](int j, int t) {
+  auto issue_fc1 = [&](int j, int t) {
     const bf16* g1 = hl_opaque(a.b[j].fc1_w) + (long long)w * ROWS1 * C;
 #pragma unroll
-    for (int i = 0; i < CPT; ++i) hl_dma16<false>(w1_s + (i * NTC + 64 * wave) * 8, g1 + ((long long)i * NTC + t) * 8);
+    for (int i = 0; i < CPT; ++i)
+      hl_dma16<false, true>(w1_s + (i * NTC + 64 * wave) * 8, g1 + ((long long)i * NTC + t) * 8);
+  };
+  auto issue_fc2 = [&](int j, int t) {
     const bf16* g2 = hl_opaque(a.b[j].fc2_w) + (long long)(w >> 1) * F * 16 + (w & 1) * 64;
     const int r = t & 7, s = (t >> 3) & 3;
 #pragma unroll
@@ -243,7 +251,13 @@ __global__ void __launch_bounds__(cs::NT) k_codec_stage(CodecStageArgs a) {
         }
         MemWT::st8(hl_opaque(a.h) + ROWS1 * w + 4 * lane, o);
       }
-      if (!grid_wait([&] { if (!last) hist(j + 1, 0); })) return;   // B3
+      if (!grid_wait([&] {
+            if (!last) {   // (here, not in the next wait: that one runs behind the next block's stream)
+              hist(j + 1, 0);
+              hist(j + 1, 2);
+            }
+          }))
+        return;   // B3
       stamp(8 * j + 4, true);
       {
         const bf16* hp = hl_opaque(a.h) + hl_vopaque(lane) * 8;   // (per-lane addresses not hoisted)
@@ -265,11 +279,12 @@ __global__ void __launch_bounds__(cs::NT) k_codec_stage(CodecStageArgs a) {
         if (last) rm_bfw(a.out, 0)[col] = o;   // the launch's end publishes it
         else MemWT::st2(a.xe + col, o);
       }
-      if (!last && !grid_wait([&] { hist(j + 1, 2); })) return;   // B6
+      if (!last && !grid_wait([] {})) return;   // B6
       stamp(8 * j + 7, true);
     }
   } else {
-    issue(0, threadIdx.x);
+    issue_fc1(0, threadIdx.x);
+    issue_fc2(0, threadIdx.x);
     for (int j = 0; j < a.depth; ++j) {
       const bool last = j + 1 == a.depth;
       __syncthreads();   // B1
@@ -312,7 +327,10 @@ __global__ void __launch_bounds__(cs::NT) k_codec_stage(CodecStageArgs a) {
       }
       __syncthreads();   // B5
       if (!last) {
-        issue(j + 1, threadIdx.x);   // the next block's slices (fc1's LDS and the registers are free)
+        // the next block's slices: fc1 into this wave's own LDS chunks (read by
+        // no other wave), then fc2 into the registers
+        issue_fc1(j + 1, hl_vopaque((int)threadIdx.x));
+        issue_fc2(j + 1, hl_vopaque((int)threadIdx.x));
         __syncthreads();   // B6
         if (!ok_s[0]) return;
       }

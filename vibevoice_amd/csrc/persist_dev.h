@@ -32,11 +32,15 @@ DEV float hl_dot8(bf16x8 w, bf16x8 x, float acc) {
 // the queue before the first LDS access nor counts it: the issuing wave waits
 // with an explicit s_waitcnt vmcnt.  SC1: the bytes were written in this launch
 // (write-through stores, MI355X_MICROARCH.md's hand-off table: sc1 loads).
-template <bool SC1>
+// NT: a weight stream read once per token (no reuse before eviction: the
+// non-temporal policy keeps it from evicting what does stay in the caches).
+template <bool SC1, bool NT = false>
 DEV void hl_dma16(const void* lds_base, const void* gptr) {
   const unsigned lds = __builtin_amdgcn_readfirstlane(
       (unsigned)(unsigned long long)(__attribute__((address_space(3))) const unsigned char*)lds_base);
-  if (SC1)
+  if (NT)
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off nt" ::"s"(lds), "v"(gptr) : "memory", "m0");
+  else if (SC1)
     asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off sc1" ::"s"(lds), "v"(gptr) : "memory", "m0");
   else
     asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(gptr) : "memory", "m0");
