@@ -8,7 +8,7 @@
 # usage: tools/ctx_sweep.sh [steps] [contexts...]
 set -u
 steps="${1:-200}"; shift || true
-ctxs="${*:-0 4096 16384 32768 49152 65000}"
+ctxs="${*:-0 4096 16384 32768 65000}"
 mkdir -p gpurun_out
 out=gpurun_out/ctx_sweep.jsonl; : > "$out"
 for c in $ctxs; do
@@ -22,8 +22,11 @@ done
 python - "$out" <<'EOF' | tee gpurun_out/ctx_sweep.txt
 import json, sys
 rows = [json.loads(l) for l in open(sys.argv[1])]
-print(f"{'context':>8} {'ms/step':>8} {'frames/s':>9} {'audio-s/s':>9} {'KV GB/step':>10} {'KV TB/s':>8}")
+# keys per step: the mean cached length over the timed steps (config.context_start .. context_end)
+print(f"{'context':>8} {'keys':>7} {'ms/step':>8} {'frames/s':>9} {'audio-s/s':>9} {'KV GB/step':>10} {'KV TB/s':>8}")
 for r in rows:
-    ms = r["ms_per_step"]; kv = 28672 * r["context"] / 1e9
-    print(f"{r['context']:>8} {ms:>8.4f} {1e3 / ms:>9.1f} {r['value']:>9.2f} {kv:>10.3f} {kv / ms:>8.3f}")
+    ms = r["ms_per_step"]
+    keys = (r["config"]["context_start"] + r["config"]["context_end"]) / 2
+    kv = 28672 * keys / 1e9
+    print(f"{r['context']:>8} {keys:>7.0f} {ms:>8.4f} {1e3 / ms:>9.1f} {r['value']:>9.2f} {kv:>10.3f} {kv / ms:>8.3f}")
 EOF
