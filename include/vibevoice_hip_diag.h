@@ -199,9 +199,10 @@ int vv_codec_stage(int on);
 /* Test query: 1 when a one-sample codec step on ctx would run the acoustic
  * decoder's first stage as the persistent launch now. */
 int vv_codec_stage_active(vv_ctx* ctx);
-/* Diagnostic: the acoustic decoder's stage launches record per-workgroup
- * s_memrealtime stamps into buf ([256][64] u64; nullptr: off). */
-int vv_codec_stage_stamps(void* buf);
+/* Diagnostic: the acoustic decoder's persistent launch of stage `stage`
+ * records per-workgroup s_memrealtime stamps into buf ([256][64] u64;
+ * nullptr: off). */
+int vv_codec_stage_stamps(void* buf, int stage);
 int vv_rmsnorm_bf16(int M, int C, const void* x, int64_t ldx, const void* w, float eps, void* y, int64_t ldy,
                     vv_stream st);
 

@@ -10,7 +10,7 @@ codec shapes (seeded weights), captured into a hipGraph and replayed.
     wait released; median / max over the 256 workgroups relative to the first
     stamp, and the phase-to-phase medians.
 
-usage: python tools/codec_stage_stamps.py"""
+usage: python tools/codec_stage_stamps.py [stage]   (the decoder's stage: 0 = C 2,048 T 1, 1 = C 1,024 T 8)"""
 import os
 import sys
 
@@ -26,6 +26,7 @@ from tiny import tiny_config  # noqa: E402
 
 
 def main():
+    stage = int(sys.argv[1]) if len(sys.argv) > 1 else 0
     L = _lib.lib()
     cfg = tiny_config(ratios=(8, 5, 5, 4, 2, 2), depths="3-3-3-3-3-3-8", nf=32)
     sd = synthetic_state_dict(cfg, seed=3, device="cpu", mode="test", with_acoustic_encoder=False)
@@ -65,13 +66,13 @@ def main():
         print(f"codec step, {'stage launch' if mode else 'launch per GEMV'}: best of 20 graph replays {best:.1f} us",
               flush=True)
     st = torch.zeros(256 * 64, dtype=torch.int64, device="cuda")
-    L.vv_codec_stage_stamps(st.data_ptr())
+    L.vv_codec_stage_stamps(st.data_ptr(), stage)
     gr = capture()   # the stamp pointer is a launch argument
     for _ in range(3):
         with torch.cuda.stream(s):
             gr.replay()
         torch.cuda.synchronize()
-    L.vv_codec_stage_stamps(None)
+    L.vv_codec_stage_stamps(None, 0)
     eng.check_sync()
     t = st.view(256, 64).cpu().double() * 10e-3   # us
     used = [k for k in range(64) if bool((st.view(256, 64)[:, k] != 0).all())]
@@ -79,7 +80,7 @@ def main():
     rel = t - t0
     names = ["front half begins", "fc1 input in LDS", "fc1 slice landed (wave 0)", "fc1 partials in LDS",
              "hidden-row wait released", "hidden row in LDS", "fc2 partials in LDS", "next-input wait released"]
-    print("acoustic decoder stage, us from the first workgroup's first stamp (median / max over workgroups):")
+    print(f"acoustic decoder stage {stage}, us from the first workgroup's first stamp (median / max over workgroups):")
     prev = None
     for k in used:
         col = rel[:, k]

@@ -79,7 +79,7 @@ EXPORTS = [
     ("vv_codec_mix_fusion", I, [I]),
     ("vv_codec_stage", I, [I]),
     ("vv_codec_stage_active", I, [P]),
-    ("vv_codec_stage_stamps", I, [P]),
+    ("vv_codec_stage_stamps", I, [P, I]),
     ("vv_chain_tune", I, [I]),
     ("vv_chain_tune_u", I, [I]),
     ("vv_chain_error", I, [P]),

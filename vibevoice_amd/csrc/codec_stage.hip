@@ -338,31 +338,345 @@ __global__ void __launch_bounds__(cs::NT) k_codec_stage(CodecStageArgs a) {
   }
 }
 
+// ============================================================================
+// C = 1,024 stages (the acoustic decoder's second, T = 8; the semantic
+// encoder's sixth, T = 2), M = T rows of one sample.  Per workgroup and block:
+// fc1 one MFMA tile (hidden units [16w, 16w + 16), 32 KB, LDS DMA), fc2 a
+// quarter tile (output columns [4w, 4w + 4), 32 KB, registers: 4 chunks per
+// compute thread); 64 KB per CU per block.  The front half (XF_MIX's, over T
+// rows: the conv runs across the new rows and the 6 history rows) is staged in
+// LDS and computed by all nine waves (the compute waves touch no global memory
+// but their weights, so their vmcnt queue stays clean); the control wave DMAs
+// the rows in, prefetches the next block's history rows and vectors during the
+// first wait, and does every store.
+namespace cs2 {
+constexpr int C = 1024, F = 4 * C, G = pk::G, CTX = 6, K7 = 7;
+constexpr int NTC = 512, NT = NTC + 64;
+constexpr int NCH = C / 8;                   // 128 chunks per row
+constexpr int CPT = 4;                       // weight chunks per compute thread per GEMV
+constexpr int ROWS1 = F / G, ROWS2 = C / G;  // 16 / 4
+static_assert(ROWS1 * C / 8 == CPT * NTC && ROWS2 * F / 8 == CPT * NTC, "codec stage (C = 1,024) geometry");
+template <int M>
+struct Lds {
+  static constexpr int W1 = 0, W1_B = ROWS1 * C * 2;                          // fc1 slice, 32 KB
+  static constexpr int XS_B = M * C * 2, AS_B = M * C * 2, H_B = M * F * 2;
+  static constexpr int HR = W1 + W1_B, HR_B = H_B > XS_B + AS_B ? H_B : XS_B + AS_B;   // hidden rows | x / y + a rows
+  static constexpr int NRM = HR + HR_B, NRM_B = (CTX + M) * C * 2;            // conv input rows
+  static constexpr int VEC = NRM + NRM_B, VEC_B = 4 * C * 2 + C * K7 * 2;     // norm, dw_b, gamma, ffn_norm; dw_w
+  static constexpr int SSP = VEC + VEC_B, SSP_B = M * NCH * 4;                // per-chunk sums of squares
+  static constexpr int RED = SSP + SSP_B, RED_B = 8 * M * ROWS1 * 4;          // compute-wave partials
+  static constexpr int SM = RED + RED_B, SM_B = (4 + 2 * M + M * ROWS2) * 4;  // ok, inv / inv2, y of the own columns
+  static constexpr int TOTAL = SM + SM_B;
+  static_assert(TOTAL <= 160 * 1024, "one workgroup per CU");
+};
+}  // namespace cs2
+
+template <int M>
+__global__ void __launch_bounds__(cs2::NT) k_codec_stage_s(CodecStageArgs a) {
+  using namespace cs2;
+  using LL = Lds<M>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16* w1_s = (bf16*)(smem + LL::W1);
+  bf16* h_s = (bf16*)(smem + LL::HR);          // fc2 phase: [M][F]
+  bf16* x_s = (bf16*)(smem + LL::HR);          // front half: [M][C] x, then y
+  bf16* a_s = x_s + M * C;                     // [M][C] fc1 input
+  bf16* nrm_s = (bf16*)(smem + LL::NRM);       // [CTX + M][C]
+  bf16* vec_s = (bf16*)(smem + LL::VEC);       // norm | dw_b | gamma | ffn_norm, each [C]; dw_w [C][7]
+  float* ssp = (float*)(smem + LL::SSP);       // [M][NCH]
+  float* red = (float*)(smem + LL::RED);
+  float* sm = (float*)(smem + LL::SM);
+  unsigned* ok_s = (unsigned*)sm;
+  float* inv_s = sm + 4;                       // [M]
+  float* inv2_s = inv_s + M;                   // [M]
+  bf16* y4_s = (bf16*)(inv2_s + M);            // [M][4] y of this workgroup's columns
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool ctl = wave == NTC / 64;
+  const int w = blockIdx.x, lane = threadIdx.x & 63;
+  const long long slot = a.slots[0];
+  unsigned g0 = 0, nwait = 0;
+  if (ctl) __builtin_amdgcn_s_setprio(3);
+  if (ctl) g0 = __hip_atomic_load((hl_gu32*)hl_gen(a.sync), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~7u;
+  auto stamp = [&](int k, bool by_ctl) {   // k_codec_stage's slots (tools/codec_stage_stamps.py)
+    if (a.stamps && threadIdx.x == (by_ctl ? NTC : 0)) a.stamps[w * 64 + k] = __builtin_amdgcn_s_memrealtime();
+  };
+
+  // ---- weights (compute waves): fc1 tile w by DMA (chunk g = i * NTC + t ->
+  // LDS 16 g), fc2 quarter tile into registers (chunk g: k-block g >> 4, k-sub
+  // (g >> 2) & 3, row g & 3 of the quarter: 64-byte runs)
+  bf16x8 w2[CPT];
+  auto issue = [&](int j, int t) {
+    const bf16* g1 = hl_opaque(a.b[j].fc1_w) + (long long)w * ROWS1 * C;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i)
+      hl_dma16<false, true>(w1_s + (i * NTC + 64 * wave) * 8, g1 + ((long long)i * NTC + t) * 8);
+    const bf16* g2 = hl_opaque(a.b[j].fc2_w) + (long long)(w >> 2) * F * 16 + (w & 3) * 32;
+    const int r = t & 3, s = (t >> 2) & 3;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int kc = (i * NTC + t) >> 4;
+      w2[i] = hl_ldnt(g2 + (long long)kc * 512 + (16 * s + r) * 8);
+    }
+  };
+  // ---- control wave: block jb's history rows -> nrm_s[0 .. CTX), its vectors -> vec_s (LDS DMA)
+  auto prefetch = [&](int jb) {
+    const int ln = hl_vopaque(lane);
+    const bf16* mb = hl_opaque(a.b[jb].mix) + slot * a.b[jb].mix_sB;
+#pragma unroll
+    for (int i = 0; i < CTX * NCH / 64; ++i) hl_dma16<false>(nrm_s + i * 512, mb + (i * 64 + ln) * 8);
+    const bf16* v4[4] = {hl_opaque(a.b[jb].norm), hl_opaque(a.b[jb].dw_b), hl_opaque(a.b[jb].gamma),
+                         hl_opaque(a.b[jb].ffn_norm)};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < NCH / 64; ++i) hl_dma16<false>(vec_s + q * C + i * 512, v4[q] + (i * 64 + ln) * 8);
+    // the depthwise taps transposed to [7][C] (so a chunk's taps are 7 conflict-free
+    // 16-byte LDS reads): column chunks ln, ln + 64 of [C][7], 7 x 16 B each
+    const bf16* dw = hl_opaque(a.b[jb].dw_w);
+#pragma unroll
+    for (int cc = 0; cc < NCH / 64; ++cc) {
+      const int c = ln + 64 * cc;
+      bf16x8 wk[K7];
+#pragma unroll
+      for (int k = 0; k < K7; ++k) wk[k] = hl_ld(dw + (long long)c * 56 + k * 8);
+#pragma unroll
+      for (int k = 0; k < K7; ++k) {
+        bf16x8 o;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int f = q * 7 + k;
+          o[q] = wk[f >> 3][f & 7];
+        }
+        *(bf16x8*)(vec_s + 4 * C + k * C + c * 8) = o;
+      }
+    }
+  };
+  // every thread: per-chunk sums of squares of rows src (XF_MIX's per-chunk order) -> ssp
+  auto chunk_ss = [&](const bf16* src) {
+    for (int e = hl_vopaque((int)threadIdx.x); e < M * NCH; e += NT) {
+      const bf16x8 v = *(const bf16x8*)(src + e * 8);
+      float s8 = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s8 += bf(v[k]) * bf(v[k]);
+      ssp[e] = s8;
+    }
+  };
+  // one wave per row: chunks lane, lane + 64 in order, wave_sum (XF_MIX's row order)
+  auto row_inv = [&](float* dst) {
+    const int ln = hl_vopaque(lane);
+    for (int m = wave; m < M; m += NT / 64) {
+      float ss = 0.f;
+      for (int c = ln; c < NCH; c += 64) ss += ssp[m * NCH + c];
+      ss = wave_sum(ss);
+      if (lane == 0) dst[m] = rsqrtf(ss / (float)C + a.eps);
+    }
+  };
+  auto grid_wait = [&](auto between) -> bool {
+    ++nwait;
+    if (ctl) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) hl_arrive(a.sync, w);
+      between();
+      if (lane == 0) ok_s[0] = hl_poll(a.sync, g0, nwait, a.err) ? 1u : 0u;
+    }
+    __syncthreads();
+    return ok_s[0] != 0;
+  };
+
+  if (!ctl) issue(0, threadIdx.x);
+  if (ctl) prefetch(0);
+  for (int j = 0; j < a.depth; ++j) {
+    const bool last = j + 1 == a.depth;
+    stamp(8 * j + 0, true);
+    // ================= front half over the M rows (all waves, from LDS)
+    if (ctl) {   // the block's input rows (this launch's: sc1)
+      const int ln = hl_vopaque(lane);
+      const bf16* src = j == 0 ? hl_opaque(a.x) : hl_opaque(a.xe);
+#pragma unroll
+      for (int i = 0; i < M * NCH / 64; ++i) {
+        if (j == 0) hl_dma16<false>(x_s + i * 512, src + (i * 64 + ln) * 8);
+        else hl_dma16<true>(x_s + i * 512, src + (i * 64 + ln) * 8);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      stamp(40 + 4 * j, true);
+    }
+    __syncthreads();
+    chunk_ss(x_s);
+    __syncthreads();
+    row_inv(inv_s);
+    __syncthreads();
+    stamp(41 + 4 * j, true);
+    for (int e = hl_vopaque((int)threadIdx.x); e < M * NCH; e += NT) {   // mixer norm -> the conv input rows
+      const int m = e / NCH, c = e - m * NCH;
+      const bf16x8 v = *(const bf16x8*)(x_s + e * 8), nw = *(const bf16x8*)(vec_s + c * 8);
+      const float rr = inv_s[m];
+      bf16x8 o;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = tobf(rb(rb(bf(v[k]) * rr) * bf(nw[k])));
+      *(bf16x8*)(nrm_s + (CTX + m) * C + c * 8) = o;
+    }
+    __syncthreads();
+    if (ctl && w == 0) {   // workgroup 0 appends the new conv-input rows to the block's buffer
+      bf16* nb = hl_opaque(a.b[j].mix) + slot * a.b[j].mix_sB + (long long)a.ctx * C;
+      for (int e = hl_vopaque(lane); e < M * NCH; e += 64) *(bf16x8*)(nb + e * 8) = *(const bf16x8*)(nrm_s + CTX * C + e * 8);
+    }
+    for (int e = hl_vopaque((int)threadIdx.x); e < M * NCH; e += NT) {   // depthwise conv + gamma residual: y over x
+      const int m = e / NCH, c = e - m * NCH;
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < K7; ++k) {
+        const bf16x8 v = *(const bf16x8*)(nrm_s + (m + k) * C + c * 8);
+        const bf16x8 wk = *(const bf16x8*)(vec_s + 4 * C + k * C + c * 8);   // tap k of the chunk's 8 columns
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] += bf(wk[q]) * bf(v[q]);
+      }
+      const bf16x8 xv = *(const bf16x8*)(x_s + e * 8), bb = *(const bf16x8*)(vec_s + C + c * 8),
+                   gv = *(const bf16x8*)(vec_s + 2 * C + c * 8);
+      bf16x8 y8;
+      float s8 = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        y8[q] = tobf(bf(xv[q]) + rb(rb(acc[q] + bf(bb[q])) * bf(gv[q])));
+        s8 += bf(y8[q]) * bf(y8[q]);
+      }
+      *(bf16x8*)(x_s + e * 8) = y8;
+      ssp[e] = s8;
+    }
+    __syncthreads();
+    stamp(42 + 4 * j, true);
+    row_inv(inv2_s);
+    __syncthreads();
+    stamp(43 + 4 * j, true);
+    for (int e = hl_vopaque((int)threadIdx.x); e < M * NCH; e += NT) {   // FFN pre-norm -> fc1's input rows
+      const int m = e / NCH, c = e - m * NCH;
+      const bf16x8 y8 = *(const bf16x8*)(x_s + e * 8), fw = *(const bf16x8*)(vec_s + 3 * C + c * 8);
+      const float rr = inv2_s[m];
+      bf16x8 o;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = tobf(rb(rb(bf(y8[k]) * rr) * bf(fw[k])));
+      *(bf16x8*)(a_s + e * 8) = o;
+    }
+    if (threadIdx.x < M * ROWS2) {   // y of this workgroup's 4 columns, for the fc2 epilogue
+      const int tt = hl_vopaque((int)threadIdx.x), m = tt / ROWS2, r = tt - m * ROWS2;
+      y4_s[tt] = x_s[m * C + ROWS2 * w + r];
+    }
+    __syncthreads();   // B1
+    stamp(8 * j + 1, true);
+    // ================= fc1: M rows x 16 hidden units
+    if (!ctl) {
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // this wave's fc1 DMA (the fc2 loads may fly)
+      stamp(8 * j + 2, false);
+      const int t = hl_vopaque((int)threadIdx.x), s = (t & 63) >> 4;
+      float acc[M];
+#pragma unroll
+      for (int m = 0; m < M; ++m) acc[m] = 0.f;
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) {
+        const int kc = 8 * i + wave;
+        const bf16x8 wv = *(const bf16x8*)(w1_s + (i * NTC + t) * 8);
+#pragma unroll
+        for (int m = 0; m < M; ++m) acc[m] = hl_dot8(wv, *(const bf16x8*)(a_s + m * C + kc * 32 + 8 * s), acc[m]);
+      }
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        acc[m] = cs_rows_sum(acc[m]);
+        if ((t & 63) < 16) red[(wave * M + m) * ROWS1 + (t & 15)] = acc[m];
+      }
+    }
+    __syncthreads();   // B2
+    stamp(8 * j + 3, true);
+    if (ctl && lane < M * ROWS1 / 4) {   // 4 hidden units per lane, epi_row8's EPI_GELU
+      const int ln = hl_vopaque(lane), m = ln / (ROWS1 / 4), u0 = 4 * (ln - m * (ROWS1 / 4));
+      const bf16x4 b1 = *(const bf16x4*)(a.b[j].fc1_b + ROWS1 * w + u0);
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float sacc = 0.f;
+#pragma unroll
+        for (int v = 0; v < NTC / 64; ++v) sacc += red[(v * M + m) * ROWS1 + u0 + e];
+        o[e] = tobf(gelu_f(rb(sacc + bf(b1[e]))));
+      }
+      MemWT::st8(hl_opaque(a.h) + (long long)m * F + ROWS1 * w + u0, o);
+    }
+    if (!grid_wait([&] { if (ctl && !last) prefetch(j + 1); })) return;   // B3
+    stamp(8 * j + 4, true);
+    // ================= fc2: M rows x 4 columns over the whole hidden rows
+    if (ctl) {
+      const bf16* hp = hl_opaque(a.h) + hl_vopaque(lane) * 8;
+#pragma unroll
+      for (int i = 0; i < M * F / 8 / 64; ++i) hl_dma16<true>(h_s + i * 512, hp + i * 512);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();   // B4
+    stamp(8 * j + 5, true);
+    if (!ctl) {
+      const int t = hl_vopaque((int)threadIdx.x), s = (t >> 2) & 3;
+      float acc[M];
+#pragma unroll
+      for (int m = 0; m < M; ++m) acc[m] = 0.f;
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) {
+        const int kc = (i * NTC + t) >> 4;
+#pragma unroll
+        for (int m = 0; m < M; ++m) acc[m] = hl_dot8(w2[i], *(const bf16x8*)(h_s + m * F + kc * 32 + 8 * s), acc[m]);
+      }
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        float v = acc[m];
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        v += __shfl_xor(v, 16);
+        v += __shfl_xor(v, 32);
+        if ((t & 63) < ROWS2) red[(wave * M + m) * ROWS2 + (t & 63)] = v;
+      }
+    }
+    __syncthreads();   // B5
+    stamp(8 * j + 6, true);
+    if (!ctl && !last) issue(j + 1, hl_vopaque((int)threadIdx.x));
+    if (ctl && lane < M * ROWS2) {   // epi_row8's EPI_RES with ffn_gamma
+      const int ln = hl_vopaque(lane), m = ln / ROWS2, r = ln - m * ROWS2, col = ROWS2 * w + r;
+      float sacc = 0.f;
+#pragma unroll
+      for (int v = 0; v < NTC / 64; ++v) sacc += red[(v * M + m) * ROWS2 + r];
+      const float yv = rb(bf(a.b[j].ffn_gamma[col]) * rb(sacc + bf(a.b[j].fc2_b[col])));
+      const bf16 o = tobf(bf(y4_s[ln]) + yv);
+      if (last) rm_bfw(a.out, m)[col] = o;
+      else MemWT::st2(hl_opaque(a.xe) + (long long)m * C + col, o);
+    }
+    if (!last && !grid_wait([] {})) return;   // B6
+    stamp(8 * j + 7, true);
+  }
+}
+
 // One workgroup per CU, all resident from the start: the plain launch checks
-// nothing, so the build is checked here (no scratch, one workgroup fits a CU).
-static bool stage_resident() {
-  static const bool ok = [] {
-    hipFuncAttributes fa{};
-    int nb = 0;
-    const void* k = (const void*)k_codec_stage;
-    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, cs::TOTAL) != hipSuccess ||
-        hipFuncGetAttributes(&fa, k) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, cs::NT, cs::TOTAL) != hipSuccess)
-      return false;
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return false;
-    return fa.localSizeBytes == 0 && nb >= 1 && cus >= cs::G;
-  }();
-  return ok;
+// nothing, so each build is checked here (no scratch, one workgroup fits a CU).
+static bool resident_check(const void* k, int nt, int lds) {
+  hipFuncAttributes fa{};
+  int nb = 0, dev = 0, cus = 0;
+  if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess ||
+      hipFuncGetAttributes(&fa, k) != hipSuccess || hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, nt, lds) != hipSuccess ||
+      hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return false;
+  return fa.localSizeBytes == 0 && nb >= 1 && cus >= pk::G;
+}
+static bool stage_resident(int C, int M) {
+  static const bool ok2048 = resident_check((const void*)k_codec_stage, cs::NT, cs::TOTAL);
+  static const bool ok1024_2 = resident_check((const void*)k_codec_stage_s<2>, cs2::NT, cs2::Lds<2>::TOTAL);
+  static const bool ok1024_8 = resident_check((const void*)k_codec_stage_s<8>, cs2::NT, cs2::Lds<8>::TOTAL);
+  if (C == cs::C && M == 1) return ok2048;
+  if (C == cs2::C && M == 2) return ok1024_2;
+  if (C == cs2::C && M == 8) return ok1024_8;
+  return false;
 }
 
 bool codec_stage_fits(int C, int T, int n, int depth) {
-  return C == cs::C && T == 1 && n == 1 && depth >= 1 && depth <= 8 && stage_resident();
+  return n == 1 && depth >= 1 && depth <= 8 && stage_resident(C, T);
 }
 
 int launch_codec_stage(const CodecStageArgs& a, hipStream_t st) {
-  if (!stage_resident()) return 3;
-  hipLaunchKernelGGL(k_codec_stage, dim3(cs::G), dim3(cs::NT), cs::TOTAL, st, a);
+  if (!stage_resident(a.C, a.M)) return 3;
+  if (a.C == cs::C) hipLaunchKernelGGL(k_codec_stage, dim3(cs::G), dim3(cs::NT), cs::TOTAL, st, a);
+  else if (a.M == 2) hipLaunchKernelGGL((k_codec_stage_s<2>), dim3(cs2::G), dim3(cs2::NT), cs2::Lds<2>::TOTAL, st, a);
+  else hipLaunchKernelGGL((k_codec_stage_s<8>), dim3(cs2::G), dim3(cs2::NT), cs2::Lds<8>::TOTAL, st, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

@@ -455,8 +455,8 @@ extern "C" int vv_codec_mix_fusion(int mask) {
   return 0;
 }
 
-// A codec stage of Block1Ds at T = 1, one sample, runs as ONE persistent launch
-// (codec_stage.hip) while the context is the device's only one registered for
+// A codec stage of Block1Ds of one sample (C = 2,048 at T = 1, C = 1,024 at
+// T = 2 / 8) runs as ONE persistent launch (codec_stage.hip) while the context is the device's only one registered for
 // persistent kernels (hl_sole); 0 = the launch-per-GEMV path (A/B and tests).
 static std::atomic<int> g_codec_stage{1};
 extern "C" int vv_codec_stage(int on) {
@@ -465,16 +465,19 @@ extern "C" int vv_codec_stage(int on) {
 }
 static bool codec_stage_any(const ConvNet& net) {
   for (int i = 0; i < net.nst; ++i)
-    if (net.T[i] == 1 && codec_stage_fits(net.chans[i], 1, 1, net.depth[i])) return true;
+    if (codec_stage_fits(net.chans[i], net.T[i], 1, net.depth[i])) return true;
   return false;
 }
 static bool codec_stage_on(vv_ctx* c, const ConvNet& net, int i, int n) {
-  return g_codec_stage && c->cs_sync.p && net.T[i] == 1 && codec_stage_fits(net.chans[i], net.T[i], n, net.depth[i]) &&
+  return g_codec_stage && c->cs_sync.p && codec_stage_fits(net.chans[i], net.T[i], n, net.depth[i]) &&
          hl_sole(c->device);
 }
 static std::atomic<unsigned long long*> g_codec_stage_stamps{nullptr};
-extern "C" int vv_codec_stage_stamps(void* buf) {   // diagnostic: [256][64] per-workgroup phase stamps
+static std::atomic<int> g_codec_stage_stamp_at{0};
+// diagnostic: the acoustic decoder's stage `stage` records [256][64] per-workgroup phase stamps
+extern "C" int vv_codec_stage_stamps(void* buf, int stage) {
   g_codec_stage_stamps = (unsigned long long*)buf;
+  g_codec_stage_stamp_at = stage;
   return 0;
 }
 extern "C" int vv_codec_stage_active(vv_ctx* c) {
@@ -532,11 +535,13 @@ static int convnet_run(vv_ctx* c, ConvNet& net, int n, const int* slots, RowMap 
       }
     }
     if (codec_stage_on(c, net, i, n)) {
-      // the whole stage (T = 1, one sample) in one persistent launch (codec_stage.hip)
+      // the whole stage (one sample) in one persistent launch (codec_stage.hip)
       CodecStageArgs A;
       memset(&A, 0, sizeof(A));
       A.depth = net.depth[i];
       A.ctx = net.mix[i][0].ctx;
+      A.C = C;
+      A.M = T;
       A.eps = eps;
       A.slots = slots;
       A.x = net.X[i];
@@ -563,7 +568,7 @@ static int convnet_run(vv_ctx* c, ConvNet& net, int n, const int* slots, RowMap 
       }
       A.sync = (unsigned*)c->cs_sync.p;
       A.err = (unsigned*)c->hf_sync.p + 10 * 32;
-      A.stamps = i == 0 ? g_codec_stage_stamps.load() : nullptr;   // (the first stage of the net: the decoder's)
+      A.stamps = net.decoder && i == g_codec_stage_stamp_at ? g_codec_stage_stamps.load() : nullptr;
       const int rc = launch_codec_stage(A, st);
       if (rc) FAIL("persistent codec stage: launch failed (" + std::to_string(rc) + ": " +
                    hipGetErrorString(hipGetLastError()) + ")");

@@ -278,8 +278,8 @@ bool head_loop_fits(int H, int F, int R, int L);
 int head_loop_grid();
 int launch_head_loop(const HeadLoopArgs& a, bool coop, hipStream_t st);
 
-// A whole codec stage of Block1Ds at T = 1, C = 2,048, one sample, in ONE
-// persistent launch (codec_stage.hip).
+// A whole codec stage of Block1Ds for one sample in ONE persistent launch
+// (codec_stage.hip): C = 2,048 at T = 1, C = 1,024 at T = 2 or 8.
 struct CodecStageBlock {
   const bf16 *norm, *dw_w, *dw_b, *gamma, *ffn_norm;   // mixer norm, depthwise conv [C][7] + bias, layer scale, FFN norm
   const bf16 *fc1_w, *fc1_b, *fc2_w, *fc2_b, *ffn_gamma;   // MFMA-packed fc1 [4C][C], fc2 [C][4C]
@@ -288,12 +288,13 @@ struct CodecStageBlock {
 };
 struct CodecStageArgs {
   int depth, ctx;
+  int C, M;                 // channels; rows = T (one sample)
   float eps;
   const int* slots;         // [1]: the sample's slot
-  const bf16* x;            // [C] stage input row
-  bf16* xe;                 // [C] block outputs between blocks (written through)
-  bf16* h;                  // [4C] hidden row (written through)
-  RowMap out;               // the last block's output row
+  const bf16* x;            // [M][C] stage input rows
+  bf16* xe;                 // [M][C] block outputs between blocks (written through)
+  bf16* h;                  // [M][4C] hidden rows (written through)
+  RowMap out;               // the last block's output rows
   CodecStageBlock b[8];
   unsigned* sync;           // 12 lines of 32 words (shards 0-7, generation 11)
   unsigned* err;            // set to 1 when a grid wait gave up
