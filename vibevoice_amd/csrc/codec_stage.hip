@@ -402,8 +402,10 @@ __global__ void __launch_bounds__(cs2::NT) k_codec_stage_s(CodecStageArgs a) {
   };
 
   // ---- weights (compute waves): fc1 tile w by DMA (chunk g = i * NTC + t ->
-  // LDS 16 g), fc2 quarter tile into registers (chunk g: k-block g >> 4, k-sub
-  // (g >> 2) & 3, row g & 3 of the quarter: 64-byte runs)
+  // LDS 16 g), fc2 quarter tile into registers (lane l of wave v, load i: row
+  // l >> 4 of the quarter, k-sub (l >> 2) & 3, k-block 32 i + 4 v + (l & 3): a
+  // wave's load covers 16 full 64-byte runs, and a row's lanes are one 16-lane
+  // group, summed by DPP)
   bf16x8 w2[CPT];
   auto issue = [&](int j, int t) {
     const bf16* g1 = hl_opaque(a.b[j].fc1_w) + (long long)w * ROWS1 * C;
@@ -411,10 +413,10 @@ __global__ void __launch_bounds__(cs2::NT) k_codec_stage_s(CodecStageArgs a) {
     for (int i = 0; i < CPT; ++i)
       hl_dma16<false, true>(w1_s + (i * NTC + 64 * wave) * 8, g1 + ((long long)i * NTC + t) * 8);
     const bf16* g2 = hl_opaque(a.b[j].fc2_w) + (long long)(w >> 2) * F * 16 + (w & 3) * 32;
-    const int r = t & 3, s = (t >> 2) & 3;
+    const int l = t & 63, r = l >> 4, s = (l >> 2) & 3, kk = l & 3;
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int kc = (i * NTC + t) >> 4;
+      const int kc = 32 * i + 4 * wave + kk;
       w2[i] = hl_ldnt(g2 + (long long)kc * 512 + (16 * s + r) * 8);
     }
   };
@@ -610,24 +612,20 @@ __global__ void __launch_bounds__(cs2::NT) k_codec_stage_s(CodecStageArgs a) {
     __syncthreads();   // B4
     stamp(8 * j + 5, true);
     if (!ctl) {
-      const int t = hl_vopaque((int)threadIdx.x), s = (t >> 2) & 3;
+      const int l = hl_vopaque((int)threadIdx.x & 63), s = (l >> 2) & 3, kk = l & 3;
       float acc[M];
 #pragma unroll
       for (int m = 0; m < M; ++m) acc[m] = 0.f;
 #pragma unroll
       for (int i = 0; i < CPT; ++i) {
-        const int kc = (i * NTC + t) >> 4;
+        const int kc = 32 * i + 4 * wave + kk;
 #pragma unroll
         for (int m = 0; m < M; ++m) acc[m] = hl_dot8(w2[i], *(const bf16x8*)(h_s + m * F + kc * 32 + 8 * s), acc[m]);
       }
 #pragma unroll
       for (int m = 0; m < M; ++m) {
-        float v = acc[m];
-        v += __shfl_xor(v, 4);
-        v += __shfl_xor(v, 8);
-        v += __shfl_xor(v, 16);
-        v += __shfl_xor(v, 32);
-        if ((t & 63) < ROWS2) red[(wave * M + m) * ROWS2 + (t & 63)] = v;
+        const float v = group_sum<16>(acc[m]);
+        if ((l & 15) == 0) red[(wave * M + m) * ROWS2 + (l >> 4)] = v;
       }
     }
     __syncthreads();   // B5

@@ -78,13 +78,14 @@ static void hl_register(int device, int delta) {
   const int before = g_hl_ctxs[device];
   const int after = before + delta;
   g_hl_ctxs[device] = after;
-  if ((before == 1) != (after == 1)) g_ws_epoch.fetch_add(1);
+  if ((before == 1) != (after == 1) || (before <= 2) != (after <= 2)) g_ws_epoch.fetch_add(1);
 }
-static bool hl_sole(int device) {
+static int hl_count(int device) {
   std::lock_guard<std::mutex> lk(g_hl_mu);
   auto it = g_hl_ctxs.find(device);
-  return it != g_hl_ctxs.end() && it->second == 1;
+  return it == g_hl_ctxs.end() ? 0 : it->second;
 }
+static bool hl_sole(int device) { return hl_count(device) == 1; }
 
 struct DevBuf {
   void* p = nullptr;
@@ -1537,7 +1538,10 @@ static int head_layer(vv_ctx* c, const HeadRun& h, int s, int l, hipStream_t st)
   GemmArgs g = gemm_args(c, h.R, 2 * F, H, h.xh_m, W(c, p + ".gu_w"), EPI_SILU_MUL, rowmap(h.act, F));
   g.xf = xf_norm(W(c, p + ".norm"), k.head_eps, mod, h.MODW, o, o + H);
   const bool partial = c->head_tp && c->tp_size > 1 && c->tp_rank > 0;
-  if (c->hf_ready && g_head_fused && head_ffn_fits(H, F, h.R)) {   // one launch: head_ffn.hip
+  // one launch (head_ffn.hip): its grid waits need the launch resident with at
+  // most one other (two workgroups per CU), so with three or more contexts of
+  // the device registered the GEMV layout runs instead where it is bound
+  if (c->hf_ready && g_head_fused && head_ffn_fits(H, F, h.R) && (hl_count(c->device) <= 2 || !c->head_gemv)) {
     HeadFfnArgs a;
     memset(&a, 0, sizeof(a));
     a.x = h.xh;
