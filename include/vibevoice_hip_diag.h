@@ -171,6 +171,10 @@ int vv_rope_table(int on);
  * (bit-identical to the same splits merged in the attention kernel); on = n >= 2:
  * passes of <= n rows (n <= 16); 0 = the attn_plan splits everywhere. */
 int vv_attn_defer(int on, int chunk);
+/* Test / A-B switch: the longest key split (keys) of the deferred-merge plan
+ * above; a context needing longer splits takes the grouped plan below.
+ * <= 0 restores the built-in 1,024. */
+int vv_attn_defer_max(int keys);
 /* Test switch: 1 (default) = decode passes of <= 16 rows over more than 8,192
  * keys run up to 120 splits of >= 256 keys merged in <= 8 groups by each
  * group's last-arriving workgroup, o_proj merging the groups; n >= 2: at most

@@ -982,6 +982,13 @@ extern "C" int vv_rope_table(int on) {
 // staging of 16 rows' partials cost more than the splits saved (5.79 vs 5.67 ms),
 // so by default only <= 4 rows defer.
 static std::atomic<int> g_attn_defer{4}, g_defer_chunk{128};
+// longest split of the deferred-merge plan (keys); longer contexts take the
+// grouped plan's many splits (diagnostic vv_attn_defer_max)
+static std::atomic<int> g_defer_max{1024};
+extern "C" int vv_attn_defer_max(int keys) {
+  g_defer_max = keys <= 0 ? 1024 : keys;
+  return 0;
+}
 extern "C" int vv_attn_defer(int on, int chunk) {
   if (chunk % 32 || chunk < 32 || on < 0) return 1;
   g_attn_defer = on == 1 ? 4 : on;   // 1: the default row limit; n >= 2: up to n rows (<= 16)
@@ -1029,7 +1036,7 @@ static AttnPassPlan attn_pass_plan(int ntok, int lm_slots, int head_dim, int n_k
       ch = ((max_pos_p1 + 7) / 8 + 31) / 32 * 32;
       ns = (max_pos_p1 + ch - 1) / ch;
     }
-    if (ns >= 2 && ns <= 8 && ch <= 1024) {
+    if (ns >= 2 && ns <= 8 && ch <= g_defer_max) {
       P.defer = 1;
       P.nsplit = ns;
       P.chunk = ch;
