@@ -80,12 +80,19 @@ def main():
     rel = t - t0
     names = ["front half begins", "fc1 input in LDS", "fc1 slice landed (wave 0)", "fc1 partials in LDS",
              "hidden-row wait released", "hidden row in LDS", "fc2 partials in LDS", "next-input wait released"]
+    # k_codec_stage_s (C = 1,024) also stamps its front half at 40 + 4j + k
+    front = ["(front) input rows landed", "(front) mixer-norm inverses", "(front) conv + residual done",
+             "(front) FFN-norm inverses"]
+
+    def label(k):
+        return f"block {k // 8} {names[k % 8]}" if k < 40 else f"block {(k - 40) // 4} {front[(k - 40) % 4]}"
     print(f"acoustic decoder stage {stage}, us from the first workgroup's first stamp (median / max over workgroups):")
     prev = None
+    used = [k for k in used if k < 40] + [k for k in used if k >= 40]   # block phases, then the front-half detail
     for k in used:
         col = rel[:, k]
         d = "" if prev is None else f"   +{(col - rel[:, prev]).median():.2f} from the previous (median)"
-        print(f"  {k:2d} block {k // 8} {names[k % 8]:26s} {col.median():8.2f} {col.max():8.2f}{d}")
+        print(f"  {k:2d} {label(k).rstrip(chr(34)):38s} {col.median():8.2f} {col.max():8.2f}{d}")
         prev = k
 
 
