@@ -92,7 +92,7 @@ def main():
     for k in used:
         col = rel[:, k]
         d = "" if prev is None else f"   +{(col - rel[:, prev]).median():.2f} from the previous (median)"
-        print(f"  {k:2d} {label(k).rstrip(chr(34)):38s} {col.median():8.2f} {col.max():8.2f}{d}")
+        print(f"  {k:2d} {label(k):38s} {col.median():8.2f} {col.max():8.2f}{d}")
         prev = k
 
 
