@@ -213,3 +213,48 @@ def test_codec_stage_persistent_launch():
             assert torch.equal(got, again), (f, name)
             assert e_o < 3e-2 and cos(got, ref) > 0.999, (f, name, e_o)
             assert e_b < 3e-2 and cos(got, base) > 0.999, (f, name, e_b)
+
+
+def test_codec_stage_only_for_the_devices_sole_context():
+    """The persistent codec stage holds one workgroup per CU and waits grid-wide:
+    with a second registered context on the device, both run the launch-per-GEMV
+    path (the same streaming state carries on, within bf16 of the stage's), and
+    the first returns to the stage when the second is destroyed (vv_ws_epoch
+    bumps each time, so captured graphs are re-captured)."""
+    from vibevoice_amd import _lib
+    L = _lib.lib()
+    cfg = tiny_config(ratios=(8, 5, 5, 4, 2, 2), depths="3-3-3-3-3-3-8", nf=32)
+    sd = synthetic_state_dict(cfg, seed=3, device="cpu", mode="test", with_acoustic_encoder=False)
+    a = Engine(cfg, sd, dev, max_batch=1, max_ctx=64)
+    assert L.vv_codec_stage_active(a.h) == 1
+    slot = torch.zeros(1, dtype=torch.int32, device=dev)
+    g = torch.Generator().manual_seed(17)
+    lats = [torch.randn(1, 64, generator=g).bfloat16().to(dev) for _ in range(3)]
+
+    def frames(eng):
+        eng.codec_reset(slot)
+        out = []
+        for lat in lats:
+            audio = torch.empty(1, cfg.hop, dtype=torch.bfloat16, device=dev)
+            eng.codec_step(slot, lat, audio)
+            out.append(audio)
+        torch.cuda.synchronize()
+        return out
+
+    solo = frames(a)
+    e0 = L.vv_ws_epoch()
+    b = Engine(cfg, sd, dev, max_batch=1, max_ctx=64)
+    assert L.vv_codec_stage_active(a.h) == 0 and L.vv_codec_stage_active(b.h) == 0
+    assert L.vv_ws_epoch() != e0
+    shared = frames(a)
+    for f, (x, y) in enumerate(zip(solo, shared)):
+        e = rel_err(x, y)
+        print(f"frame {f}: stage vs launch-per-GEMV audio rel {e:.3e}")
+        assert e < 3e-2 and cos(x, y) > 0.999
+    e1 = L.vv_ws_epoch()
+    b.close()
+    assert L.vv_codec_stage_active(a.h) == 1 and L.vv_ws_epoch() != e1
+    again = frames(a)
+    for x, y in zip(solo, again):
+        assert torch.equal(x, y)
+    a.close()
