@@ -136,6 +136,13 @@ int vv_head_fused(int on);
  * The persistent head runs only while its context is the device's only one
  * with it bound (two cannot be resident together). */
 int vv_head_loop(int on);
+/* Test / A-B switch: 1 (default) = at 4 < 2n <= 16 rows each head FFN layer
+ * is one launch with one grid-wide hand-off (head_m16.hip; within bf16 of the
+ * GEMV pair, not bitwise) while ctx is the device's only registered context;
+ * 0 = gate|up + down GEMV launches. */
+int vv_head_m16(int on);
+/* Test query: 1 when a head layer of n samples on ctx would run head_m16 now. */
+int vv_head_m16_active(vv_ctx* ctx, int n);
 /* Test query: 1 when vv_diffusion_sample of n samples on ctx would run the
  * persistent head now. */
 int vv_head_loop_active(vv_ctx* ctx, int n);

@@ -278,3 +278,61 @@ def test_head_loop_only_for_the_devices_sole_context():
     b.close()
     assert L.vv_head_loop_active(a.h, 1) == 1 and L.vv_ws_epoch() != e1
     a.close()
+
+
+@pytest.mark.parametrize("n", [3, 8])
+def test_head_m16_vs_oracle_and_gemv_pair(n):
+    """configs[2]'s head (B = 8: 2n = 16 rows; n = 3: 6 rows, padded): each FFN
+    layer as ONE launch with one grid-wide hand-off (head_m16.hip: gate|up by
+    MFMA over 2-3 tiles per workgroup, down over half a tile per two-tile
+    workgroup) vs the oracle (rel < 2e-2, cosine > 0.999) and vs the
+    gate|up + down GEMV launches (within bf16: the GEMM sums run in another
+    order), the real 1.5B head shapes, S = 10, CFG 1.3; repeated calls and graph
+    replays bitwise equal."""
+    from vibevoice_amd import _lib
+    L = _lib.lib()
+    g = torch.Generator().manual_seed(60 + n)
+    sdh, hc, H = real_head_sd(g)
+    cfg = tiny_config(hidden=H, layers=1, heads=12, kv_heads=2, inter=256)
+    sd = synthetic_state_dict(cfg, seed=0, device="cpu", mode="test", with_acoustic_encoder=False)
+    for k, v in sdh.items():
+        sd["model.prediction_head." + k] = v
+    eng = Engine(cfg, sd, dev, max_batch=8, max_ctx=64)   # the GEMV layout (max_batch > 2)
+    eng.set_steps(10)
+    assert L.vv_head_m16_active(eng.h, n) == 1
+    pos = torch.randn(n, H, generator=g).bfloat16()
+    neg = torch.randn(n, H, generator=g).bfloat16()
+    noise = torch.randn(2 * n, 64, generator=g).bfloat16()
+    ref = ohead.sample_speech_tokens(sdh, pos, neg, noise, 10, 1.3, hc.head_layers)
+    outs = {}
+    try:
+        for mode in (1, 0, 1):
+            L.vv_head_m16(mode)
+            x = noise[:n].to(dev).contiguous()
+            eng.diffusion_sample(pos.to(dev), neg.to(dev), x, 1.3)
+            torch.cuda.synchronize()
+            outs.setdefault(mode, []).append(x.clone())
+        # graph replay of the one-launch layers (operands on the device before the capture)
+        L.vv_head_m16(1)
+        s = torch.cuda.Stream()
+        pd, nd = pos.to(dev), neg.to(dev)
+        xg = noise[:n].to(dev).contiguous()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s):
+            gr = torch.cuda.CUDAGraph()
+            gr.capture_begin(capture_error_mode="thread_local")
+            eng.diffusion_sample(pd, nd, xg, 1.3, stream=s)
+            gr.capture_end()
+        xg.copy_(noise[:n].to(dev))
+        with torch.cuda.stream(s):
+            gr.replay()
+        torch.cuda.synchronize()
+    finally:
+        L.vv_head_m16(1)
+    eng.check_sync()
+    m16, pair = outs[1][0], outs[0][0]
+    e, ep, eb = rel_err(m16, ref), rel_err(pair, ref), rel_err(m16, pair)
+    print(f"head m16 n={n}: rel {e:.3e} vs oracle (GEMV pair {ep:.3e}), {eb:.3e} vs the GEMV pair")
+    assert torch.equal(m16, outs[1][1]) and torch.equal(m16, xg)
+    assert e < 2e-2 and cos(m16, ref) > 0.999
+    assert eb < 2e-2 and cos(m16, pair) > 0.999

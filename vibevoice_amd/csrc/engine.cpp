@@ -850,10 +850,12 @@ int vv_finalize(vv_ctx* c) {
   CHK(convnet_alloc(c->dec, 7));
   CHK(convnet_alloc(c->sem, 7));
   // the persistent codec stage's wait counters; a context that can run it (or
-  // the persistent head) counts in the device's registry (hl_register)
+  // the persistent head, or the one-launch head layer at 16 rows) counts in the
+  // device's registry (hl_register)
   CHK(c->cs_sync.ensure(12 * 128));
   HIPCHK(hipMemset(c->cs_sync.p, 0, 12 * 128));
-  if (!c->hl_registered && (codec_stage_any(c->dec) || codec_stage_any(c->sem))) {
+  if (!c->hl_registered && (codec_stage_any(c->dec) || codec_stage_any(c->sem) ||
+                            (c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 16)))) {
     c->hl_registered = true;
     hl_register(c->device, +1);
   }
@@ -1366,7 +1368,7 @@ int vv_sync_error(vv_ctx* c) {
       FAIL("vv_sync_error: reading the error word failed (hipMemcpy)");
     // a launch that gave up left the wait counters part-advanced: with nothing in
     // flight (the device is synchronised) every counter restarts from 0
-    if (v) HIPCHK(hipMemset(c->hf_sync.p, 0, 12 * 128));
+    if (v) HIPCHK(hipMemset(c->hf_sync.p, 0, 13 * 128));
     if (v && c->cs_sync.p) HIPCHK(hipMemset(c->cs_sync.p, 0, 12 * 128));
   }
   return v ? 1 : 0;
@@ -1530,6 +1532,20 @@ static int head_noisy(vv_ctx* c, const HeadRun& h, const void* x_io, hipStream_t
                    st);
 }
 
+// 4 < 2n <= 16 rows: the layer as one launch (head_m16.hip) while the context is
+// the device's only registered one; 0 = two GEMV launches (A/B and tests)
+static std::atomic<int> g_head_m16{1};
+extern "C" int vv_head_m16(int on) {
+  g_head_m16 = on ? 1 : 0;
+  return 0;
+}
+extern "C" int vv_head_m16_active(vv_ctx* c, int n) {
+  const vv_config& k = c->cfg;
+  return c && c->finalized && g_head_m16 && !c->head_tp && c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 2 * n) &&
+                 hl_sole(c->device)
+             ? 1
+             : 0;
+}
 // layer l of step s: modulate(norm(x)) -> gate|up -> SiLU*up -> down -> x += gate * (.)
 // With the FFN sharded (vv_tp_shard_head) this rank holds head_ffn / tp_size of
 // the hidden columns: gate|up column-parallel, down row-parallel; rank 0 adds
@@ -1570,6 +1586,29 @@ static int head_layer(vv_ctx* c, const HeadRun& h, int s, int l, hipStream_t st)
     a.err = (unsigned*)c->hf_sync.p + 10 * 32;
     a.stamps = g_head_ffn_stamps;
     KCHK(launch_head_ffn(a, st));
+    return 0;
+  }
+  if (g_head_m16 && !c->head_tp && c->head_gemv && head_m16_fits(H, F, h.R) && hl_sole(c->device)) {
+    // 4 < 2n <= 16 rows: one launch with one grid-wide hand-off (head_m16.hip)
+    HeadM16Args a;
+    memset(&a, 0, sizeof(a));
+    a.x = h.xh;
+    a.out = h.xh;
+    a.ldx = H;
+    a.mod = mod;
+    a.ldmod = h.MODW;
+    a.shift_off = o;
+    a.scale_off = o + H;
+    a.gate_off = o + 2 * H;
+    a.R = h.R;
+    a.eps = k.head_eps;
+    a.nw = W(c, p + ".norm");
+    a.gu = W(c, p + ".gu_w");
+    a.dn = W(c, p + ".down_w");
+    a.act = h.act;
+    a.sync = (unsigned*)c->hf_sync.p;
+    a.err = (unsigned*)c->hf_sync.p + 10 * 32;
+    KCHK(launch_head_m16(a, st));
     return 0;
   }
   if (!c->head_gemv)

@@ -251,6 +251,25 @@ bool head_ffn_fits(int H, int F, int R);
 int head_ffn_grid();
 int launch_head_ffn(const HeadFfnArgs& a, hipStream_t st);
 
+// ---- one head FFN layer at 4 < 2n <= 16 rows in one launch (head_m16.hip), GEMV layout weights
+struct HeadM16Args {
+  const bf16* x;            // [R][H] state rows (ld ldx), read before the grid wait
+  bf16* out;                // [R][H] (ld ldx): x + gate * ffn (in place: out == x)
+  const bf16* mod;          // adaLN rows [R][ldmod]: shift / scale / gate at the offsets
+  long long ldx, ldmod;
+  int shift_off, scale_off, gate_off, R;
+  float eps;
+  int pad_;
+  const bf16* nw;           // RMSNorm weight [H]
+  const bf16* gu;           // gate|up, MFMA-packed [2F][H] (EPI_SILU_MUL pairing)
+  const bf16* dn;           // down, MFMA-packed [H][F]
+  bf16* act;                // [16][F] SiLU(gate) * up rows (workspace, written through)
+  unsigned* sync;           // the head's wait lines: shards 0-7, this kernel's generation at line 12
+  unsigned* err;            // set to 1 when the grid wait gave up
+};
+bool head_m16_fits(int H, int F, int R);
+int launch_head_m16(const HeadM16Args& a, hipStream_t st);
+
 // ---- the whole diffusion of a token in one persistent launch (head_loop.hip):
 // steps [s0, s1) of noisy -> L FFN layers -> final + CFG + DPM-Solver++ at 2n <= 4 rows
 struct HeadLoopArgs {
