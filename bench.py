@@ -369,8 +369,11 @@ def measure_head_layers(model, B, reps=10, iters=4):
     per_layer = (times[1] - times[0]) / (reps * L)
     alg = 3 * F * H * 2 + R * H * 2 * 2
     fused = R <= 4 and head_fused_layout(eng.w, B)
+    m16 = R > 4 and lib.vv_head_m16_active(eng.h, B) == 1
     kernel = (f"k_head_ffn<{R}, false> (fused head FFN layer: norm + adaLN, gate|up, SiLU*up, down, gated "
               f"residual in one launch)" if fused else
+              "k_head_m16 (one head FFN layer at 4 < 2n <= 16 rows in one launch: MFMA gate|up + SiLU*up, one "
+              "grid-wide hand-off, MFMA down + gated residual)" if m16 else
               "k_gemv1 gate|up + k_gemv/k_gemv1 down (one head FFN layer = two GEMV launches, timed together)")
     traffic = None
     pf = os.path.join(ROOT, "profiles", f"r05_pmc_head_r{R}.json")

@@ -11,7 +11,8 @@ usage (GPU box):
   python tools/pmc_traffic.py collect-loop [R]  # the persistent diffusion head (k_head_loop<R>, S = 10)
                                               # -> profiles/r05_pmc_head_loop_r<R>.json
   python tools/pmc_traffic.py collect-head [R]  # the same for the diffusion head's FFN layer kernel
-                                              # (k_head_ffn<R>, R = 2n rows) -> profiles/r05_pmc_head_r<R>.json
+                                              # (k_head_ffn<R> at R = 2n <= 4 rows, k_head_m16 above)
+                                              # -> profiles/r05_pmc_head_r<R>.json
 M = 2 (B = 1, one tile per workgroup) or 16 (B = 8: the balanced form, 4-5 tiles per workgroup).
 """
 import csv
@@ -95,8 +96,8 @@ def run_head_loop():
 
 HEAD = len(sys.argv) > 1 and sys.argv[1].endswith("head")
 LOOP = len(sys.argv) > 1 and sys.argv[1].endswith("loop")
-if HEAD:
-    KERNEL, NL = f"k_head_ffn<{M}, false>", 4
+if HEAD:   # 2n <= 4 rows: the fused layer; 4 < 2n <= 16: the one-launch layer of head_m16.hip
+    KERNEL, NL = (f"k_head_ffn<{M}, false>" if M <= 4 else "k_head_m16"), 4
     N, K = 4608, 1536                     # F, H
 if LOOP:
     KERNEL, NL = f"k_head_loop<{M}, false>", 1
