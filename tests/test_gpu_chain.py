@@ -6,8 +6,9 @@
   * the balanced plan (mode 1) re-splits K, so it differs from the per-op path
     by summation order only: deterministic run to run, rel L2 < 1e-2 against it;
   * no dependency wait gave up (vv_chain_error == 0).
-The per-op reference runs with the fused head FFN layer switched off (it sums in
-a different order; tests/test_gpu_head.py pins it).
+The per-op reference runs with the fused head FFN layer and the one-launch
+16-row layer switched off (they sum in a different order; tests/test_gpu_head.py
+pins them).
 Real VibeVoice-1.5B head shapes (H = 1536, FFN 4608, 4 layers), S = 10, CFG 1.3.
 """
 import pytest
@@ -37,9 +38,11 @@ def head_engine():
     # the chain mirrors the per-op GEMV launches (gate|up, down); the fused FFN
     # layer (head_ffn.hip, the default at n <= 2) is a different summation order
     _lib.lib().vv_head_fused(0)
+    _lib.lib().vv_head_m16(0)   # nor the one-launch layer at 4 < 2n <= 16 rows (head_m16.hip)
     yield eng, H, g
     _lib.lib().vv_chain_tune(0)
     _lib.lib().vv_head_fused(1)
+    _lib.lib().vv_head_m16(1)
 
 
 def run(eng, mode, pos, neg, noise, n, sde=None):
