@@ -80,19 +80,14 @@ __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
 
   bf16x8 wb[WB];
   const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-  if (!ctl) {   // this wave's k-blocks of each of the workgroup's gate|up tiles
-    const bf16* gw = hl_opaque(a.gu) + (long long)t0 * KC1 * 512 + lane * 8;
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-#pragma unroll
-      for (int kk = 0; kk < KPW1; ++kk)
-        wb[j * KPW1 + kk] = j < nt ? hl_ldnt(gw + ((long long)j * KC1 + wave * KPW1 + kk) * 512) : zero8;
-  }
-  if (ctl) {   // the A side: state rows, shift / scale rows, norm weight (LDS DMA); x and gate of the down columns
+  if (!ctl) {
+    // the A side first (rows wave, wave + 8: state, shift, scale; wave 0 also the
+    // norm weight; LDS DMA), then this wave's k-blocks of each gate|up tile: the
+    // DMA waits below count only the weight loads behind it
     const int ln = hl_vopaque(lane);
     const bf16* xp = hl_opaque(a.x);
     const bf16* mp = hl_opaque(a.mod);
-    for (int m = 0; m < R; ++m) {
+    for (int m = wave; m < R; m += NTC / 64) {
 #pragma unroll
       for (int i = 0; i < NCH / 64; ++i) {
         const int c = i * 64 + ln;
@@ -101,13 +96,25 @@ __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
         hl_dma16<false>(sc_s + m * H + i * 512, mp + (long long)m * a.ldmod + a.scale_off + c * 8);
       }
     }
+    if (wave == 0)
 #pragma unroll
-    for (int i = 0; i < NCH / 64; ++i) hl_dma16<false>(nw_s + i * 512, hl_opaque(a.nw) + (i * 64 + ln) * 8);
-    if (owner && ln < R) {
-      *(bf16x8*)(gate_s + ln * 8) = hl_ld(mp + (long long)ln * a.ldmod + a.gate_off + col0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (owner && ln < R) *(bf16x8*)(xraw_s + ln * 8) = *(const bf16x8*)(xs + ln * H + col0);
+      for (int i = 0; i < NCH / 64; ++i) hl_dma16<false>(nw_s + i * 512, hl_opaque(a.nw) + (i * 64 + ln) * 8);
+    // (every load unconditional: a guarded load compiles to a branch and a
+    // vmcnt(0) at its join, which drained the whole queue here; a two-tile
+    // workgroup's third set reads one line of tile t0 and is never stored)
+    const bf16* gw = hl_opaque(a.gu) + (long long)t0 * KC1 * 512 + lane * 8;
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int kk = 0; kk < KPW1; ++kk)
+        wb[j * KPW1 + kk] = hl_ldnt(j < nt ? gw + ((long long)j * KC1 + wave * KPW1 + kk) * 512 : gw - lane * 8);
+    asm volatile("s_waitcnt vmcnt(18)" ::: "memory");   // this wave's A-side DMA landed (18 weight loads may fly)
+  }
+  if (ctl && owner && lane < R) {   // x and adaLN gate of this workgroup's down columns
+    const bf16* xp = hl_opaque(a.x);
+    const bf16* mp = hl_opaque(a.mod);
+    *(bf16x8*)(gate_s + lane * 8) = hl_ld(mp + (long long)lane * a.ldmod + a.gate_off + col0);
+    *(bf16x8*)(xraw_s + lane * 8) = hl_ld(xp + (long long)lane * a.ldx + col0);
   }
   __syncthreads();
   for (int m = wave; m < R; m += NT / 64) {   // inverse RMS in k_rmsnorm's order
@@ -156,11 +163,13 @@ __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
     for (int j = 0; j < 3; ++j)
       if (j < nt) *(f32x4*)(red1 + (j * 8 + wave) * 256 + ln * 4) = acc[j];
     if (owner) {   // this workgroup's half down tile into the registers (in flight through the wait)
+      // lanes of the other half of the tile feed only output columns this
+      // workgroup does not store: they read one line instead (unconditional loads)
       const bf16* dw = hl_opaque(a.dn) + (long long)(d >> 1) * KC2 * 512 + ln * 8;
       const bool mine = ((ln & 15) >> 3) == (d & 1);
 #pragma unroll
       for (int kk = 0; kk < KPW2; ++kk)
-        wb[kk] = mine ? hl_ldnt(dw + (long long)(wave * KPW2 + kk) * 512) : zero8;
+        wb[kk] = hl_ldnt(mine ? dw + (long long)(wave * KPW2 + kk) * 512 : dw - ln * 8);
     }
   }
   __syncthreads();
