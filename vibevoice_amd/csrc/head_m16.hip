@@ -21,6 +21,8 @@
 //     products, so the stream runs through the wait), MFMA over all 4,608 k
 //     with the act rows DMA'd into LDS; gated residual; plain stores (the
 //     launch's end publishes them).
+// Weights are read with the default cache policy: the head's 170 MB are read S
+// times per token and stay in the Infinity Cache (gemv_dev.h ldw<KEEP>).
 // Arithmetic: xform<XF_NORM>'s rounding points and k_rmsnorm's row order for
 // the norm; the GEMM sums are fp32 MFMA sums in another order than the GEMV
 // kernels', so the layer is within bf16 of the two-launch path, not bitwise
@@ -107,7 +109,7 @@ __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
     for (int j = 0; j < 3; ++j)
 #pragma unroll
       for (int kk = 0; kk < KPW1; ++kk)
-        wb[j * KPW1 + kk] = hl_ldnt(j < nt ? gw + ((long long)j * KC1 + wave * KPW1 + kk) * 512 : gw - lane * 8);
+        wb[j * KPW1 + kk] = hl_ld(j < nt ? gw + ((long long)j * KC1 + wave * KPW1 + kk) * 512 : gw - lane * 8);
     asm volatile("s_waitcnt vmcnt(18)" ::: "memory");   // this wave's A-side DMA landed (18 weight loads may fly)
   }
   if (ctl && owner && lane < R) {   // x and adaLN gate of this workgroup's down columns
@@ -169,7 +171,7 @@ __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
       const bool mine = ((ln & 15) >> 3) == (d & 1);
 #pragma unroll
       for (int kk = 0; kk < KPW2; ++kk)
-        wb[kk] = hl_ldnt(mine ? dw + (long long)(wave * KPW2 + kk) * 512 : dw - ln * 8);
+        wb[kk] = hl_ld(mine ? dw + (long long)(wave * KPW2 + kk) * 512 : dw - ln * 8);
     }
   }
   __syncthreads();
