@@ -143,6 +143,13 @@ int vv_head_loop(int on);
 int vv_head_m16(int on);
 /* Test query: 1 when a head layer of n samples on ctx would run head_m16 now. */
 int vv_head_m16_active(vv_ctx* ctx, int n);
+/* Diagnostic: per-workgroup s_memrealtime stamps of every head_m16 launch into
+ * buf ([256][16] u64, overwritten per launch; NULL = off). */
+int vv_head_m16_stamps(void* buf);
+/* Diagnostic switch: head layers l >= 1 at 4 < 2n <= 16 rows build their A side
+ * distributed from the previous layer's row partials (1, default) or transform
+ * it whole in every workgroup (0). */
+int vv_head_m16_pre(int on);
 /* Test query: 1 when vv_diffusion_sample of n samples on ctx would run the
  * persistent head now. */
 int vv_head_loop_active(vv_ctx* ctx, int n);

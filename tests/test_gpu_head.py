@@ -288,7 +288,10 @@ def test_head_m16_vs_oracle_and_gemv_pair(n):
     workgroup) vs the oracle (rel < 2e-2, cosine > 0.999) and vs the
     gate|up + down GEMV launches (within bf16: the GEMM sums run in another
     order), the real 1.5B head shapes, S = 10, CFG 1.3; repeated calls and graph
-    replays bitwise equal."""
+    replays bitwise equal.  Layers l >= 1 build their A side distributed from the
+    previous layer's row partials (default); the form that transforms the whole A
+    side in every workgroup is checked the same way (its inverse RMS sums run in
+    another order: within bf16 of it)."""
     from vibevoice_amd import _lib
     L = _lib.lib()
     g = torch.Generator().manual_seed(60 + n)
@@ -306,12 +309,14 @@ def test_head_m16_vs_oracle_and_gemv_pair(n):
     ref = ohead.sample_speech_tokens(sdh, pos, neg, noise, 10, 1.3, hc.head_layers)
     outs = {}
     try:
-        for mode in (1, 0, 1):
+        for mode, pre in ((1, 1), (0, 1), (1, 1), (1, 0)):
             L.vv_head_m16(mode)
+            L.vv_head_m16_pre(pre)
             x = noise[:n].to(dev).contiguous()
             eng.diffusion_sample(pos.to(dev), neg.to(dev), x, 1.3)
             torch.cuda.synchronize()
-            outs.setdefault(mode, []).append(x.clone())
+            outs.setdefault(mode + 2 * (1 - pre), []).append(x.clone())
+        L.vv_head_m16_pre(1)
         # graph replay of the one-launch layers (operands on the device before the capture)
         L.vv_head_m16(1)
         s = torch.cuda.Stream()
@@ -329,10 +334,14 @@ def test_head_m16_vs_oracle_and_gemv_pair(n):
         torch.cuda.synchronize()
     finally:
         L.vv_head_m16(1)
+        L.vv_head_m16_pre(1)
     eng.check_sync()
-    m16, pair = outs[1][0], outs[0][0]
+    m16, pair, whole = outs[1][0], outs[0][0], outs[3][0]
     e, ep, eb = rel_err(m16, ref), rel_err(pair, ref), rel_err(m16, pair)
-    print(f"head m16 n={n}: rel {e:.3e} vs oracle (GEMV pair {ep:.3e}), {eb:.3e} vs the GEMV pair")
+    ew, ewd = rel_err(whole, ref), rel_err(m16, whole)
+    print(f"head m16 n={n}: rel {e:.3e} vs oracle (GEMV pair {ep:.3e}, whole-A-side form {ew:.3e}), "
+          f"{eb:.3e} vs the GEMV pair, {ewd:.3e} vs the whole-A-side form")
     assert torch.equal(m16, outs[1][1]) and torch.equal(m16, xg)
     assert e < 2e-2 and cos(m16, ref) > 0.999
     assert eb < 2e-2 and cos(m16, pair) > 0.999
+    assert ew < 2e-2 and cos(whole, ref) > 0.999 and ewd < 2e-2

@@ -80,6 +80,8 @@ EXPORTS = [
     ("vv_codec_stage", I, [I]),
     ("vv_head_m16", I, [I]),
     ("vv_head_m16_active", I, [P, I]),
+    ("vv_head_m16_stamps", I, [P]),
+    ("vv_head_m16_pre", I, [I]),
     ("vv_attn_defer_max", I, [I]),
     ("vv_codec_stage_active", I, [P]),
     ("vv_codec_stage_stamps", I, [P, I]),

@@ -187,6 +187,7 @@ struct vv_ctx {
   DevBuf chain_sync, chain_slabs, chain_err, coef_dev;
   // fused head FFN layer (head_ffn.hip): partial-sum slabs, grid-wait words + error word
   DevBuf hf_slab, hf_sync;
+  DevBuf m16_buf;   // head_m16.hip's distributed A side: row partial sums of squares [16][192] f32 + rows [16][H]
   DevBuf hl_lat;           // persistent head (head_loop.hip): [D][2] latent hand-off
   DevBuf cs_sync;          // persistent codec stage (codec_stage.hip): its wait counters
   bool hl_registered = false;   // counted in g_hl_ctxs (its device's persistent-head contexts)
@@ -728,7 +729,7 @@ void vv_destroy(vv_ctx* c) {
   DevBuf* bufs[] = {&c->norm_ws, &c->kv_k, &c->kv_v, &c->lm_ws, &c->attn_part, &c->attn_cnt, &c->valid_ids, &c->splitk_ws, &c->splitk_cnt,
                     &c->temb, &c->tfreq_tmp, &c->head_ws, &c->codec_ws, &c->slot_scratch, &c->unit_sb,
                     &c->chain_sync, &c->chain_slabs, &c->chain_err, &c->coef_dev, &c->rope_tab, &c->zero_rows,
-                    &c->hf_slab, &c->hf_sync, &c->hl_lat, &c->cs_sync};
+                    &c->hf_slab, &c->hf_sync, &c->hl_lat, &c->cs_sync, &c->m16_buf};
   for (DevBuf* b : bufs) b->release();
   for (auto& kv : c->head_chain) kv.second.ops.release();
   ConvNet* nets[] = {&c->dec, &c->sem, &c->aenc, &c->senc};
@@ -854,6 +855,8 @@ int vv_finalize(vv_ctx* c) {
   // device's registry (hl_register)
   CHK(c->cs_sync.ensure(12 * 128));
   HIPCHK(hipMemset(c->cs_sync.p, 0, 12 * 128));
+  if (c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 16))
+    CHK(c->m16_buf.ensure(16 * 192 * sizeof(float) + 16 * (size_t)k.hidden * sizeof(bf16)));
   if (!c->hl_registered && (codec_stage_any(c->dec) || codec_stage_any(c->sem) ||
                             (c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 16)))) {
     c->hl_registered = true;
@@ -1535,8 +1538,20 @@ static int head_noisy(vv_ctx* c, const HeadRun& h, const void* x_io, hipStream_t
 // 4 < 2n <= 16 rows: the layer as one launch (head_m16.hip) while the context is
 // the device's only registered one; 0 = two GEMV launches (A/B and tests)
 static std::atomic<int> g_head_m16{1};
+// layers l >= 1 build the A side distributed (HeadM16Args::pre) from the previous
+// layer's row partials; 0 = every workgroup transforms the whole A side
+static std::atomic<int> g_head_m16_pre{1};
+extern "C" int vv_head_m16_pre(int on) {
+  g_head_m16_pre = on;
+  return 0;
+}
+static std::atomic<unsigned long long*> g_head_m16_stamps{nullptr};
+extern "C" int vv_head_m16_stamps(void* buf) {   // diagnostic: [256][16] per-workgroup phase stamps
+  g_head_m16_stamps = (unsigned long long*)buf;
+  return 0;
+}
 extern "C" int vv_head_m16(int on) {
-  g_head_m16 = on ? 1 : 0;
+  g_head_m16 = on;   // A/B variants: bit 1 HeadM16Args::a_first, bit 2 the down weights' earlier issue point
   return 0;
 }
 extern "C" int vv_head_m16_active(vv_ctx* c, int n) {
@@ -1588,7 +1603,7 @@ static int head_layer(vv_ctx* c, const HeadRun& h, int s, int l, hipStream_t st)
     KCHK(launch_head_ffn(a, st));
     return 0;
   }
-  if (g_head_m16 && !c->head_tp && c->head_gemv && head_m16_fits(H, F, h.R) && hl_sole(c->device)) {
+  if (g_head_m16 && !c->head_tp && c->head_gemv && c->m16_buf.p && head_m16_fits(H, F, h.R) && hl_sole(c->device)) {
     // 4 < 2n <= 16 rows: one launch with one grid-wide hand-off (head_m16.hip)
     HeadM16Args a;
     memset(&a, 0, sizeof(a));
@@ -1608,6 +1623,12 @@ static int head_layer(vv_ctx* c, const HeadRun& h, int s, int l, hipStream_t st)
     a.act = h.act;
     a.sync = (unsigned*)c->hf_sync.p;
     a.err = (unsigned*)c->hf_sync.p + 10 * 32;
+    a.stamps = g_head_m16_stamps;
+    a.a_first = (g_head_m16.load() & 2) ? 1 : 0;
+    a.late_down = (g_head_m16.load() & 4) ? 0 : 1;
+    a.ssp = (float*)c->m16_buf.p;
+    a.xt = (bf16*)((char*)c->m16_buf.p + 16 * 192 * sizeof(float));
+    a.pre = l > 0 && g_head_m16_pre ? 1 : 0;   // layer 0's x comes from the noisy projection (no partials)
     KCHK(launch_head_m16(a, st));
     return 0;
   }

@@ -36,12 +36,16 @@ constexpr int KC1 = H / 32, KC2 = F / 32; // 48 / 144 k-blocks
 constexpr int T1 = 2 * F / 16;            // 576 gate|up tiles
 constexpr int KPW1 = KC1 / 8, KPW2 = KC2 / 8;   // k-blocks per compute wave: 6 / 18
 constexpr int NCH = H / 8;                // 192 chunks per state row
+constexpr int NOWN = 192;                 // down-column owners (8 columns each) = ssp partials per row
 constexpr int WB = 3 * KPW1 > KPW2 ? 3 * KPW1 : KPW2;   // weight registers per lane (18 chunks)
 // LDS, phase A: xs | sh | sc (each [16][H] bf16) | nw [H] | small;   the gate|up
 // partial tiles [3][8 waves][256] fp32 reuse sh after the transform.
 // Phase B: act [16][F] bf16 over xs / sh / sc | the down partials [8 waves][256]
 // fp32 after the small region.
-constexpr int XS = 0, SH = XS + RMAX * H * 2, SC = SH + RMAX * H * 2, NW = SC + RMAX * H * 2;
+// xs / act rows padded by 16 B: the MFMA A reads (lane l: row l & 15) of an
+// unpadded 3,072 / 9,216 B row stride all hit the same 4 banks (16-way conflicts)
+constexpr int XST = H + 8, AST = F + 8;
+constexpr int XS = 0, SH = XS + RMAX * XST * 2, SC = SH + RMAX * H * 2, NW = SC + RMAX * H * 2;
 constexpr int SM = NW + H * 2;
 constexpr int SM_B = (4 + RMAX + 3 * RMAX * 8) * 4 + 2 * RMAX * 8 * 2;   // ok, inv, silu*up values, xraw / gate
 // (the down partials go after the small region, which holds the x / gate values
@@ -49,7 +53,7 @@ constexpr int SM_B = (4 + RMAX + 3 * RMAX * 8) * 4 + 2 * RMAX * 8 * 2;   // ok, 
 constexpr int ACT = 0, RED2 = (SM + SM_B + 15) / 16 * 16;
 constexpr int TOTAL = RED2 + 8 * 256 * 4;
 static_assert(TOTAL <= 160 * 1024 && 3 * 8 * 256 * 4 <= RMAX * H * 2, "head m16 LDS");
-static_assert(ACT + RMAX * F * 2 <= SM, "the act rows stay clear of the small region");
+static_assert(ACT + RMAX * AST * 2 <= SM, "the act rows stay clear of the small region");
 }  // namespace hm
 
 __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
@@ -77,12 +81,52 @@ __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
   const int d = 3 * (w >> 2) + (w & 3);                           // down columns [8d, 8d + 8)
   const int col0 = 8 * d;
   unsigned g0 = 0;
+  // diagnostics: 0 entry, 1 A side landed (wave 0), 2 row norms, 3 transform,
+  // 4 gate|up partials in LDS, 5 SiLU * up, 6 hand-off released, 7 act rows in
+  // LDS, 8 down partials in LDS, 9 end (owners); 10 A side landed (wave 7),
+  // 11 gate / x columns landed (control wave), 12 / 13 wave 0's norm / transform
+  // loop done (before the barrier)
+  auto stamp = [&](int k, bool by_ctl) {
+    if (a.stamps && threadIdx.x == (by_ctl ? NTC : 0)) a.stamps[w * 16 + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0, true);
   if (ctl) __builtin_amdgcn_s_setprio(3);
   if (ctl) g0 = __hip_atomic_load((hl_gu32*)(a.sync + 12 * pk::LINE), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~7u;
 
   bf16x8 wb[WB];
   const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-  if (!ctl) {
+  // this workgroup's half down tile into the registers (in flight through the
+  // hand-off); lanes of the other half of the tile feed only output columns this
+  // workgroup does not store: they read one line instead (unconditional loads)
+  auto down_chunk = [&](int kk) {
+    const int ln = hl_vopaque(lane);
+    const bf16* dw = hl_opaque(a.dn) + (long long)(d >> 1) * KC2 * 512 + ln * 8;
+    const bool mine = ((ln & 15) >> 3) == (d & 1);
+    return mine ? dw + (long long)(wave * KPW2 + kk) * 512 : dw - ln * 8;
+  };
+  auto load_down = [&]() {
+#pragma unroll
+    for (int kk = 0; kk < KPW2; ++kk) wb[kk] = hl_ld(down_chunk(kk));
+  };
+  if (ctl && owner && lane < R) {   // x and adaLN gate of this workgroup's down columns (LDS DMA, first in the queue)
+    hl_dma16<false>(gate_s, hl_opaque(a.mod) + (long long)lane * a.ldmod + a.gate_off + col0);
+    hl_dma16<false>(xraw_s, hl_opaque(a.x) + (long long)lane * a.ldx + col0);
+  }
+  if (a.pre && ctl && owner) {
+    // this workgroup's slice of the A side: its 8 columns of shift / scale / norm
+    // weight, and the previous launch's row partial sums of squares (into the
+    // dead sh / sc regions; the raw x columns are xraw_s)
+    const bf16* mp = hl_opaque(a.mod);
+    if (lane < R) {
+      hl_dma16<false>(sc_s, mp + (long long)lane * a.ldmod + a.scale_off + col0);
+      hl_dma16<false>(sc_s + RMAX * 8, mp + (long long)lane * a.ldmod + a.shift_off + col0);
+    }
+    if (lane == 0) hl_dma16<false>(nw_s, hl_opaque(a.nw) + col0);
+    const float* sp = hl_opaque((const float*)a.ssp);
+    for (int i = 0; i * 64 < R * NOWN / 4; ++i)
+      if (i * 64 + lane < R * NOWN / 4) hl_dma16<false>(sh_s + i * 512, sp + (i * 64 + lane) * 4);
+  }
+  if (!a.pre && !ctl) {
     // the A side first (rows wave, wave + 8: state, shift, scale; wave 0 also the
     // norm weight; LDS DMA), then this wave's k-blocks of each gate|up tile: the
     // DMA waits below count only the weight loads behind it
@@ -93,7 +137,7 @@ __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
 #pragma unroll
       for (int i = 0; i < NCH / 64; ++i) {
         const int c = i * 64 + ln;
-        hl_dma16<false>(xs + m * H + i * 512, xp + (long long)m * a.ldx + c * 8);
+        hl_dma16<false>(xs + m * XST + i * 512, xp + (long long)m * a.ldx + c * 8);
         hl_dma16<false>(sh_s + m * H + i * 512, mp + (long long)m * a.ldmod + a.shift_off + c * 8);
         hl_dma16<false>(sc_s + m * H + i * 512, mp + (long long)m * a.ldmod + a.scale_off + c * 8);
       }
@@ -101,6 +145,9 @@ __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
     if (wave == 0)
 #pragma unroll
       for (int i = 0; i < NCH / 64; ++i) hl_dma16<false>(nw_s + i * 512, hl_opaque(a.nw) + (i * 64 + ln) * 8);
+  }
+  if (a.a_first) __builtin_amdgcn_s_barrier();   // (uniform) the whole A side queued ahead of the weights
+  if (!ctl) {
     // (every load unconditional: a guarded load compiles to a branch and a
     // vmcnt(0) at its join, which drained the whole queue here; a two-tile
     // workgroup's third set reads one line of tile t0 and is never stored)
@@ -110,32 +157,77 @@ __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
 #pragma unroll
       for (int kk = 0; kk < KPW1; ++kk)
         wb[j * KPW1 + kk] = hl_ld(j < nt ? gw + ((long long)j * KC1 + wave * KPW1 + kk) * 512 : gw - lane * 8);
-    asm volatile("s_waitcnt vmcnt(18)" ::: "memory");   // this wave's A-side DMA landed (18 weight loads may fly)
+    if (!a.pre) {
+      asm volatile("s_waitcnt vmcnt(18)" ::: "memory");   // this wave's A-side DMA landed (18 weight loads may fly)
+      stamp(1, false);
+      if (wave == NTC / 64 - 1 && a.stamps && lane == 0) a.stamps[w * 16 + 10] = __builtin_amdgcn_s_memrealtime();
+    }
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the gate / x columns (and the slice) landed
+    stamp(11, true);
   }
-  if (ctl && owner && lane < R) {   // x and adaLN gate of this workgroup's down columns
-    const bf16* xp = hl_opaque(a.x);
-    const bf16* mp = hl_opaque(a.mod);
-    *(bf16x8*)(gate_s + lane * 8) = hl_ld(mp + (long long)lane * a.ldmod + a.gate_off + col0);
-    *(bf16x8*)(xraw_s + lane * 8) = hl_ld(xp + (long long)lane * a.ldx + col0);
-  }
+  if (a.pre) {
+    // the distributed transform: owner rows' inverse RMS from the 192 partials
+    // (fixed order: 4 lanes per row, 48 partials each, then pairwise), its 8
+    // columns modulated (xform<XF_NORM>'s rounding points) and written through
+    if (ctl && owner) {
+      const int m = lane >> 2, q = lane & 3;
+      const float* ps = (const float*)sh_s + m * NOWN + q * (NOWN / 4);
+      float ss = 0.f;
+      for (int i = 0; i < NOWN / 4; ++i) ss += ps[i];
+      ss += __shfl_xor(ss, 1);
+      ss += __shfl_xor(ss, 2);
+      const float inv = rsqrtf(ss / (float)H + a.eps);
+      const float invm = __shfl(inv, 4 * (lane & 15));
+      if (lane < R) {
+        const bf16x8 xv = *(const bf16x8*)(xraw_s + lane * 8), wv = *(const bf16x8*)nw_s;
+        const bf16x8 scv = *(const bf16x8*)(sc_s + lane * 8), shv = *(const bf16x8*)(sc_s + RMAX * 8 + lane * 8);
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float t = rb(bf(xv[j]) * invm);
+          t = rb(t * bf(wv[j]));
+          t = rb(rb(t * rb(1.0f + bf(scv[j]))) + bf(shv[j]));
+          o[j] = tobf(t);
+        }
+        bf16* dst = hl_opaque(a.xt) + (long long)lane * H + col0;
+        MemWT::st8(dst, __builtin_shufflevector(o, o, 0, 1, 2, 3));
+        MemWT::st8(dst + 4, __builtin_shufflevector(o, o, 4, 5, 6, 7));
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (ctl && lane == 0) ok_s[1] = hl_grid_wait_gen(a.sync, 12, g0, 1, w, a.err) ? 1u : 0u;
+    __syncthreads();
+    stamp(2, true);
+    if (!ok_s[1]) return;
+    if (!ctl) {   // the transformed rows (rows >= R stay unset: their MFMA rows are never read)
+      const bf16* xp = hl_opaque((const bf16*)a.xt);
+      for (int b = wave; b < R * NCH / 64; b += NTC / 64) hl_dma16<true>(xs + (b / (NCH / 64)) * XST + (b % (NCH / 64)) * 512, xp + (b * 64 + lane) * 8);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    stamp(3, true);
+  } else {
   __syncthreads();
   for (int m = wave; m < R; m += NT / 64) {   // inverse RMS in k_rmsnorm's order
     const int ln = hl_vopaque(lane);
     float ss = 0.f;
     for (int c = ln; c < NCH; c += 64) {
-      const bf16x8 v = *(const bf16x8*)(xs + m * H + c * 8);
+      const bf16x8 v = *(const bf16x8*)(xs + m * XST + c * 8);
 #pragma unroll
       for (int j = 0; j < 8; ++j) ss += bf(v[j]) * bf(v[j]);
     }
     ss = wave_sum(ss);
     if (ln == 0) inv_s[m] = rsqrtf(ss / (float)H + a.eps);
   }
+  if (wave == 0 && a.stamps && lane == 0) a.stamps[w * 16 + 12] = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
+  stamp(2, true);
   for (int e = hl_vopaque((int)threadIdx.x); e < RMAX * NCH; e += NT) {   // xform<XF_NORM>, in place; rows >= R zero
     const int m = e / NCH, c = e - m * NCH;
     bf16x8 o = zero8;
     if (m < R) {
-      const bf16x8 xv = *(const bf16x8*)(xs + e * 8), wv = *(const bf16x8*)(nw_s + c * 8);
+      const bf16x8 xv = *(const bf16x8*)(xs + m * XST + c * 8), wv = *(const bf16x8*)(nw_s + c * 8);
       const bf16x8 shv = *(const bf16x8*)(sh_s + e * 8), scv = *(const bf16x8*)(sc_s + e * 8);
       const float inv = inv_s[m];
 #pragma unroll
@@ -146,9 +238,12 @@ __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
         o[j] = tobf(t);
       }
     }
-    *(bf16x8*)(xs + e * 8) = o;
+    *(bf16x8*)(xs + m * XST + c * 8) = o;
   }
+  if (wave == 0 && a.stamps && lane == 0) a.stamps[w * 16 + 13] = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
+  stamp(3, true);
+  }
   if (!ctl) {   // gate|up: D[row][tile row] over this wave's 6 k-blocks, per tile
     const int ln = hl_vopaque(lane);
     f32x4 acc[3];
@@ -157,24 +252,17 @@ __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
 #pragma unroll
     for (int kk = 0; kk < KPW1; ++kk) {
       const int kc = wave * KPW1 + kk;
-      const bf16x8 av = *(const bf16x8*)(xs + (ln & 15) * H + kc * 32 + 8 * (ln >> 4));
+      const bf16x8 av = *(const bf16x8*)(xs + (ln & 15) * XST + kc * 32 + 8 * (ln >> 4));
 #pragma unroll
       for (int j = 0; j < 3; ++j) acc[j] = mfma16(av, wb[j * KPW1 + kk], acc[j]);
     }
 #pragma unroll
     for (int j = 0; j < 3; ++j)
       if (j < nt) *(f32x4*)(red1 + (j * 8 + wave) * 256 + ln * 4) = acc[j];
-    if (owner) {   // this workgroup's half down tile into the registers (in flight through the wait)
-      // lanes of the other half of the tile feed only output columns this
-      // workgroup does not store: they read one line instead (unconditional loads)
-      const bf16* dw = hl_opaque(a.dn) + (long long)(d >> 1) * KC2 * 512 + ln * 8;
-      const bool mine = ((ln & 15) >> 3) == (d & 1);
-#pragma unroll
-      for (int kk = 0; kk < KPW2; ++kk)
-        wb[kk] = hl_ld(mine ? dw + (long long)(wave * KPW2 + kk) * 512 : dw - ln * 8);
-    }
+    if (owner && !a.late_down) load_down();   // (the earlier issue point: A/B)
   }
   __syncthreads();
+  stamp(4, true);
   for (int e = hl_vopaque((int)threadIdx.x); e < nt * RMAX * 8; e += NT) {   // SiLU(gate) * up (epi_silu8)
     const int j = e / (RMAX * 8), r = e - j * (RMAX * 8), m = r >> 3, c = r & 7;
     // D[m][n]: lane (n + 16 * (m >> 2)), element m & 3
@@ -187,6 +275,11 @@ __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
     su_s[e] = tobf(rb(silu_f(rb(g))) * rb(u));
   }
   __syncthreads();
+  stamp(5, true);
+  // the down weights, in flight through the hand-off (issued here rather than
+  // after the gate|up products: the 144 loads per CU took the waves ~1 us to
+  // issue, delaying SiLU * up and the arrival; DESIGN.md "B = 8 head layer")
+  if (!ctl && owner && a.late_down) load_down();
   if (ctl) {   // act[m][8 (t0 + j) .. + 8], written through
     for (int q = lane; q < nt * R * 2; q += 64) {
       const int j = q / (R * 2), r = q - j * R * 2, m = r >> 1, half = r & 1;
@@ -194,9 +287,10 @@ __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
                  *(const bf16x4*)(su_s + (j * RMAX + m) * 8 + 4 * half));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) ok_s[0] = hl_grid_wait_gen(a.sync, 12, g0, 1, w, a.err) ? 1u : 0u;
+    if (lane == 0) ok_s[0] = hl_grid_wait_gen(a.sync, 12, g0, a.pre ? 2 : 1, w, a.err) ? 1u : 0u;
   }
   __syncthreads();
+  stamp(6, true);
   if (!ok_s[0] || !owner) return;
   // ================= down: act rows -> 8 output columns, gated residual
   if (!ctl) {
@@ -206,46 +300,58 @@ __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
 #pragma unroll
       for (int i = 0; i < F / 8 / NTC; ++i) {   // 576 chunks per row: (m, i) covers chunks [512 i, 512 i + 512) ...
         const int c = i * NTC + t;
-        hl_dma16<true>(act_s + m * F + (i * NTC + 64 * wave) * 8, ap + (long long)m * F + c * 8);
+        hl_dma16<true>(act_s + m * AST + (i * NTC + 64 * wave) * 8, ap + (long long)m * F + c * 8);
       }
     if (F / 8 % NTC) {   // the 64 chunks left per row (576 = 512 + 64): wave 0
       for (int m = 0; m < R; ++m)
-        if (wave == 0) hl_dma16<true>(act_s + m * F + (F / 8 / NTC) * NTC * 8, ap + (long long)m * F + ((F / 8 / NTC) * NTC + t) * 8);
+        if (wave == 0) hl_dma16<true>(act_s + m * AST + (F / 8 / NTC) * NTC * 8, ap + (long long)m * F + ((F / 8 / NTC) * NTC + t) * 8);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  stamp(7, true);
   if (!ctl) {
     const int ln = hl_vopaque(lane);
     f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kk = 0; kk < KPW2; ++kk) {
+    auto a_blk = [&](int kk) {
       const int kc = wave * KPW2 + kk;
-      const bf16x8 av = (ln & 15) < R ? *(const bf16x8*)(act_s + (ln & 15) * F + kc * 32 + 8 * (ln >> 4)) : zero8;
-      acc = mfma16(av, wb[kk], acc);
-    }
+      return (ln & 15) < R ? *(const bf16x8*)(act_s + (ln & 15) * AST + kc * 32 + 8 * (ln >> 4)) : zero8;
+    };
+#pragma unroll
+    for (int kk = 0; kk < KPW2; ++kk) acc = mfma16(a_blk(kk), wb[kk], acc);
     *(f32x4*)(red2 + wave * 256 + ln * 4) = acc;
   }
   __syncthreads();
+  stamp(8, true);
   if (threadIdx.x < RMAX * 8) {   // epi_row8's EPI_RES with the adaLN gate; rows m < R
     const int m = threadIdx.x >> 3, c = threadIdx.x & 7;
+    float q = 0.f;
     if (m < R) {
       const int n = c + 8 * (d & 1);   // the tile row of column col0 + c
       float s = 0.f;
 #pragma unroll
       for (int v = 0; v < 8; ++v) s += red2[v * 256 + (n + 16 * (m >> 2)) * 4 + (m & 3)];
       const float y = rb(bf(gate_s[m * 8 + c]) * rb(s));
-      a.out[(long long)m * a.ldx + col0 + c] = tobf(bf(xraw_s[m * 8 + c]) + y);
+      const bf16 ov = tobf(bf(xraw_s[m * 8 + c]) + y);
+      a.out[(long long)m * a.ldx + col0 + c] = ov;
+      q = bf(ov) * bf(ov);
+    }
+    if (a.ssp) {   // the next launch's row partial sums of squares (8 columns, fixed pairwise order)
+      q += __shfl_xor(q, 1);
+      q += __shfl_xor(q, 2);
+      q += __shfl_xor(q, 4);
+      if (c == 0 && m < R) a.ssp[m * NOWN + d] = q;
     }
   }
+  stamp(9, false);
 }
 
 bool head_m16_fits(int H, int F, int R) {
   if (H != hm::H || F != hm::F || R <= 4 || R > hm::RMAX) return false;
   static const bool ok = [] {
+    const void* k = (const void*)k_head_m16;
     hipFuncAttributes fa{};
     int nb = 0, dev = 0, cus = 0;
-    const void* k = (const void*)k_head_m16;
     if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, hm::TOTAL) != hipSuccess ||
         hipFuncGetAttributes(&fa, k) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, hm::NT, hm::TOTAL) != hipSuccess ||

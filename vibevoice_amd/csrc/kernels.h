@@ -266,6 +266,17 @@ struct HeadM16Args {
   bf16* act;                // [16][F] SiLU(gate) * up rows (workspace, written through)
   unsigned* sync;           // the head's wait lines: shards 0-7, this kernel's generation at line 12
   unsigned* err;            // set to 1 when the grid wait gave up
+  unsigned long long* stamps;   // diagnostics (tools/head_m16_stamps.py): [G][16] s_memrealtime, or nullptr
+  int a_first;              // 1: every wave's A-side DMA issued before any weight load (a barrier between)
+  int late_down;            // 1 (default): the down weights issued after SiLU * up (during the hand-off); 0: after the gate|up products
+  // the distributed A side (DESIGN.md "B = 8 head layer"): every launch's epilogue
+  // writes per (row, owner) sums of squares of the rows it produced into ssp
+  // [16][192]; with pre = 1 a launch builds the transformed A side from them --
+  // each owner its 8 columns into xt [16][H], one grid wait, then every
+  // workgroup DMAs xt (48 KB) instead of the raw rows, shift and scale (144 KB)
+  float* ssp;               // nullptr: no partials written (and pre must be 0)
+  bf16* xt;
+  int pre;
 };
 bool head_m16_fits(int H, int F, int R);
 int launch_head_m16(const HeadM16Args& a, hipStream_t st);
