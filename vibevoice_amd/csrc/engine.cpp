@@ -856,7 +856,10 @@ int vv_finalize(vv_ctx* c) {
   CHK(c->cs_sync.ensure(12 * 128));
   HIPCHK(hipMemset(c->cs_sync.p, 0, 12 * 128));
   if (c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 16))
+  {
     CHK(c->m16_buf.ensure(16 * 192 * sizeof(float) + 16 * (size_t)k.hidden * sizeof(bf16)));
+    HIPCHK(hipMemset(c->m16_buf.p, 0, 16 * 192 * sizeof(float)));
+  }
   if (!c->hl_registered && (codec_stage_any(c->dec) || codec_stage_any(c->sem) ||
                             (c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 16)))) {
     c->hl_registered = true;
@@ -1528,13 +1531,6 @@ static int head_mods(vv_ctx* c, const HeadRun& h, int s, hipStream_t st) {
   return 0;
 }
 
-// x = noisy_images_proj(cat[x, x])  -- both halves read the same n latent rows
-static int head_noisy(vv_ctx* c, const HeadRun& h, const void* x_io, hipStream_t st) {
-  const int H = c->cfg.hidden, D = c->cfg.latent_dim;
-  return head_gemm(c, h, gemm_args(c, h.R, H, D, rowmap(x_io, D, h.n, 0), W(c, "head.noisy_w"), EPI_STORE, h.xh_m),
-                   st);
-}
-
 // 4 < 2n <= 16 rows: the layer as one launch (head_m16.hip) while the context is
 // the device's only registered one; 0 = two GEMV launches (A/B and tests)
 static std::atomic<int> g_head_m16{1};
@@ -1554,6 +1550,32 @@ extern "C" int vv_head_m16(int on) {
   g_head_m16 = on;   // A/B variants: bit 1 HeadM16Args::a_first, bit 2 the down weights' earlier issue point
   return 0;
 }
+// the one-launch layer applies (4 < R <= 16 rows, GEMV layout, unsharded, sole context)
+static bool m16_on(vv_ctx* c, int R) {
+  return g_head_m16 && !c->head_tp && c->head_gemv && c->m16_buf.p && head_m16_fits(c->cfg.hidden, c->cfg.head_ffn, R) &&
+         hl_sole(c->device);
+}
+
+// x = noisy_images_proj(cat[x, x])  -- both halves read the same n latent rows
+static int head_noisy(vv_ctx* c, const HeadRun& h, const void* x_io, hipStream_t st) {
+  const int H = c->cfg.hidden, D = c->cfg.latent_dim;
+  if (g_head_m16_pre && m16_on(c, h.R)) {   // + the row partials layer 0's distributed A side reads
+    HeadNoisyArgs a;
+    a.lat = (const bf16*)x_io;
+    a.w = (const bf16*)W(c, "head.noisy_w");
+    a.x = (bf16*)h.xh;
+    a.ssp = (float*)c->m16_buf.p;
+    a.n = h.n;
+    a.R = h.R;
+    a.D = D;
+    a.ldx = H;
+    KCHK(launch_head_noisy16(a, st));
+    return 0;
+  }
+  return head_gemm(c, h, gemm_args(c, h.R, H, D, rowmap(x_io, D, h.n, 0), W(c, "head.noisy_w"), EPI_STORE, h.xh_m),
+                   st);
+}
+
 extern "C" int vv_head_m16_active(vv_ctx* c, int n) {
   const vv_config& k = c->cfg;
   return c && c->finalized && g_head_m16 && !c->head_tp && c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 2 * n) &&
@@ -1603,7 +1625,7 @@ static int head_layer(vv_ctx* c, const HeadRun& h, int s, int l, hipStream_t st)
     KCHK(launch_head_ffn(a, st));
     return 0;
   }
-  if (g_head_m16 && !c->head_tp && c->head_gemv && c->m16_buf.p && head_m16_fits(H, F, h.R) && hl_sole(c->device)) {
+  if (m16_on(c, h.R)) {
     // 4 < 2n <= 16 rows: one launch with one grid-wide hand-off (head_m16.hip)
     HeadM16Args a;
     memset(&a, 0, sizeof(a));
@@ -1628,7 +1650,7 @@ static int head_layer(vv_ctx* c, const HeadRun& h, int s, int l, hipStream_t st)
     a.late_down = (g_head_m16.load() & 4) ? 0 : 1;
     a.ssp = (float*)c->m16_buf.p;
     a.xt = (bf16*)((char*)c->m16_buf.p + 16 * 192 * sizeof(float));
-    a.pre = l > 0 && g_head_m16_pre ? 1 : 0;   // layer 0's x comes from the noisy projection (no partials)
+    a.pre = g_head_m16_pre ? 1 : 0;   // (layer 0: the partials of k_head_noisy16)
     KCHK(launch_head_m16(a, st));
     return 0;
   }

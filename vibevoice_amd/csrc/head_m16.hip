@@ -346,6 +346,39 @@ __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
   stamp(9, false);
 }
 
+// One workgroup per owner d (columns [8d, 8d + 8)), thread (row m = t >> 3,
+// column c = t & 7): the K = 64 dot in k order (fp32 fmaf of exact bf16
+// products), rounded to bf16 at the store; the row's sum of squares over the 8
+// columns in k_head_m16's epilogue order.
+__global__ void __launch_bounds__(128) k_head_noisy16(HeadNoisyArgs a) {
+  using namespace hm;
+  const int d = blockIdx.x, t = threadIdx.x, m = t >> 3, c = t & 7;
+  const int j = 8 * d + c;
+  float q = 0.f;
+  if (m < a.R) {
+    const bf16* lr = a.lat + (long long)(m % a.n) * a.D;
+    float acc = 0.f;
+    for (int k = 0; k < a.D; k += 8) {
+      const bf16x8 wv = *(const bf16x8*)hl_packed(a.w, a.D, j, k), xv = *(const bf16x8*)(lr + k);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc = fmaf(bf(xv[e]), bf(wv[e]), acc);
+    }
+    const bf16 ov = tobf(acc);
+    a.x[(long long)m * a.ldx + j] = ov;
+    q = bf(ov) * bf(ov);
+  }
+  q += __shfl_xor(q, 1);
+  q += __shfl_xor(q, 2);
+  q += __shfl_xor(q, 4);
+  if (c == 0 && m < a.R) a.ssp[m * NOWN + d] = q;
+}
+
+int launch_head_noisy16(const HeadNoisyArgs& a, hipStream_t st) {
+  if (a.R <= 4 || a.R > hm::RMAX || a.D % 32 || a.ldx < hm::H) return 3;
+  hipLaunchKernelGGL(k_head_noisy16, dim3(hm::NOWN), dim3(128), 0, st, a);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
 bool head_m16_fits(int H, int F, int R) {
   if (H != hm::H || F != hm::F || R <= 4 || R > hm::RMAX) return false;
   static const bool ok = [] {

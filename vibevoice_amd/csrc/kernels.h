@@ -280,6 +280,17 @@ struct HeadM16Args {
 };
 bool head_m16_fits(int H, int F, int R);
 int launch_head_m16(const HeadM16Args& a, hipStream_t st);
+// x = noisy_images_proj(latents) at 4 < R <= 16 rows (rows m and m + n read
+// latent row m % n) with the row partial sums of squares k_head_m16's
+// distributed A side reads for layer 0 (head_m16.hip)
+struct HeadNoisyArgs {
+  const bf16* lat;   // [n][D] latents
+  const bf16* w;     // noisy_images_proj [H][D], MFMA-packed
+  bf16* x;           // [R][ldx] state rows
+  float* ssp;        // [16][192]
+  int n, R, D, ldx;
+};
+int launch_head_noisy16(const HeadNoisyArgs& a, hipStream_t st);
 
 // ---- the whole diffusion of a token in one persistent launch (head_loop.hip):
 // steps [s0, s1) of noisy -> L FFN layers -> final + CFG + DPM-Solver++ at 2n <= 4 rows
