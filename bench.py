@@ -314,9 +314,10 @@ def measure_head_loop(model, B, reps=4, iters=4):
 
 def measure_head_layers(model, B, reps=10, iters=4):
     """The diffusion head's FFN layers as the loop runs them at this batch
-    (vv_head_layers_replay: at 2B <= 4 rows the fused layer k_head_ffn, one
-    launch per layer -- the largest kernel of the B = 1 step by time; else the
-    gate|up + down GEMVs), S x head_layers of them per token.  Two graphs (1 and
+    (vv_head_layers_replay: k_head_m16, one launch per layer, in the default
+    GEMV layout -- the largest kernel of the B = 1 and B = 8 steps by time; the
+    fused layer k_head_ffn on the fused streams; else the gate|up + down
+    GEMVs), S x head_layers of them per token.  Two graphs (1 and
     1 + reps passes over the layers, each after the same condition / adaLN set-up)
     are replayed on one stream between HIP events; their difference over reps x
     head_layers is the time per layer.  Algorithmic bytes per layer: the layer's
@@ -369,11 +370,11 @@ def measure_head_layers(model, B, reps=10, iters=4):
     per_layer = (times[1] - times[0]) / (reps * L)
     alg = 3 * F * H * 2 + R * H * 2 * 2
     fused = R <= 4 and head_fused_layout(eng.w, B)
-    m16 = R > 4 and lib.vv_head_m16_active(eng.h, B) == 1
+    m16 = not fused and lib.vv_head_m16_active(eng.h, B) == 1
     kernel = (f"k_head_ffn<{R}, false> (fused head FFN layer: norm + adaLN, gate|up, SiLU*up, down, gated "
               f"residual in one launch)" if fused else
-              "k_head_m16 (one head FFN layer at 4 < 2n <= 16 rows in one launch: MFMA gate|up + SiLU*up, one "
-              "grid-wide hand-off, MFMA down + gated residual)" if m16 else
+              "k_head_m16 (one head FFN layer at 2n <= 16 rows in one launch: MFMA gate|up + SiLU*up, one "
+              "grid-wide hand-off, MFMA down + gated residual; above 4 rows the A side built distributed)" if m16 else
               "k_gemv1 gate|up + k_gemv/k_gemv1 down (one head FFN layer = two GEMV launches, timed together)")
     traffic = None
     pf = os.path.join(ROOT, "profiles", f"r05_pmc_head_r{R}.json")

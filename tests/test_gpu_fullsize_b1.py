@@ -1,12 +1,13 @@
 """Full-size parity of the SHIPPED B = 1 path (configs[1] / configs[0]'s
 workload) on the MI355X: a VibeVoice-1.5B model built as bench.py builds it
-(max_batch 1, so the head's FFN weights are bound in the fused stream layout)
-and alone on the device, so the loop runs the persistent diffusion head
-(k_head_loop, one launch per token) and the persistent codec stages
-(k_codec_stage / k_codec_stage_s) -- asserted, not assumed.  Teacher forcing
-against oracle/loop.py exactly as tests/test_gpu_fullsize.py (whose shared
-max_batch-8 model runs the GEMV head layout): per step and quantity, rel L2
-under the fixed bounds of tests/teacher.py and within 2.5x the bf16
+(max_batch 1: the head's FFN weights in the GEMV layout, weights.head_layout_for)
+and alone on the device, so the loop runs each diffusion-head FFN layer as one
+k_head_m16 launch (2 rows, whole A side) and the persistent codec stages
+(k_codec_stage / k_codec_stage_s) -- asserted, not assumed.  The persistent
+head loop on the fused streams (head_layout="fused") is the second case.
+Teacher forcing against oracle/loop.py exactly as tests/test_gpu_fullsize.py
+(whose shared max_batch-8 model runs two samples): per step and quantity, rel
+L2 under the fixed bounds of tests/teacher.py and within 2.5x the bf16
 reference's own deviation from fp32."""
 import gc
 import os
@@ -26,24 +27,28 @@ pytestmark = pytest.mark.gpu
 dev = "cuda"
 
 
-@pytest.fixture(scope="module")
-def m1():
+@pytest.fixture(scope="module", params=["default", "fused"])
+def m1(request):
     gc.collect()   # the persistent kernels run only for the device's sole registered context
     torch.set_num_threads(min(16, os.cpu_count() or 1))
     cfg = VibeVoiceConfig.builtin("1.5B")
     sd_dev = synthetic_state_dict(cfg, seed=5, device=dev, mode="test")
-    model = VibeVoiceForConditionalGenerationInference(cfg, sd_dev, dev, max_batch=1, max_ctx=1024)
+    kw = {} if request.param == "default" else {"head_layout": "fused"}
+    model = VibeVoiceForConditionalGenerationInference(cfg, sd_dev, dev, max_batch=1, max_ctx=1024, **kw)
     model.set_ddpm_inference_steps(STEPS)
-    yield cfg, model, _cpu_copy(sd_dev)
+    yield request.param, cfg, model, _cpu_copy(sd_dev)
     del model
     gc.collect()
 
 
 @pytest.mark.parametrize("steps", [10, 5])
 def test_teacher_forced_shipped_b1_path(m1, steps):
-    cfg, model, sd = m1
+    layout, cfg, model, sd = m1
     L = _lib.lib()
-    assert L.vv_head_loop_active(model.engine.h, 1) == 1, "the persistent head does not run"
+    if layout == "default":
+        assert L.vv_head_m16_active(model.engine.h, 1) == 1, "the one-launch head layer does not run"
+    else:
+        assert L.vv_head_loop_active(model.engine.h, 1) == 1, "the persistent head does not run"
     assert L.vv_codec_stage_active(model.engine.h) == 1, "the persistent codec stage does not run"
     inp = synthetic_inputs(batch=1, speakers=1, voice_seconds=3.0, text_tokens=64, seed=100)
     sched = [[D] * 6 + [E, S, D, D, X]]
@@ -58,4 +63,4 @@ def test_teacher_forced_shipped_b1_path(m1, steps):
         model.set_ddpm_inference_steps(STEPS)
     assert len(got["latents"]) == len(rec16["latents"]) == 8
     assert torch.equal(sess.result().sequences, seqs)
-    per_step_check(got, rec16, rec32, f"1.5B B=1 S={steps}, shipped path (persistent head + codec stages)")
+    per_step_check(got, rec16, rec32, f"1.5B B=1 S={steps}, {layout} head layout + codec stages")

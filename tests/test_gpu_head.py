@@ -280,9 +280,10 @@ def test_head_loop_only_for_the_devices_sole_context():
     a.close()
 
 
-@pytest.mark.parametrize("n", [3, 8])
+@pytest.mark.parametrize("n", [1, 3, 8])
 def test_head_m16_vs_oracle_and_gemv_pair(n):
-    """configs[2]'s head (B = 8: 2n = 16 rows; n = 3: 6 rows, padded): each FFN
+    """configs[2]'s head (B = 8: 2n = 16 rows; n = 3, 1: 6, 2 rows, padded -- a
+    GEMV-layout engine serving fewer samples): each FFN
     layer as ONE launch with one grid-wide hand-off (head_m16.hip: gate|up by
     MFMA over 2-3 tiles per workgroup, down over half a tile per two-tile
     workgroup) vs the oracle (rel < 2e-2, cosine > 0.999) and vs the

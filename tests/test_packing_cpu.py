@@ -47,12 +47,13 @@ def test_pack_emits_fused_streams_for_the_instantiated_shape():
 
 
 def test_one_head_layout_resident():
-    """an engine packs ONE copy of the head FFN -- the fused
-    streams where every call has 2n <= 4 rows (max_batch <= 2) at the shape the
-    fused kernels are built for, else the GEMV layout -- and "both" only when
-    asked (tests switching paths on one engine).  1.5B: 170 MB saved."""
+    """an engine packs ONE copy of the head FFN -- by default
+    the GEMV layout at every batch size (k_head_m16 runs 2 <= 2n <= 16 rows from
+    it, faster at B = 1 than the persistent loop on the fused streams), the
+    fused streams when asked -- and "both" only for tests switching paths on one
+    engine.  1.5B: 170 MB saved."""
     cfg = VibeVoiceConfig.builtin("1.5B")
-    assert head_layout_for(cfg, 1) == "fused" and head_layout_for(cfg, 2) == "fused"
+    assert head_layout_for(cfg, 1) == "gemv" and head_layout_for(cfg, 2) == "gemv"   # k_head_m16 at 2n <= 16
     assert head_layout_for(cfg, 3) == "gemv" and head_layout_for(cfg, 8) == "gemv"
     assert head_layout_for(cfg, 1, tp_size=2, tp_head=True) == "gemv"          # sharded width
     assert head_layout_for(VibeVoiceConfig.builtin("Large"), 1) == "gemv"

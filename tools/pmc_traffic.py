@@ -11,7 +11,7 @@ usage (GPU box):
   python tools/pmc_traffic.py collect-loop [R]  # the persistent diffusion head (k_head_loop<R>, S = 10)
                                               # -> profiles/r05_pmc_head_loop_r<R>.json
   python tools/pmc_traffic.py collect-head [R]  # the same for the diffusion head's FFN layer kernel
-                                              # (k_head_ffn<R> at R = 2n <= 4 rows, k_head_m16 above)
+                                              # (k_head_m16 at R = 2n rows)
                                               # -> profiles/r05_pmc_head_r<R>.json
 M = 2 (B = 1, one tile per workgroup) or 16 (B = 8: the balanced form, 4-5 tiles per workgroup).
 """
@@ -50,9 +50,9 @@ def run():
 
 
 def run_head():
-    """The diffusion head's FFN layers as the B = 1 loop runs them (the fused layer
-    k_head_ffn<R>, 40 launches per token at S = 10): vv_head_layers_replay on the
-    real 1.5B head, a warm-up pass then 24 more layers."""
+    """The diffusion head's FFN layers as the loop runs them (k_head_m16 in the
+    default GEMV layout, 40 launches per token at S = 10): vv_head_layers_replay
+    on the real 1.5B head, a warm-up pass then 24 more layers."""
     import torch
     from vibevoice_amd import _lib
     from vibevoice_amd.modeling_vibevoice_inference import VibeVoiceForConditionalGenerationInference
@@ -79,7 +79,8 @@ def run_head_loop():
     from vibevoice_amd.modeling_vibevoice_inference import VibeVoiceForConditionalGenerationInference
     n = M // 2
     model = VibeVoiceForConditionalGenerationInference.from_pretrained("synthetic:1.5B", device_map="cuda",
-                                                                        synthetic_seed=0, max_batch=n, max_ctx=256)
+                                                                        synthetic_seed=0, max_batch=n, max_ctx=256,
+                                                                        head_layout="fused")
     model.set_ddpm_inference_steps(10)
     model.engine.set_steps(10)
     cond = torch.randn(2 * n, 1536, device="cuda").bfloat16()
@@ -96,8 +97,8 @@ def run_head_loop():
 
 HEAD = len(sys.argv) > 1 and sys.argv[1].endswith("head")
 LOOP = len(sys.argv) > 1 and sys.argv[1].endswith("loop")
-if HEAD:   # 2n <= 4 rows: the fused layer; 4 < 2n <= 16: the one-launch layer of head_m16.hip
-    KERNEL, NL = (f"k_head_ffn<{M}, false>" if M <= 4 else "k_head_m16"), 4
+if HEAD:   # the one-launch layer of head_m16.hip (the default GEMV head layout, 2n <= 16 rows)
+    KERNEL, NL = "k_head_m16", 4
     N, K = 4608, 1536                     # F, H
 if LOOP:
     KERNEL, NL = f"k_head_loop<{M}, false>", 1

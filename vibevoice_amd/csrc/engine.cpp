@@ -1531,7 +1531,7 @@ static int head_mods(vv_ctx* c, const HeadRun& h, int s, hipStream_t st) {
   return 0;
 }
 
-// 4 < 2n <= 16 rows: the layer as one launch (head_m16.hip) while the context is
+// 2n <= 16 rows in the GEMV layout: the layer as one launch (head_m16.hip) while the context is
 // the device's only registered one; 0 = two GEMV launches (A/B and tests)
 static std::atomic<int> g_head_m16{1};
 // layers l >= 1 build the A side distributed (HeadM16Args::pre) from the previous
@@ -1550,16 +1550,22 @@ extern "C" int vv_head_m16(int on) {
   g_head_m16 = on;   // A/B variants: bit 1 HeadM16Args::a_first, bit 2 the down weights' earlier issue point
   return 0;
 }
-// the one-launch layer applies (4 < R <= 16 rows, GEMV layout, unsharded, sole context)
+// the one-launch layer applies (R <= 16 rows, GEMV layout, unsharded, sole context)
 static bool m16_on(vv_ctx* c, int R) {
   return g_head_m16 && !c->head_tp && c->head_gemv && c->m16_buf.p && head_m16_fits(c->cfg.hidden, c->cfg.head_ffn, R) &&
          hl_sole(c->device);
 }
 
+// ... with the A side built distributed (HeadM16Args::pre) above 4 rows: at 2 -
+// 4 rows the whole A side is 18 - 36 KB per CU and the extra grid wait costs more
+// than it saves (n = 1 head sample 659 us whole vs 688 us distributed,
+// tools/head_m16_stamps.py)
+static bool m16_pre(vv_ctx* c, int R) { return g_head_m16_pre && R > 4 && m16_on(c, R); }
+
 // x = noisy_images_proj(cat[x, x])  -- both halves read the same n latent rows
 static int head_noisy(vv_ctx* c, const HeadRun& h, const void* x_io, hipStream_t st) {
   const int H = c->cfg.hidden, D = c->cfg.latent_dim;
-  if (g_head_m16_pre && m16_on(c, h.R)) {   // + the row partials layer 0's distributed A side reads
+  if (m16_pre(c, h.R)) {   // + the row partials layer 0's distributed A side reads
     HeadNoisyArgs a;
     a.lat = (const bf16*)x_io;
     a.w = (const bf16*)W(c, "head.noisy_w");
@@ -1626,7 +1632,7 @@ static int head_layer(vv_ctx* c, const HeadRun& h, int s, int l, hipStream_t st)
     return 0;
   }
   if (m16_on(c, h.R)) {
-    // 4 < 2n <= 16 rows: one launch with one grid-wide hand-off (head_m16.hip)
+    // 2n <= 16 rows, GEMV layout: one launch with two grid-wide waits (head_m16.hip)
     HeadM16Args a;
     memset(&a, 0, sizeof(a));
     a.x = h.xh;
@@ -1650,7 +1656,7 @@ static int head_layer(vv_ctx* c, const HeadRun& h, int s, int l, hipStream_t st)
     a.late_down = (g_head_m16.load() & 4) ? 0 : 1;
     a.ssp = (float*)c->m16_buf.p;
     a.xt = (bf16*)((char*)c->m16_buf.p + 16 * 192 * sizeof(float));
-    a.pre = g_head_m16_pre ? 1 : 0;   // (layer 0: the partials of k_head_noisy16)
+    a.pre = m16_pre(c, h.R) ? 1 : 0;   // (layer 0: the partials of k_head_noisy16)
     KCHK(launch_head_m16(a, st));
     return 0;
   }

@@ -1,4 +1,4 @@
-// One diffusion-head FFN layer at 4 < 2n <= 16 rows (configs[2]: B = 8 -> 16
+// One diffusion-head FFN layer at 2 <= 2n <= 16 rows (configs[2]: B = 8 -> 16
 // rows) in ONE launch of 256 workgroups with one grid-wide hand-off, reading
 // the GEMV layout the engine binds at that batch (weights.py mfma_pack: gate|up
 // [2F][H] in 16-row tiles of 8 gate + 8 up rows, down [H][F]):
@@ -223,20 +223,19 @@ __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
   if (wave == 0 && a.stamps && lane == 0) a.stamps[w * 16 + 12] = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
   stamp(2, true);
-  for (int e = hl_vopaque((int)threadIdx.x); e < RMAX * NCH; e += NT) {   // xform<XF_NORM>, in place; rows >= R zero
+  // xform<XF_NORM>, in place, rows < R (rows >= R stay unset: their MFMA rows are never read)
+  for (int e = hl_vopaque((int)threadIdx.x); e < R * NCH; e += NT) {
     const int m = e / NCH, c = e - m * NCH;
-    bf16x8 o = zero8;
-    if (m < R) {
-      const bf16x8 xv = *(const bf16x8*)(xs + m * XST + c * 8), wv = *(const bf16x8*)(nw_s + c * 8);
-      const bf16x8 shv = *(const bf16x8*)(sh_s + e * 8), scv = *(const bf16x8*)(sc_s + e * 8);
-      const float inv = inv_s[m];
+    bf16x8 o;
+    const bf16x8 xv = *(const bf16x8*)(xs + m * XST + c * 8), wv = *(const bf16x8*)(nw_s + c * 8);
+    const bf16x8 shv = *(const bf16x8*)(sh_s + e * 8), scv = *(const bf16x8*)(sc_s + e * 8);
+    const float inv = inv_s[m];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float t = rb(bf(xv[j]) * inv);
-        t = rb(t * bf(wv[j]));
-        t = rb(rb(t * rb(1.0f + bf(scv[j]))) + bf(shv[j]));
-        o[j] = tobf(t);
-      }
+    for (int j = 0; j < 8; ++j) {
+      float t = rb(bf(xv[j]) * inv);
+      t = rb(t * bf(wv[j]));
+      t = rb(rb(t * rb(1.0f + bf(scv[j]))) + bf(shv[j]));
+      o[j] = tobf(t);
     }
     *(bf16x8*)(xs + m * XST + c * 8) = o;
   }
@@ -374,13 +373,13 @@ __global__ void __launch_bounds__(128) k_head_noisy16(HeadNoisyArgs a) {
 }
 
 int launch_head_noisy16(const HeadNoisyArgs& a, hipStream_t st) {
-  if (a.R <= 4 || a.R > hm::RMAX || a.D % 32 || a.ldx < hm::H) return 3;
+  if (a.R < 2 || a.R > hm::RMAX || a.D % 32 || a.ldx < hm::H) return 3;
   hipLaunchKernelGGL(k_head_noisy16, dim3(hm::NOWN), dim3(128), 0, st, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
 bool head_m16_fits(int H, int F, int R) {
-  if (H != hm::H || F != hm::F || R <= 4 || R > hm::RMAX) return false;
+  if (H != hm::H || F != hm::F || R < 2 || R > hm::RMAX) return false;
   static const bool ok = [] {
     const void* k = (const void*)k_head_m16;
     hipFuncAttributes fa{};

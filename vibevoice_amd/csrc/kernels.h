@@ -251,7 +251,7 @@ bool head_ffn_fits(int H, int F, int R);
 int head_ffn_grid();
 int launch_head_ffn(const HeadFfnArgs& a, hipStream_t st);
 
-// ---- one head FFN layer at 4 < 2n <= 16 rows in one launch (head_m16.hip), GEMV layout weights
+// ---- one head FFN layer at 2 <= 2n <= 16 rows in one launch (head_m16.hip), GEMV layout weights
 struct HeadM16Args {
   const bf16* x;            // [R][H] state rows (ld ldx), read before the grid wait
   bf16* out;                // [R][H] (ld ldx): x + gate * ffn (in place: out == x)
@@ -280,7 +280,7 @@ struct HeadM16Args {
 };
 bool head_m16_fits(int H, int F, int R);
 int launch_head_m16(const HeadM16Args& a, hipStream_t st);
-// x = noisy_images_proj(latents) at 4 < R <= 16 rows (rows m and m + n read
+// x = noisy_images_proj(latents) at 2 <= R <= 16 rows (rows m and m + n read
 // latent row m % n) with the row partial sums of squares k_head_m16's
 // distributed A side reads for layer 0 (head_m16.hip)
 struct HeadNoisyArgs {

@@ -173,13 +173,15 @@ class VibeVoiceTokenConstraintProcessor:
 
 class VibeVoiceForConditionalGenerationInference:
     def __init__(self, config: VibeVoiceConfig, state_dict, device="cuda", attn_implementation="hip",
-                 max_batch=8, max_ctx=8192, tp_group=None, tp_head=None):
+                 max_batch=8, max_ctx=8192, tp_group=None, tp_head=None, head_layout=None):
         """tp_group: a torch.distributed process group whose ranks (one per GPU)
         tensor-parallel-shard the Qwen2 backbone over RCCL; every
         rank then runs generate() on the same inputs (SPMD) and gets the same
         result.  None: the whole model on this GPU.  tp_head: shard the
         diffusion head's FFN over the group too (None: when its per-step
-        weights exceed the Infinity Cache, i.e. VibeVoice-Large)."""
+        weights exceed the Infinity Cache, i.e. VibeVoice-Large).  head_layout:
+        the head FFN weights' layout (None: weights.head_layout_for; "fused" for
+        the persistent head loop at max_batch <= 2)."""
         self.config = config
         self.attn_implementation = attn_implementation
         self.device = torch.device(device)
@@ -197,7 +199,7 @@ class VibeVoiceForConditionalGenerationInference:
         self.tp_head = head_tp_default(config, tp_size) if tp_head is None else bool(tp_head and tp_size > 1)
         self.engine = Engine(config, state_dict, self.device, max_batch=max_batch, tp_head=self.tp_head,
                              max_ctx=min(max_ctx, config.decoder_config.max_position_embeddings),
-                             tp_rank=tp_rank, tp_size=tp_size, tp_unique_id=uid)
+                             tp_rank=tp_rank, tp_size=tp_size, tp_unique_id=uid, head_layout=head_layout)
         self.ddpm_inference_steps = config.diffusion_head_config.ddpm_num_inference_steps
         self.model = _ModelView(self)
         self.use_graphs = True          # capture the steady-state loop body into hipGraphs

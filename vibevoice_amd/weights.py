@@ -293,14 +293,14 @@ def head_tp_default(cfg: VibeVoiceConfig, tp_size):
 
 def head_layout_for(cfg: VibeVoiceConfig, max_batch, tp_size=1, tp_head=False):
     """The diffusion head FFN's weight layout an engine of this capacity packs
-    (ONE copy resident): "fused" -- the fused layer's /
-    persistent head's streams (head.<l>.gu_rows / dn_rows) -- where every
-    diffusion call has 2n <= 4 rows (max_batch <= 2) and the shape is the one
-    those kernels are built for; else "gemv" (head.<l>.gu_w / down_w, MFMA
-    packed), which every batch size can run."""
-    hc = cfg.diffusion_head_config
-    F = int(hc.hidden_size * hc.head_ffn_ratio) // (tp_size if tp_head and tp_size > 1 else 1)
-    return "fused" if max_batch <= 2 and (hc.hidden_size, F) == HEAD_FFN_SHAPE else "gemv"
+    (ONE copy resident): "gemv" (head.<l>.gu_w / down_w, MFMA
+    packed) at every batch size.  It feeds the one-launch layer of head_m16.hip
+    (2 <= 2n <= 16 rows) and the GEMV pair beyond; at B = 1 that path measured
+    3.095 ms per step against 3.18-3.23 ms for the persistent head loop on the
+    "fused" streams (head.<l>.gu_rows / dn_rows; same-box interleaved A/B,
+    profiles/r05_ab_head_layout.txt), which stay available as head_layout="fused"
+    (or "both") for the 2n <= 4 kernels (k_head_ffn, k_head_loop)."""
+    return "gemv"
 
 
 def pack(sd, cfg: VibeVoiceConfig, device, with_acoustic_encoder=True, tp_rank=0, tp_size=1, tp_head=False,
