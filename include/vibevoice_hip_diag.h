@@ -146,6 +146,11 @@ int vv_head_m16_active(vv_ctx* ctx, int n);
 /* Diagnostic: per-workgroup s_memrealtime stamps of every head_m16 launch into
  * buf ([256][16] u64, overwritten per launch; NULL = off). */
 int vv_head_m16_stamps(void* buf);
+/* Diagnostic switch: the LM MLP block at decode with <= 2 rows as one launch
+ * (lm_ffn.hip; 1, default) or the gate|up + down GEMV pair (0); and whether
+ * the one-launch block applies to this context at ntok rows. */
+int vv_lm_ffn(int on);
+int vv_lm_ffn_active(vv_ctx* ctx, int ntok);
 /* Diagnostic switch: head layers l >= 1 at 4 < 2n <= 16 rows build their A side
  * distributed from the previous layer's row partials (1, default) or transform
  * it whole in every workgroup (0). */

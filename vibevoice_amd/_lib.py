@@ -81,6 +81,8 @@ EXPORTS = [
     ("vv_head_m16", I, [I]),
     ("vv_head_m16_active", I, [P, I]),
     ("vv_head_m16_stamps", I, [P]),
+    ("vv_lm_ffn", I, [I]),
+    ("vv_lm_ffn_active", I, [P, I]),
     ("vv_head_m16_pre", I, [I]),
     ("vv_attn_defer_max", I, [I]),
     ("vv_codec_stage_active", I, [P]),

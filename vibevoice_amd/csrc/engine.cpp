@@ -187,6 +187,7 @@ struct vv_ctx {
   DevBuf chain_sync, chain_slabs, chain_err, coef_dev;
   // fused head FFN layer (head_ffn.hip): partial-sum slabs, grid-wait words + error word
   DevBuf hf_slab, hf_sync;
+  DevBuf lf_sync;   // lm_ffn.hip's wait counters
   DevBuf m16_buf;   // head_m16.hip's distributed A side: row partial sums of squares [16][192] f32 + rows [16][H]
   DevBuf hl_lat;           // persistent head (head_loop.hip): [D][2] latent hand-off
   DevBuf cs_sync;          // persistent codec stage (codec_stage.hip): its wait counters
@@ -729,7 +730,7 @@ void vv_destroy(vv_ctx* c) {
   DevBuf* bufs[] = {&c->norm_ws, &c->kv_k, &c->kv_v, &c->lm_ws, &c->attn_part, &c->attn_cnt, &c->valid_ids, &c->splitk_ws, &c->splitk_cnt,
                     &c->temb, &c->tfreq_tmp, &c->head_ws, &c->codec_ws, &c->slot_scratch, &c->unit_sb,
                     &c->chain_sync, &c->chain_slabs, &c->chain_err, &c->coef_dev, &c->rope_tab, &c->zero_rows,
-                    &c->hf_slab, &c->hf_sync, &c->hl_lat, &c->cs_sync, &c->m16_buf};
+                    &c->hf_slab, &c->hf_sync, &c->hl_lat, &c->cs_sync, &c->m16_buf, &c->lf_sync};
   for (DevBuf* b : bufs) b->release();
   for (auto& kv : c->head_chain) kv.second.ops.release();
   ConvNet* nets[] = {&c->dec, &c->sem, &c->aenc, &c->senc};
@@ -855,13 +856,16 @@ int vv_finalize(vv_ctx* c) {
   // device's registry (hl_register)
   CHK(c->cs_sync.ensure(12 * 128));
   HIPCHK(hipMemset(c->cs_sync.p, 0, 12 * 128));
+  CHK(c->lf_sync.ensure(12 * 128));
+  HIPCHK(hipMemset(c->lf_sync.p, 0, 12 * 128));
   if (c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 16))
   {
     CHK(c->m16_buf.ensure(16 * 192 * sizeof(float) + 16 * (size_t)k.hidden * sizeof(bf16)));
     HIPCHK(hipMemset(c->m16_buf.p, 0, 16 * 192 * sizeof(float)));
   }
   if (!c->hl_registered && (codec_stage_any(c->dec) || codec_stage_any(c->sem) ||
-                            (c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 16)))) {
+                            (c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 16)) ||
+                            lm_ffn_fits(k.hidden, k.intermediate, 2))) {
     c->hl_registered = true;
     hl_register(c->device, +1);
   }
@@ -1196,11 +1200,47 @@ static int lm_attn_half(vv_ctx* c, LmPass& P, int l, hipStream_t st) {
   return 0;
 }
 
+// the LM MLP block in one launch (lm_ffn.hip) at decode with <= 2 rows, unsharded,
+// while the context is the device's only registered one; 0 = two GEMV launches
+static std::atomic<int> g_lm_ffn{1};
+extern "C" int vv_lm_ffn(int on) {
+  g_lm_ffn = on ? 1 : 0;
+  return 0;
+}
+static bool lm_ffn_on(vv_ctx* c, const LmPass& P) {
+  const vv_config& k = c->cfg;
+  return g_lm_ffn && c->lf_sync.p && !P.prefill && P.ntok <= 2 && c->tp_size == 1 && !c->comm && !P.hm.idx &&
+         P.hm.sT == k.hidden && P.hm.T >= P.ntok && lm_ffn_fits(k.hidden, k.intermediate, P.ntok) && hl_sole(c->device);
+}
+extern "C" int vv_lm_ffn_active(vv_ctx* c, int ntok) {
+  LmPass P;
+  P.ntok = ntok;
+  P.hm = rowmap(nullptr, c->cfg.hidden);
+  return c && c->finalized && lm_ffn_on(c, P) ? 1 : 0;
+}
+
 // post_attention_layernorm .. down_proj (+ residual on rank 0)
 static int lm_mlp_half(vv_ctx* c, LmPass& P, int l, hipStream_t st) {
   const vv_config& k = c->cfg;
   const int H = k.hidden, I = k.intermediate;
   const std::string p = "lm." + std::to_string(l);
+  if (lm_ffn_on(c, P)) {
+    LmFfnArgs a;
+    memset(&a, 0, sizeof(a));
+    a.x = (const bf16*)P.hm.base;
+    a.out = (bf16*)P.hm.base;
+    a.ldx = H;
+    a.R = P.ntok;
+    a.eps = k.rms_eps;
+    a.nw = W(c, p + ".post_norm");
+    a.gu = W(c, p + ".gu_w");
+    a.dn = W(c, p + ".down_w");
+    a.act = P.act;
+    a.sync = (unsigned*)c->lf_sync.p;
+    a.err = (unsigned*)c->hf_sync.p + 10 * 32;
+    KCHK(launch_lm_ffn(a, st));
+    return 0;
+  }
   // post_attention_layernorm fused into gate|up's A load
   GemmArgs g = gemm_args(c, P.ntok, 2 * I, H, P.hm, W(c, p + ".gu_w"), EPI_SILU_MUL, rowmap(P.act, I));
   g.xf = xf_norm(W(c, p + ".post_norm"), k.rms_eps);
@@ -1376,6 +1416,7 @@ int vv_sync_error(vv_ctx* c) {
     // flight (the device is synchronised) every counter restarts from 0
     if (v) HIPCHK(hipMemset(c->hf_sync.p, 0, 13 * 128));
     if (v && c->cs_sync.p) HIPCHK(hipMemset(c->cs_sync.p, 0, 12 * 128));
+    if (v && c->lf_sync.p) HIPCHK(hipMemset(c->lf_sync.p, 0, 12 * 128));
   }
   return v ? 1 : 0;
 }

@@ -292,6 +292,22 @@ struct HeadNoisyArgs {
 };
 int launch_head_noisy16(const HeadNoisyArgs& a, hipStream_t st);
 
+// ---- one LM MLP block at decode (R <= 2 rows) in one launch (lm_ffn.hip), GEMV layout weights
+struct LmFfnArgs {
+  const bf16* x;     // [R][ldx] hidden rows (read: the A side and the residual)
+  bf16* out;         // [R][ldx] (may alias x)
+  int ldx, R;
+  float eps;
+  const bf16* nw;    // post_attention_layernorm weight [H]
+  const bf16* gu;    // gate|up [2F][H], MFMA-packed (8 gate + 8 up rows per tile)
+  const bf16* dn;    // down [H][F], MFMA-packed
+  bf16* act;         // [R][F] SiLU(gate) * up, the hand-off rows
+  unsigned* sync;    // shards 0-7, generation at line 11
+  unsigned* err;     // set to 1 when the grid wait gave up
+};
+bool lm_ffn_fits(int H, int F, int R);
+int launch_lm_ffn(const LmFfnArgs& a, hipStream_t st);
+
 // ---- the whole diffusion of a token in one persistent launch (head_loop.hip):
 // steps [s0, s1) of noisy -> L FFN layers -> final + CFG + DPM-Solver++ at 2n <= 4 rows
 struct HeadLoopArgs {

@@ -1,0 +1,250 @@
+// One Qwen2 MLP block of the LM at decode (R = 2 rows: B = 1's positive and
+// negative streams) in ONE launch of 256 workgroups with one grid-wide hand-off,
+// reading the GEMV layout the LM binds (weights.py mfma_pack: gate|up [2I][H] in
+// 16-row tiles of 8 gate + 8 up rows, down [H][I]):
+//   x <- x + down(SiLU(gate_proj(a)) * up_proj(a)),  a = RMSNorm(x) * w
+// (post_attention_layernorm + Qwen2MLP + residual, modeling_vibevoice.py:169-209
+// via transformers' Qwen2DecoderLayer).
+//
+// Why (DESIGN.md "LM MLP in one launch"): as two GEMV launches the block took
+// 13.5 + 11.6 us per layer at B = 1 (the down GEMV reaches 192 CUs at 2.4 TB/s).
+// The decomposition is head_m16.hip's at I = 8,960:
+//   * gate|up: workgroup w owns tiles [35w/8, 35(w+1)/8) of the 1,120 (4 or 5);
+//     tiles 0-2 stream into registers, tiles 3-4 into LDS by DMA (non-temporal:
+//     read once per token); the 8 waves split K (6 of the 48 k-blocks each),
+//     MFMA 16x16x32 over the 2 rows (padded to 16), partial tiles summed in a
+//     fixed order; SiLU * up -> the act columns, written through;
+//   * one grid wait (the act rows gathered: 2 x 8,960 bf16);
+//   * down: the 192 workgroups w % 4 != 3 own 8 output columns (half a 16-row
+//     down tile over all 8,960 k, 140 KB: 18 k-blocks per wave in registers, 17
+//     by DMA into LDS, only this workgroup's 8 rows of each block); issued after
+//     SiLU * up so they stream through the hand-off; MFMA; residual.
+// Arithmetic: xform<XF_NORM>'s rounding points (norm weight, no modulation), the
+// residual as epi_row8's EPI_RES; the GEMM sums are fp32 MFMA sums in another
+// order than the GEMV kernels' (tests/test_gpu_lm.py: within bf16 of them).
+#include "persist_dev.h"
+
+namespace lf {
+constexpr int H = 1536, F = 8960, G = pk::G, RMAX = 2;
+constexpr int NTC = 512, NT = NTC + 64;   // 8 compute waves + the control wave
+constexpr int KC1 = H / 32, KC2 = F / 32; // 48 / 280 k-blocks
+constexpr int T1 = 2 * F / 16;            // 1,120 gate|up tiles
+constexpr int KPW1 = KC1 / 8, KPW2 = KC2 / 8;   // 6 / 35 k-blocks per compute wave
+constexpr int NREG2 = 18, NLDS2 = KPW2 - NREG2; // down k-blocks per wave in registers / in LDS (17)
+constexpr int SLOT2 = 18;                 // LDS down slots per wave (17 + 1 padding: DMA pairs)
+constexpr int NCH = H / 8;                // 192 chunks per row
+constexpr int XST = H + 8, AST = F + 8;   // padded LDS row strides (MFMA A reads)
+constexpr int XS = 0, XS_B = RMAX * XST * 2;
+constexpr int NW = XS + XS_B, NW_B = H * 2;
+constexpr int WT = NW + NW_B, WT_B = 2 * KC1 * 1024;        // gate|up tiles 3, 4 (96 KB); then the down blocks
+constexpr int RED1 = WT + WT_B, RED1_B = 5 * 8 * 256 * 4;    // gate|up partial tiles; then the act rows
+constexpr int SM = RED1 + RED1_B, SM_B = 256;                // ok, inv, SiLU*up values, x columns
+constexpr int TOTAL = SM + SM_B;
+constexpr int DN2 = WT, RED2 = WT + 8 * SLOT2 * 512;        // phase B: down blocks [8][18][256] bf16 | partials [8][256]
+static_assert(TOTAL <= 160 * 1024 && XS_B % 16 == 0 && NW % 16 == 0 && WT % 16 == 0, "lm ffn LDS");
+static_assert(RMAX * AST * 2 <= RED1_B && RED2 + 8 * 256 * 4 <= WT + WT_B, "lm ffn phase-B LDS");
+static_assert(4 * 4 + RMAX * 4 + 5 * RMAX * 8 * 2 + RMAX * 8 * 2 <= SM_B, "lm ffn small region");
+}  // namespace lf
+
+__global__ void __launch_bounds__(lf::NT) k_lm_ffn(LmFfnArgs a) {
+  using namespace lf;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16* xs = (bf16*)(smem + XS);
+  bf16* nw_s = (bf16*)(smem + NW);
+  bf16* wt_s = (bf16*)(smem + WT);
+  float* red1 = (float*)(smem + RED1);
+  bf16* act_s = (bf16*)(smem + RED1);          // phase B: [R][AST]
+  bf16* dn_s = (bf16*)(smem + DN2);            // phase B: [8 waves][18][256]
+  float* red2 = (float*)(smem + RED2);
+  unsigned* ok_s = (unsigned*)(smem + SM);
+  float* inv_s = (float*)(smem + SM + 16);     // [RMAX]
+  bf16* su_s = (bf16*)(smem + SM + 16 + RMAX * 4);   // [5][RMAX][8]
+  bf16* xraw_s = su_s + 5 * RMAX * 8;                 // [RMAX][8] this workgroup's columns of x
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool ctl = wave == NTC / 64;
+  const int w = blockIdx.x, lane = threadIdx.x & 63, R = a.R;
+  const int t0 = (w * 35) >> 3, nt = (((w + 1) * 35) >> 3) - t0;   // gate|up tiles (4 or 5)
+  const bool owner = (w & 3) != 3;
+  const int d = 3 * (w >> 2) + (w & 3);                             // down columns [8d, 8d + 8)
+  const int col0 = 8 * d;
+  unsigned g0 = 0;
+  if (ctl) __builtin_amdgcn_s_setprio(3);
+  if (ctl) g0 = __hip_atomic_load((hl_gu32*)(a.sync + 11 * pk::LINE), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~7u;
+
+  bf16x8 wb[NREG2];
+  const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+  if (ctl && owner && lane < R) hl_dma16<false>(xraw_s, hl_opaque(a.x) + (long long)lane * a.ldx + col0);
+  if (!ctl) {
+    const int ln = hl_vopaque(lane);
+    // the A side first (row `wave`, wave 0 also the norm weight), then the
+    // register tiles, then the LDS tiles: the norm waits only for the A side
+    if (wave < R)
+#pragma unroll
+      for (int i = 0; i < NCH / 64; ++i)
+        hl_dma16<false>(xs + wave * XST + i * 512, hl_opaque(a.x) + (long long)wave * a.ldx + (i * 64 + ln) * 8);
+    if (wave == 0)
+#pragma unroll
+      for (int i = 0; i < NCH / 64; ++i) hl_dma16<false>(nw_s + i * 512, hl_opaque(a.nw) + (i * 64 + ln) * 8);
+    const bf16* gw = hl_opaque(a.gu) + (long long)t0 * KC1 * 512 + ln * 8;
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int kk = 0; kk < KPW1; ++kk) wb[j * KPW1 + kk] = hl_ldnt(gw + ((long long)j * KC1 + wave * KPW1 + kk) * 512);
+    // tiles 3 and 4 (a four-tile workgroup re-reads tile 3 into the unused slot)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < KPW1; ++kk) {
+        const int tj = 3 + (j < nt - 3 ? j : 0);
+        hl_dma16<false, true>(wt_s + (j * KC1 + wave * KPW1 + kk) * 512, gw + ((long long)tj * KC1 + wave * KPW1 + kk) * 512);
+      }
+    asm volatile("s_waitcnt vmcnt(30)" ::: "memory");   // this wave's A-side DMA landed (18 loads + 12 DMAs may fly)
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the x columns landed
+  }
+  __syncthreads();
+  for (int m = wave; m < R; m += NT / 64) {   // inverse RMS in k_rmsnorm's order
+    const int ln = hl_vopaque(lane);
+    float ss = 0.f;
+    for (int c = ln; c < NCH; c += 64) {
+      const bf16x8 v = *(const bf16x8*)(xs + m * XST + c * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += bf(v[j]) * bf(v[j]);
+    }
+    ss = wave_sum(ss);
+    if (ln == 0) inv_s[m] = rsqrtf(ss / (float)H + a.eps);
+  }
+  __syncthreads();
+  for (int e = hl_vopaque((int)threadIdx.x); e < R * NCH; e += NT) {   // xform<XF_NORM> (norm weight only), in place
+    const int m = e / NCH, c = e - m * NCH;
+    const bf16x8 xv = *(const bf16x8*)(xs + m * XST + c * 8), wv = *(const bf16x8*)(nw_s + c * 8);
+    const float inv = inv_s[m];
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = tobf(rb(rb(bf(xv[j]) * inv) * bf(wv[j])));
+    *(bf16x8*)(xs + m * XST + c * 8) = o;
+  }
+  __syncthreads();
+  if (!ctl) {   // gate|up: D[row][tile row] over this wave's 6 k-blocks, per tile (rows >= R: never read)
+    const int ln = hl_vopaque(lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the LDS tiles (and the register tiles)
+    f32x4 acc[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < KPW1; ++kk) {
+      const int kc = wave * KPW1 + kk;
+      const bf16x8 av = *(const bf16x8*)(xs + (ln & 15) * XST + kc * 32 + 8 * (ln >> 4));
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc[j] = mfma16(av, wb[j * KPW1 + kk], acc[j]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[3 + j] = mfma16(av, *(const bf16x8*)(wt_s + (j * KC1 + kc) * 512 + ln * 8), acc[3 + j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+      if (j < nt) *(f32x4*)(red1 + (j * 8 + wave) * 256 + ln * 4) = acc[j];
+  }
+  __syncthreads();
+  for (int e = hl_vopaque((int)threadIdx.x); e < nt * R * 8; e += NT) {   // SiLU(gate) * up (epi_silu8)
+    const int j = e / (R * 8), r = e - j * (R * 8), m = r >> 3, c = r & 7;
+    float g = 0.f, u = 0.f;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      g += red1[(j * 8 + v) * 256 + (c + 16 * (m >> 2)) * 4 + (m & 3)];
+      u += red1[(j * 8 + v) * 256 + (c + 8 + 16 * (m >> 2)) * 4 + (m & 3)];
+    }
+    su_s[(j * RMAX + m) * 8 + c] = tobf(rb(silu_f(rb(g))) * rb(u));
+  }
+  __syncthreads();
+  if (!ctl && owner) {
+    // the down weights, in flight through the hand-off: k-blocks [35 wave,
+    // +18) into the registers (lanes of the other half tile read one line:
+    // unconditional loads), [+18, +35) by DMA into LDS slot wave, only this
+    // workgroup's 8 rows of each 1 KB block (512 B: lanes 0-31 block b, 32-63
+    // block b + 1; the last pair's second block is padding)
+    const int ln = hl_vopaque(lane);
+    const bf16* dw = hl_opaque(a.dn) + (long long)(d >> 1) * KC2 * 512;
+    const bool mine = ((ln & 15) >> 3) == (d & 1);
+#pragma unroll
+    for (int kk = 0; kk < NREG2; ++kk)
+      wb[kk] = hl_ldnt(mine ? dw + (long long)(wave * KPW2 + kk) * 512 + ln * 8 : dw);
+    const int p = ln & 31, L = 16 * (p >> 3) + 8 * (d & 1) + (p & 7);   // compact position p <- packed lane L
+#pragma unroll
+    for (int q = 0; q < SLOT2 / 2; ++q) {
+      int kb = NREG2 + 2 * q + (ln >> 5);
+      kb = kb < KPW2 ? kb : KPW2 - 1;
+      hl_dma16<false, true>(dn_s + (wave * SLOT2 + 2 * q) * 256, dw + (long long)(wave * KPW2 + kb) * 512 + L * 8);
+    }
+  }
+  if (ctl) {   // act[m][8 (t0 + j) .. + 8], written through
+    for (int q = lane; q < nt * R * 2; q += 64) {
+      const int j = q / (R * 2), r = q - j * R * 2, m = r >> 1, half = r & 1;
+      MemWT::st8(hl_opaque(a.act) + (long long)m * F + 8 * (t0 + j) + 4 * half,
+                 *(const bf16x4*)(su_s + (j * RMAX + m) * 8 + 4 * half));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) ok_s[0] = hl_grid_wait_gen(a.sync, 11, g0, 1, w, a.err) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!ok_s[0] || !owner) return;
+  // ================= down: act rows -> 8 output columns, residual
+  if (!ctl) {
+    const bf16* ap = hl_opaque(a.act);
+    const int ln = hl_vopaque(lane);
+    for (int q = wave; q < R * 18; q += NTC / 64) {   // row m, 64-chunk block i (1,120 chunks: 17.5 blocks)
+      const int m = q / 18, i = q - m * 18, c = i * 64 + ln;
+      if (c < F / 8) hl_dma16<true>(act_s + m * AST + i * 512, ap + (long long)m * F + c * 8);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the act rows, the down registers and the LDS blocks
+  }
+  __syncthreads();
+  if (!ctl) {
+    const int ln = hl_vopaque(lane);
+    const int p = (ln >> 4) * 8 + (ln & 7);   // this lane's compact position (the other half tile's lanes: garbage, never stored)
+    f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+    auto a_blk = [&](int kk) {
+      const int kc = wave * KPW2 + kk;
+      return (ln & 15) < R ? *(const bf16x8*)(act_s + (ln & 15) * AST + kc * 32 + 8 * (ln >> 4)) : zero8;
+    };
+#pragma unroll
+    for (int kk = 0; kk < NREG2; ++kk) acc = mfma16(a_blk(kk), wb[kk], acc);
+#pragma unroll
+    for (int kk = NREG2; kk < KPW2; ++kk)
+      acc = mfma16(a_blk(kk), *(const bf16x8*)(dn_s + (wave * SLOT2 + kk - NREG2) * 256 + p * 8), acc);
+    *(f32x4*)(red2 + wave * 256 + ln * 4) = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x < RMAX * 8) {   // epi_row8's EPI_RES (no bias, no gamma); rows m < R
+    const int m = threadIdx.x >> 3, c = threadIdx.x & 7;
+    if (m < R) {
+      const int n = c + 8 * (d & 1);   // the tile row of column col0 + c
+      float s = 0.f;
+#pragma unroll
+      for (int v = 0; v < 8; ++v) s += red2[v * 256 + (n + 16 * (m >> 2)) * 4 + (m & 3)];
+      a.out[(long long)m * a.ldx + col0 + c] = tobf(bf(xraw_s[m * 8 + c]) + rb(s));
+    }
+  }
+}
+
+bool lm_ffn_fits(int H, int F, int R) {
+  if (H != lf::H || F != lf::F || R < 1 || R > lf::RMAX) return false;
+  static const bool ok = [] {
+    hipFuncAttributes fa{};
+    int nb = 0, dev = 0, cus = 0;
+    const void* k = (const void*)k_lm_ffn;
+    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lf::TOTAL) != hipSuccess ||
+        hipFuncGetAttributes(&fa, k) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, lf::NT, lf::TOTAL) != hipSuccess ||
+        hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return false;
+    return fa.localSizeBytes == 0 && nb >= 1 && cus >= lf::G;
+  }();
+  return ok;
+}
+
+int launch_lm_ffn(const LmFfnArgs& a, hipStream_t st) {
+  if (!lm_ffn_fits(lf::H, lf::F, a.R) || a.ldx < lf::H) return 3;
+  hipLaunchKernelGGL(k_lm_ffn, dim3(lf::G), dim3(lf::NT), lf::TOTAL, st, a);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
