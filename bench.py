@@ -237,6 +237,72 @@ def measure_gemv(model, B, iters=6):
     return roof(kernel, shape, alg, avg_s, traffic, launches_per_token=nl)
 
 
+def measure_lm_ffn(model, B, reps=2, iters=4):
+    """The LM MLP block as the B = 1 loop runs it: ONE k_lm_ffn launch per layer
+    (lm_ffn.hip: post-norm + gate|up + SiLU*up + down + residual, one grid-wide
+    hand-off; decode with 2B <= 2 rows).  vv_lm_mlp_replay runs 1 or 1 + reps
+    passes over the 28 layers' blocks inside two captured graphs (rotating over
+    2.3 GB of weights: no cache reuse); the difference of their replay times
+    (HIP events on the replay stream) over reps x layers is the time per block.
+    Algorithmic bytes per block: gate|up + down weights + the rows in / out."""
+    from vibevoice_amd import _lib
+    eng = model.engine
+    lmc = model.config.decoder_config
+    H, I, nl = lmc.hidden_size, lmc.intermediate_size, lmc.num_hidden_layers
+    M = 2 * B
+    lib = _lib.lib()
+    if lib.vv_lm_ffn_active(eng.h, M) != 1:
+        return None
+    x = (torch.randn(M, H, device=model.device) * 0.5).bfloat16()
+    act = torch.empty(M, I, device=model.device, dtype=torch.bfloat16)
+    stream = torch.cuda.Stream(model.device)
+
+    def call(n):
+        return lib.vv_lm_mlp_replay(eng.h, M, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(act.data_ptr()), n,
+                                    ctypes.c_void_p(stream.cuda_stream))
+    with torch.cuda.stream(stream):
+        _lib.check(call(1), "lm_mlp_replay")
+    stream.synchronize()
+
+    def graph(n):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(stream):
+            g.capture_begin(capture_error_mode="thread_local")
+            try:
+                rc = call(n)
+            finally:
+                g.capture_end()
+        _lib.check(rc, "lm_mlp_replay")
+        return g
+    g1, gn = graph(1), graph(1 + reps)
+    times = []
+    with torch.cuda.stream(stream):
+        for g in (g1, gn):
+            g.replay()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(iters):
+                g.replay()
+            e1.record(stream)
+            e1.synchronize()
+            times.append(e0.elapsed_time(e1) / 1e3 / iters)
+    eng.check_sync()
+    per = (times[1] - times[0]) / (reps * nl)
+    alg = 3 * I * H * 2 + M * H * 2 * 2
+    shape = f"rows={M} H={H} I={I}"
+    traffic = None
+    pf = os.path.join(ROOT, "profiles", f"r05_pmc_lm_ffn_r{M}.json")
+    if os.path.exists(pf):
+        with open(pf) as f:
+            pmc = json.load(f)
+        if pmc.get("kernel") == "k_lm_ffn" and pmc.get("shape") == shape:
+            traffic = pmc["hbm_bytes_per_launch"]
+    return roof("k_lm_ffn (LM post-norm + gate|up + SiLU*up + down + residual in one launch, one grid-wide "
+                "hand-off; graph-replayed)", shape, alg, per, traffic, launches_per_token=nl,
+                note="graph-replayed MLP blocks of the 28 layers (vv_lm_mlp_replay), HIP events on the replay "
+                     "stream; weights read once per pass (2.3 GB rotation), non-temporal")
+
+
 def measure_head_loop(model, B, reps=4, iters=4):
     """The persistent diffusion head (head_loop.hip: every step of a token's
     diffusion -- noisy projection, 4 FFN layers, final layer, CFG + DPM update --
@@ -636,7 +702,12 @@ def main():
     bpt = bytes_per_token(wb, model.config, B, S, ctx_avg, (ctx0 + ctx1) / 2 - L)
     # `roofline`: the head FFN layer, the largest unit of the step by time at B = 1 and B = 8
     # (profiles/r04_steps_b1_headffn.txt, r04_steps_b8_v.txt); `roofline_lm`: the LM gate|up GEMV
-    roof_lm = measure_gemv(model, B)
+    try:   # the LM MLP block in one launch (B = 1), else the LM gate|up GEMV
+        roof_lm = measure_lm_ffn(model, B)
+    except Exception as e:   # noqa: BLE001
+        print(f"bench: LM MLP block roofline not measured: {e}", file=sys.stderr, flush=True)
+        roof_lm = None
+    roof_lm = roof_lm or measure_gemv(model, B)
     roof_head = None
     if world == 1 or T == 1:
         try:

@@ -151,6 +151,9 @@ int vv_head_m16_stamps(void* buf);
  * the one-launch block applies to this context at ntok rows. */
 int vv_lm_ffn(int on);
 int vv_lm_ffn_active(vv_ctx* ctx, int ntok);
+/* Diagnostic (bench.py): `reps` passes over the LM layers' MLP blocks alone on
+ * ntok decode rows (hidden [ntok][H] in place, act [ntok][I] scratch). */
+int vv_lm_mlp_replay(vv_ctx* ctx, int ntok, void* hidden, void* act, int reps, vv_stream stream);
 /* Diagnostic switch: head layers l >= 1 at 4 < 2n <= 16 rows build their A side
  * distributed from the previous layer's row partials (1, default) or transform
  * it whole in every workgroup (0). */

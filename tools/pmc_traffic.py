@@ -13,6 +13,8 @@ usage (GPU box):
   python tools/pmc_traffic.py collect-head [R]  # the same for the diffusion head's FFN layer kernel
                                               # (k_head_m16 at R = 2n rows)
                                               # -> profiles/r05_pmc_head_r<R>.json
+  python tools/pmc_traffic.py collect-lmffn 2  # the LM MLP block in one launch (k_lm_ffn, B = 1)
+                                              # -> profiles/r05_pmc_lm_ffn_r2.json
 M = 2 (B = 1, one tile per workgroup) or 16 (B = 8: the balanced form, 4-5 tiles per workgroup).
 """
 import csv
@@ -95,7 +97,32 @@ def run_head_loop():
     model.engine.check_sync()
 
 
+def run_lm_ffn():
+    """The LM MLP blocks as the B = 1 loop runs them (k_lm_ffn, 28 launches per LM
+    pass): vv_lm_mlp_replay on the 1.5B LM shapes, a warm-up pass then 3 more."""
+    import torch
+    from vibevoice_amd import _lib
+    from vibevoice_amd.modeling_vibevoice_inference import VibeVoiceForConditionalGenerationInference
+    n = M // 2
+    model = VibeVoiceForConditionalGenerationInference.from_pretrained("synthetic:1.5B", device_map="cuda",
+                                                                        synthetic_seed=0, max_batch=n, max_ctx=256)
+    L = _lib.lib()
+    assert L.vv_lm_ffn_active(model.engine.h, M) == 1
+    x = (torch.randn(M, 1536, device="cuda") * 0.5).bfloat16()
+    act = torch.empty(M, 8960, device="cuda", dtype=torch.bfloat16)
+    sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for reps in (1, 3):
+        _lib.check(L.vv_lm_mlp_replay(model.engine.h, M, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(act.data_ptr()),
+                                      reps, sp), "lm_mlp_replay")
+    torch.cuda.synchronize()
+    model.engine.check_sync()
+
+
 HEAD = len(sys.argv) > 1 and sys.argv[1].endswith("head")
+LMF = len(sys.argv) > 1 and sys.argv[1].endswith("lmffn")
+if LMF:
+    KERNEL, NL = "k_lm_ffn", 28
+    N, K = 8960, 1536                     # I, H
 LOOP = len(sys.argv) > 1 and sys.argv[1].endswith("loop")
 if HEAD:   # the one-launch layer of head_m16.hip (the default GEMV head layout, 2n <= 16 rows)
     KERNEL, NL = "k_head_m16", 4
@@ -117,12 +144,13 @@ def per_dispatch(path, counter):
 
 
 def collect():
-    out = os.path.join(ROOT, "gpurun_out", f"pmc_{'head_r' if HEAD else 'loop_r' if LOOP else 'm'}{M}")
+    out = os.path.join(ROOT, "gpurun_out", f"pmc_{'head_r' if HEAD else 'loop_r' if LOOP else 'lmffn_r' if LMF else 'm'}{M}")
     res = {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = os.path.join(out, counter.lower())
         cmd = ["rocprofv3", "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
-               sys.executable, os.path.abspath(__file__), "run-head" if HEAD else "run-loop" if LOOP else "run",
+               sys.executable, os.path.abspath(__file__),
+               "run-head" if HEAD else "run-loop" if LOOP else "run-lmffn" if LMF else "run",
                str(M)]
         subprocess.run(cmd, check=True, timeout=120)
         files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
@@ -138,6 +166,8 @@ def collect():
     write = res["WRITE_SIZE"] * 1024
     if HEAD:   # the layer's gate|up + down weights + its rows in / out
         alg, shape = 3 * N * K * 2 + M * K * 2 * 2, f"rows={M} H={K} F={N}"
+    elif LMF:  # the block's gate|up + down weights + its rows in / out
+        alg, shape = 3 * N * K * 2 + M * K * 2 * 2, f"rows={M} H={K} I={N}"
     elif LOOP:  # S = 10 steps x (4 x (gate|up + down + norm) + noisy + final) + each layer's rows in / out
         alg, shape = 10 * (4 * (3 * N * K * 2 + K * 2) + 2 * 64 * K * 2 + 4 * M * K * 2 * 2), f"rows={M} H={K} S=10"
     else:
@@ -149,7 +179,7 @@ def collect():
                    method="rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, tools/pmc_traffic.py run; "
                           "FETCH_SIZE x 2 (gfx950), KiB -> bytes")
     name = (f"r05_pmc_head_r{M}.json" if HEAD else f"r05_pmc_head_loop_r{M}.json" if LOOP else
-            f"r05_pmc_traffic_m{M}.json")
+            f"r05_pmc_lm_ffn_r{M}.json" if LMF else f"r05_pmc_traffic_m{M}.json")
     for path in (os.path.join(ROOT, "profiles", name), os.path.join(out, "pmc_traffic.json")):
         with open(path, "w") as f:
             json.dump(summary, f, indent=1)
@@ -158,4 +188,4 @@ def collect():
 
 if __name__ == "__main__":
     {"run": run, "collect": collect, "run-head": run_head, "collect-head": collect, "run-loop": run_head_loop,
-     "collect-loop": collect}[sys.argv[1]]()
+     "collect-loop": collect, "run-lmffn": run_lm_ffn, "collect-lmffn": collect}[sys.argv[1]]()

@@ -1259,6 +1259,22 @@ static int lm_mlp_half(vv_ctx* c, LmPass& P, int l, hipStream_t st) {
   return 0;
 }
 
+// Diagnostic (bench.py's roofline of the LM MLP block): `reps` passes over the
+// LM layers' MLP blocks alone on `ntok` decode rows (hidden [ntok][H], act
+// [ntok][I] scratch), as lm_mlp_half runs them (k_lm_ffn or the GEMV pair).
+extern "C" int vv_lm_mlp_replay(vv_ctx* c, int ntok, void* hidden, void* act, int reps, vv_stream vst) {
+  if (!c || !c->finalized || ntok < 1 || ntok > 2 * c->cfg.max_batch || !hidden || !act)
+    FAIL("vv_lm_mlp_replay: bad arguments");
+  LmPass P;
+  P.ntok = ntok;
+  P.h = (bf16*)hidden;
+  P.hm = rowmap(hidden, c->cfg.hidden);
+  P.act = (bf16*)act;
+  for (int r = 0; r < reps; ++r)
+    for (int l = 0; l < c->cfg.n_layers; ++l) CHK(lm_mlp_half(c, P, l, (hipStream_t)vst));
+  return 0;
+}
+
 // Benchmarks only (bench.py --tp: the collective's share of an LM pass):
 // skip the all-reduces of a communicator engine — the outputs are then wrong.
 static std::atomic<int> g_tp_null{0};
