@@ -9,9 +9,9 @@
 // Why (DESIGN.md "LM MLP in one launch"): as two GEMV launches the block took
 // 13.5 + 11.6 us per layer at B = 1 (the down GEMV reaches 192 CUs at 2.4 TB/s).
 // The decomposition is head_m16.hip's at I = 8,960:
-//   * gate|up: workgroup w owns tiles [35w/8, 35(w+1)/8) of the 1,120 (4 or 5);
-//     tiles 0-2 stream into registers, tiles 3-4 into LDS by DMA (non-temporal:
-//     read once per token); the 8 waves split K (6 of the 48 k-blocks each),
+//   * gate|up: the 192 down owners stream 4 of the 1,120 tiles each into
+//     registers, the other 64 workgroups 5 or 6 (the 5th and 6th into LDS by
+//     DMA), so no CU carries more than 332 KB (non-temporal: read once per token); the 8 waves split K (6 of the 48 k-blocks each),
 //     MFMA 16x16x32 over the 2 rows (padded to 16), partial tiles summed in a
 //     fixed order; SiLU * up -> the act columns, written through;
 //   * one grid wait (the act rows gathered: 2 x 8,960 bf16);
@@ -30,6 +30,7 @@ constexpr int NTC = 512, NT = NTC + 64;   // 8 compute waves + the control wave
 constexpr int KC1 = H / 32, KC2 = F / 32; // 48 / 280 k-blocks
 constexpr int T1 = 2 * F / 16;            // 1,120 gate|up tiles
 constexpr int KPW1 = KC1 / 8, KPW2 = KC2 / 8;   // 6 / 35 k-blocks per compute wave
+constexpr int NREG1 = 4;                  // gate|up tiles in registers (24 chunks per wave); up to 2 more in LDS
 constexpr int NREG2 = 18, NLDS2 = KPW2 - NREG2; // down k-blocks per wave in registers / in LDS (17)
 constexpr int SLOT2 = 18;                 // LDS down slots per wave (17 + 1 padding: DMA pairs)
 constexpr int NCH = H / 8;                // 192 chunks per row
@@ -37,13 +38,13 @@ constexpr int XST = H + 8, AST = F + 8;   // padded LDS row strides (MFMA A read
 constexpr int XS = 0, XS_B = RMAX * XST * 2;
 constexpr int NW = XS + XS_B, NW_B = H * 2;
 constexpr int WT = NW + NW_B, WT_B = 2 * KC1 * 1024;        // gate|up tiles 3, 4 (96 KB); then the down blocks
-constexpr int RED1 = WT + WT_B, RED1_B = 5 * 8 * 256 * 4;    // gate|up partial tiles; then the act rows
+constexpr int RED1 = WT + WT_B, RED1_B = 6 * 8 * 256 * 4;    // gate|up partial tiles; then the act rows
 constexpr int SM = RED1 + RED1_B, SM_B = 256;                // ok, inv, SiLU*up values, x columns
 constexpr int TOTAL = SM + SM_B;
 constexpr int DN2 = WT, RED2 = WT + 8 * SLOT2 * 512;        // phase B: down blocks [8][18][256] bf16 | partials [8][256]
 static_assert(TOTAL <= 160 * 1024 && XS_B % 16 == 0 && NW % 16 == 0 && WT % 16 == 0, "lm ffn LDS");
 static_assert(RMAX * AST * 2 <= RED1_B && RED2 + 8 * 256 * 4 <= WT + WT_B, "lm ffn phase-B LDS");
-static_assert(4 * 4 + RMAX * 4 + 5 * RMAX * 8 * 2 + RMAX * 8 * 2 <= SM_B, "lm ffn small region");
+static_assert(4 * 4 + RMAX * 4 + 6 * RMAX * 8 * 2 + RMAX * 8 * 2 <= SM_B, "lm ffn small region");
 }  // namespace lf
 
 __global__ void __launch_bounds__(lf::NT) k_lm_ffn(LmFfnArgs a) {
@@ -58,21 +59,27 @@ __global__ void __launch_bounds__(lf::NT) k_lm_ffn(LmFfnArgs a) {
   float* red2 = (float*)(smem + RED2);
   unsigned* ok_s = (unsigned*)(smem + SM);
   float* inv_s = (float*)(smem + SM + 16);     // [RMAX]
-  bf16* su_s = (bf16*)(smem + SM + 16 + RMAX * 4);   // [5][RMAX][8]
-  bf16* xraw_s = su_s + 5 * RMAX * 8;                 // [RMAX][8] this workgroup's columns of x
+  bf16* su_s = (bf16*)(smem + SM + 16 + RMAX * 4);   // [6][RMAX][8]
+  bf16* xraw_s = su_s + 6 * RMAX * 8;                 // [RMAX][8] this workgroup's columns of x
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool ctl = wave == NTC / 64;
   const int w = blockIdx.x, lane = threadIdx.x & 63, R = a.R;
-  const int t0 = (w * 35) >> 3, nt = (((w + 1) * 35) >> 3) - t0;   // gate|up tiles (4 or 5)
+  // the 192 down owners (w % 4 != 3) stream 4 gate|up tiles each (tiles [0, 768));
+  // the other 64 the remaining 352 (5 or 6 each): per CU 332 KB (owner: 4 tiles
+  // + 140 KB of down) or 240-288 KB, against 380 KB when owners took 5
   const bool owner = (w & 3) != 3;
   const int d = 3 * (w >> 2) + (w & 3);                             // down columns [8d, 8d + 8)
+  const int u = w >> 2;
+  const int t0 = owner ? 4 * d : 768 + ((352 * u) >> 6);
+  const int nt = owner ? 4 : 768 + ((352 * (u + 1)) >> 6) - t0;   // 4, or 5 / 6
+  const int nlds = nt - NREG1;                                      // tiles in LDS (0, 1, 2; uniform)
   const int col0 = 8 * d;
   unsigned g0 = 0;
   if (ctl) __builtin_amdgcn_s_setprio(3);
   if (ctl) g0 = __hip_atomic_load((hl_gu32*)(a.sync + 11 * pk::LINE), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~7u;
 
-  bf16x8 wb[NREG2];
+  bf16x8 wb[NREG1 * KPW1];
   const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
   if (ctl && owner && lane < R) hl_dma16<false>(xraw_s, hl_opaque(a.x) + (long long)lane * a.ldx + col0);
   if (!ctl) {
@@ -88,18 +95,19 @@ __global__ void __launch_bounds__(lf::NT) k_lm_ffn(LmFfnArgs a) {
       for (int i = 0; i < NCH / 64; ++i) hl_dma16<false>(nw_s + i * 512, hl_opaque(a.nw) + (i * 64 + ln) * 8);
     const bf16* gw = hl_opaque(a.gu) + (long long)t0 * KC1 * 512 + ln * 8;
 #pragma unroll
-    for (int j = 0; j < 3; ++j)
+    for (int j = 0; j < NREG1; ++j)
 #pragma unroll
       for (int kk = 0; kk < KPW1; ++kk) wb[j * KPW1 + kk] = hl_ldnt(gw + ((long long)j * KC1 + wave * KPW1 + kk) * 512);
-    // tiles 3 and 4 (a four-tile workgroup re-reads tile 3 into the unused slot)
+    // tiles 4 and 5 into LDS (uniform per workgroup: 0, 1 or 2 of them)
+    for (int j = 0; j < nlds; ++j)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int kk = 0; kk < KPW1; ++kk) {
-        const int tj = 3 + (j < nt - 3 ? j : 0);
-        hl_dma16<false, true>(wt_s + (j * KC1 + wave * KPW1 + kk) * 512, gw + ((long long)tj * KC1 + wave * KPW1 + kk) * 512);
-      }
-    asm volatile("s_waitcnt vmcnt(30)" ::: "memory");   // this wave's A-side DMA landed (18 loads + 12 DMAs may fly)
+      for (int kk = 0; kk < KPW1; ++kk)
+        hl_dma16<false, true>(wt_s + (j * KC1 + wave * KPW1 + kk) * 512,
+                              gw + ((long long)(NREG1 + j) * KC1 + wave * KPW1 + kk) * 512);
+    // this wave's A-side DMA landed (the 24 register loads + 6 nlds DMAs behind it may fly)
+    if (nlds == 0) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if (nlds == 1) asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the x columns landed
   }
@@ -129,20 +137,21 @@ __global__ void __launch_bounds__(lf::NT) k_lm_ffn(LmFfnArgs a) {
   if (!ctl) {   // gate|up: D[row][tile row] over this wave's 6 k-blocks, per tile (rows >= R: never read)
     const int ln = hl_vopaque(lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the LDS tiles (and the register tiles)
-    f32x4 acc[5];
+    f32x4 acc[6];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 6; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kk = 0; kk < KPW1; ++kk) {
       const int kc = wave * KPW1 + kk;
       const bf16x8 av = *(const bf16x8*)(xs + (ln & 15) * XST + kc * 32 + 8 * (ln >> 4));
 #pragma unroll
-      for (int j = 0; j < 3; ++j) acc[j] = mfma16(av, wb[j * KPW1 + kk], acc[j]);
+      for (int j = 0; j < NREG1; ++j) acc[j] = mfma16(av, wb[j * KPW1 + kk], acc[j]);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[3 + j] = mfma16(av, *(const bf16x8*)(wt_s + (j * KC1 + kc) * 512 + ln * 8), acc[3 + j]);
+      for (int j = 0; j < 2; ++j)   // (unfilled slots: products never stored)
+        acc[NREG1 + j] = mfma16(av, *(const bf16x8*)(wt_s + (j * KC1 + kc) * 512 + ln * 8), acc[NREG1 + j]);
     }
 #pragma unroll
-    for (int j = 0; j < 5; ++j)
+    for (int j = 0; j < 6; ++j)
       if (j < nt) *(f32x4*)(red1 + (j * 8 + wave) * 256 + ln * 4) = acc[j];
   }
   __syncthreads();
