@@ -35,6 +35,7 @@ sys.path.insert(0, ROOT)
 
 SR, HOP = 24000, 3200
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+IC_MEASURED_GBS = 8600.0       # Infinity-Cache-resident reads, measured (MI355X_MICROARCH.md "Indexed rows")
 METRIC = "audio-sec/wall-sec (RTF) + acoustic tokens/sec, VibeVoice-1.5B at 1/2/4/8 GPU"
 
 
@@ -102,26 +103,17 @@ def tp_groups(world, rank, T):
 HEAD_SC = 16   # engine.cpp: the adaLN modulations of up to 16 diffusion steps come from ONE batched GEMM
 
 
-def head_fused_layout(w, B):
-    """True when the loop's head FFN layers at this batch read the fused layer's
-    weight streams (head.<l>.gu_rows / dn_rows: 2B <= 4 rows and the streams
-    packed), else the GEMV layout (head.<l>.gu_w / down_w).  Each role is
-    counted once, in the layout the loop actually reads."""
-    return 2 * B <= 4 and "head.0.gu_rows" in w
-
-
 def weight_bytes(w, B=1, S=10):
     """Bytes of the packed device weights the loop reads, by role (SURVEY.md §8d
     conventions).  head_step: read by EVERY diffusion step (noisy / final
     projections, the per-layer norms and FFN weights in the layout the loop
-    reads at this batch); head_token: read once per token (cond_proj, and the
+    reads); head_token: read once per token (cond_proj, and the
     stacked adaLN matrix once per HEAD_SC steps -- its GEMM covers the steps'
     modulations at once)."""
     def sz(pred):
         return sum(t.numel() * t.element_size() for k, t in w.items() if pred(k))
     H = w["lm.norm"].numel()
-    fused = head_fused_layout(w, B)
-    ffn = (".gu_rows", ".dn_rows") if fused else (".gu_w", ".down_w")
+    ffn = (".gu_w", ".down_w")
 
     def per_step(k):
         if k in ("head.noisy_w", "head.final_w"):
@@ -135,7 +127,7 @@ def weight_bytes(w, B=1, S=10):
         head_token=sz(lambda k: k == "head.cond_w") + -(-S // HEAD_SC) * sz(lambda k: k == "head.ada_w"),
         codec=sz(lambda k: k.startswith("dec.") or k.startswith("sem.")),
         conn=sz(lambda k: k.startswith("conn.")),
-        head_layout="fused layer streams (gu_rows / dn_rows)" if fused else "GEMV layout (gu_w / down_w)",
+        head_layout="GEMV layout (gu_w / down_w)",
     )
 
 
@@ -303,87 +295,10 @@ def measure_lm_ffn(model, B, reps=2, iters=4):
                      "stream; weights read once per pass (2.3 GB rotation), non-temporal")
 
 
-def measure_head_loop(model, B, reps=4, iters=4):
-    """The persistent diffusion head (head_loop.hip: every step of a token's
-    diffusion -- noisy projection, 4 FFN layers, final layer, CFG + DPM update --
-    in ONE launch at 2B <= 4 rows; the largest kernel of the B = 1 step).
-    vv_head_loop_replay sets up the condition rows and modulations, then 1 or
-    1 + reps launches inside two captured graphs; the difference of their replay
-    times (HIP events on the replay stream) over reps is the time per launch.
-    Algorithmic bytes per launch: S x the per-step head weights (bench.py
-    weight_bytes head_step, read once per step) + each FFN layer's rows in / out."""
-    from vibevoice_amd import _lib
-    eng = model.engine
-    hc = model.config.diffusion_head_config
-    H, L = hc.hidden_size, hc.head_layers
-    S = min(model.ddpm_inference_steps, HEAD_SC)
-    R = 2 * B
-    if eng.tp_head or not head_fused_layout(eng.w, B):
-        return None
-    cond = torch.randn(R, H, device=model.device).bfloat16()
-    x = torch.randn(B, hc.latent_size, device=model.device).bfloat16()
-    lib = _lib.lib()
-    stream = torch.cuda.Stream(model.device)
-
-    def call(n_rep):
-        return lib.vv_head_loop_replay(eng.h, B, ctypes.c_void_p(cond.data_ptr()),
-                                       ctypes.c_void_p(cond[B:].data_ptr()), ctypes.c_void_p(x.data_ptr()), 1.3,
-                                       n_rep, ctypes.c_void_p(stream.cuda_stream))
-
-    with torch.cuda.stream(stream):   # eager warm-up (plans, workspaces); "not applicable" -> None
-        if call(1) != 0:
-            return None
-    stream.synchronize()
-
-    def graph(n_rep):
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.stream(stream):
-            g.capture_begin(capture_error_mode="thread_local")
-            try:
-                rc = call(n_rep)
-            finally:
-                g.capture_end()
-        _lib.check(rc, "head_loop_replay")
-        return g
-    g1, gn = graph(1), graph(1 + reps)
-    times = []
-    with torch.cuda.stream(stream):   # replays launch on the current stream: time them there
-        for g in (g1, gn):
-            g.replay()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            for _ in range(iters):
-                g.replay()
-            e1.record(stream)
-            e1.synchronize()
-            times.append(e0.elapsed_time(e1) / 1e3 / iters)
-    eng.check_sync()
-    per_launch = (times[1] - times[0]) / reps
-    wb = weight_bytes(eng.w, B, S)
-    alg = S * (wb["head_step"] + L * R * H * 2 * 2)
-    kernel = f"k_head_loop<{R}, false>"
-    traffic = None
-    pf = os.path.join(ROOT, "profiles", f"r05_pmc_head_loop_r{R}.json")
-    if os.path.exists(pf):
-        with open(pf) as f:
-            pmc = json.load(f)
-        if pmc.get("kernel") == kernel and pmc.get("shape") == f"rows={R} H={H} S={S}":
-            traffic = pmc["hbm_bytes_per_launch"]
-    return roof(kernel + " (persistent diffusion head: S x [noisy, 4 FFN layers, final + CFG + DPM] in one launch)",
-                f"rows={R} H={H} S={S}", alg, per_launch, traffic, launches_per_token=-(-model.ddpm_inference_steps //
-                                                                                      HEAD_SC),
-                per_step_us=round(per_launch / S * 1e6, 2),
-                note="graph-replayed persistent launches (vv_head_loop_replay), HIP events on the replay stream; "
-                     "head weights kept in the Infinity Cache across the S steps (default cache policy), the 8 TB/s "
-                     "HBM figure is the stated peak")
-
-
 def measure_head_layers(model, B, reps=10, iters=4):
     """The diffusion head's FFN layers as the loop runs them at this batch
-    (vv_head_layers_replay: k_head_m16, one launch per layer, in the default
-    GEMV layout -- the largest kernel of the B = 1 and B = 8 steps by time; the
-    fused layer k_head_ffn on the fused streams; else the gate|up + down
-    GEMVs), S x head_layers of them per token.  Two graphs (1 and
+    (vv_head_layers_replay: k_head_m16, one launch per layer at 2 <= 2n <= 16
+    rows; else the gate|up + down GEMVs), S x head_layers of them per token.  Two graphs (1 and
     1 + reps passes over the layers, each after the same condition / adaLN set-up)
     are replayed on one stream between HIP events; their difference over reps x
     head_layers is the time per layer.  Algorithmic bytes per layer: the layer's
@@ -435,11 +350,8 @@ def measure_head_layers(model, B, reps=10, iters=4):
     eng.check_sync()
     per_layer = (times[1] - times[0]) / (reps * L)
     alg = 3 * F * H * 2 + R * H * 2 * 2
-    fused = R <= 4 and head_fused_layout(eng.w, B)
-    m16 = not fused and lib.vv_head_m16_active(eng.h, B) == 1
-    kernel = (f"k_head_ffn<{R}, false> (fused head FFN layer: norm + adaLN, gate|up, SiLU*up, down, gated "
-              f"residual in one launch)" if fused else
-              "k_head_m16 (one head FFN layer at 2n <= 16 rows in one launch: MFMA gate|up + SiLU*up, one "
+    m16 = lib.vv_head_m16_active(eng.h, B) == 1
+    kernel = ("k_head_m16 (one head FFN layer at 2n <= 16 rows in one launch: MFMA gate|up + SiLU*up, one "
               "grid-wide hand-off, MFMA down + gated residual; above 4 rows the A side built distributed)" if m16 else
               "k_gemv1 gate|up + k_gemv/k_gemv1 down (one head FFN layer = two GEMV launches, timed together)")
     traffic = None
@@ -452,8 +364,51 @@ def measure_head_layers(model, B, reps=10, iters=4):
     return roof(kernel, f"rows={R} H={H} F={F}", alg, per_layer, traffic,
                 launches_per_token=int(model.ddpm_inference_steps * L),
                 note="graph-replayed head FFN layers (vv_head_layers_replay), HIP events on the replay stream; "
-                     "weights kept in the Infinity Cache across the S steps (default cache policy), the 8 TB/s "
-                     "HBM figure is the stated peak")
+                     "the head's 170 MB are re-read by each of the S steps and served from the 256 MB Infinity "
+                     "Cache (default cache policy), so the bound is the Infinity-Cache read rate, not HBM",
+                ic_roof=dict(peak=IC_MEASURED_GBS, unit="GB/s",
+                             frac=round(alg / per_layer / 1e9 / IC_MEASURED_GBS, 4) if per_layer > 0 else None,
+                             source="MI355X_MICROARCH.md 'Indexed rows: gather into LDS': a 38 MB "
+                                    "Infinity-Cache-resident table read at 8.6 TB/s chip-wide (a measured "
+                                    "rate; the guide states no spec peak for the Infinity Cache)"))
+
+
+def us_per_step(r):
+    """A roofline candidate's time per loop step: avg x launches per step."""
+    if not r or "error" in r or not r.get("avg_us"):
+        return -1.0
+    return r["avg_us"] * r.get("launches_per_token", 1)
+
+
+def pick_roofline(*cands):
+    """(roofline, roofline_2): the candidates ordered by time per step, largest
+    first -- the dominant kernel of the step is the line's `roofline`."""
+    c = sorted([r for r in cands if r is not None], key=us_per_step, reverse=True)
+    return (c[0] if c else None), (c[1] if len(c) > 1 else None)
+
+
+# the committed step profile of this round (tools/prof_step.sh: rocprofv3 --kernel-trace --stats over
+# graph-replayed loop steps) per batch: its per-kernel averages are the in-loop figures
+STEP_PROFILE = {1: "r06_kernel_stats_b1.csv", 8: "r06_kernel_stats_b8.csv"}
+
+
+def in_loop_average(r, B):
+    """Beside the isolated replay: the kernel's average duration in the loop
+    itself, from the committed rocprofv3 step profile (if one exists for this
+    batch), and the roofline fraction at that average."""
+    name = STEP_PROFILE.get(B)
+    path = os.path.join(ROOT, "profiles", name) if name else None
+    if not path or not os.path.exists(path):
+        return
+    import csv
+    kern = r["kernel"].split(" (")[0]
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row.get("Name", "").split("(")[0].strip() == kern.split("(")[0].strip():
+                avg_us = float(row["AverageNs"]) / 1e3
+                r["in_loop"] = dict(avg_us=round(avg_us, 2), source=f"profiles/{name}",
+                                    frac=round(r["alg_bytes_per_launch"] / (avg_us * 1e-6) / 1e9 / r["peak"], 4))
+                return
 
 
 # ------------------------------------------------------------------ TP collective share
@@ -535,7 +490,7 @@ def lm_pass_maker(model, sess):
 
 
 # ------------------------------------------------------------------ CPU baseline (oracle)
-def cpu_baseline(cfg, tokens, S):
+def cpu_baseline(cfg, tokens, S, model_name="1.5B"):
     """The oracle's fp32 eager restatement of the reference loop (the
     reference's own CPU path runs fp32 + eager/sdpa attention,
     demo/inference_from_file.py:268) on the host cores: text prompt, forced
@@ -590,7 +545,7 @@ def cpu_baseline(cfg, tokens, S):
     stage_ms["other"] = round(per * 1e3 - sum(stage_ms.values()), 2)
     return dict(value=round(tps * HOP / SR, 4), unit="audio-sec/wall-sec", tokens_per_s=round(tps, 3),
                 cores=torch.get_num_threads(), kind="port", stage_ms_per_token=stage_ms,
-                sample=f"oracle/loop.py fp32 eager on CPU, VibeVoice-1.5B shapes (seeded random weights), "
+                sample=f"oracle/loop.py fp32 eager on CPU, VibeVoice-{model_name} shapes (seeded random weights), "
                        f"B=1, S={S}, {tokens} timed diffusion tokens after a 1-token run (difference of two runs)")
 
 
@@ -700,8 +655,9 @@ def main():
     wb = weight_bytes(model.engine.w, B, S)
     ctx_avg = (ctx0 + ctx1) / 2
     bpt = bytes_per_token(wb, model.config, B, S, ctx_avg, (ctx0 + ctx1) / 2 - L)
-    # `roofline`: the head FFN layer, the largest unit of the step by time at B = 1 and B = 8
-    # (profiles/r04_steps_b1_headffn.txt, r04_steps_b8_v.txt); `roofline_lm`: the LM gate|up GEMV
+    # `roofline` = whichever of the two candidates (the LM MLP block, the head FFN
+    # layer) takes more time per step (avg x launches per step), i.e. the top row
+    # of the step profile (profiles/r06_steps_b1.txt); the other is `roofline_2`
     try:   # the LM MLP block in one launch (B = 1), else the LM gate|up GEMV
         roof_lm = measure_lm_ffn(model, B)
     except Exception as e:   # noqa: BLE001
@@ -711,14 +667,14 @@ def main():
     roof_head = None
     if world == 1 or T == 1:
         try:
-            roof_head = measure_head_loop(model, B) or measure_head_layers(model, B)
+            roof_head = measure_head_layers(model, B)
         except Exception as e:   # noqa: BLE001
             print(f"bench: head roofline not measured: {e}", file=sys.stderr, flush=True)
             roof_head = {"error": str(e)[:200]}
-    if roof_head is None or "error" in roof_head:   # sharded head (TP) or a failed measurement
-        roofline, roofline_2 = roof_lm, roof_head
-    else:
-        roofline, roofline_2 = roof_head, roof_lm
+    roofline, roofline_2 = pick_roofline(roof_lm, roof_head)
+    for r in (roofline, roofline_2):
+        if r and "error" not in r:
+            in_loop_average(r, B)
     tp_coll = None
     if T > 1:   # after the timed loop: the null-collective passes corrupt the session's state
         tp_coll = measure_tp_collective(lm_pass_maker(model, sess), model.config.decoder_config.num_hidden_layers,
@@ -735,7 +691,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:   # bounded CPU sample, N=1 only
-        cpu = cpu_baseline(model.config, args.cpu_tokens, S)
+        cpu = cpu_baseline(model.config, args.cpu_tokens, S, args.model)
 
     if rank == 0:
         line = {

@@ -145,18 +145,31 @@ int vv_embed(vv_ctx* ctx, int n, const int* ids, void* embeds_out, vv_stream st)
  * per-step draws [steps][2n][latent] (step()'s randn, dpm_solver.py:985-987). */
 int vv_diffusion_sample(vv_ctx* ctx, int n, const void* pos_h, const void* neg_h, void* x_io, float cfg_scale,
                         const float* sde_noise, vv_stream st);
-/* At 2n <= 4 rows each head layer is ONE launch when the engine has the fused
- * layer's weight streams bound (head.<l>.gu_rows / head.<l>.dn_rows): its
- * workgroups wait for each other inside the launch (bounded, ~200 ms).  If a
- * wait ever gave up (workgroups not co-resident, e.g. more than two such
- * launches from other contexts on the device at once), every output since is
- * invalid: vv_sync_error returns 1 (and resets), else 0; it synchronises the
- * device.  vv_sync_error_async is its stream-ordered form: it enqueues on st
- * a copy of the error word into dst (4 bytes of pinned host or device memory)
- * and the word's reset, so a host that reads dst after an event recorded
- * behind it sees every launch queued before the call.  GenerateSession reads
- * it with every step's logits read-back and, when a streamer is attached,
- * before the step's audio leaves (step() raises; no invalid chunk is put). */
+/* Grid-waiting kernels.  Where this context is the device's only one with them
+ * enabled, the LM MLP block at B = 1 (k_lm_ffn), each diffusion-head FFN layer
+ * at 2 <= 2n <= 16 rows (k_head_m16) and the codec's C = 2,048 / 1,024 stages
+ * of one sample (k_codec_stage*) each run as ONE launch of one workgroup per CU
+ * whose workgroups wait for each other inside the launch (bounded, ~200 ms;
+ * the occupancy query must show the whole grid co-resident, else the GEMV
+ * launches run).  If a wait ever gave up (workgroups not co-resident, e.g.
+ * another process's kernels holding CUs), every output since is invalid:
+ * vv_sync_error returns 1 (and resets the counters), else 0; it synchronises
+ * the device.  vv_sync_error_async is its stream-ordered form: it enqueues on
+ * st a copy of the error word into dst (4 bytes of pinned host or device
+ * memory) and the word's reset, so a host that reads dst after an event
+ * recorded behind it sees every launch queued before the call; a host that
+ * reads 1 must call vv_sync_reset (synchronises; zeroes every wait counter of
+ * the context) before launching again.  GenerateSession reads it with every
+ * step's logits read-back and before the step's audio leaves for a streamer
+ * (step() raises; no invalid chunk is put).
+ * vv_set_persistent(ctx, 0) turns the grid-waiting kernels off for ctx (the
+ * process default is on unless the environment sets VIBEVOICE_PERSISTENT=0):
+ * for GPUs shared by several processes, whose contexts this library cannot
+ * see. */
+int vv_set_persistent(vv_ctx* ctx, int on);
+/* 1 when ctx launches its grid-waiting kernels now (enabled, sole context). */
+int vv_persistent_active(vv_ctx* ctx);
+int vv_sync_reset(vv_ctx* ctx);
 int vv_sync_error(vv_ctx* ctx);
 int vv_sync_error_async(vv_ctx* ctx, void* dst, vv_stream st);
 

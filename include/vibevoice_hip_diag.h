@@ -103,39 +103,12 @@ int vv_attn_tune(int chunk, int merge_in);
  * per slot of the engine -> the 32-row-tile prefill kernel), 0 = always the
  * per-row decode kernel, 1 = always the prefill kernel. */
 int vv_attn_prefill(int mode);
-/* Switch (benchmarks / tests): persistent GEMV chains (chain.hip) -- the
- * diffusion head's S steps run as ONE launch of one workgroup per CU instead of
- * S x (2 + 2L) GEMV launches.  0 (default, -1) = per-op launches; 1 = chains
- * with the balanced work split; 2 = chains with the per-op launch plan mirrored
- * (bit-identical to 0, the hand-off test).  Measured slower than 0 on MI355X
- * (DESIGN.md "Persistent chains"), so off by default. */
-int vv_chain_tune(int mode);
-/* Tuning hook (benchmarks only): weight chunks per wave per load batch of the
- * chain kernel (4 or 8 = built-in). */
-int vv_chain_tune_u(int u);
-/* Diagnostic: nonzero (1 + op index) if a chain launch's dependency wait gave
- * up (a producer never signalled within ~200 ms); reading resets it. */
-int vv_chain_error(vv_ctx* c);
-/* Diagnostic (benchmarks only): chain launches write s_memrealtime stamps per
- * (workgroup, op): wait begun, inputs ready, op signalled (uint64[G][nops][4]);
- * NULL: off. */
-int vv_chain_stamps(void* buf);
 /* Diagnostic (benchmarks only): vv_gemm_bf16 reads A in MFMA-fragment order
  * (as the packed weights; the 256 x 256 tile only). */
 int vv_gemm_tune_apack(int on);
 /* Tuning hook (benchmarks only): override the GEMV plan (waves, K splits, chunks
  * in flight, tiles per workgroup) for one weight shape N x K at M <= mmax rows;
  * up to 8 overrides; N <= 0 clears them. */
-/* Test / A-B switch: 1 (default) = the fused head FFN layer (head_ffn.hip)
- * where it applies; 0 = gate|up + down GEMV launches per layer. */
-int vv_head_fused(int on);
-/* Test / A-B switch: 2 (default) = at 2n <= 4 rows the whole diffusion of a
- * token runs as one persistent launch per 16 steps (head_loop.hip), plain
- * launch; 1 = the same launched cooperatively (measured +0.35 ms per loop
- * step); 0 = one fused-layer launch per FFN layer + the noisy / final GEMVs.
- * The persistent head runs only while its context is the device's only one
- * with it bound (two cannot be resident together). */
-int vv_head_loop(int on);
 /* Test / A-B switch: 1 (default) = at 4 < 2n <= 16 rows each head FFN layer
  * is one launch with one grid-wide hand-off (head_m16.hip; within bf16 of the
  * GEMV pair, not bitwise) while ctx is the device's only registered context;
@@ -158,27 +131,24 @@ int vv_lm_mlp_replay(vv_ctx* ctx, int ntok, void* hidden, void* act, int reps, v
  * distributed from the previous layer's row partials (1, default) or transform
  * it whole in every workgroup (0). */
 int vv_head_m16_pre(int on);
-/* Test query: 1 when vv_diffusion_sample of n samples on ctx would run the
- * persistent head now. */
-int vv_head_loop_active(vv_ctx* ctx, int n);
-/* Diagnostic: per-workgroup phase stamps of the persistent head launch into buf
- * ([256][64] u64, the last step's phases; NULL = off). */
-int vv_head_loop_stamps(void* buf);
-/* Diagnostic (bench.py): the head's condition rows and the first 16 steps'
- * modulations for n samples, then `reps` persistent head launches over those
- * steps (x_io updated by each), asynchronously on st. */
-int vv_head_loop_replay(vv_ctx* ctx, int n, const void* pos_h, const void* neg_h, void* x_io, float cfg_scale,
-                        int reps, vv_stream st);
-/* Diagnostic: per-workgroup s_memrealtime stamps of every fused head layer
- * launch into buf ([256][8] u64, overwritten per launch; NULL = off). */
-int vv_head_ffn_stamps(void* buf);
 /* Diagnostic (bench.py): the head's condition rows and step-0 modulations for
  * n samples, then `reps` passes over its FFN layers alone (the kernels the loop
  * runs for them at this n), asynchronously on st. */
 int vv_head_layers_replay(vv_ctx* ctx, int n, const void* pos_h, const void* neg_h, int reps, vv_stream st);
 /* Test hook: raise the engine's grid-wait error word as a wait that gave up
- * would (synchronises the device first). */
+ * would, and leave its wait counters part-advanced as such a launch does
+ * (synchronises the device first). */
 int vv_diag_raise_sync_error(vv_ctx* ctx);
+/* Test hook: word 0 of the 13 counter lines of each wait family (head, codec
+ * stage, LM MLP) into out[39]; consistent between launches when every shard
+ * line (0-7) is a multiple of 32 and every generation line a multiple of 8. */
+int vv_diag_sync_words(vv_ctx* ctx, unsigned* out);
+/* The rule every grid-waiting launch applies (kernels.h persist_resident + the
+ * context half): 1 when a grid of `grid` one-per-CU workgroups with the
+ * occupancy query's blocks_per_cu on `cus` CUs and `scratch_bytes` of scratch
+ * is resident, the context has the kernels enabled and it is the device's only
+ * registered context.  Pure function (no device work). */
+int vv_persist_decision(int blocks_per_cu, int cus, int scratch_bytes, int grid, int contexts_on_device, int enabled);
 /* A/B switch: 1 (default) = the balanced many-tile GEMV plan at M >= 8 (one
  * workgroup per CU, 4-5 weight tiles each); 0 = ntile / 8 workgroups. */
 int vv_gemv_tune_bal(int on);

@@ -100,7 +100,7 @@ class _FakeEngine:
     made = []
 
     def __init__(self, cfg, sd, device, max_batch, max_ctx, tp_rank=0, tp_size=1, tp_unique_id=None, tp_head=False,
-                 head_layout=None):
+                 persistent=True):
         self.args = dict(tp_rank=tp_rank, tp_size=tp_size, uid=tp_unique_id, tp_head=tp_head)
         self.schedule = None
         self.max_batch = max_batch

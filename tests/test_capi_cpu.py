@@ -148,3 +148,18 @@ def test_attention_pass_plan_rules():
     # a prompt: the prefill kernel (>= 256 rows and >= 32 rows per slot), no splits
     p = _attn(512, 512)
     assert (p["prefill"], p["nsplit"]) == (1, 1)
+
+
+def test_persist_decision_rule():
+    """The rule every grid-waiting launch applies before it is issued (VERDICT
+    r5 item 8; host logic only): the whole one-per-CU grid resident by the
+    occupancy query, no scratch, the kernels enabled for the context, and the
+    context the device's only registered one -- else the GEMV launches run."""
+    d = _lib.lib().vv_persist_decision
+    assert d(1, 256, 0, 256, 1, 1) == 1
+    assert d(2, 256, 0, 256, 1, 1) == 1          # more room than needed
+    assert d(1, 240, 0, 256, 1, 1) == 0          # fewer CUs (e.g. a CU mask) than workgroups
+    assert d(0, 256, 0, 256, 1, 1) == 0          # the build does not fit a CU
+    assert d(1, 256, 64, 256, 1, 1) == 0         # scratch: waves may wait for slots
+    assert d(1, 256, 0, 256, 2, 1) == 0          # a second registered context on the device
+    assert d(1, 256, 0, 256, 1, 0) == 0          # switched off (VIBEVOICE_PERSISTENT=0 / vv_set_persistent)

@@ -123,7 +123,7 @@ def test_streamer_and_stop_check():
 
 
 def test_grid_wait_error_raises_before_audio_is_streamed():
-    """A grid wait of a fused head layer that gave up (raised here by the
+    """A grid wait of a one-launch kernel that gave up (raised here by the
     diagnostic hook, as the kernel's bounded wait would) invalidates that step's
     latents: the error word is read back behind every diffusion step
     (vv_sync_error_async), and step() raises before that step's audio reaches
@@ -148,11 +148,59 @@ def test_grid_wait_error_raises_before_audio_is_streamed():
             sess.result() if end_with_result else sess.step()
         assert [len(c) for c in st.chunks] == [3, 3]          # step 3's chunk never reached the streamer
         assert not sess.step()                                # the session is over
+        _assert_counters_consistent(m)                        # vv_sync_reset ran before the raise
         # the word was reset by its read-back: a fresh session runs clean
         st2 = RecordingStreamer(2)
         out = m.generate(input_ids=ids, attention_mask=mask, tokenizer=TOK, cfg_scale=1.3,
                          forced_tokens=[[D, D, X]] * 2, audio_streamer=st2, show_progress_bar=False)
         assert [len(c) for c in st2.chunks] == [2, 2] and out.speech_outputs[0].shape[-1] == 2 * m.engine.hop
+
+
+def _assert_counters_consistent(m):
+    """vv_diag_sync_words: every shard line a multiple of 32 arrivals, every
+    generation line a multiple of 8 -- the state between two launches.  The
+    raise hook leaves shard 0 at +5 and the generations at +3, as a launch that
+    gave up does; only vv_sync_reset makes them consistent again."""
+    import ctypes
+    from vibevoice_amd import _lib
+    words = (ctypes.c_uint * 39)()
+    _lib.check(_lib.lib().vv_diag_sync_words(m.engine.h, words), "sync_words")
+    for fam in range(3):
+        w = list(words[fam * 13:(fam + 1) * 13])
+        assert all(v % 32 == 0 for v in w[:8]), (fam, w)
+        assert w[11] % 8 == 0 and w[12] % 8 == 0, (fam, w)
+
+
+def test_grid_wait_error_on_the_last_step_without_streamer():
+    """with no streamer, a wait that gave up in the LAST diffusion
+    step (no logits read-back after it) still raises -- result() drains the
+    queued error-word copy -- and the counters it left part-advanced are reset,
+    so the next generate() equals a run that never saw the error."""
+    from vibevoice_amd import _lib
+    cfg = tiny_config(hidden=256, layers=2, heads=2, kv_heads=1, inter=512)
+    sd = synthetic_state_dict(cfg, seed=11, device="cpu", mode="test", with_acoustic_encoder=False)
+    m = _model(sd, cfg)
+    ids, mask = _inputs()
+    sched = [[D, D, D, X]] * 2
+
+    def run():
+        torch.manual_seed(7)
+        return m.generate(input_ids=ids, attention_mask=mask, tokenizer=TOK, cfg_scale=1.3, forced_tokens=sched,
+                          show_progress_bar=False)
+    clean = run()
+    torch.manual_seed(7)
+    sess = m.generate_session(input_ids=ids, attention_mask=mask, tokenizer=TOK, cfg_scale=1.3,
+                              forced_tokens=[[D] * 8 + [X]] * 2)
+    assert sess.step() and sess.step()
+    _lib.check(_lib.lib().vv_diag_raise_sync_error(m.engine.h), "raise")
+    assert sess.step()                     # the last diffusion step before result(): no read-back after it
+    with pytest.raises(RuntimeError, match="grid wait gave up"):
+        sess.result()
+    _assert_counters_consistent(m)
+    again = run()
+    assert torch.equal(clean.sequences, again.sequences)
+    for b in range(2):
+        assert torch.equal(clean.speech_outputs[b].cpu(), again.speech_outputs[b].cpu())
 
 
 def test_noise_scheduler_swap_sde():

@@ -1,10 +1,11 @@
 """Full-size parity of the SHIPPED B = 1 path (configs[1] / configs[0]'s
 workload) on the MI355X: a VibeVoice-1.5B model built as bench.py builds it
-(max_batch 1: the head's FFN weights in the GEMV layout, weights.head_layout_for)
-and alone on the device, so the loop runs each diffusion-head FFN layer as one
-k_head_m16 launch (2 rows, whole A side) and the persistent codec stages
-(k_codec_stage / k_codec_stage_s) -- asserted, not assumed.  The persistent
-head loop on the fused streams (head_layout="fused") is the second case.
+(max_batch 1) and alone on the device, so the loop runs the LM MLP block as one
+k_lm_ffn launch, each diffusion-head FFN layer as one k_head_m16 launch (2
+rows, whole A side) and the persistent codec stages (k_codec_stage /
+k_codec_stage_s) -- asserted, not assumed.  The second case is the same model
+with the grid-waiting kernels switched off (persistent=False: the GEMV
+launches every shared-GPU deployment falls back to).
 Teacher forcing against oracle/loop.py exactly as tests/test_gpu_fullsize.py
 (whose shared max_batch-8 model runs two samples): per step and quantity, rel
 L2 under the fixed bounds of tests/teacher.py and within 2.5x the bf16
@@ -27,13 +28,13 @@ pytestmark = pytest.mark.gpu
 dev = "cuda"
 
 
-@pytest.fixture(scope="module", params=["default", "fused"])
+@pytest.fixture(scope="module", params=["default", "no_persistent"])
 def m1(request):
     gc.collect()   # the persistent kernels run only for the device's sole registered context
     torch.set_num_threads(min(16, os.cpu_count() or 1))
     cfg = VibeVoiceConfig.builtin("1.5B")
     sd_dev = synthetic_state_dict(cfg, seed=5, device=dev, mode="test")
-    kw = {} if request.param == "default" else {"head_layout": "fused"}
+    kw = {} if request.param == "default" else {"persistent": False}
     model = VibeVoiceForConditionalGenerationInference(cfg, sd_dev, dev, max_batch=1, max_ctx=1024, **kw)
     model.set_ddpm_inference_steps(STEPS)
     yield request.param, cfg, model, _cpu_copy(sd_dev)
@@ -45,11 +46,10 @@ def m1(request):
 def test_teacher_forced_shipped_b1_path(m1, steps):
     layout, cfg, model, sd = m1
     L = _lib.lib()
-    if layout == "default":
-        assert L.vv_head_m16_active(model.engine.h, 1) == 1, "the one-launch head layer does not run"
-    else:
-        assert L.vv_head_loop_active(model.engine.h, 1) == 1, "the persistent head does not run"
-    assert L.vv_codec_stage_active(model.engine.h) == 1, "the persistent codec stage does not run"
+    on = layout == "default"
+    assert (L.vv_head_m16_active(model.engine.h, 1) == 1) == on, "k_head_m16"
+    assert (L.vv_lm_ffn_active(model.engine.h, 2) == 1) == on, "k_lm_ffn"
+    assert (L.vv_codec_stage_active(model.engine.h) == 1) == on, "k_codec_stage"
     inp = synthetic_inputs(batch=1, speakers=1, voice_seconds=3.0, text_tokens=64, seed=100)
     sched = [[D] * 6 + [E, S, D, D, X]]
     vn = _voice_noise(inp, cfg.acoustic_vae_dim)

@@ -26,8 +26,8 @@ dev = "cuda"
 @pytest.fixture(autouse=True)
 def _collect_engines():
     """Engines of earlier tests / modules that are garbage but not yet collected
-    still count as live contexts with the persistent head bound (engine.cpp
-    hl_register: it runs only for a device's sole such context)."""
+    still count as live contexts registered for the grid-waiting kernels
+    (engine.cpp hl_register: they run only for a device's sole such context)."""
     import gc
     gc.collect()
     yield
@@ -37,8 +37,7 @@ def engine_with_head(cfg, head_sd, seed=0):
     sd = synthetic_state_dict(cfg, seed=seed, device="cpu", mode="test", with_acoustic_encoder=False)
     for k, v in head_sd.items():
         sd["model.prediction_head." + k] = v
-    # both head layouts: these tests switch between the fused / persistent and the GEMV paths on one engine
-    return Engine(cfg, sd, dev, max_batch=4, max_ctx=256, head_layout="both"), sd
+    return Engine(cfg, sd, dev, max_batch=4, max_ctx=256), sd
 
 
 @pytest.mark.parametrize("S", [5, 10])
@@ -111,14 +110,14 @@ def test_head_sde_vs_oracle(n):
     assert err < 2e-2 and c > 0.999
 
 
-@pytest.mark.parametrize("fused", [1, 0])
+@pytest.mark.parametrize("m16", [1, 0])
 @pytest.mark.parametrize("n", [1, 2, 3])
-def test_head_real_shape_vs_oracle(n, fused):
-    """n = 1, 2 (2n <= 4 rows) run the fused FFN layer (head_ffn.hip) by
-    default; fused=0 forces gate|up + down launches for every n."""
+def test_head_real_shape_vs_oracle(n, m16):
+    """2n <= 16 rows run each FFN layer as one k_head_m16 launch by default;
+    m16=0 forces the gate|up + down GEMV launches."""
     from vibevoice_amd import _lib
     from vibevoice_amd.config import VibeVoiceConfig
-    _lib.lib().vv_head_fused(fused)
+    _lib.lib().vv_head_m16(m16)
     cfg = VibeVoiceConfig.builtin("1.5B")
     hc = cfg.diffusion_head_config
     g = torch.Generator().manual_seed(11)
@@ -153,117 +152,31 @@ def test_head_real_shape_vs_oracle(n, fused):
         eng.diffusion_sample(pos.to(dev), neg.to(dev), x, 1.3)
         torch.cuda.synchronize()
     finally:
-        _lib.lib().vv_head_fused(1)
+        _lib.lib().vv_head_m16(1)
     eng.check_sync()
     ref = ohead.sample_speech_tokens(sd, pos, neg, noise, S, 1.3, hc.head_layers)
     err, c = rel_err(x, ref), cos(x, ref)
-    print(f"n={n} fused={fused} rel_err={err:.3e} cos={c:.6f}")
+    print(f"n={n} m16={m16} rel_err={err:.3e} cos={c:.6f}")
     assert err < 2e-2 and c > 0.999
 
 
-@pytest.mark.parametrize("n", [1, 2])
-def test_head_fused_deterministic_and_close(n):
-    """The fused layer's split-K reduction is fixed-order: repeated calls give
-    identical bits (also inside a graph replay); it stays within bf16 noise of
-    the two-launch form (different summation order, same rounding points)."""
-    from vibevoice_amd import _lib
-    g = torch.Generator().manual_seed(21)
-    sd, hc, H = real_head_sd(g)
-    tiny = tiny_config(hidden=H, layers=1, heads=12, kv_heads=2, inter=256)
-    eng, _ = engine_with_head(tiny, sd)
-    eng.set_steps(10)
-    pos = torch.randn(n, H, generator=g).bfloat16().to(dev)
-    neg = torch.randn(n, H, generator=g).bfloat16().to(dev)
-    x0 = torch.randn(n, 64, generator=g).bfloat16().to(dev)
-    outs = []
-    for fused in (1, 1, 0):
-        _lib.lib().vv_head_fused(fused)
-        x = x0.clone()
-        eng.diffusion_sample(pos, neg, x, 1.3)
-        torch.cuda.synchronize()
-        outs.append(x.float().cpu())
-    _lib.lib().vv_head_fused(1)
-    # graph replay of the fused form, twice
-    s = torch.cuda.Stream()
-    xg = x0.clone()
-    with torch.cuda.stream(s):
-        gr = torch.cuda.CUDAGraph()
-        gr.capture_begin(capture_error_mode="thread_local")
-        eng.diffusion_sample(pos, neg, xg, 1.3, stream=s)
-        gr.capture_end()
-    for _ in range(2):
-        xg.copy_(x0)
-        gr.replay()
-        torch.cuda.synchronize()
-        outs.append(xg.float().cpu())
-    eng.check_sync()
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[3]) and torch.equal(outs[3], outs[4])
-    err = rel_err(outs[0], outs[2])
-    print(f"n={n} fused vs two-launch rel {err:.3e}")
-    assert err < 1e-2
-
-
-@pytest.mark.parametrize("n,S,sde", [(1, 10, False), (2, 10, False), (1, 5, False), (2, 20, False), (1, 10, True),
-                                     (2, 10, True)])
-def test_head_loop_vs_oracle_and_layer_launches(n, S, sde):
-    """2n <= 4 rows: the whole diffusion runs as ONE persistent launch per 16
-    steps (head_loop.hip; S = 20 takes two, the DPM history crossing the launch
-    boundary through global memory).  Checked against the oracle (real 1.5B head
-    shapes, bound 2e-2 as every head path), against the per-layer launches
-    (vv_head_loop(0): the same FFN layer arithmetic, noisy / final projections by
-    the MFMA GEMV -- a different summation order), and for determinism."""
-    from vibevoice_amd import _lib
-    from vibevoice_amd.schedule import Schedule
-    L = _lib.lib()
-    g = torch.Generator().manual_seed(31 + n + S)
-    sd, hc, H = real_head_sd(g)
-    tiny = tiny_config(hidden=H, layers=1, heads=12, kv_heads=2, inter=256)
-    eng, _ = engine_with_head(tiny, sd)
-    if sde:
-        eng.set_schedule(Schedule.from_config(eng.schedule.config, algorithm_type="sde-dpmsolver++",
-                                              beta_schedule="squaredcos_cap_v2"))
-    eng.set_steps(S)
-    pos = torch.randn(n, H, generator=g).bfloat16()
-    neg = torch.randn(n, H, generator=g).bfloat16()
-    noise = torch.randn(2 * n, 64, generator=g).bfloat16()
-    z = torch.randn(S, 2 * n, 64, generator=g) if sde else None
-    outs = []
-    assert L.vv_head_loop_active(eng.h, n) == 1
-    try:
-        for loop in (2, 2, 0, 1):   # plain launch (default) twice, per-layer launches, cooperative launch
-            L.vv_head_loop(loop)
-            x = noise[:n].to(dev).contiguous()
-            eng.diffusion_sample(pos.to(dev), neg.to(dev), x, 1.3, sde_noise=None if z is None else z.to(dev))
-            torch.cuda.synchronize()
-            outs.append(x.float().cpu())
-    finally:
-        L.vv_head_loop(2)
-    eng.check_sync()
-    ref = ohead.sample_speech_tokens(sd, pos, neg, noise, S, 1.3, hc.head_layers, sde_noise=z)
-    err, c = rel_err(outs[0], ref), cos(outs[0], ref)
-    e_layer = rel_err(outs[0], outs[2])
-    print(f"head loop n={n} S={S} sde={sde}: vs oracle rel {err:.3e} cos {c:.6f} (per-layer launches "
-          f"{rel_err(outs[2], ref):.3e}); loop vs per-layer rel {e_layer:.3e}")
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[3])
-    assert err < 2e-2 and c > 0.999
-    assert e_layer < 1e-2
-
-
-def test_head_loop_only_for_the_devices_sole_context():
-    """Two persistent head launches cannot be resident together (one workgroup
-    per CU each): with a second context of the same head bound on the device,
-    both take the per-layer launches; the first goes back to the persistent
-    head when the second is destroyed (graphs re-captured: vv_ws_epoch)."""
+def test_one_launch_layer_only_for_the_devices_sole_context():
+    """Two grid-waiting launches cannot be resident together (one workgroup per
+    CU each): with a second registered context on the device, both take the
+    GEMV launches; the first goes back to k_head_m16 when the second is
+    destroyed, or when the second is switched off (vv_set_persistent: the
+    standalone tokenizer API's codec context) -- graphs re-captured
+    (vv_ws_epoch).  The GEMV path still matches the oracle."""
     from vibevoice_amd import _lib
     L = _lib.lib()
     g = torch.Generator().manual_seed(41)
     sd, hc, H = real_head_sd(g)
     tiny = tiny_config(hidden=H, layers=1, heads=12, kv_heads=2, inter=256)
     a, _ = engine_with_head(tiny, sd)
-    assert L.vv_head_loop_active(a.h, 1) == 1
+    assert L.vv_head_m16_active(a.h, 1) == 1 and a.persistent_active()
     e0 = L.vv_ws_epoch()
     b, _ = engine_with_head(tiny, sd)
-    assert L.vv_head_loop_active(a.h, 1) == 0 and L.vv_head_loop_active(b.h, 1) == 0
+    assert L.vv_head_m16_active(a.h, 1) == 0 and L.vv_head_m16_active(b.h, 1) == 0
     assert L.vv_ws_epoch() != e0
     a.set_steps(10)
     pos = torch.randn(1, H, generator=g).bfloat16()
@@ -275,9 +188,18 @@ def test_head_loop_only_for_the_devices_sole_context():
     ref = ohead.sample_speech_tokens(sd, pos, neg, noise, 10, 1.3, hc.head_layers)
     assert rel_err(x, ref) < 2e-2
     e1 = L.vv_ws_epoch()
+    _lib.check(L.vv_set_persistent(b.h, 0), "set_persistent")
+    assert L.vv_head_m16_active(a.h, 1) == 1 and not b.persistent_active() and L.vv_ws_epoch() != e1
+    _lib.check(L.vv_set_persistent(b.h, 1), "set_persistent")
+    assert L.vv_head_m16_active(a.h, 1) == 0
     b.close()
-    assert L.vv_head_loop_active(a.h, 1) == 1 and L.vv_ws_epoch() != e1
+    assert L.vv_head_m16_active(a.h, 1) == 1
     a.close()
+    # a context created with persistent=False never registers
+    c = Engine(tiny, synthetic_state_dict(tiny, seed=0, device="cpu", mode="test", with_acoustic_encoder=False), dev,
+               max_batch=1, max_ctx=64, persistent=False)
+    assert not c.persistent_active() and L.vv_head_m16_active(c.h, 1) == 0
+    c.close()
 
 
 @pytest.mark.parametrize("n", [1, 3, 8])

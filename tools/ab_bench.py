@@ -1,7 +1,7 @@
 """A/B a library switch on one box: python tools/ab_bench.py <switch> <value> [bench args]
 (switch: codec_mix_fusion; or "lib" <path> to load another build of the
-library, e.g. an older commit's build kept under tools/lib_*.so; or
-"head_layout" fused|gemv|both for the engine's head FFN weight layout).  Runs bench.py's main with it set first."""
+library, e.g. an older commit's build kept under tools/lib_*.so).  Runs
+bench.py's main with it set first."""
 import os
 import sys
 
@@ -11,10 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vibevoice_amd import _lib  # noqa: E402
 
 name, val = sys.argv[1], sys.argv[2]
-if name == "head_layout":   # the engine's head FFN weight layout ("fused" / "gemv" / "both") instead of head_layout_for's
-    from vibevoice_amd import engine as _engine  # noqa: E402
-    _engine.head_layout_for = lambda *a_, **k_: val
-elif name == "lib":
+if name == "lib":
     import ctypes
     _lib.LIB_PATH = os.path.abspath(val)
     probe = ctypes.CDLL(_lib.LIB_PATH)     # an older build may lack newer (diagnostic) exports

@@ -8,8 +8,6 @@ usage (GPU box):
   python tools/pmc_traffic.py run [M]         # the workload alone (what rocprofv3 wraps)
   python tools/pmc_traffic.py collect [M]     # both rocprofv3 passes + summary ->
                                               # profiles/r05_pmc_traffic_m<M>.json
-  python tools/pmc_traffic.py collect-loop [R]  # the persistent diffusion head (k_head_loop<R>, S = 10)
-                                              # -> profiles/r05_pmc_head_loop_r<R>.json
   python tools/pmc_traffic.py collect-head [R]  # the same for the diffusion head's FFN layer kernel
                                               # (k_head_m16 at R = 2n rows)
                                               # -> profiles/r05_pmc_head_r<R>.json
@@ -73,30 +71,6 @@ def run_head():
     model.engine.check_sync()
 
 
-def run_head_loop():
-    """The persistent diffusion head (k_head_loop<R>, one launch per token at S = 10):
-    vv_head_loop_replay on the real 1.5B head, 1 + 6 launches."""
-    import torch
-    from vibevoice_amd import _lib
-    from vibevoice_amd.modeling_vibevoice_inference import VibeVoiceForConditionalGenerationInference
-    n = M // 2
-    model = VibeVoiceForConditionalGenerationInference.from_pretrained("synthetic:1.5B", device_map="cuda",
-                                                                        synthetic_seed=0, max_batch=n, max_ctx=256,
-                                                                        head_layout="fused")
-    model.set_ddpm_inference_steps(10)
-    model.engine.set_steps(10)
-    cond = torch.randn(2 * n, 1536, device="cuda").bfloat16()
-    x = torch.randn(n, 64, device="cuda").bfloat16()
-    L = _lib.lib()
-    sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    for reps in (1, 6):
-        _lib.check(L.vv_head_loop_replay(model.engine.h, n, ctypes.c_void_p(cond.data_ptr()),
-                                         ctypes.c_void_p(cond[n:].data_ptr()), ctypes.c_void_p(x.data_ptr()), 1.3,
-                                         reps, sp), "head_loop_replay")
-    torch.cuda.synchronize()
-    model.engine.check_sync()
-
-
 def run_lm_ffn():
     """The LM MLP blocks as the B = 1 loop runs them (k_lm_ffn, 28 launches per LM
     pass): vv_lm_mlp_replay on the 1.5B LM shapes, a warm-up pass then 3 more."""
@@ -123,13 +97,9 @@ LMF = len(sys.argv) > 1 and sys.argv[1].endswith("lmffn")
 if LMF:
     KERNEL, NL = "k_lm_ffn", 28
     N, K = 8960, 1536                     # I, H
-LOOP = len(sys.argv) > 1 and sys.argv[1].endswith("loop")
 if HEAD:   # the one-launch layer of head_m16.hip (the default GEMV head layout, 2n <= 16 rows)
     KERNEL, NL = "k_head_m16", 4
     N, K = 4608, 1536                     # F, H
-if LOOP:
-    KERNEL, NL = f"k_head_loop<{M}, false>", 1
-    N, K = 4608, 1536
 
 
 def per_dispatch(path, counter):
@@ -144,13 +114,13 @@ def per_dispatch(path, counter):
 
 
 def collect():
-    out = os.path.join(ROOT, "gpurun_out", f"pmc_{'head_r' if HEAD else 'loop_r' if LOOP else 'lmffn_r' if LMF else 'm'}{M}")
+    out = os.path.join(ROOT, "gpurun_out", f"pmc_{'head_r' if HEAD else 'lmffn_r' if LMF else 'm'}{M}")
     res = {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = os.path.join(out, counter.lower())
         cmd = ["rocprofv3", "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
                sys.executable, os.path.abspath(__file__),
-               "run-head" if HEAD else "run-loop" if LOOP else "run-lmffn" if LMF else "run",
+               "run-head" if HEAD else "run-lmffn" if LMF else "run",
                str(M)]
         subprocess.run(cmd, check=True, timeout=120)
         files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
@@ -168,8 +138,6 @@ def collect():
         alg, shape = 3 * N * K * 2 + M * K * 2 * 2, f"rows={M} H={K} F={N}"
     elif LMF:  # the block's gate|up + down weights + its rows in / out
         alg, shape = 3 * N * K * 2 + M * K * 2 * 2, f"rows={M} H={K} I={N}"
-    elif LOOP:  # S = 10 steps x (4 x (gate|up + down + norm) + noisy + final) + each layer's rows in / out
-        alg, shape = 10 * (4 * (3 * N * K * 2 + K * 2) + 2 * 64 * K * 2 + 4 * M * K * 2 * 2), f"rows={M} H={K} S=10"
     else:
         alg, shape = N * K * 2 + M * K * 2 + M * (N // 2) * 2, f"M={M} N={N} K={K}"
     summary = dict(kernel=KERNEL, shape=shape, fetch_size_kib_raw=round(res["FETCH_SIZE"], 1),
@@ -178,8 +146,8 @@ def collect():
                    alg_bytes_per_launch=alg, traffic_over_alg=round((fetch + write) / alg, 4),
                    method="rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, tools/pmc_traffic.py run; "
                           "FETCH_SIZE x 2 (gfx950), KiB -> bytes")
-    name = (f"r05_pmc_head_r{M}.json" if HEAD else f"r05_pmc_head_loop_r{M}.json" if LOOP else
-            f"r05_pmc_lm_ffn_r{M}.json" if LMF else f"r05_pmc_traffic_m{M}.json")
+    name = (f"r05_pmc_head_r{M}.json" if HEAD else f"r05_pmc_lm_ffn_r{M}.json" if LMF else
+            f"r05_pmc_traffic_m{M}.json")
     for path in (os.path.join(ROOT, "profiles", name), os.path.join(out, "pmc_traffic.json")):
         with open(path, "w") as f:
             json.dump(summary, f, indent=1)
@@ -187,5 +155,5 @@ def collect():
 
 
 if __name__ == "__main__":
-    {"run": run, "collect": collect, "run-head": run_head, "collect-head": collect, "run-loop": run_head_loop,
-     "collect-loop": collect, "run-lmffn": run_lm_ffn, "collect-lmffn": collect}[sys.argv[1]]()
+    {"run": run, "collect": collect, "run-head": run_head, "collect-head": collect, "run-lmffn": run_lm_ffn,
+     "collect-lmffn": collect}[sys.argv[1]]()

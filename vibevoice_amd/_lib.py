@@ -88,27 +88,22 @@ EXPORTS = [
     ("vv_attn_defer_max", I, [I]),
     ("vv_codec_stage_active", I, [P]),
     ("vv_codec_stage_stamps", I, [P, I]),
-    ("vv_chain_tune", I, [I]),
-    ("vv_chain_tune_u", I, [I]),
-    ("vv_chain_error", I, [P]),
-    ("vv_chain_stamps", I, [P]),
     ("vv_gemm_tune_apack", I, [I]),
     ("vv_gemv_tune_shape", I, [I, I, I, I, I, I, I]),
     ("vv_rope_table", I, [I]),
     ("vv_attn_defer", I, [I, I]),
     ("vv_attn_group", I, [I]),
     ("vv_attn_pass_plan", I, [I, I, I, I, I, ctypes.POINTER(I)]),
-    ("vv_head_fused", I, [I]),
-    ("vv_head_loop", I, [I]),
-    ("vv_head_loop_stamps", I, [P]),
-    ("vv_head_loop_active", I, [P, I]),
-    ("vv_head_loop_replay", I, [P, I, P, P, P, F, I, P]),
     ("vv_gemv_tune_bal", I, [I]),
-    ("vv_head_ffn_stamps", I, [P]),
     ("vv_head_layers_replay", I, [P, I, P, P, I, P]),
     ("vv_sync_error", I, [P]),
     ("vv_sync_error_async", I, [P, P, P]),
     ("vv_diag_raise_sync_error", I, [P]),
+    ("vv_diag_sync_words", I, [P, P]),
+    ("vv_sync_reset", I, [P]),
+    ("vv_set_persistent", I, [P, I]),
+    ("vv_persist_decision", I, [I, I, I, I, I, I]),
+    ("vv_persistent_active", I, [P]),
     ("vv_norm_pack", I, [I]),
 ]
 

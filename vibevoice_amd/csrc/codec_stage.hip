@@ -647,20 +647,20 @@ __global__ void __launch_bounds__(cs2::NT) k_codec_stage_s(CodecStageArgs a) {
 }
 
 // One workgroup per CU, all resident from the start: the plain launch checks
-// nothing, so each build is checked here (no scratch, one workgroup fits a CU).
-static bool resident_check(const void* k, int nt, int lds) {
+// nothing, so each build is checked here (kernels.h persist_resident).
+bool persist_resident_kernel(const void* k, int nt, int lds, int grid) {
   hipFuncAttributes fa{};
   int nb = 0, dev = 0, cus = 0;
   if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess ||
       hipFuncGetAttributes(&fa, k) != hipSuccess || hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, nt, lds) != hipSuccess ||
       hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return false;
-  return fa.localSizeBytes == 0 && nb >= 1 && cus >= pk::G;
+  return persist_resident(nb, cus, (long long)fa.localSizeBytes, grid);
 }
 static bool stage_resident(int C, int M) {
-  static const bool ok2048 = resident_check((const void*)k_codec_stage, cs::NT, cs::TOTAL);
-  static const bool ok1024_2 = resident_check((const void*)k_codec_stage_s<2>, cs2::NT, cs2::Lds<2>::TOTAL);
-  static const bool ok1024_8 = resident_check((const void*)k_codec_stage_s<8>, cs2::NT, cs2::Lds<8>::TOTAL);
+  static const bool ok2048 = persist_resident_kernel((const void*)k_codec_stage, cs::NT, cs::TOTAL, cs::G);
+  static const bool ok1024_2 = persist_resident_kernel((const void*)k_codec_stage_s<2>, cs2::NT, cs2::Lds<2>::TOTAL, cs2::G);
+  static const bool ok1024_8 = persist_resident_kernel((const void*)k_codec_stage_s<8>, cs2::NT, cs2::Lds<8>::TOTAL, cs2::G);
   if (C == cs::C && M == 1) return ok2048;
   if (C == cs2::C && M == 2) return ok1024_2;
   if (C == cs2::C && M == 8) return ok1024_8;

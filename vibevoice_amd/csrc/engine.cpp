@@ -66,11 +66,13 @@ struct ConvBuf {
 // Bumped whenever a workspace moves: a hipGraph captured earlier bakes the old
 // pointers in, so the host drops its graphs when this changes (vv_ws_epoch).
 static std::atomic<int> g_ws_epoch{0};
-// Contexts per device that could run the persistent diffusion head (head_loop.hip:
-// one workgroup per CU, grid-wide waits).  Two such launches from two contexts
-// cannot be resident together, so the persistent head runs only while ONE
-// finalized context of the device has it bound; a change of that count bumps the
-// epoch, so hosts re-capture graphs that baked in the other path.
+// Contexts per device that may run the one-launch kernels with grid-wide waits
+// (k_lm_ffn, k_head_m16, k_codec_stage*: one workgroup per CU).  Two such
+// launches from two contexts cannot be resident together, so they run only while
+// ONE finalized context of the device is registered; a change of that count bumps
+// the epoch, so hosts re-capture graphs that baked in the other path.  Contexts
+// of OTHER processes are invisible here: a shared-GPU deployment turns the
+// kernels off (VIBEVOICE_PERSISTENT=0 or vv_set_persistent).
 static std::mutex g_hl_mu;
 static std::map<int, int> g_hl_ctxs;
 static void hl_register(int device, int delta) {
@@ -85,7 +87,19 @@ static int hl_count(int device) {
   auto it = g_hl_ctxs.find(device);
   return it == g_hl_ctxs.end() ? 0 : it->second;
 }
-static bool hl_sole(int device) { return hl_count(device) == 1; }
+
+// wait counters + error word of a grid-waiting kernel family (persist_dev.h: 13 lines of 32 words)
+static constexpr size_t SYNC_BYTES = 2048;
+
+// Process default for new contexts: VIBEVOICE_PERSISTENT=0 in the environment
+// turns the grid-waiting kernels off (e.g. several processes sharing one GPU).
+static bool persist_env_default() {
+  static const bool on = [] {
+    const char* e = getenv("VIBEVOICE_PERSISTENT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 struct DevBuf {
   void* p = nullptr;
@@ -176,24 +190,16 @@ struct vv_ctx {
   int head_tp = 0;      // 1: the diffusion head's FFN is sharded too (vv_tp_shard_head; head_ffn is local)
   ncclComm_t comm = nullptr;
   DevBuf zero_rows;     // [2 * max_batch][H] zeros: the residual of a sharded head's rank > 0
-  // persistent chains (chain.hip): op tables per diffusing-row count n for the
-  // current schedule; sync words (zeroed per launch), split slabs, error word
-  struct Chain {
-    DevBuf ops;
-    int nops = 0, nsync = 0, mode = -1;
-    size_t lds = 0;
-  };
-  std::unordered_map<int, Chain> head_chain;
-  DevBuf chain_sync, chain_slabs, chain_err, coef_dev;
-  // fused head FFN layer (head_ffn.hip): partial-sum slabs, grid-wait words + error word
-  DevBuf hf_slab, hf_sync;
+  // grid-wide waits of the one-launch kernels (persist_dev.h): head_m16.hip's
+  // counters (lines 0-7 shards, line 12 its generation) + the error word (line 10)
+  DevBuf hf_sync;
   DevBuf lf_sync;   // lm_ffn.hip's wait counters
   DevBuf m16_buf;   // head_m16.hip's distributed A side: row partial sums of squares [16][192] f32 + rows [16][H]
-  DevBuf hl_lat;           // persistent head (head_loop.hip): [D][2] latent hand-off
   DevBuf cs_sync;          // persistent codec stage (codec_stage.hip): its wait counters
-  bool hl_registered = false;   // counted in g_hl_ctxs (its device's persistent-head contexts)
+  bool persist_ok = true;       // this context may run one-launch (grid-waiting) kernels (vv_set_persistent)
+  bool persist_capable = false; // some grid-waiting kernel fits this engine's shapes (vv_finalize)
+  bool hl_registered = false;   // counted in g_hl_ctxs (its device's grid-waiting contexts)
   bool head_gemv = true;        // the head FFN's GEMV layout is bound (head.<l>.gu_w / down_w)
-  bool hf_ready = false;   // its weights are bound (head.<l>.gu_rows / dn_rows) and the shape fits
   DevBuf rope_tab;   // [max_ctx][cos 64 | sin 64] bf16 (k_rope_table)
 };
 
@@ -301,6 +307,20 @@ static int rmsnorm(int M, int C, RowMap in, RowMap out, const bf16* w, float eps
   a.scale_off = scale_off;
   KCHK(launch_rmsnorm(a, st));
   return 0;
+}
+
+// ------------------------------------------------------------------ grid-waiting kernels
+// The context half of the decision every one-launch (grid-waiting) kernel takes
+// before its launch; the kernel half is its *_fits (shape + persist_resident on
+// the occupancy query).  Both halves are vv_persist_decision for the tests.
+static bool persist_ctx_ok(int enabled, int contexts_on_device) { return enabled && contexts_on_device == 1; }
+static bool persist_on(vv_ctx* c) {
+  return persist_ctx_ok(c->persist_ok && c->hl_registered ? 1 : 0, hl_count(c->device));
+}
+extern "C" int vv_persist_decision(int blocks_per_cu, int cus, int scratch_bytes, int grid, int contexts_on_device,
+                                   int enabled) {
+  return persist_resident(blocks_per_cu, cus, scratch_bytes, grid) && persist_ctx_ok(enabled, contexts_on_device) ? 1
+                                                                                                                   : 0;
 }
 
 // ------------------------------------------------------------------ codec layout
@@ -460,7 +480,7 @@ extern "C" int vv_codec_mix_fusion(int mask) {
 
 // A codec stage of Block1Ds of one sample (C = 2,048 at T = 1, C = 1,024 at
 // T = 2 / 8) runs as ONE persistent launch (codec_stage.hip) while the context is the device's only one registered for
-// persistent kernels (hl_sole); 0 = the launch-per-GEMV path (A/B and tests).
+// persistent kernels (persist_on); 0 = the launch-per-GEMV path (A/B and tests).
 static std::atomic<int> g_codec_stage{1};
 extern "C" int vv_codec_stage(int on) {
   g_codec_stage = on ? 1 : 0;
@@ -473,7 +493,7 @@ static bool codec_stage_any(const ConvNet& net) {
 }
 static bool codec_stage_on(vv_ctx* c, const ConvNet& net, int i, int n) {
   return g_codec_stage && c->cs_sync.p && codec_stage_fits(net.chans[i], net.T[i], n, net.depth[i]) &&
-         hl_sole(c->device);
+         persist_on(c);
 }
 static std::atomic<unsigned long long*> g_codec_stage_stamps{nullptr};
 static std::atomic<int> g_codec_stage_stamp_at{0};
@@ -718,6 +738,7 @@ int vv_create(const vv_config* cfg, int device, vv_ctx** out) {
   vv_ctx* c = new vv_ctx();
   c->cfg = *cfg;
   c->device = device;
+  c->persist_ok = persist_env_default();
   *out = c;
   return 0;
 }
@@ -729,10 +750,8 @@ void vv_destroy(vv_ctx* c) {
   if (c->hl_registered) hl_register(c->device, -1);
   DevBuf* bufs[] = {&c->norm_ws, &c->kv_k, &c->kv_v, &c->lm_ws, &c->attn_part, &c->attn_cnt, &c->valid_ids, &c->splitk_ws, &c->splitk_cnt,
                     &c->temb, &c->tfreq_tmp, &c->head_ws, &c->codec_ws, &c->slot_scratch, &c->unit_sb,
-                    &c->chain_sync, &c->chain_slabs, &c->chain_err, &c->coef_dev, &c->rope_tab, &c->zero_rows,
-                    &c->hf_slab, &c->hf_sync, &c->hl_lat, &c->cs_sync, &c->m16_buf, &c->lf_sync};
+                    &c->rope_tab, &c->zero_rows, &c->hf_sync, &c->cs_sync, &c->m16_buf, &c->lf_sync};
   for (DevBuf* b : bufs) b->release();
-  for (auto& kv : c->head_chain) kv.second.ops.release();
   ConvNet* nets[] = {&c->dec, &c->sem, &c->aenc, &c->senc};
   for (ConvNet* n : nets) {
     n->state.release();
@@ -787,41 +806,18 @@ int vv_finalize(vv_ctx* c) {
   CHK(need(c, "head.t0_w", {H, 256}));
   CHK(need(c, "head.t2_w", {H, H}));
   CHK(need(c, "head.ada_w", {(3LL * L + 2) * H, H}));
-  // the FFN in either layout, or both (weights.py head_layout_for): the GEMV
-  // layout (any batch), the fused layer's streams (2n <= 4 rows)
-  c->head_gemv = c->w.count("head.0.gu_w") > 0;
+  // the FFN in the GEMV layout (weights.py: 16-row gate|up tiles of 8 gate + 8 up rows)
+  c->head_gemv = true;
   for (int l = 0; l < L; ++l) {
     const std::string p = "head." + std::to_string(l);
     CHK(need(c, p + ".norm", {H}));
-    if (c->head_gemv) {
-      CHK(need(c, p + ".gu_w", {2LL * F, H}));
-      CHK(need(c, p + ".down_w", {H, F}));
-    }
+    CHK(need(c, p + ".gu_w", {2LL * F, H}));
+    CHK(need(c, p + ".down_w", {H, F}));
   }
-  if (!c->head_gemv && !(head_ffn_fits(H, F, 2) && c->w.count("head.0.gu_rows")))
-    FAIL("diffusion head FFN: neither the GEMV layout (head.<l>.gu_w / down_w) nor the fused layer's streams "
-         "(head.<l>.gu_rows / dn_rows, this shape) are bound");
   CHK(need(c, "head.final_w", {D, H}));
-  // the fused FFN layer's streams (optional: without them every layer runs gate|up + down)
-  c->hf_ready = false;
   // grid-wait words + the error word (always present: vv_sync_error_async reads it)
-  // (+ 256 arrival flags of the persistent head at word 12 * 32, head_loop.hip)
-  CHK(c->hf_sync.ensure(12 * 128 + 1024));
-  HIPCHK(hipMemset(c->hf_sync.p, 0, 12 * 128 + 1024));
-  if (head_ffn_fits(H, F, 2) && c->w.count("head.0.gu_rows")) {
-    for (int l = 0; l < L; ++l) {
-      const std::string p = "head." + std::to_string(l);
-      CHK(need(c, p + ".gu_rows", {2LL * F, H}));
-      CHK(need(c, p + ".dn_rows", {F, H}));
-    }
-    CHK(c->hf_slab.ensure((size_t)head_ffn_grid() * 4 * H * sizeof(float)));
-    CHK(c->hl_lat.ensure((size_t)D * 2 * sizeof(bf16) + 256));
-    c->hf_ready = true;
-    if (!c->hl_registered && head_loop_fits(H, F, 2, L)) {
-      c->hl_registered = true;
-      hl_register(c->device, +1);
-    }
-  }
+  CHK(c->hf_sync.ensure(SYNC_BYTES));
+  HIPCHK(hipMemset(c->hf_sync.p, 0, SYNC_BYTES));
   // ---- connectors + latent scaling
   CHK(need(c, "conn.ac.fc1_w", {H, D}));
   CHK(need(c, "conn.se.fc1_w", {H, k.semantic_dim}));
@@ -854,18 +850,19 @@ int vv_finalize(vv_ctx* c) {
   // the persistent codec stage's wait counters; a context that can run it (or
   // the persistent head, or the one-launch head layer at 16 rows) counts in the
   // device's registry (hl_register)
-  CHK(c->cs_sync.ensure(12 * 128));
-  HIPCHK(hipMemset(c->cs_sync.p, 0, 12 * 128));
-  CHK(c->lf_sync.ensure(12 * 128));
-  HIPCHK(hipMemset(c->lf_sync.p, 0, 12 * 128));
+  CHK(c->cs_sync.ensure(SYNC_BYTES));
+  HIPCHK(hipMemset(c->cs_sync.p, 0, SYNC_BYTES));
+  CHK(c->lf_sync.ensure(SYNC_BYTES));
+  HIPCHK(hipMemset(c->lf_sync.p, 0, SYNC_BYTES));
   if (c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 16))
   {
     CHK(c->m16_buf.ensure(16 * 192 * sizeof(float) + 16 * (size_t)k.hidden * sizeof(bf16)));
     HIPCHK(hipMemset(c->m16_buf.p, 0, 16 * 192 * sizeof(float)));
   }
-  if (!c->hl_registered && (codec_stage_any(c->dec) || codec_stage_any(c->sem) ||
-                            (c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 16)) ||
-                            lm_ffn_fits(k.hidden, k.intermediate, 2))) {
+  c->persist_capable = codec_stage_any(c->dec) || codec_stage_any(c->sem) ||
+                       (c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 16)) ||
+                       lm_ffn_fits(k.hidden, k.intermediate, 2);
+  if (c->persist_ok && c->persist_capable && !c->hl_registered) {
     c->hl_registered = true;
     hl_register(c->device, +1);
   }
@@ -947,13 +944,7 @@ int vv_set_schedule(vv_ctx* c, int steps, const float* coef, const void* tfreq, 
   KCHK(launch_silu(steps * H, t1, t1, st));
   CHK(gemm(c, gemm_args(c, steps, H, H, rowmap(t1, H), W(c, "head.t2_w"), EPI_STORE, rowmap(c->temb.p, H)), st));
   c->steps = steps;
-  // the chain's per-step DPM coefficients (cfg is bound per call); tables are per schedule
-  CHK(c->coef_dev.ensure((size_t)1000 * sizeof(DpmCoef)));
-  HIPCHK(hipMemcpyAsync(c->coef_dev.p, c->coef.data(), (size_t)steps * sizeof(DpmCoef), hipMemcpyHostToDevice, st));
   HIPCHK(hipStreamSynchronize(st));
-  if (!c->head_chain.empty()) g_ws_epoch.fetch_add(1);   // captured chain launches point at the old tables
-  for (auto& kv : c->head_chain) kv.second.ops.release();
-  c->head_chain.clear();
   return 0;
 }
 
@@ -1210,7 +1201,7 @@ extern "C" int vv_lm_ffn(int on) {
 static bool lm_ffn_on(vv_ctx* c, const LmPass& P) {
   const vv_config& k = c->cfg;
   return g_lm_ffn && c->lf_sync.p && !P.prefill && P.ntok <= 2 && c->tp_size == 1 && !c->comm && !P.hm.idx &&
-         P.hm.sT == k.hidden && P.hm.T >= P.ntok && lm_ffn_fits(k.hidden, k.intermediate, P.ntok) && hl_sole(c->device);
+         P.hm.sT == k.hidden && P.hm.T >= P.ntok && lm_ffn_fits(k.hidden, k.intermediate, P.ntok) && persist_on(c);
 }
 extern "C" int vv_lm_ffn_active(vv_ctx* c, int ntok) {
   LmPass P;
@@ -1366,60 +1357,22 @@ int vv_tp_init(vv_ctx* c, int rank, int size, const void* unique_id) {
   return 0;
 }
 
-// ------------------------------------------------------------------ persistent chains
-// 0 (default): per-op launches; 1: chains with the balanced plan; 2: chains
-// with the per-op launch plan mirrored (bit-identical to 0; tests).  Measured
-// on MI355X (tools/chain_bench.py, DESIGN.md "Persistent chains"): the
-// in-launch hand-off is 0.5-1.2 us, but each op's span keeps its dependent
-// memory round trips (A rows, residual, write-through drain, arrival), so a
-// 100-op head chain takes 1.05 ms against 0.87 ms of per-op launches.
-static std::atomic<int> g_chain{0};
-static std::atomic<unsigned long long*> g_chain_stamps{nullptr};
-extern "C" int vv_chain_stamps(void* buf) {
-  g_chain_stamps = (unsigned long long*)buf;
+// Every grid-wait counter of the context back to 0 and the error word cleared,
+// with nothing in flight (the device is synchronised): after a wait gave up, the
+// counters of that launch stay part-advanced, and a later launch's base
+// generation (persist_dev.h) would let a wait release early.
+int vv_sync_reset(vv_ctx* c) {
+  if (!c->finalized) FAIL("vv_sync_reset before vv_finalize");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipDeviceSynchronize());
+  for (DevBuf* b : {&c->hf_sync, &c->cs_sync, &c->lf_sync})
+    if (b->p) HIPCHK(hipMemset(b->p, 0, SYNC_BYTES));
+  HIPCHK(hipDeviceSynchronize());
   return 0;
 }
-extern "C" int vv_chain_tune(int mode) {
-  g_chain = mode < 0 ? 0 : mode;
-  return 0;
-}
-// error word of the last chain launches (1 + the op a wait gave up on), reset on read
-extern "C" int vv_chain_error(vv_ctx* c) {
-  if (!c->chain_err.p) return 0;
-  unsigned v = 0;
-  if (hipMemcpy(&v, c->chain_err.p, 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  if (v) (void)hipMemset(c->chain_err.p, 0, 4);
-  return (int)v;
-}
-
-// Fused head FFN layer (head_ffn.hip) where its weights are bound and the shape
-// fits; 0 = gate|up + down launches (diagnostic vv_head_fused, A/B and tests)
-static std::atomic<int> g_head_fused{1};
-extern "C" int vv_head_fused(int on) {
-  g_head_fused = on ? 1 : 0;
-  return 0;
-}
-// The whole diffusion in one persistent launch (head_loop.hip) where the fused
-// layer's streams are bound and the shape fits; 0 = one k_head_ffn launch per
-// layer (A/B and tests)
-static std::atomic<int> g_head_loop{2};
-extern "C" int vv_head_loop(int on) {   // 2 (default): plain launch, 1: cooperative launch, 0: off
-  g_head_loop = on < 0 ? 0 : on > 2 ? 2 : on;
-  return 0;
-}
-static std::atomic<unsigned long long*> g_head_loop_stamps{nullptr};
-extern "C" int vv_head_loop_stamps(void* buf) {   // diagnostic: [256][64] per-workgroup phase stamps
-  g_head_loop_stamps = (unsigned long long*)buf;
-  return 0;
-}
-static std::atomic<unsigned long long*> g_head_ffn_stamps{nullptr};
-extern "C" int vv_head_ffn_stamps(void* buf) {   // diagnostic: [256][8] per-workgroup stamps of each launch
-  g_head_ffn_stamps = (unsigned long long*)buf;
-  return 0;
-}
-// A grid wait of the fused head layer gave up (workgroups not co-resident):
+// A grid wait of a one-launch kernel gave up (workgroups not co-resident):
 // every output since the last call is invalid.  Reset on read (with the wait
-// counters).
+// counters: vv_sync_reset).
 // (hipMemcpy on the null stream does not wait for non-blocking streams, where
 // the host's generate() runs: synchronise the device first)
 int vv_sync_error(vv_ctx* c) {
@@ -1428,11 +1381,7 @@ int vv_sync_error(vv_ctx* c) {
     HIPCHK(hipDeviceSynchronize());
     if (hipMemcpy(&v, (unsigned*)c->hf_sync.p + 10 * 32, 4, hipMemcpyDeviceToHost) != hipSuccess)
       FAIL("vv_sync_error: reading the error word failed (hipMemcpy)");
-    // a launch that gave up left the wait counters part-advanced: with nothing in
-    // flight (the device is synchronised) every counter restarts from 0
-    if (v) HIPCHK(hipMemset(c->hf_sync.p, 0, 13 * 128));
-    if (v && c->cs_sync.p) HIPCHK(hipMemset(c->cs_sync.p, 0, 12 * 128));
-    if (v && c->lf_sync.p) HIPCHK(hipMemset(c->lf_sync.p, 0, 12 * 128));
+    if (v) CHK(vv_sync_reset(c));
   }
   return v ? 1 : 0;
 }
@@ -1440,7 +1389,7 @@ int vv_sync_error(vv_ctx* c) {
 // pinned host or device memory) and its reset, behind everything queued before.
 // The host reads dst once an event recorded after this call has completed
 // (GenerateSession: with each step's logits read-back, and before audio leaves
-// for a streamer).
+// for a streamer); when it reads 1 it calls vv_sync_reset before anything else.
 int vv_sync_error_async(vv_ctx* c, void* dst, vv_stream vst) {
   hipStream_t st = (hipStream_t)vst;
   if (!dst) FAIL("vv_sync_error_async: dst is NULL");
@@ -1450,76 +1399,59 @@ int vv_sync_error_async(vv_ctx* c, void* dst, vv_stream vst) {
   HIPCHK(hipMemsetAsync(word, 0, 4, st));
   return 0;
 }
+// Per-context switch of the grid-waiting kernels (default: on unless
+// VIBEVOICE_PERSISTENT=0).  Off: the context neither launches them nor counts in
+// the device's registry, so it never demotes another context (the standalone
+// tokenizer API's codec context) nor contends with it.  Bumps the workspace
+// epoch: graphs captured with the other path are re-captured.
+int vv_set_persistent(vv_ctx* c, int on) {
+  if (!c) FAIL("vv_set_persistent: null context");
+  c->persist_ok = on != 0;
+  if (c->finalized) {
+    if (!c->persist_ok && c->hl_registered) {
+      c->hl_registered = false;
+      hl_register(c->device, -1);
+    } else if (c->persist_ok && c->persist_capable && !c->hl_registered) {
+      c->hl_registered = true;
+      hl_register(c->device, +1);
+    }
+  }
+  g_ws_epoch.fetch_add(1);
+  return 0;
+}
+int vv_persistent_active(vv_ctx* c) { return c && c->finalized && persist_on(c) ? 1 : 0; }
 // Diagnostic (tests): raise the error word as a grid wait that gave up would.
 extern "C" int vv_diag_raise_sync_error(vv_ctx* c) {
   if (!c->finalized) FAIL("vv_diag_raise_sync_error before vv_finalize");
   HIPCHK(hipDeviceSynchronize());
   const unsigned one = 1;
   HIPCHK(hipMemcpy((unsigned*)c->hf_sync.p + 10 * 32, &one, 4, hipMemcpyHostToDevice));
-  return 0;
-}
-
-// Plan every op of `ops` (chain.hip), lay out slabs and tickets, upload.
-static int chain_upload(vv_ctx* c, std::vector<ChainOp>& ops, vv_ctx::Chain& T) {
-  const int G = chain_grid();
-  if (G <= 0) FAIL("chain: no device");
-  long long slabs = 0;
-  int tickets = 0;
-  size_t lds = 0;
-  for (ChainOp& op : ops) {
-    const size_t l = chain_plan_op(&op, G, g_chain == 2 ? 1 : 0);
-    if (!l) return 1;   // a shape the chain does not take: caller runs per-op launches
-    lds = std::max(lds, l);
-    if (op.nunit > op.nu1) {
-      const int rem = op.g.N / 16 - op.t1;
-      if (rem > CH_TMAX) return 1;
-      op.slab_off = slabs;
-      op.ticket_off = tickets;
-      slabs += (long long)rem * op.ks2 * 256;
-      tickets += rem;
+  // ... and leave the counters part-advanced as a launch that gave up does: 5
+  // arrivals on shard 0, 3 generation bumps (lines 11 and 12) of every family
+  for (DevBuf* b : {&c->hf_sync, &c->cs_sync, &c->lf_sync}) {
+    if (!b->p) continue;
+    for (int line : {0, 11, 12}) {
+      unsigned v = 0;
+      unsigned* p = (unsigned*)b->p + line * 32;
+      HIPCHK(hipMemcpy(&v, p, 4, hipMemcpyDeviceToHost));
+      v += line == 0 ? 5u : 3u;
+      HIPCHK(hipMemcpy(p, &v, 4, hipMemcpyHostToDevice));
     }
   }
-  if (lds > 151552) return 1;
-  const int nops = (int)ops.size();
-  T.nops = nops;
-  T.nsync = nops * 9 * 32 + ((tickets + 3) & ~3);
-  T.lds = lds;
-  T.mode = g_chain;
-  CHK(T.ops.ensure(ops.size() * sizeof(ChainOp)));
-  HIPCHK(hipMemcpy(T.ops.p, ops.data(), ops.size() * sizeof(ChainOp), hipMemcpyHostToDevice));
-  CHK(c->chain_sync.ensure((size_t)T.nsync * 4));
-  CHK(c->chain_slabs.ensure((size_t)std::max(slabs, 256LL) * 4));
-  if (!c->chain_err.p) {
-    CHK(c->chain_err.ensure(16));
-    HIPCHK(hipMemset(c->chain_err.p, 0, 16));
-  }
   return 0;
 }
-
-static int chain_launch(vv_ctx* c, const vv_ctx::Chain& T, ChainArgs A, hipStream_t st) {
-  A.ops = (const ChainOp*)T.ops.p;
-  A.nops = T.nops;
-  A.done = (unsigned*)c->chain_sync.p;
-  A.tickets = A.done + (size_t)T.nops * 9 * 32;
-  A.stamps = g_chain_stamps;
-  A.slabs = (float*)c->chain_slabs.p;
-  A.err = (unsigned*)c->chain_err.p;
-  HIPCHK(hipMemsetAsync(c->chain_sync.p, 0, (size_t)T.nsync * 4, st));
-  KCHK(launch_chain(A, T.lds, st));
-  // Eager launches (the chain is an opt-in switch): a dependency wait that gave
-  // up (not every workgroup co-resident, e.g. CUs held by another stream) left
-  // latents built from stale inputs — report it instead of returning success.
-  // Inside a graph capture the caller checks vv_chain_error after replay.
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  HIPCHK(hipStreamIsCapturing(st, &cap));
-  if (cap == hipStreamCaptureStatusNone) {
-    // (a host sync per eager chain launch: the chain is an opt-in diagnostic switch)
-    HIPCHK(hipStreamSynchronize(st));
-    const int e = vv_chain_error(c);
-    if (e < 0) FAIL("persistent chain: reading the error word failed (hipMemcpy)");
-    if (e) FAIL("persistent chain: a dependency wait gave up at op " + std::to_string(e - 1) +
-                " (workgroups not co-resident); outputs are invalid");
-  }
+// Diagnostic (tests): word 0 of the 13 counter lines of each wait family
+// (head, codec stage, LM MLP) -> out[39].  Between launches a consistent set has
+// every shard line (0-7) a multiple of 32 and every generation line a multiple of 8.
+extern "C" int vv_diag_sync_words(vv_ctx* c, unsigned* out) {
+  if (!c->finalized) FAIL("vv_diag_sync_words before vv_finalize");
+  HIPCHK(hipDeviceSynchronize());
+  int i = 0;
+  for (DevBuf* b : {&c->hf_sync, &c->cs_sync, &c->lf_sync})
+    for (int line = 0; line < 13; ++line, ++i) {
+      out[i] = 0;
+      if (b->p) HIPCHK(hipMemcpy(out + i, (unsigned*)b->p + line * 32, 4, hipMemcpyDeviceToHost));
+    }
   return 0;
 }
 
@@ -1610,7 +1542,7 @@ extern "C" int vv_head_m16(int on) {
 // the one-launch layer applies (R <= 16 rows, GEMV layout, unsharded, sole context)
 static bool m16_on(vv_ctx* c, int R) {
   return g_head_m16 && !c->head_tp && c->head_gemv && c->m16_buf.p && head_m16_fits(c->cfg.hidden, c->cfg.head_ffn, R) &&
-         hl_sole(c->device);
+         persist_on(c);
 }
 
 // ... with the A side built distributed (HeadM16Args::pre) above 4 rows: at 2 -
@@ -1642,7 +1574,7 @@ static int head_noisy(vv_ctx* c, const HeadRun& h, const void* x_io, hipStream_t
 extern "C" int vv_head_m16_active(vv_ctx* c, int n) {
   const vv_config& k = c->cfg;
   return c && c->finalized && g_head_m16 && !c->head_tp && c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 2 * n) &&
-                 hl_sole(c->device)
+                 persist_on(c)
              ? 1
              : 0;
 }
@@ -1661,33 +1593,6 @@ static int head_layer(vv_ctx* c, const HeadRun& h, int s, int l, hipStream_t st)
   GemmArgs g = gemm_args(c, h.R, 2 * F, H, h.xh_m, W(c, p + ".gu_w"), EPI_SILU_MUL, rowmap(h.act, F));
   g.xf = xf_norm(W(c, p + ".norm"), k.head_eps, mod, h.MODW, o, o + H);
   const bool partial = c->head_tp && c->tp_size > 1 && c->tp_rank > 0;
-  // one launch (head_ffn.hip): its grid waits need the launch resident with at
-  // most one other (two workgroups per CU), so with three or more contexts of
-  // the device registered the GEMV layout runs instead where it is bound
-  if (c->hf_ready && g_head_fused && head_ffn_fits(H, F, h.R) && (hl_count(c->device) <= 2 || !c->head_gemv)) {
-    HeadFfnArgs a;
-    memset(&a, 0, sizeof(a));
-    a.x = h.xh;
-    a.out = h.xh;
-    a.res = partial ? (const bf16*)c->zero_rows.p : h.xh;
-    a.ldx = a.ldres = H;
-    a.nw = W(c, p + ".norm");
-    a.mod = mod;
-    a.ldmod = h.MODW;
-    a.shift_off = o;
-    a.scale_off = o + H;
-    a.gate_off = o + 2 * H;
-    a.R = h.R;
-    a.eps = k.head_eps;
-    a.gu = W(c, p + ".gu_rows");
-    a.dn = W(c, p + ".dn_rows");
-    a.slab = (float*)c->hf_slab.p;
-    a.sync = (unsigned*)c->hf_sync.p;
-    a.err = (unsigned*)c->hf_sync.p + 10 * 32;
-    a.stamps = g_head_ffn_stamps;
-    KCHK(launch_head_ffn(a, st));
-    return 0;
-  }
   if (m16_on(c, h.R)) {
     // 2n <= 16 rows, GEMV layout: one launch with two grid-wide waits (head_m16.hip)
     HeadM16Args a;
@@ -1772,75 +1677,6 @@ extern "C" int vv_head_layers_replay(vv_ctx* c, int n, const void* pos_h, const 
   return 0;
 }
 
-// The persistent head (head_loop.hip) applies: fused streams bound, 2n <= 4 rows,
-// unsharded, the switches on.
-static bool head_loop_on(vv_ctx* c, int R, bool sharded) {
-  return c->hf_ready && g_head_fused && g_head_loop && !sharded && !g_chain &&
-         head_loop_fits(c->cfg.hidden, c->cfg.head_ffn, R, c->cfg.head_layers) && hl_sole(c->device);
-}
-// One persistent launch over steps [s0, min(steps, s0 + HEAD_SC)); head_mods(s0)
-// must have run on the stream before it.
-static int head_loop_launch(vv_ctx* c, const HeadRun& h, int s0, void* x_io, float cfg_scale, const float* sde_noise,
-                            hipStream_t st) {
-  const vv_config& k = c->cfg;
-  const int L = k.head_layers;
-  HeadLoopArgs A;
-  memset(&A, 0, sizeof(A));
-  A.n = h.n;
-  A.R = h.R;
-  A.s0 = s0;
-  A.s1 = std::min(c->steps, s0 + HEAD_SC);
-  A.L = L;
-  A.eps = k.head_eps;
-  A.cfg = cfg_scale;
-  A.x = (bf16*)x_io;
-  A.m1 = h.m1;
-  A.noise = sde_noise;
-  A.coef = (const DpmCoef*)c->coef_dev.p;
-  A.mods = h.mods;
-  A.modw = h.MODW;
-  A.noisy_w = W(c, "head.noisy_w");
-  A.final_w = W(c, "head.final_w");
-  for (int l = 0; l < L; ++l) {
-    const std::string p = "head." + std::to_string(l);
-    A.nw[l] = W(c, p + ".norm");
-    A.gu[l] = W(c, p + ".gu_rows");
-    A.dn[l] = W(c, p + ".dn_rows");
-  }
-  A.xh = h.xh;
-  A.lat = (bf16*)c->hl_lat.p;
-  A.slab = (float*)c->hf_slab.p;
-  A.sync = (unsigned*)c->hf_sync.p;
-  A.err = (unsigned*)c->hf_sync.p + 10 * 32;
-  A.stamps = g_head_loop_stamps;
-  const int rc = launch_head_loop(A, g_head_loop != 2, st);
-  if (rc) FAIL("persistent diffusion head: launch failed (" + std::to_string(rc) + ": " +
-               hipGetErrorString(hipGetLastError()) + ")");
-  return 0;
-}
-
-// Diagnostic (tests): 1 when vv_diffusion_sample(n) of this context would run the
-// persistent head now
-extern "C" int vv_head_loop_active(vv_ctx* c, int n) {
-  return head_loop_on(c, 2 * n, c->head_tp && (c->tp_size > 1 || c->comm)) ? 1 : 0;
-}
-
-// Diagnostic (bench.py's roofline of the persistent head): the condition rows and
-// the first HEAD_SC steps' modulations as vv_diffusion_sample sets them up, then
-// `reps` persistent launches over those steps (x_io updated by each).
-extern "C" int vv_head_loop_replay(vv_ctx* c, int n, const void* pos_h, const void* neg_h, void* x_io, float cfg_scale,
-                                   int reps, vv_stream vst) {
-  hipStream_t st = (hipStream_t)vst;
-  if (!c->finalized || c->steps == 0) FAIL("vv_head_loop_replay: engine not finalized or no schedule");
-  if (n <= 0 || n > c->cfg.max_batch) FAIL("vv_head_loop_replay: bad n");
-  if (!head_loop_on(c, 2 * n, c->head_tp && (c->tp_size > 1 || c->comm))) FAIL("vv_head_loop_replay: not applicable");
-  HeadRun h;
-  CHK(head_begin(c, n, pos_h, neg_h, h, st));
-  CHK(head_mods(c, h, 0, st));
-  for (int r = 0; r < reps; ++r) CHK(head_loop_launch(c, h, 0, x_io, cfg_scale, nullptr, st));
-  return 0;
-}
-
 int vv_tp_shard_head(vv_ctx* c, int on) {
   if (on && c->tp_size > 1 && c->cfg.head_ffn % 32) FAIL("vv_tp_shard_head: the local head FFN width must be a multiple of 32");
   c->head_tp = on ? 1 : 0;
@@ -1862,80 +1698,6 @@ int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, 
   CHK(head_begin(c, n, pos_h, neg_h, h, st));
   const int R = h.R;
   const long long MODW = h.MODW;
-  if (head_loop_on(c, R, sharded)) {
-    // every step of the diffusion in one persistent launch per HEAD_SC steps (the
-    // adaLN GEMM before it covers exactly those steps' modulations)
-    for (int s0 = 0; s0 < c->steps; s0 += HEAD_SC) {
-      CHK(head_mods(c, h, s0, st));
-      CHK(head_loop_launch(c, h, s0, x_io, cfg_scale, sde_noise, st));
-    }
-    return 0;
-  }
-  bf16 *mods = h.mods, *act = h.act, *v = h.v, *m1 = h.m1, *sa = h.sa;
-  const int F = k.head_ffn;
-  RowMap xh_m = h.xh_m;
-  if (g_chain && R <= 16 && c->steps <= HEAD_SC && !sharded && c->head_gemv) {
-    // all S steps (noisy, L x [gate|up, down], final + CFG + DPM) in one persistent launch
-    auto it = c->head_chain.find(n);
-    if (it == c->head_chain.end() || it->second.mode != g_chain) {
-      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-      HIPCHK(hipStreamIsCapturing(st, &cs));
-      if (cs == hipStreamCaptureStatusNone) {   // tables are built by an eager call, never inside a capture
-        vv_ctx::Chain& T = c->head_chain[n];
-        T.ops.release();
-        std::vector<ChainOp> ops;
-        for (int s = 0; s < c->steps; ++s) {
-          const bf16* mod = mods + (size_t)(s % HEAD_SC) * R * MODW;
-          auto add = [&](const GemmArgs& g, int bind) {
-            ChainOp op;
-            memset(&op, 0, sizeof(op));
-            op.g = g;
-            op.g.keep = 1;
-            op.bind = bind;
-            op.rep = s;
-            ops.push_back(op);
-          };
-          add(gemm_args(c, R, H, D, rowmap(nullptr, D, n, 0), W(c, "head.noisy_w"), EPI_STORE, xh_m), CH_BIND_AX);
-          for (int l = 0; l < L; ++l) {
-            const std::string p = "head." + std::to_string(l);
-            const int o = 3 * H * l;
-            GemmArgs g = gemm_args(c, R, 2 * F, H, xh_m, W(c, p + ".gu_w"), EPI_SILU_MUL, rowmap(act, F));
-            g.xf = xf_norm(W(c, p + ".norm"), k.head_eps, mod, MODW, o, o + H);
-            add(g, 0);
-            g = gemm_args(c, R, H, F, rowmap(act, F), W(c, p + ".down_w"), EPI_RES, xh_m);
-            g.epi.res = xh_m;
-            g.epi.gate = rowmap(mod + o + 2 * H, MODW);
-            add(g, 0);
-          }
-          GemmArgs g = gemm_args(c, R, D, H, xh_m, W(c, "head.final_w"), EPI_CFG_DPM, rowmap(v, D));
-          g.xf = xf_norm(nullptr, k.head_eps, mod, MODW, 3 * H * L, 3 * H * L + H);
-          g.dpm.n = n;
-          g.dpm.m1 = m1;
-          add(g, CH_BIND_DPM);
-        }
-        const int rc = chain_upload(c, ops, T);
-        if (rc < 0) return rc;
-        if (rc > 0) {   // not chainable: per-op launches below
-          T.nops = 0;
-          T.mode = g_chain;
-        }
-        it = c->head_chain.find(n);
-      }
-    }
-    if (it != c->head_chain.end() && it->second.nops > 0) {
-      KCHK(launch_head_cond(c->steps, R, H, h.condp, (const bf16*)c->temb.p, sa, st));
-      CHK(gemm(c, gemm_args(c, c->steps * R, (int)MODW, H, rowmap(sa, H), W(c, "head.ada_w"), EPI_STORE,
-                            rowmap(mods, MODW)), st));
-      ChainArgs A;
-      memset(&A, 0, sizeof(A));
-      A.x = (bf16*)x_io;
-      A.noise = sde_noise;
-      A.noise_rep = (long long)R * D;
-      A.coef = (const DpmCoef*)c->coef_dev.p;
-      A.cfg = cfg_scale;
-      return chain_launch(c, it->second, A, st);
-    }
-  }
   for (int s = 0; s < c->steps; ++s) {
     CHK(head_mods(c, h, s, st));
     CHK(head_noisy(c, h, x_io, st));

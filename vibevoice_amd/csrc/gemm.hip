@@ -1697,6 +1697,19 @@ size_t gemv_mix_lds(int M, int T, int C) {
 
 // The decode-GEMV launch plan for a (M <= 64): waves, K split, tiles per
 // workgroup; sets a.ksplit / a.handoff / a.tpw (launch_gemm, vv_gemv_plan).
+// CUs of the current device (cached per device)
+static int device_cus() {
+  static std::atomic<int> cache[16];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 0;
+  int v = cache[dev].load();
+  if (!v) {
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cache[dev] = v;
+  }
+  return v;
+}
+
 static GemmPlan gemv_resolve(GemmArgs& a) {
   const int mrep = (a.M + 15) / 16;
   GemmPlan p = gemv_plan(a.N, a.K, a.M);
@@ -1727,7 +1740,7 @@ static GemmPlan gemv_resolve(GemmArgs& a) {
   // stream per workgroup).  Balanced form: one workgroup per CU, an even share of
   // 4 or 5 tiles each, 2 waves per tile (k_gemv1<.., 5, ..>).
   if (g_gemv_bal && a.tpw == 8 && a.M >= 8 && a.xf.kind != XF_ATTN_MERGE) {
-    const int ncu = head_ffn_grid(), tiles = a.N / 16;
+    const int ncu = device_cus(), tiles = a.N / 16;
     if (ncu > 0 && (tiles + ncu - 1) / ncu == 5) {
       a.tpw = 5;
       p.nw = 10;
@@ -1735,21 +1748,6 @@ static GemmPlan gemv_resolve(GemmArgs& a) {
     }
   }
   return p;
-}
-
-// The plan launch_gemm would run for a decode GEMV on k_gemv1 (chain.hip's
-// mirror mode reproduces it bit for bit): gemv_resolve's, so one function owns
-// the plan.  Returns 1 if the shape takes another kernel.
-int gemv_plan_query(const GemmArgs& a0, int* nw, int* ksplit, int* tpw, int* fast) {
-  GemmArgs a = a0;
-  if (a.M <= 0 || a.M > 16 || a.K % 32 || a.N % 16 || a.xf.kind == XF_MIX || a.xf.kind == XF_ATTN_MERGE) return 1;
-  const GemmPlan p = gemv_resolve(a);
-  if (!gemv1_fits(a) || p.grid) return 1;   // (the chain has no balanced many-tile form)
-  *nw = p.nw;
-  *ksplit = a.ksplit;
-  *tpw = a.tpw;
-  *fast = 64 * p.nw;   // k_gemv1's fast staging: M * n8 <= 4 * blockDim.x
-  return 0;
 }
 
 // Host-only plan query (no device work; tests and tools): the kernel form and

@@ -380,17 +380,7 @@ int launch_head_noisy16(const HeadNoisyArgs& a, hipStream_t st) {
 
 bool head_m16_fits(int H, int F, int R) {
   if (H != hm::H || F != hm::F || R < 2 || R > hm::RMAX) return false;
-  static const bool ok = [] {
-    const void* k = (const void*)k_head_m16;
-    hipFuncAttributes fa{};
-    int nb = 0, dev = 0, cus = 0;
-    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, hm::TOTAL) != hipSuccess ||
-        hipFuncGetAttributes(&fa, k) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, hm::NT, hm::TOTAL) != hipSuccess ||
-        hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return false;
-    return fa.localSizeBytes == 0 && nb >= 1 && cus >= hm::G;
-  }();
+  static const bool ok = persist_resident_kernel((const void*)k_head_m16, hm::NT, hm::TOTAL, hm::G);
   return ok;
 }
 

@@ -189,67 +189,18 @@ struct SumRows {
   bf16* p[8];
 };
 
-// ---- persistent GEMV chains (chain.hip)
-constexpr int CH_TMAX = 256;     // split-segment tiles of one op (ticket words per op)
-enum { CH_BIND_AX = 1, CH_BIND_DPM = 2 };   // per-call operands bound at launch (ChainArgs)
 
-struct ChainOp {
-  int xf, fast, bind, rep;  // A transform; k_gemv1 staging: fast path iff M * K_split / 8 <= 4 * fast;
-                            // CH_BIND_*; diffusion step of the op
-  int t1, tpw, kw;          // tiles [0, t1): units of tpw whole tiles, kw waves per tile
-  int ks2, kw2;             // tiles [t1, N/16): split ks2 ways along K, kw2 waves per split
-  int nu1, nunit;           // whole-tile units; all units
-  unsigned target;          // done[] count of a finished op (its tiles)
-  long long slab_off;       // floats into ChainArgs::slabs (split segment: [tile - t1][ks][256])
-  int ticket_off, pad_;     // words into ChainArgs::tickets (split segment: [tile - t1])
-  GemmArgs g;
-};
-
-struct ChainArgs {
-  const ChainOp* ops;
-  int nops, pad_;
-  unsigned* done;           // [nops][9][32]: 8 shard + 1 top counter lines per op, zeroed before every launch
-  unsigned* tickets;        // split-segment tiles of every op, zeroed before every launch
-  float* slabs;
-  unsigned* err;            // != 0: a wait gave up (1 + the op it waited for)
-  bf16* x;                  // CH_BIND_AX: A rows base; CH_BIND_DPM: the latents updated in place
-  const float* noise;       // CH_BIND_DPM: sde noise of step s at noise + s * noise_rep, or nullptr
-  long long noise_rep;
-  const DpmCoef* coef;      // CH_BIND_DPM: per-step coefficients (cfg from `cfg`)
-  float cfg;
-  int pad2_;
-  unsigned long long* stamps;   // diagnostics (tools/chain_bench.py): [G][nops][4] s_memrealtime, or nullptr
-};
-
-size_t chain_plan_op(ChainOp* op, int G, int mode);
-int chain_grid();
-int launch_chain(const ChainArgs& A, size_t lds, hipStream_t st);
-// the per-op kernel's plan for a decode GEMV (gemm.hip): 0 and the plan when it runs k_gemv1
-// (*fast = its workgroup's threads)
-int gemv_plan_query(const GemmArgs& a, int* nw, int* ksplit, int* tpw, int* fast);
-
-// ---- fused diffusion-head FFN layer (head_ffn.hip): modulate(norm(x)) -> gate|up
-// -> SiLU*up -> down -> x += gate * (.), one launch per layer at 2n <= 4 rows
-struct HeadFfnArgs {
-  const bf16* x;            // [R][H] rows (ld ldx), read for the norm
-  bf16* out;                // [R][H] rows (ld ldx): x + gate * ffn (in place: out == x)
-  const bf16* res;          // residual rows (ld ldres): x, or zero rows on a sharded rank > 0
-  const bf16* nw;           // RMSNorm weight [H]
-  const bf16* mod;          // adaLN rows [R][ldmod]: shift / scale / gate at the offsets
-  long long ldx, ldres, ldmod;
-  int shift_off, scale_off, gate_off, R;
-  float eps;
-  int pad_;
-  const bf16* gu;           // gate / up rows in the kernel's stream order (weights.py: head_ffn_pack)
-  const bf16* dn;           // down_proj transposed: [F][H]
-  float* slab;              // [G][R][H] fp32 partial sums of down, one per workgroup
-  unsigned* sync;           // 10 lines of 32 words: 8 shard counters, top counter, generation
-  unsigned* err;            // set to 1 when the grid wait gave up
-  unsigned long long* stamps;   // diagnostics (tools/head_ffn_stamps.py): [G][8] s_memrealtime, or nullptr
-};
-bool head_ffn_fits(int H, int F, int R);
-int head_ffn_grid();
-int launch_head_ffn(const HeadFfnArgs& a, hipStream_t st);
+// ---- the one-launch kernels with grid-wide waits (persist_dev.h): k_head_m16,
+// k_lm_ffn, k_codec_stage*.  Residency rule: every workgroup of the grid must be
+// resident at once -- the occupancy query's blocks per CU times the device's CUs
+// covers the grid, and no scratch (a wave waiting for a scratch slot is not
+// resident).  The engine also requires the context to be the device's only
+// registered one and the kernels switched on (vv_persist_decision).
+inline bool persist_resident(int blocks_per_cu, int cus, long long scratch_bytes, int grid) {
+  return scratch_bytes == 0 && blocks_per_cu >= 1 && (long long)blocks_per_cu * cus >= grid;
+}
+// the occupancy query of kernel k (nt threads, lds bytes of dynamic LDS) -> persist_resident
+bool persist_resident_kernel(const void* k, int nt, int lds, int grid);
 
 // ---- one head FFN layer at 2 <= 2n <= 16 rows in one launch (head_m16.hip), GEMV layout weights
 struct HeadM16Args {
@@ -307,33 +258,6 @@ struct LmFfnArgs {
 };
 bool lm_ffn_fits(int H, int F, int R);
 int launch_lm_ffn(const LmFfnArgs& a, hipStream_t st);
-
-// ---- the whole diffusion of a token in one persistent launch (head_loop.hip):
-// steps [s0, s1) of noisy -> L FFN layers -> final + CFG + DPM-Solver++ at 2n <= 4 rows
-struct HeadLoopArgs {
-  int n, R, s0, s1, L, pad_;
-  float eps, cfg;
-  bf16* x;                  // [n][D] latents: in (noise / current), out (after step s1 - 1)
-  bf16* m1;                 // [n][D] previous x0 (2nd-order history), in / out
-  const float* noise;       // sde-dpmsolver++: step s's [2n][D] fp32 at noise + s*2n*D; nullptr (ODE)
-  const DpmCoef* coef;      // [steps] (cfg from `cfg`)
-  const bf16* mods;         // step s's adaLN rows [2n][modw] at mods + (s - s0) * 2n * modw
-  long long modw;
-  const bf16* noisy_w;      // [H][D] MFMA-packed
-  const bf16* final_w;      // [D][H] MFMA-packed
-  const bf16* nw[4];        // per-layer RMSNorm weights [H]
-  const bf16* gu[4];        // gate / up rows in head_ffn_pack's stream order
-  const bf16* dn[4];        // down_proj^T [F][H]
-  bf16* xh;                 // [2n][H] state (workspace)
-  bf16* lat;                // [D][2] latents of the previous step (workspace; hand-off)
-  float* slab;              // [G][2n][H] fp32 partials of down (workspace)
-  unsigned* sync;           // 12 lines of 32 words: 8 shard counters, (k_head_ffn's two), error word, generation
-  unsigned* err;            // set to 1 when a grid wait gave up
-  unsigned long long* stamps;   // diagnostics: [G][64] s_memrealtime per phase, or nullptr
-};
-bool head_loop_fits(int H, int F, int R, int L);
-int head_loop_grid();
-int launch_head_loop(const HeadLoopArgs& a, bool coop, hipStream_t st);
 
 // A whole codec stage of Block1Ds for one sample in ONE persistent launch
 // (codec_stage.hip): C = 2,048 at T = 1, C = 1,024 at T = 2 or 8.

@@ -238,17 +238,7 @@ __global__ void __launch_bounds__(lf::NT) k_lm_ffn(LmFfnArgs a) {
 
 bool lm_ffn_fits(int H, int F, int R) {
   if (H != lf::H || F != lf::F || R < 1 || R > lf::RMAX) return false;
-  static const bool ok = [] {
-    hipFuncAttributes fa{};
-    int nb = 0, dev = 0, cus = 0;
-    const void* k = (const void*)k_lm_ffn;
-    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lf::TOTAL) != hipSuccess ||
-        hipFuncGetAttributes(&fa, k) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, lf::NT, lf::TOTAL) != hipSuccess ||
-        hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return false;
-    return fa.localSizeBytes == 0 && nb >= 1 && cus >= lf::G;
-  }();
+  static const bool ok = persist_resident_kernel((const void*)k_lm_ffn, lf::NT, lf::TOTAL, lf::G);
   return ok;
 }
 

@@ -10,7 +10,7 @@ import torch
 from . import _lib
 from .config import VibeVoiceConfig
 from .schedule import Schedule
-from .weights import codec_channels, head_layout_for, head_tp_check, pack
+from .weights import codec_channels, head_tp_check, pack
 
 _VALID_IDS_DEFAULT = None
 
@@ -65,7 +65,7 @@ class Engine:
 
     def __init__(self, cfg: VibeVoiceConfig, state_dict, device="cuda", max_batch=1, max_ctx=4096,
                  valid_ids=None, tp_rank=0, tp_size=1, tp_unique_id=None, packed=None, tp_head=False,
-                 head_layout=None):
+                 persistent=True):
         """tp_size > 1: rank tp_rank's shard of the LM; tp_unique_id (bytes of
         vv_tp_unique_id, shared by the group) creates its RCCL communicator, None
         leaves it for a single-process group (lm_forward_group).
@@ -74,9 +74,10 @@ class Engine:
         weights (the standalone tokenizer API's own codec slots).
         tp_head: shard the diffusion head's FFN over the TP group as well
         (vv_tp_shard_head).
-        head_layout: the head FFN weights' layout (weights.head_layout_for by
-        default: one copy, the one this capacity runs; "both" for tests that
-        switch paths on one engine)."""
+        persistent: False keeps this context off the grid-waiting one-launch
+        kernels (vv_set_persistent): it then neither runs them nor counts as a
+        second context of the device (the standalone tokenizer API's codec
+        context)."""
         L = _lib.lib()
         self.cfg = cfg
         self.device = torch.device(device)
@@ -92,10 +93,8 @@ class Engine:
         if self.tp_head:
             head_tp_check(cfg, tp_size)
         with torch.cuda.device(self.device):
-            layout = head_layout or head_layout_for(cfg, max_batch, tp_size, self.tp_head)
             self.w = packed if packed is not None else pack(state_dict, cfg, self.device, tp_rank=tp_rank,
-                                                            tp_size=tp_size, tp_head=self.tp_head,
-                                                            head_layout=layout)
+                                                            tp_size=tp_size, tp_head=self.tp_head)
             h = ctypes.c_void_p()
             self._ecfg = engine_config(cfg, max_batch, max_ctx, tp_size, self.tp_head)
             _lib.check(L.vv_create(ctypes.byref(self._ecfg), self.device.index or 0, ctypes.byref(h)), "create")
@@ -106,6 +105,8 @@ class Engine:
                 _lib.check(L.vv_tp_init(h, tp_rank, tp_size, uid), "tp_init")
                 if self.tp_head:
                     _lib.check(L.vv_tp_shard_head(h, 1), "tp_shard_head")
+            if not persistent:
+                _lib.check(L.vv_set_persistent(h, 0), "set_persistent")
             for name, t in self.w.items():
                 shape = (ctypes.c_int64 * max(1, t.dim()))(*t.shape)
                 _lib.check(L.vv_bind_weight(h, name.encode(), _ptr(t), shape, t.dim()), f"bind {name}")
@@ -134,14 +135,23 @@ class Engine:
         self.n_valid = len(ids)
 
     def check_sync(self):
-        """Raise if a fused head layer's in-launch grid wait gave up since the
-        last check (its outputs are then invalid; vv_sync_error).  Synchronises."""
+        """Raise if a grid-waiting kernel's in-launch wait gave up since the last
+        check (its outputs are then invalid; vv_sync_error, which also resets the
+        wait counters).  Synchronises."""
         r = _lib.lib().vv_sync_error(self.h)
         if r < 0:
             _lib.check(r, "sync_error")
         if r:
-            raise RuntimeError("fused diffusion-head layer: an in-launch grid wait gave up (workgroups not "
-                               "co-resident); the outputs since the last check are invalid")
+            raise RuntimeError("one-launch kernel: an in-launch grid wait gave up (workgroups not co-resident); "
+                               "the outputs since the last check are invalid")
+
+    def sync_reset(self):
+        """Zero every grid-wait counter of this context (vv_sync_reset; after a
+        wait gave up).  Synchronises the device."""
+        _lib.check(_lib.lib().vv_sync_reset(self.h), "sync_reset")
+
+    def persistent_active(self):
+        return _lib.lib().vv_persistent_active(self.h) == 1
 
     def sync_error_async(self, dst, stream=None):
         """Queue on the stream a copy of the grid-wait error word into dst (a

@@ -173,15 +173,15 @@ class VibeVoiceTokenConstraintProcessor:
 
 class VibeVoiceForConditionalGenerationInference:
     def __init__(self, config: VibeVoiceConfig, state_dict, device="cuda", attn_implementation="hip",
-                 max_batch=8, max_ctx=8192, tp_group=None, tp_head=None, head_layout=None):
+                 max_batch=8, max_ctx=8192, tp_group=None, tp_head=None, persistent=True):
         """tp_group: a torch.distributed process group whose ranks (one per GPU)
         tensor-parallel-shard the Qwen2 backbone over RCCL; every
         rank then runs generate() on the same inputs (SPMD) and gets the same
         result.  None: the whole model on this GPU.  tp_head: shard the
         diffusion head's FFN over the group too (None: when its per-step
-        weights exceed the Infinity Cache, i.e. VibeVoice-Large).  head_layout:
-        the head FFN weights' layout (None: weights.head_layout_for; "fused" for
-        the persistent head loop at max_batch <= 2)."""
+        weights exceed the Infinity Cache, i.e. VibeVoice-Large).  persistent:
+        False keeps the engine off the grid-waiting one-launch kernels
+        (vv_set_persistent; for a GPU shared by several processes)."""
         self.config = config
         self.attn_implementation = attn_implementation
         self.device = torch.device(device)
@@ -199,7 +199,7 @@ class VibeVoiceForConditionalGenerationInference:
         self.tp_head = head_tp_default(config, tp_size) if tp_head is None else bool(tp_head and tp_size > 1)
         self.engine = Engine(config, state_dict, self.device, max_batch=max_batch, tp_head=self.tp_head,
                              max_ctx=min(max_ctx, config.decoder_config.max_position_embeddings),
-                             tp_rank=tp_rank, tp_size=tp_size, tp_unique_id=uid, head_layout=head_layout)
+                             tp_rank=tp_rank, tp_size=tp_size, tp_unique_id=uid, persistent=persistent)
         self.ddpm_inference_steps = config.diffusion_head_config.ddpm_num_inference_steps
         self.model = _ModelView(self)
         self.use_graphs = True          # capture the steady-state loop body into hipGraphs
@@ -487,6 +487,7 @@ class GenerateSession:
         # only once the word covering its diffusion has been read as clear
         self.err_pin = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         self.err_ready = torch.cuda.Event()
+        self.err_queued = False      # a copy of the word is queued and err_pin not yet checked
         self.pending_put = None
         self.graphs = model._graph_cache
         self.seen = model._graph_seen
@@ -629,13 +630,25 @@ class GenerateSession:
         return rows, state
 
     def _check_err(self):
-        """Raise if the error word read back last (err_pin) is set: a fused head
-        layer's in-launch grid wait gave up, the latents of that step are invalid."""
+        """Raise if the error word read back last (err_pin) is set: a one-launch
+        kernel's in-launch grid wait gave up, the latents / audio of that step are
+        invalid.  The wait counters that launch left part-advanced are reset
+        first (vv_sync_reset), so the next generate() starts from a clean state."""
+        self.err_queued = False
         if int(self.err_pin[0]):
             self.pending_put = None
             self.done = True
-            raise RuntimeError("fused diffusion-head layer: an in-launch grid wait gave up (workgroups not "
-                               "co-resident); this step's latents and audio are invalid and were not streamed")
+            self.err_pin.zero_()
+            self.eng.sync_reset()
+            raise RuntimeError("one-launch kernel: an in-launch grid wait gave up (workgroups not co-resident); "
+                               "this step's latents and audio are invalid and were not streamed")
+
+    def _drain_err(self):
+        """Wait for the last queued error-word copy (if any) and check it: the
+        loop's exits, where no later logits read-back covers it."""
+        if self.err_queued:
+            self.err_ready.synchronize()
+            self._check_err()
 
     def _flush_audio(self, sync):
         """Put the previous diffusion step's audio into the streamer once the
@@ -662,6 +675,7 @@ class GenerateSession:
         does nothing) once the loop has ended."""
         if self.done or self.step_idx >= self.max_steps:
             self.done = True
+            self._drain_err()
             return False
         B, eng, dev, step = self.B, self.eng, self.dev, self.step_idx
         st = self.audio_streamer
@@ -670,16 +684,20 @@ class GenerateSession:
                 self._flush_audio(sync=True)
                 st.end()
             self.done = True
+            self._drain_err()
             return False
         if st is not None and any(getattr(st, "finished_flags", [])):     # :443-447
             self.done = True
+            self._drain_err()
             return False
         if bool(self.finished.all()):                                      # :449
             self.done = True
+            self._drain_err()
             return False
         if self.L + step >= self.max_length:                               # :454-459
             self.reach_max[~self.finished] = True
             self.done = True
+            self._drain_err()
             return False
         if step > 0:
             if not self.pos_pushed:   # normally sent with the previous step's ids (_push_controls)
@@ -765,6 +783,7 @@ class GenerateSession:
             audio = self.audio_dev[:n].clone()
             self.eng.sync_error_async(self.err_pin)
             self.err_ready.record()
+            self.err_queued = True
             for i, b in enumerate(didx.tolist()):
                 self.audio_chunks[b].append(audio[i:i + 1])
             if st is not None:      # streamed once the next read-back shows the error word clear
@@ -781,6 +800,7 @@ class GenerateSession:
     def result(self, return_speech=True):
         if self.pending_put is not None:
             self._flush_audio(sync=True)
+        self._drain_err()            # with or without a streamer: the last step's word
         self.eng.check_sync()
         if self.audio_streamer is not None:
             self.audio_streamer.end()

@@ -96,8 +96,10 @@ class _SlotPool:
             m = self.model.engine
             # same TP coordinates as the owner: its packed LM weights are this rank's shards
             # (no communicator: the views only run the replicated codec / connectors)
+            # (persistent=False: this codec context neither demotes the model's own
+            # context from the one-launch kernels nor contends with them)
             self._eng = Engine(self.model.config, None, m.device, max_batch=self.n, max_ctx=64, packed=m.w,
-                               tp_rank=m.tp_rank, tp_size=m.tp_size, tp_head=m.tp_head)
+                               tp_rank=m.tp_rank, tp_size=m.tp_size, tp_head=m.tp_head, persistent=False)
         return self._eng
 
     def _i32(self, xs):

@@ -189,31 +189,6 @@ def _gu(gate, up):
     return torch.stack([gate.reshape(I // 8, 8, H), up.reshape(I // 8, 8, H)], dim=1).reshape(2 * I, H)
 
 
-# The fused head FFN layer (csrc/head_ffn.hip) at its one instantiated shape:
-# G = 256 workgroups, each owning F / G hidden units, 16 lanes per gate / up row.
-HEAD_FFN_SHAPE = (1536, 4608)   # (hidden, head FFN width)
-
-
-def head_ffn_pack(gate, up, G=256, KS=16):
-    """gate / up [F, H] -> head_ffn.hip's stream order, returned as [2F, H]:
-    workgroup w's block [CPT][NT][8] holds, at (i, t = rho * KS + kap), the
-    8 columns of chunk i * KS + kap of row rho (rho = 2u: gate of hidden unit
-    w * F / G + u, 2u + 1: its up)."""
-    F, H = gate.shape
-    HPW, CPT = F // G, H // 8 // KS
-    x = torch.stack([gate.reshape(G, HPW, CPT, KS, 8), up.reshape(G, HPW, CPT, KS, 8)], dim=2)
-    return x.permute(0, 3, 1, 2, 4, 5).contiguous().reshape(2 * F, H)
-
-
-def head_ffn_unpack(p, G=256, KS=16):
-    """Inverse of head_ffn_pack: -> (gate, up)."""
-    F2, H = p.shape
-    F = F2 // 2
-    HPW, CPT = F // G, H // 8 // KS
-    x = p.reshape(G, CPT, HPW, 2, KS, 8).permute(0, 2, 3, 1, 4, 5)
-    return x[:, :, 0].reshape(F, H), x[:, :, 1].reshape(F, H)
-
-
 def mfma_pack(w):
     """[N, K] -> the same shape in MFMA-fragment order (csrc/gemm.hip header):
     block (tile t, chunk c) of 16 rows x 32 columns is 1 KB contiguous, lane l
@@ -291,24 +266,12 @@ def head_tp_default(cfg: VibeVoiceConfig, tp_size):
     return tp_size > 1 and hc.head_layers * 3 * F * hc.hidden_size * 2 > (192 << 20)
 
 
-def head_layout_for(cfg: VibeVoiceConfig, max_batch, tp_size=1, tp_head=False):
-    """The diffusion head FFN's weight layout an engine of this capacity packs
-    (ONE copy resident): "gemv" (head.<l>.gu_w / down_w, MFMA
-    packed) at every batch size.  It feeds the one-launch layer of head_m16.hip
-    (2 <= 2n <= 16 rows) and the GEMV pair beyond; at B = 1 that path measured
-    3.095 ms per step against 3.18-3.23 ms for the persistent head loop on the
-    "fused" streams (head.<l>.gu_rows / dn_rows; same-box interleaved A/B,
-    profiles/r05_ab_head_layout.txt), which stay available as head_layout="fused"
-    (or "both") for the 2n <= 4 kernels (k_head_ffn, k_head_loop)."""
-    return "gemv"
-
-
-def pack(sd, cfg: VibeVoiceConfig, device, with_acoustic_encoder=True, tp_rank=0, tp_size=1, tp_head=False,
-         head_layout="both"):
+def pack(sd, cfg: VibeVoiceConfig, device, with_acoustic_encoder=True, tp_rank=0, tp_size=1, tp_head=False):
     """Reference state dict -> {engine name: contiguous device tensor}.
 
-    head_layout: "gemv", "fused" (head_layout_for) or "both" (tests that switch
-    between the two paths on one engine; byte accounting).
+    The diffusion head's FFN is packed once, in the GEMV layout (gate|up tiles of
+    8 gate + 8 up rows, MFMA-packed): k_head_m16 at 2 <= 2n <= 16 rows and the
+    GEMV pair beyond read the same copy.
 
     tp_size > 1: this rank's Megatron shard of the Qwen2 layers
     (configuration_vibevoice.py:175-183): q/k/v rows of its heads and
@@ -368,14 +331,8 @@ def pack(sd, cfg: VibeVoiceConfig, device, with_acoustic_encoder=True, tp_rank=0
     for i in range(hc.head_layers):
         p = f"{HEAD}layers.{i}."
         out[f"head.{i}.norm"] = t(sd[p + "norm.weight"])
-        fits = (hc.hidden_size, hs.stop - hs.start) == HEAD_FFN_SHAPE
-        if head_layout != "fused" or not fits:
-            out[f"head.{i}.gu_w"] = t(_gu(sd[p + "ffn.gate_proj.weight"][hs], sd[p + "ffn.up_proj.weight"][hs]))
-            out[f"head.{i}.down_w"] = t(sd[p + "ffn.down_proj.weight"][:, hs])
-        if head_layout != "gemv" and fits:   # the fused layer's streams
-            out[f"head.{i}.gu_rows"] = t(head_ffn_pack(sd[p + "ffn.gate_proj.weight"][hs],
-                                                       sd[p + "ffn.up_proj.weight"][hs]))
-            out[f"head.{i}.dn_rows"] = t(sd[p + "ffn.down_proj.weight"][:, hs].t())
+        out[f"head.{i}.gu_w"] = t(_gu(sd[p + "ffn.gate_proj.weight"][hs], sd[p + "ffn.up_proj.weight"][hs]))
+        out[f"head.{i}.down_w"] = t(sd[p + "ffn.down_proj.weight"][:, hs])
     out["head.final_w"] = t(sd[HEAD + "final_layer.linear.weight"])
 
     for src, dst in (("acoustic", "ac"), ("semantic", "se")):
