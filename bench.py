@@ -387,28 +387,25 @@ def pick_roofline(*cands):
     return (c[0] if c else None), (c[1] if len(c) > 1 else None)
 
 
-# the committed step profile of this round (tools/prof_step.sh: rocprofv3 --kernel-trace --stats over
-# graph-replayed loop steps) per batch: its per-kernel averages are the in-loop figures
-STEP_PROFILE = {1: "r06_kernel_stats_b1.csv", 8: "r06_kernel_stats_b8.csv"}
+# the committed step profile of this round per batch (tools/prof_step.sh: rocprofv3 --kernel-trace over
+# bench.py's timed loop, profiles/summarize.py over its last 20 steps): the per-kernel averages in the loop
+STEP_PROFILE = {1: "r06_step_kernels_b1.json", 8: "r06_step_kernels_b8.json"}
 
 
 def in_loop_average(r, B):
-    """Beside the isolated replay: the kernel's average duration in the loop
-    itself, from the committed rocprofv3 step profile (if one exists for this
-    batch), and the roofline fraction at that average."""
+    """Beside the isolated replay: the kernel's average duration inside the loop
+    itself, from the committed step profile for this batch (if one exists), and
+    the roofline fraction at that average."""
     name = STEP_PROFILE.get(B)
     path = os.path.join(ROOT, "profiles", name) if name else None
     if not path or not os.path.exists(path):
         return
-    import csv
-    kern = r["kernel"].split(" (")[0]
     with open(path) as f:
-        for row in csv.DictReader(f):
-            if row.get("Name", "").split("(")[0].strip() == kern.split("(")[0].strip():
-                avg_us = float(row["AverageNs"]) / 1e3
-                r["in_loop"] = dict(avg_us=round(avg_us, 2), source=f"profiles/{name}",
-                                    frac=round(r["alg_bytes_per_launch"] / (avg_us * 1e-6) / 1e9 / r["peak"], 4))
-                return
+        prof = json.load(f)["kernels"]
+    k = prof.get(r["kernel"].split(" (")[0])
+    if k:
+        r["in_loop"] = dict(avg_us=k["avg_us"], us_per_step=k["us_per_step"], source=f"profiles/{name}",
+                            frac=round(r["alg_bytes_per_launch"] / (k["avg_us"] * 1e-6) / 1e9 / r["peak"], 4))
 
 
 # ------------------------------------------------------------------ TP collective share

@@ -149,6 +149,11 @@ int vv_diag_sync_words(vv_ctx* ctx, unsigned* out);
  * is resident, the context has the kernels enabled and it is the device's only
  * registered context.  Pure function (no device work). */
 int vv_persist_decision(int blocks_per_cu, int cus, int scratch_bytes, int grid, int contexts_on_device, int enabled);
+/* A/B / test switch: 1 (default) = each narrow codec stage (C <= 128) as ONE
+ * launch (codec_tile.hip: transition conv + 3 Block1Ds [+ head conv], halo
+ * recomputed per workgroup); 0 = one k_block launch per Block1D + the
+ * transition GEMMs. */
+int vv_codec_tile(int on);
 /* A/B switch: 1 (default) = the balanced many-tile GEMV plan at M >= 8 (one
  * workgroup per CU, 4-5 weight tiles each); 0 = ntile / 8 workgroups. */
 int vv_gemv_tune_bal(int on);

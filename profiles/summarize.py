@@ -3,8 +3,11 @@
 Steps are delimited by the restricted lm_head launch (k_final_head, one per LM
 pass).  For the last N steps it reports GPU busy time, wall time, idle gap and
 the per-kernel (name, grid) breakdown, plus each kernel's average duration.
-Usage: python profiles/summarize.py <run_kernel_trace.csv> [n_steps]
+Usage: python profiles/summarize.py <run_kernel_trace.csv> [n_steps] [out.json]
+(out.json: {kernel: {calls_per_step, us_per_step, avg_us}} of those steps -- the
+in-loop figures bench.py reports beside its isolated replays.)
 """
+import json
 import collections
 import csv
 import re
@@ -23,7 +26,7 @@ def short(name):
     return n[:60]
 
 
-def main(path, n_steps=None):
+def main(path, n_steps=None, out_json=None):
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
@@ -51,6 +54,11 @@ def main(path, n_steps=None):
     for (n, g), (c, t) in per.items():
         byname[n][0] += c
         byname[n][1] += t
+    if out_json:
+        with open(out_json, "w") as f:
+            json.dump({"steps": k, "busy_us_per_step": round(busy / k / 1e3, 1), "wall_us_per_step": round(wall / k / 1e3, 1),
+                       "kernels": {n: {"calls_per_step": round(c / k, 2), "us_per_step": round(t / k / 1e3, 2),
+                                       "avg_us": round(t / c / 1e3, 3)} for n, (c, t) in byname.items()}}, f, indent=1)
     print(f"{'kernel':60s} {'calls/step':>10s} {'us/step':>9s} {'avg us':>8s}")
     for n, (c, t) in sorted(byname.items(), key=lambda x: -x[1][1]):
         print(f"{n:60s} {c / k:10.1f} {t / k / 1e3:9.1f} {t / c / 1e3:8.2f}")
@@ -60,4 +68,4 @@ def main(path, n_steps=None):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else None)
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else None, sys.argv[3] if len(sys.argv) > 3 else None)

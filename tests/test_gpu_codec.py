@@ -258,3 +258,60 @@ def test_codec_stage_only_for_the_devices_sole_context():
     for x, y in zip(solo, again):
         assert torch.equal(x, y)
     a.close()
+
+
+@pytest.mark.parametrize("slots_sched", [[[1]] * 4, [[0, 2], [0, 1, 2], [2], [0, 1, 2]]])
+def test_codec_tile_narrow_stages(slots_sched):
+    """The narrow stages (C = 128 / 64 / 32) as ONE launch each (codec_tile.hip:
+    transition conv + 3 Block1Ds [+ head conv], each workgroup recomputing its
+    causal halo; 6 launches per codec step instead of 24) vs the oracle and vs
+    the launch-per-Block1D path, over four streamed frames -- one sample, and
+    several samples with a slot skipping frames (its conv histories must not
+    move) -- and bitwise equal run to run.  Both paths are bf16 chains 60+ layers
+    deep that sum the transition convs in different orders: the codec tolerance
+    (rel L2 < 3e-2, cosine > 0.999) against the oracle and against each other."""
+    from vibevoice_amd import _lib
+    L = _lib.lib()
+    cfg = tiny_config(ratios=(8, 5, 5, 4, 2, 2), depths="3-3-3-3-3-3-8", nf=32)
+    sd = synthetic_state_dict(cfg, seed=3, device="cpu", mode="test", with_acoustic_encoder=False)
+    eng = Engine(cfg, sd, dev, max_batch=3, max_ctx=64)
+    H = cfg.decoder_config.hidden_size
+    dd = ocodec.codec_dims(cfg.acoustic_tokenizer_config, "decoder")
+    ed = ocodec.codec_dims(cfg.semantic_tokenizer_config, "encoder")
+    sd_a, sd_s = sub(sd, "model.acoustic_tokenizer."), sub(sd, "model.semantic_tokenizer.")
+    s_f, b_f = sd["model.speech_scaling_factor"], sd["model.speech_bias_factor"]
+    g = torch.Generator().manual_seed(23)
+    lats = [torch.randn(len(s), 64, generator=g).bfloat16() for s in slots_sched]
+    outs = {}
+    try:
+        for mode in (1, 0, 1):
+            L.vv_codec_tile(mode)
+            eng.codec_reset(torch.arange(3, dtype=torch.int32, device=dev))
+            res = []
+            for slots, lat in zip(slots_sched, lats):
+                n = len(slots)
+                sl = torch.tensor(slots, dtype=torch.int32, device=dev)
+                audio = torch.empty(n, cfg.hop, dtype=torch.bfloat16, device=dev)
+                sem = torch.empty(n, 128, dtype=torch.bfloat16, device=dev)
+                emb = torch.zeros(3, H, dtype=torch.bfloat16, device=dev)
+                eng.codec_step(sl, lat.to(dev), audio, sem, emb, sl)
+                res.append((audio, sem, emb[sl.long()]))
+            torch.cuda.synchronize()
+            outs.setdefault(mode, []).append(res)
+    finally:
+        L.vv_codec_tile(1)
+    eng.check_sync()
+    st_a, st_s = ocodec.StreamState(3), ocodec.StreamState(3)
+    for f, (slots, lat) in enumerate(zip(slots_sched, lats)):
+        idx = torch.tensor(slots)
+        a_ref = ocodec.decode(sd_a, dd, (lat / s_f - b_f).unsqueeze(-1), st_a, idx)
+        s_ref = ocodec.encode(sd_s, ed, a_ref, st_s, idx)[:, 0]
+        e_ref = connector(sd, "model.acoustic_connector.", lat) + connector(sd, "model.semantic_connector.", s_ref)
+        for k, (name, ref) in enumerate((("audio", a_ref[:, 0]), ("sem", s_ref), ("emb", e_ref))):
+            got, base, again = outs[1][0][f][k], outs[0][0][f][k], outs[1][1][f][k]
+            e_o, e_b = rel_err(got, ref), rel_err(got, base)
+            print(f"frame {f} slots {slots} {name}: rel {e_o:.3e} vs oracle ({rel_err(base, ref):.3e} per-block "
+                  f"path), {e_b:.3e} vs the per-block path")
+            assert torch.equal(got, again), (f, name)
+            assert e_o < 3e-2 and cos(got, ref) > 0.999, (f, name, e_o)
+            assert e_b < 3e-2 and cos(got, base) > 0.999, (f, name, e_b)

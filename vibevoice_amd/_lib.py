@@ -78,6 +78,7 @@ EXPORTS = [
     ("vv_attn_prefill", I, [I]),
     ("vv_codec_mix_fusion", I, [I]),
     ("vv_codec_stage", I, [I]),
+    ("vv_codec_tile", I, [I]),
     ("vv_head_m16", I, [I]),
     ("vv_head_m16_active", I, [P, I]),
     ("vv_head_m16_stamps", I, [P]),

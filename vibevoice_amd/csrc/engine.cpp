@@ -507,6 +507,28 @@ extern "C" int vv_codec_stage_active(vv_ctx* c) {
   return c && c->finalized && codec_stage_on(c, c->dec, 0, 1) ? 1 : 0;
 }
 
+// The narrow stages (C <= 128) as ONE launch each (codec_tile.hip: transition
+// conv + three Block1Ds [+ the decoder's head conv], halo recomputed per
+// workgroup); 0 = k_block per Block1D + the transition GEMMs (A/B and tests).
+static std::atomic<int> g_codec_tile{1};
+extern "C" int vv_codec_tile(int on) {
+  g_codec_tile = on ? 1 : 0;
+  return 0;
+}
+// the transition fused into stage i's tile launch (CT_PRE_*), or -1: none applies
+static int tile_pre(const ConvNet& net, int i) {
+  const int C = net.chans[i];
+  int pre = CT_PRE_NONE;
+  if (net.decoder && i > 0 && net.rat[i] == 2 && net.chans[i - 1] == 2 * C) pre = CT_PRE_CONVT;
+  if (!net.decoder && i > 0 && net.rat[i] == 2 && 2 * net.chans[i - 1] == C) pre = CT_PRE_SCONV;
+  if (!net.decoder && i == 0 && net.in_ch == 1) pre = CT_PRE_STEM;
+  if (net.decoder && i == 0) return -1;   // (the decoder's stem stage is the widest)
+  const int post = net.decoder && i == net.nst - 1 ? CT_POST_HEAD : CT_POST_NONE;
+  if (!g_codec_tile || !codec_tile_fits(C, pre, post, net.depth[i], net.mix[i].empty() ? 0 : net.mix[i][0].ctx))
+    return -1;
+  return pre;
+}
+
 // diffusion steps whose adaLN modulations are computed in one GEMM
 static constexpr int HEAD_SC = 16;
 
@@ -517,8 +539,8 @@ static int convnet_run(vv_ctx* c, ConvNet& net, int n, const int* slots, RowMap 
   const std::string& p = net.wp;
   const float eps = c->cfg.codec_eps;
   const int k = 7;
-  // ---- stem
-  {
+  // ---- stem (the encoders' is fused into stage 0's tile launch where it applies)
+  if (net.decoder || tile_pre(net, 0) != CT_PRE_STEM) {
     const int T = net.T[0], C = net.chans[0];
     RowMap xo = rowmap(net.X[0], C, T, (long long)T * C);
     if (net.decoder) {
@@ -537,10 +559,12 @@ static int convnet_run(vv_ctx* c, ConvNet& net, int n, const int* slots, RowMap 
       KCHK(launch_conv_cin1(a, st));
     }
   }
+  bool head_done = false;
   for (int i = 0; i < net.nst; ++i) {
     const int T = net.T[i], C = net.chans[i];
     RowMap X = rowmap(net.X[i], C, T, (long long)T * C);
-    if (i > 0) {
+    const int tpre = tile_pre(net, i);
+    if (i > 0 && tpre != CT_PRE_CONVT && tpre != CT_PRE_SCONV) {
       const ConvBuf& tb = net.tr[i];
       const int Ci = net.chans[i - 1], r = net.rat[i];
       const std::string t = p + ".tr" + std::to_string(i);
@@ -556,6 +580,61 @@ static int convnet_run(vv_ctx* c, ConvNet& net, int n, const int* slots, RowMap 
         GemmArgs g = gemm_args(c, n * T, C, 2 * r * Ci, a, W(c, t + "_w"), EPI_STORE, X, W(c, t + "_b"));
         CHK(gemm(c, g, st));
       }
+    }
+    if (tpre >= 0) {
+      // the whole narrow stage in one launch (codec_tile.hip)
+      CodecTileArgs A;
+      memset(&A, 0, sizeof(A));
+      A.n = n;
+      A.T = T;
+      A.depth = net.depth[i];
+      A.eps = eps;
+      A.slots = slots;
+      A.x = net.X[i];
+      if (tpre == CT_PRE_STEM) {
+        A.pre_buf = net.stem.base;
+        A.pre_sB = net.stem.sB;
+        A.pre_w = W(c, p + ".stem_w");
+        A.pre_b = W(c, p + ".stem_b");
+      } else if (tpre != CT_PRE_NONE) {
+        const std::string t = p + ".tr" + std::to_string(i);
+        A.pre_buf = net.tr[i].base;
+        A.pre_sB = net.tr[i].sB;
+        A.pre_w = W(c, t + "_w");
+        A.pre_b = W(c, t + "_b");
+      }
+      for (int j = 0; j < net.depth[i]; ++j) {
+        const std::string b = p + ".s" + std::to_string(i) + ".b" + std::to_string(j);
+        CodecTileBlock& Bk = A.b[j];
+        Bk.norm = W(c, b + ".norm");
+        Bk.dw_w = W(c, b + ".dw_w");
+        Bk.dw_b = W(c, b + ".dw_b");
+        Bk.gamma = W(c, b + ".gamma");
+        Bk.ffn_norm = W(c, b + ".ffn_norm");
+        Bk.fc1_w = W(c, b + ".fc1_w");
+        Bk.fc1_b = W(c, b + ".fc1_b");
+        Bk.fc2_w = W(c, b + ".fc2_w");
+        Bk.fc2_b = W(c, b + ".fc2_b");
+        Bk.ffn_gamma = W(c, b + ".ffn_gamma");
+        Bk.mix = net.mix[i][j].base;
+        Bk.mix_sB = net.mix[i][j].sB;
+      }
+      int post = CT_POST_NONE;
+      if (net.decoder && i == net.nst - 1) {
+        post = CT_POST_HEAD;
+        A.head_w = W(c, p + ".head_w");
+        A.head_b = W(c, p + ".head_b");
+        A.head_buf = net.head.base;
+        A.head_sB = net.head.sB;
+        A.audio = out;
+        A.audio2 = out2;
+        head_done = true;
+      } else {
+        const ConvBuf& nb = (i + 1 < net.nst) ? net.tr[i + 1] : net.head;
+        A.out = buf_in_rows(nb, T, slots);
+      }
+      KCHK(launch_codec_tile(A, C, tpre, post, st));
+      continue;
     }
     if (codec_stage_on(c, net, i, n)) {
       // the whole stage (one sample) in one persistent launch (codec_stage.hip)
@@ -698,7 +777,8 @@ static int convnet_run(vv_ctx* c, ConvNet& net, int n, const int* slots, RowMap 
   }
   // ---- head (disable_last_norm: no final norm, modular_vibevoice_tokenizer.py:908-911)
   const int Tl = net.T[net.nst - 1], Cl = net.chans[net.nst - 1];
-  if (net.decoder) {
+  if (head_done) {
+  } else if (net.decoder) {
     Conv1Args a;
     a.M = n * Tl;
     a.C = Cl;

@@ -284,6 +284,37 @@ struct CodecStageArgs {
 bool codec_stage_fits(int C, int T, int n, int depth);
 int launch_codec_stage(const CodecStageArgs& a, hipStream_t st);
 
+// A whole narrow codec stage (C = 128 / 64 / 32) in ONE launch, halo recomputed
+// per workgroup (codec_tile.hip): the transition conv that feeds it, its three
+// Block1Ds and (decoder) the head conv.
+enum { CT_PRE_NONE = 0, CT_PRE_CONVT = 1, CT_PRE_SCONV = 2, CT_PRE_STEM = 3 };
+enum { CT_POST_NONE = 0, CT_POST_HEAD = 1 };
+struct CodecTileBlock {
+  const bf16 *norm, *dw_w, *dw_b, *gamma, *ffn_norm;      // mixer norm, depthwise conv [C][7] + bias, layer scale, FFN norm
+  const bf16 *fc1_w, *fc1_b, *fc2_w, *fc2_b, *ffn_gamma;  // MFMA-packed fc1 [4C][C], fc2 [C][4C]
+  bf16* mix;                // the block's conv buffer (6 history rows, then this frame's rows)
+  long long mix_sB;         // elements per slot
+};
+struct CodecTileArgs {
+  int n, T, depth;          // samples, rows per sample (the stage's), blocks (3)
+  float eps;
+  const int* slots;         // [n] codec slots
+  const bf16* x;            // CT_PRE_NONE: stage input rows [n][T][C]
+  const bf16* pre_buf;      // the transition's input ConvBuf (history rows first), by slot
+  long long pre_sB;
+  const bf16* pre_w;        // convT [2C][4C] / sconv [C][2C] MFMA-packed; stem [C][7]
+  const bf16* pre_b;        // convT [2C] (repeated per phase) / sconv, stem [C]
+  CodecTileBlock b[3];
+  RowMap out;               // CT_POST_NONE: stage output rows (row = sample * T + t)
+  const bf16* head_w;       // CT_POST_HEAD: [7][C], bias [1]
+  const bf16* head_b;
+  bf16* head_buf;           // the head conv's ConvBuf (6 history rows | T rows)
+  long long head_sB;
+  RowMap audio, audio2;     // audio rows (row = sample * T + t); audio2 optional
+};
+bool codec_tile_fits(int C, int pre, int post, int depth, int ctx);
+int launch_codec_tile(const CodecTileArgs& a, int C, int pre, int post, hipStream_t st);
+
 size_t gemv_mix_lds(int M, int T, int C);
 int launch_gemm(GemmArgs a, hipStream_t st);
 int launch_sum_rows(SumRows s, long long count, hipStream_t st);
