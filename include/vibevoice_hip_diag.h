@@ -154,6 +154,18 @@ int vv_persist_decision(int blocks_per_cu, int cus, int scratch_bytes, int grid,
  * recomputed per workgroup); 0 = one k_block launch per Block1D + the
  * transition GEMMs. */
 int vv_codec_tile(int on);
+/* Diagnostic: the tile launches record per-workgroup s_memrealtime phase stamps
+ * ([n][tiles][16] u64 at buf + 4096 x (3 x net + stage), net 0 = decoder, 1 =
+ * encoder; stage 0..2 in run order); NULL = off. */
+int vv_codec_tile_stamps(void* buf);
+/* A/B / test switch: 1 (default) = each wide codec stage (C = 256 / 512) as ONE
+ * launch of workgroup clusters (codec_wide.hip) where the grid-waiting kernels
+ * run; 0 = k_mix + fc1 / fc2 GEMMs per Block1D.  _active: whether a codec step
+ * of n samples on ctx runs them now.  _stamps: per-workgroup phase stamps
+ * ([n][tiles x S][16] u64 at buf + 8192 x (2 x net + (C == 512))); NULL = off. */
+int vv_codec_wide(int on);
+int vv_codec_wide_active(vv_ctx* ctx, int n);
+int vv_codec_wide_stamps(void* buf);
 /* A/B switch: 1 (default) = the balanced many-tile GEMV plan at M >= 8 (one
  * workgroup per CU, 4-5 weight tiles each); 0 = ntile / 8 workgroups. */
 int vv_gemv_tune_bal(int on);

@@ -315,3 +315,60 @@ def test_codec_tile_narrow_stages(slots_sched):
             assert torch.equal(got, again), (f, name)
             assert e_o < 3e-2 and cos(got, ref) > 0.999, (f, name, e_o)
             assert e_b < 3e-2 and cos(got, base) > 0.999, (f, name, e_b)
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_codec_wide_stages(n):
+    """The wide stages (C = 256 at T = 200, C = 512 at T = 40; decoder and
+    semantic encoder) as ONE launch each (codec_wide.hip: clusters of C / 32
+    workgroups per 16-row time tile, each owning 128 hidden units, partials
+    reduce-scattered and block outputs all-gathered inside the cluster) vs the
+    oracle and vs the k_mix + GEMM path over four streamed frames, n samples
+    (their conv histories carried frame to frame), bitwise equal run to run
+    (the member order of the partial sums is fixed).  The codec tolerance: rel L2
+    < 3e-2, cosine > 0.999."""
+    from vibevoice_amd import _lib
+    L = _lib.lib()
+    cfg = tiny_config(ratios=(8, 5, 5, 4, 2, 2), depths="3-3-3-3-3-3-8", nf=32)
+    sd = synthetic_state_dict(cfg, seed=3, device="cpu", mode="test", with_acoustic_encoder=False)
+    eng = Engine(cfg, sd, dev, max_batch=2, max_ctx=64)
+    assert L.vv_codec_wide_active(eng.h, n) == 1
+    H = cfg.decoder_config.hidden_size
+    dd = ocodec.codec_dims(cfg.acoustic_tokenizer_config, "decoder")
+    ed = ocodec.codec_dims(cfg.semantic_tokenizer_config, "encoder")
+    sd_a, sd_s = sub(sd, "model.acoustic_tokenizer."), sub(sd, "model.semantic_tokenizer.")
+    s_f, b_f = sd["model.speech_scaling_factor"], sd["model.speech_bias_factor"]
+    g = torch.Generator().manual_seed(29 + n)
+    lats = [torch.randn(n, 64, generator=g).bfloat16() for _ in range(4)]
+    sl = torch.arange(n, dtype=torch.int32, device=dev)
+    outs = {}
+    try:
+        for mode in (1, 0, 1):
+            L.vv_codec_wide(mode)
+            eng.codec_reset(sl)
+            res = []
+            for lat in lats:
+                audio = torch.empty(n, cfg.hop, dtype=torch.bfloat16, device=dev)
+                sem = torch.empty(n, 128, dtype=torch.bfloat16, device=dev)
+                emb = torch.zeros(n, H, dtype=torch.bfloat16, device=dev)
+                eng.codec_step(sl, lat.to(dev), audio, sem, emb, sl)
+                res.append((audio, sem, emb))
+            torch.cuda.synchronize()
+            outs.setdefault(mode, []).append(res)
+    finally:
+        L.vv_codec_wide(1)
+    eng.check_sync()
+    st_a, st_s = ocodec.StreamState(2), ocodec.StreamState(2)
+    idx = torch.arange(n)
+    for f, lat in enumerate(lats):
+        a_ref = ocodec.decode(sd_a, dd, (lat / s_f - b_f).unsqueeze(-1), st_a, idx)
+        s_ref = ocodec.encode(sd_s, ed, a_ref, st_s, idx)[:, 0]
+        e_ref = connector(sd, "model.acoustic_connector.", lat) + connector(sd, "model.semantic_connector.", s_ref)
+        for k, (name, ref) in enumerate((("audio", a_ref[:, 0]), ("sem", s_ref), ("emb", e_ref))):
+            got, base, again = outs[1][0][f][k], outs[0][0][f][k], outs[1][1][f][k]
+            e_o, e_b = rel_err(got, ref), rel_err(got, base)
+            print(f"n={n} frame {f} {name}: rel {e_o:.3e} vs oracle ({rel_err(base, ref):.3e} k_mix + GEMM path), "
+                  f"{e_b:.3e} vs that path")
+            assert torch.equal(got, again), (f, name)
+            assert e_o < 3e-2 and cos(got, ref) > 0.999, (f, name, e_o)
+            assert e_b < 3e-2 and cos(got, base) > 0.999, (f, name, e_b)

@@ -79,6 +79,10 @@ EXPORTS = [
     ("vv_codec_mix_fusion", I, [I]),
     ("vv_codec_stage", I, [I]),
     ("vv_codec_tile", I, [I]),
+    ("vv_codec_tile_stamps", I, [P]),
+    ("vv_codec_wide", I, [I]),
+    ("vv_codec_wide_active", I, [P, I]),
+    ("vv_codec_wide_stamps", I, [P]),
     ("vv_head_m16", I, [I]),
     ("vv_head_m16_active", I, [P, I]),
     ("vv_head_m16_stamps", I, [P]),

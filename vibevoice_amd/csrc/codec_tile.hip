@@ -19,10 +19,12 @@
 // RMSNorm (one 16-byte chunk per thread, a row's chunks in one lane group so the
 // row sums are DPP reductions in registers) -> fc1 (MFMA 16x16x32, weights in
 // registers, hidden rows + GELU into LDS) -> fc2 (MFMA) -> ffn_gamma residual.
-// The arithmetic is k_block's / k_mix's term for term (codec_block.hip), so the
-// blocks are bit-identical to the launch-per-block path given the same input
-// rows.  The transition GEMM sums its 32-wide K chunks in order in one fp32
-// accumulator (EPI_STORE's rounding); the head conv is k_conv_cout1's order.
+// The arithmetic is k_block's / k_mix's term for term (codec_block.hip) except
+// the GELU: erf by a 5-term rational approximation (gelu_fast, |error| <= 1.5e-7
+// before the bf16 rounding of the output) instead of ocml's erff, whose two
+// branch paths made fc1 + GELU ~8 us of a C = 128 block (tools/codec_tile_stamps.py).
+// The transition GEMM sums its 32-wide K chunks in order in one fp32 accumulator
+// (EPI_STORE's rounding); the head conv is k_conv_cout1's order.
 //
 // Weight stream (8 waves, weights shared by every workgroup through L2): each
 // wave holds its fragments of one GEMM in registers; block j+1's fc1 fragments
@@ -36,7 +38,7 @@ namespace ct {
 constexpr int NTH = 512, NW = 8;   // 8 waves
 template <int C>
 struct Geo {
-  static constexpr int R = 2048 / C;             // output rows per workgroup (16 / 32 / 64)
+  static constexpr int R = 16;                   // output rows per workgroup (one MFMA row tile)
   static constexpr int N8 = C / 8;               // 16-byte chunks per row
   static constexpr int RPP = NTH / N8;           // rows per elementwise pass
   static constexpr int F = 4 * C;
@@ -47,8 +49,9 @@ struct Geo {
   static constexpr int X = 0, X_B = NLP * XLD * 2;                    // block input / output rows
   static constexpr int Y = X + X_B, Y_B = NLP * XLD * 2;              // mixer residual y
   static constexpr int NRM = Y + Y_B, NRM_B = (NLP + 6) * XLD * 2;    // conv input rows (6 before row L0)
-  static constexpr int A = NRM + NRM_B, A_B = NLP * XLD * 2;          // fc1 input rows
-  static constexpr int H = A + A_B, H_B = NLP * HLD * 2;              // hidden rows (transition input first)
+  // (+16 rows: a block's row tiles start at its first output row, so the last one may run 15 rows past NLP)
+  static constexpr int A = NRM + NRM_B, A_B = (NLP + 16) * XLD * 2;   // fc1 input rows
+  static constexpr int H = A + A_B, H_B = (NLP + 16) * HLD * 2;       // hidden rows (transition input first)
   static constexpr int TOTAL = H + H_B;
   static_assert(TOTAL <= 160 * 1024, "one workgroup per CU at most");
   static_assert(NTH % N8 == 0 && 64 % N8 == 0, "a row's chunks in one lane group");
@@ -93,6 +96,13 @@ __global__ void __launch_bounds__(ct::NTH, 1) k_codec_tile(CodecTileArgs a) {
   const int S_lo = max(0, L0);                  // first stage-input row computed
   const int c2 = tid % G::N8, rp = tid / G::N8; // this thread's chunk, row-in-pass
   const bool last_tile = B == T;
+  // diagnostics (tools/codec_tile_stamps.py): 0 start, 1 input rows in LDS, 2 transition done,
+  // per block j 3 + 4j mixer norm, 4 + 4j conv / FFN norm, 5 + 4j fc1, 6 + 4j fc2; 15 end
+  auto stamp = [&](int k) {
+    if (a.stamps && tid == 0)
+      a.stamps[((long long)blockIdx.y * gridDim.x + blockIdx.x) * 16 + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
 
   // ---------------------------------------------------------------- input rows
   // PRE none: the stage input rows; convT: transition buffer rows [S_lo / 2,
@@ -206,6 +216,7 @@ __global__ void __launch_bounds__(ct::NTH, 1) k_codec_tile(CodecTileArgs a) {
     }
   }
   __syncthreads();
+  stamp(1);
   if (GEMM_PRE) {
     // transition GEMM over its rows: convT row u = S_lo / 2 + m reads buffer rows
     // m, m + 1 (local) and yields stage rows 2u, 2u + 1; sconv row S_lo + m reads
@@ -238,6 +249,7 @@ __global__ void __launch_bounds__(ct::NTH, 1) k_codec_tile(CodecTileArgs a) {
     load_w2(0);
     __syncthreads();
   }
+  stamp(2);
 
   // ---------------------------------------------------------------- the blocks
 #pragma unroll
@@ -268,6 +280,7 @@ __global__ void __launch_bounds__(ct::NTH, 1) k_codec_tile(CodecTileArgs a) {
       }
     }
     __syncthreads();
+    stamp(3 + 4 * j);
     // ---- M2: depthwise conv + gamma residual -> y; FFN norm -> fc1's input rows
     for (int p = lo; p < B; p += G::RPP) {
       const int t = p + rp, tc = min(t, B - 1);
@@ -300,14 +313,17 @@ __global__ void __launch_bounds__(ct::NTH, 1) k_codec_tile(CodecTileArgs a) {
       }
     }
     __syncthreads();
-    const int mt_lo = (lo - L0) >> 4, mt_hi = (B - L0 + 15) >> 4;
+    stamp(4 + 4 * j);
+    // row tiles start at the block's first output row (local row lo - L0), not on a
+    // 16-row boundary: a block of 28 / 22 / 16 rows takes 2 / 2 / 1 tiles
+    const int rb0 = lo - L0, nmt = (B - lo + 15) >> 4;
     // ---- F1: fc1 + bias + GELU -> hidden rows
     {
       bf16x4 b1c[S1::NTW];
 #pragma unroll
       for (int i = 0; i < S1::NTW; ++i) b1c[i] = ax.b1[i];
-      for (int mt = mt_lo; mt < mt_hi; ++mt) {
-        const bf16* xrow = as + (mt * 16 + r16) * G::XLD + 8 * g4;
+      for (int mt = 0; mt < nmt; ++mt) {
+        const bf16* xrow = as + (rb0 + mt * 16 + r16) * G::XLD + 8 * g4;
 #pragma unroll
         for (int i = 0; i < S1::NTW; ++i) {
           f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -315,8 +331,8 @@ __global__ void __launch_bounds__(ct::NTH, 1) k_codec_tile(CodecTileArgs a) {
           for (int c = 0; c < G::NK1; ++c) acc = mfma16(w1[i * G::NK1 + c], *(const bf16x8*)(xrow + c * 32), acc);
           bf16x4 o;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = tobf(gelu_f(rb(acc[q] + bf(b1c[i][q]))));
-          *(bf16x4*)(hs + (mt * 16 + r16) * G::HLD + (nt1 + i) * 16 + 4 * g4) = o;
+          for (int q = 0; q < 4; ++q) o[q] = tobf(gelu_fast(rb(acc[q] + bf(b1c[i][q]))));
+          *(bf16x4*)(hs + (rb0 + mt * 16 + r16) * G::HLD + (nt1 + i) * 16 + 4 * g4) = o;
         }
       }
       if (j < 2) {   // block j+1's operands, then its fc1 fragments
@@ -324,13 +340,14 @@ __global__ void __launch_bounds__(ct::NTH, 1) k_codec_tile(CodecTileArgs a) {
         ct_load_frags<K1>(w1, a.b[j + 1].fc1_w, G::NK1, nt1, lane);
       }
       __syncthreads();
+      stamp(5 + 4 * j);
       // ---- F2: fc2 + bias, ffn_gamma, + y -> the block output rows (X)
-      for (int mt = mt_lo + rs2; mt < mt_hi; mt += S2::RS) {
-        const bf16* hrow = hs + (mt * 16 + r16) * G::HLD + 8 * g4;
+      for (int mt = rs2; mt < nmt; mt += S2::RS) {
+        const bf16* hrow = hs + (rb0 + mt * 16 + r16) * G::HLD + 8 * g4;
         f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int c = 0; c < G::NK2; ++c) acc = mfma16(w2[c], *(const bf16x8*)(hrow + c * 32), acc);
-        const int t = L0 + mt * 16 + r16;
+        const int t = lo + mt * 16 + r16;
         const int n = nt2 * 16 + 4 * g4;
         if (t >= lo && t < B) {
           const bf16x4 yv = *(const bf16x4*)(ys + (t - L0) * G::XLD + n);
@@ -343,6 +360,7 @@ __global__ void __launch_bounds__(ct::NTH, 1) k_codec_tile(CodecTileArgs a) {
       }
       if (j < 2) load_w2(j + 1);
       __syncthreads();
+      stamp(6 + 4 * j);
     }
   }
 
@@ -384,6 +402,7 @@ __global__ void __launch_bounds__(ct::NTH, 1) k_codec_tile(CodecTileArgs a) {
       if (a.audio2.base) *rm_bfw(a.audio2, smp * T + t) = y;
     }
   }
+  stamp(15);
 }
 
 // ================================================================ host

@@ -45,6 +45,17 @@ DEV float silu_f(float x) { return x / (1.0f + __expf(-x)); }
 // GELU, exact erf form (transformers ACT2FN["gelu"]; modular_vibevoice_tokenizer.py:589)
 DEV float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
+// GELU with erf by Abramowitz & Stegun 7.1.26 (|erf error| <= 1.5e-7, branch-free:
+// one reciprocal, one exp, a degree-5 polynomial) -- for VALU-bound epilogues over
+// many rows (codec_tile.hip); the result is rounded to bf16 by the caller.
+DEV float gelu_fast(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __frcp_rn(1.0f + 0.3275911f * z);
+  const float p = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  const float e = 1.0f - p * __expf(-z * z);          // erf(|x| / sqrt 2)
+  return 0.5f * x * (1.0f + copysignf(e, x));
+}
+
 // Whole-wave sum: the four 16-lane rows by DPP butterflies (quad xor 1, 2,
 // half-row and row mirror), then across rows by gfx950's v_permlane16_swap /
 // v_permlane32_swap -- VALU moves instead of six dependent ds_bpermute LDS round

@@ -90,6 +90,7 @@ static int hl_count(int device) {
 
 // wait counters + error word of a grid-waiting kernel family (persist_dev.h: 13 lines of 32 words)
 static constexpr size_t SYNC_BYTES = 2048;
+static constexpr int CW_LINES = 256;   // wide codec stage clusters per C (n x tiles <= 256 by residency)
 
 // Process default for new contexts: VIBEVOICE_PERSISTENT=0 in the environment
 // turns the grid-waiting kernels off (e.g. several processes sharing one GPU).
@@ -196,6 +197,8 @@ struct vv_ctx {
   DevBuf lf_sync;   // lm_ffn.hip's wait counters
   DevBuf m16_buf;   // head_m16.hip's distributed A side: row partial sums of squares [16][192] f32 + rows [16][H]
   DevBuf cs_sync;          // persistent codec stage (codec_stage.hip): its wait counters
+  DevBuf cw_sync;          // wide codec stages (codec_wide.hip): one counter line per cluster, per C
+  DevBuf cw_slab, cw_xbuf; // ... their partial slabs and block outputs
   bool persist_ok = true;       // this context may run one-launch (grid-waiting) kernels (vv_set_persistent)
   bool persist_capable = false; // some grid-waiting kernel fits this engine's shapes (vv_finalize)
   bool hl_registered = false;   // counted in g_hl_ctxs (its device's grid-waiting contexts)
@@ -515,6 +518,13 @@ extern "C" int vv_codec_tile(int on) {
   g_codec_tile = on ? 1 : 0;
   return 0;
 }
+// diagnostic: tile launches record [n][tiles][16] phase stamps at buf + 4096 x (3 x net + stage index among
+// the tiled stages) (net 0 decoder, 1 encoders); nullptr: off
+static std::atomic<unsigned long long*> g_codec_tile_stamps{nullptr};
+extern "C" int vv_codec_tile_stamps(void* buf) {
+  g_codec_tile_stamps = (unsigned long long*)buf;
+  return 0;
+}
 // the transition fused into stage i's tile launch (CT_PRE_*), or -1: none applies
 static int tile_pre(const ConvNet& net, int i) {
   const int C = net.chans[i];
@@ -527,6 +537,29 @@ static int tile_pre(const ConvNet& net, int i) {
   if (!g_codec_tile || !codec_tile_fits(C, pre, post, net.depth[i], net.mix[i].empty() ? 0 : net.mix[i][0].ctx))
     return -1;
   return pre;
+}
+
+// The wide stages (C = 256 / 512) as ONE launch each (codec_wide.hip: clusters of
+// C / 32 workgroups per 16-row tile) under the grid-waiting kernels' rule
+// (persist_on: the launch's workgroups must be co-resident); 0 = k_mix + fc1 /
+// fc2 GEMMs per Block1D (A/B and tests).
+static std::atomic<int> g_codec_wide{1};
+extern "C" int vv_codec_wide(int on) {
+  g_codec_wide = on ? 1 : 0;
+  return 0;
+}
+static std::atomic<unsigned long long*> g_codec_wide_stamps{nullptr};
+extern "C" int vv_codec_wide_stamps(void* buf) {   // diagnostic: [n][tiles x S][16] at buf + 8192 x (2 x net + (C == 512))
+  g_codec_wide_stamps = (unsigned long long*)buf;
+  return 0;
+}
+static bool wide_on(vv_ctx* c, const ConvNet& net, int i, int n) {
+  const int C = net.chans[i];
+  return g_codec_wide && (C == 256 || C == 512) && persist_on(c) && c->cw_sync.p && !net.mix[i].empty() &&
+         codec_wide_fits(C, net.T[i], n, net.depth[i], net.mix[i][0].ctx) && n * ((net.T[i] + 15) / 16) <= CW_LINES;
+}
+extern "C" int vv_codec_wide_active(vv_ctx* c, int n) {
+  return c && c->finalized && wide_on(c, c->dec, 2, n) && wide_on(c, c->dec, 3, n) ? 1 : 0;
 }
 
 // diffusion steps whose adaLN modulations are computed in one GEMM
@@ -633,7 +666,48 @@ static int convnet_run(vv_ctx* c, ConvNet& net, int n, const int* slots, RowMap 
         const ConvBuf& nb = (i + 1 < net.nst) ? net.tr[i + 1] : net.head;
         A.out = buf_in_rows(nb, T, slots);
       }
+      if (unsigned long long* sp = g_codec_tile_stamps.load())
+        A.stamps = sp + 4096 * (3 * (net.decoder ? 0 : 1) + (C == 128 ? (net.decoder ? 0 : 2) : C == 64 ? 1 : (net.decoder ? 2 : 0)));
       KCHK(launch_codec_tile(A, C, tpre, post, st));
+      continue;
+    }
+    if (wide_on(c, net, i, n)) {
+      // the whole wide stage in one launch of clusters (codec_wide.hip)
+      CodecWideArgs A;
+      memset(&A, 0, sizeof(A));
+      A.n = n;
+      A.T = T;
+      A.depth = net.depth[i];
+      A.eps = eps;
+      A.slots = slots;
+      A.x = net.X[i];
+      for (int j = 0; j < net.depth[i]; ++j) {
+        const std::string b = p + ".s" + std::to_string(i) + ".b" + std::to_string(j);
+        CodecTileBlock& Bk = A.b[j];
+        Bk.norm = W(c, b + ".norm");
+        Bk.dw_w = W(c, b + ".dw_w");
+        Bk.dw_b = W(c, b + ".dw_b");
+        Bk.gamma = W(c, b + ".gamma");
+        Bk.ffn_norm = W(c, b + ".ffn_norm");
+        Bk.fc1_w = W(c, b + ".fc1_w");
+        Bk.fc1_b = W(c, b + ".fc1_b");
+        Bk.fc2_w = W(c, b + ".fc2_w");
+        Bk.fc2_b = W(c, b + ".fc2_b");
+        Bk.ffn_gamma = W(c, b + ".ffn_gamma");
+        Bk.mix = net.mix[i][j].base;
+        Bk.mix_sB = net.mix[i][j].sB;
+      }
+      const ConvBuf& nb = (i + 1 < net.nst) ? net.tr[i + 1] : net.head;
+      A.out = buf_in_rows(nb, T, slots);
+      CHK(c->cw_slab.ensure(codec_wide_slab_floats(C, T, n) * sizeof(float)));
+      CHK(c->cw_xbuf.ensure(codec_wide_xbuf_elems(C, T, n) * sizeof(bf16)));
+      A.sync = (unsigned*)c->cw_sync.p + (C == 512 ? CW_LINES * 32 : 0);
+      A.err = (unsigned*)c->hf_sync.p + 10 * 32;
+      A.slab = (float*)c->cw_slab.p;
+      A.xbuf = (bf16*)c->cw_xbuf.p;
+      if (unsigned long long* sp = g_codec_wide_stamps.load()) A.stamps = sp + 8192 * (2 * (net.decoder ? 0 : 1) + (C == 512));
+      const int rc = launch_codec_wide(A, C, st);
+      if (rc) FAIL("wide codec stage: launch failed (" + std::to_string(rc) + ")");
       continue;
     }
     if (codec_stage_on(c, net, i, n)) {
@@ -830,7 +904,8 @@ void vv_destroy(vv_ctx* c) {
   if (c->hl_registered) hl_register(c->device, -1);
   DevBuf* bufs[] = {&c->norm_ws, &c->kv_k, &c->kv_v, &c->lm_ws, &c->attn_part, &c->attn_cnt, &c->valid_ids, &c->splitk_ws, &c->splitk_cnt,
                     &c->temb, &c->tfreq_tmp, &c->head_ws, &c->codec_ws, &c->slot_scratch, &c->unit_sb,
-                    &c->rope_tab, &c->zero_rows, &c->hf_sync, &c->cs_sync, &c->m16_buf, &c->lf_sync};
+                    &c->rope_tab, &c->zero_rows, &c->hf_sync, &c->cs_sync, &c->m16_buf, &c->lf_sync,
+                    &c->cw_sync, &c->cw_slab, &c->cw_xbuf};
   for (DevBuf* b : bufs) b->release();
   ConvNet* nets[] = {&c->dec, &c->sem, &c->aenc, &c->senc};
   for (ConvNet* n : nets) {
@@ -934,12 +1009,14 @@ int vv_finalize(vv_ctx* c) {
   HIPCHK(hipMemset(c->cs_sync.p, 0, SYNC_BYTES));
   CHK(c->lf_sync.ensure(SYNC_BYTES));
   HIPCHK(hipMemset(c->lf_sync.p, 0, SYNC_BYTES));
+  CHK(c->cw_sync.ensure(2 * CW_LINES * 128));
+  HIPCHK(hipMemset(c->cw_sync.p, 0, 2 * CW_LINES * 128));
   if (c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 16))
   {
     CHK(c->m16_buf.ensure(16 * 192 * sizeof(float) + 16 * (size_t)k.hidden * sizeof(bf16)));
     HIPCHK(hipMemset(c->m16_buf.p, 0, 16 * 192 * sizeof(float)));
   }
-  c->persist_capable = codec_stage_any(c->dec) || codec_stage_any(c->sem) ||
+  c->persist_capable = codec_stage_any(c->dec) || codec_stage_any(c->sem) || codec_wide_fits(256, 200, 1, 3, 6) ||
                        (c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 16)) ||
                        lm_ffn_fits(k.hidden, k.intermediate, 2);
   if (c->persist_ok && c->persist_capable && !c->hl_registered) {
@@ -1447,6 +1524,7 @@ int vv_sync_reset(vv_ctx* c) {
   HIPCHK(hipDeviceSynchronize());
   for (DevBuf* b : {&c->hf_sync, &c->cs_sync, &c->lf_sync})
     if (b->p) HIPCHK(hipMemset(b->p, 0, SYNC_BYTES));
+  if (c->cw_sync.p) HIPCHK(hipMemset(c->cw_sync.p, 0, c->cw_sync.bytes));
   HIPCHK(hipDeviceSynchronize());
   return 0;
 }

@@ -311,9 +311,32 @@ struct CodecTileArgs {
   bf16* head_buf;           // the head conv's ConvBuf (6 history rows | T rows)
   long long head_sB;
   RowMap audio, audio2;     // audio rows (row = sample * T + t); audio2 optional
+  unsigned long long* stamps;   // diagnostics: [n][tiles][16] s_memrealtime per phase, or nullptr
 };
 bool codec_tile_fits(int C, int pre, int post, int depth, int ctx);
 int launch_codec_tile(const CodecTileArgs& a, int C, int pre, int post, hipStream_t st);
+
+// A whole wide codec stage (C = 256 / 512) in ONE launch (codec_wide.hip): a
+// cluster of C / 32 workgroups per 16-row time tile, each owning 128 hidden
+// units; partials reduce-scattered and block outputs all-gathered inside the
+// cluster (write-through hand-offs, bounded cluster-wide waits).
+struct CodecWideArgs {
+  int n, T, depth;
+  float eps;
+  const int* slots;
+  const bf16* x;            // stage input rows [n][T][C]
+  CodecTileBlock b[3];
+  RowMap out;               // stage output rows (row = sample * T + t)
+  unsigned* sync;           // one 32-word line per cluster (n x tiles), monotonic counters
+  unsigned* err;            // set to 1 when a wait gave up
+  float* slab;              // [n x tiles][S][40][C] fp32 partials
+  bf16* xbuf;               // [n x tiles][40][C] block outputs
+  unsigned long long* stamps;   // diagnostics: [n][tiles x S][16] s_memrealtime, or nullptr
+};
+bool codec_wide_fits(int C, int T, int n, int depth, int ctx);
+size_t codec_wide_slab_floats(int C, int T, int n);
+size_t codec_wide_xbuf_elems(int C, int T, int n);
+int launch_codec_wide(const CodecWideArgs& a, int C, hipStream_t st);
 
 size_t gemv_mix_lds(int M, int T, int C);
 int launch_gemm(GemmArgs a, hipStream_t st);
