@@ -165,7 +165,11 @@ int vv_diffusion_sample(vv_ctx* ctx, int n, const void* pos_h, const void* neg_h
  * vv_set_persistent(ctx, 0) turns the grid-waiting kernels off for ctx (the
  * process default is on unless the environment sets VIBEVOICE_PERSISTENT=0):
  * for GPUs shared by several processes, whose contexts this library cannot
- * see. */
+ * see.  vv_set_persistent(ctx, 2) ("follow"): ctx does not register, and runs
+ * the kernels while exactly one context of the device is registered -- a second
+ * context over the same model (the standalone tokenizer API's codec slots) then
+ * computes with the owner's kernels, bit-identically, without demoting it; the
+ * two must not launch concurrently on different streams. */
 int vv_set_persistent(vv_ctx* ctx, int on);
 /* 1 when ctx launches its grid-waiting kernels now (enabled, sole context). */
 int vv_persistent_active(vv_ctx* ctx);

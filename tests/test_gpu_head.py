@@ -199,7 +199,16 @@ def test_one_launch_layer_only_for_the_devices_sole_context():
     c = Engine(tiny, synthetic_state_dict(tiny, seed=0, device="cpu", mode="test", with_acoustic_encoder=False), dev,
                max_batch=1, max_ctx=64, persistent=False)
     assert not c.persistent_active() and L.vv_head_m16_active(c.h, 1) == 0
+    # "follow" (the tokenizer API's codec context): runs the kernels while the
+    # owner is the sole registered context, never demotes it
+    f = Engine(tiny, synthetic_state_dict(tiny, seed=0, device="cpu", mode="test", with_acoustic_encoder=False), dev,
+               max_batch=1, max_ctx=64, persistent="follow")
+    assert not f.persistent_active()          # nobody registered
+    o, _ = engine_with_head(tiny, sd)
+    assert o.persistent_active() and f.persistent_active() and L.vv_head_m16_active(o.h, 1) == 1
     c.close()
+    f.close()
+    o.close()
 
 
 @pytest.mark.parametrize("n", [1, 3, 8])

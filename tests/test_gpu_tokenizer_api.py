@@ -11,7 +11,9 @@ modular_vibevoice_tokenizer.py:193-256, 1081-1108).
   decode (rel L2 < 3e-2, cosine > 0.999: the codec tolerance of
   test_gpu_codec.py).
 * The API frame for frame is bit-identical to the fused vv_codec_step that
-  generate() runs (same kernels; latent scaling done by the caller in bf16).
+  generate() runs (same kernels: the API's codec context follows its owner's
+  one-launch kernels, vv_set_persistent 2; latent scaling done by the caller
+  in bf16).
 """
 import pytest
 import torch

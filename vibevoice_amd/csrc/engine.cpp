@@ -201,6 +201,7 @@ struct vv_ctx {
   DevBuf cw_slab, cw_xbuf; // ... their partial slabs and block outputs
   bool persist_ok = true;       // this context may run one-launch (grid-waiting) kernels (vv_set_persistent)
   bool persist_capable = false; // some grid-waiting kernel fits this engine's shapes (vv_finalize)
+  bool persist_follow = false;  // unregistered, runs them while exactly one context is registered (vv_set_persistent 2)
   bool hl_registered = false;   // counted in g_hl_ctxs (its device's grid-waiting contexts)
   bool head_gemv = true;        // the head FFN's GEMV layout is bound (head.<l>.gu_w / down_w)
   DevBuf rope_tab;   // [max_ctx][cos 64 | sin 64] bf16 (k_rope_table)
@@ -318,7 +319,7 @@ static int rmsnorm(int M, int C, RowMap in, RowMap out, const bf16* w, float eps
 // the occupancy query).  Both halves are vv_persist_decision for the tests.
 static bool persist_ctx_ok(int enabled, int contexts_on_device) { return enabled && contexts_on_device == 1; }
 static bool persist_on(vv_ctx* c) {
-  return persist_ctx_ok(c->persist_ok && c->hl_registered ? 1 : 0, hl_count(c->device));
+  return persist_ctx_ok(c->persist_ok && (c->hl_registered || c->persist_follow) ? 1 : 0, hl_count(c->device));
 }
 extern "C" int vv_persist_decision(int blocks_per_cu, int cus, int scratch_bytes, int grid, int contexts_on_device,
                                    int enabled) {
@@ -1019,7 +1020,7 @@ int vv_finalize(vv_ctx* c) {
   c->persist_capable = codec_stage_any(c->dec) || codec_stage_any(c->sem) || codec_wide_fits(256, 200, 1, 3, 6) ||
                        (c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 16)) ||
                        lm_ffn_fits(k.hidden, k.intermediate, 2);
-  if (c->persist_ok && c->persist_capable && !c->hl_registered) {
+  if (c->persist_ok && !c->persist_follow && c->persist_capable && !c->hl_registered) {
     c->hl_registered = true;
     hl_register(c->device, +1);
   }
@@ -1564,12 +1565,15 @@ int vv_sync_error_async(vv_ctx* c, void* dst, vv_stream vst) {
 // epoch: graphs captured with the other path are re-captured.
 int vv_set_persistent(vv_ctx* c, int on) {
   if (!c) FAIL("vv_set_persistent: null context");
+  if (on < 0 || on > 2) FAIL("vv_set_persistent: 0 (off), 1 (on) or 2 (follow)");
   c->persist_ok = on != 0;
+  c->persist_follow = on == 2;
+  if (on == 2) c->persist_ok = true;
   if (c->finalized) {
-    if (!c->persist_ok && c->hl_registered) {
+    if ((!c->persist_ok || c->persist_follow) && c->hl_registered) {
       c->hl_registered = false;
       hl_register(c->device, -1);
-    } else if (c->persist_ok && c->persist_capable && !c->hl_registered) {
+    } else if (c->persist_ok && !c->persist_follow && c->persist_capable && !c->hl_registered) {
       c->hl_registered = true;
       hl_register(c->device, +1);
     }

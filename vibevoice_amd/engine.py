@@ -75,9 +75,10 @@ class Engine:
         tp_head: shard the diffusion head's FFN over the TP group as well
         (vv_tp_shard_head).
         persistent: False keeps this context off the grid-waiting one-launch
-        kernels (vv_set_persistent): it then neither runs them nor counts as a
-        second context of the device (the standalone tokenizer API's codec
-        context)."""
+        kernels (vv_set_persistent 0); "follow" runs them while exactly one
+        context of the device is registered, without registering itself (the
+        standalone tokenizer API's codec context: it computes with its owner's
+        kernels and never demotes it)."""
         L = _lib.lib()
         self.cfg = cfg
         self.device = torch.device(device)
@@ -105,8 +106,8 @@ class Engine:
                 _lib.check(L.vv_tp_init(h, tp_rank, tp_size, uid), "tp_init")
                 if self.tp_head:
                     _lib.check(L.vv_tp_shard_head(h, 1), "tp_shard_head")
-            if not persistent:
-                _lib.check(L.vv_set_persistent(h, 0), "set_persistent")
+            if persistent is not True:
+                _lib.check(L.vv_set_persistent(h, 2 if persistent == "follow" else 0), "set_persistent")
             for name, t in self.w.items():
                 shape = (ctypes.c_int64 * max(1, t.dim()))(*t.shape)
                 _lib.check(L.vv_bind_weight(h, name.encode(), _ptr(t), shape, t.dim()), f"bind {name}")

@@ -96,10 +96,11 @@ class _SlotPool:
             m = self.model.engine
             # same TP coordinates as the owner: its packed LM weights are this rank's shards
             # (no communicator: the views only run the replicated codec / connectors)
-            # (persistent=False: this codec context neither demotes the model's own
-            # context from the one-launch kernels nor contends with them)
+            # (persistent="follow": this codec context runs the owner's one-launch
+            # kernels -- bit-identical to its codec step -- without registering, so
+            # it never demotes the owner's context)
             self._eng = Engine(self.model.config, None, m.device, max_batch=self.n, max_ctx=64, packed=m.w,
-                               tp_rank=m.tp_rank, tp_size=m.tp_size, tp_head=m.tp_head, persistent=False)
+                               tp_rank=m.tp_rank, tp_size=m.tp_size, tp_head=m.tp_head, persistent="follow")
         return self._eng
 
     def _i32(self, xs):
