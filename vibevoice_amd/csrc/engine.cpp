@@ -554,13 +554,22 @@ extern "C" int vv_codec_wide_stamps(void* buf) {   // diagnostic: [n][tiles x S]
   g_codec_wide_stamps = (unsigned long long*)buf;
   return 0;
 }
+// some stage of the net has a wide-stage shape the cluster kernel takes (one sample)
+static bool codec_wide_any(const ConvNet& net) {
+  for (int i = 0; i < net.nst; ++i)
+    if (!net.mix[i].empty() && codec_wide_fits(net.chans[i], net.T[i], 1, net.depth[i], net.mix[i][0].ctx)) return true;
+  return false;
+}
 static bool wide_on(vv_ctx* c, const ConvNet& net, int i, int n) {
   const int C = net.chans[i];
   return g_codec_wide && (C == 256 || C == 512) && persist_on(c) && c->cw_sync.p && !net.mix[i].empty() &&
          codec_wide_fits(C, net.T[i], n, net.depth[i], net.mix[i][0].ctx) && n * ((net.T[i] + 15) / 16) <= CW_LINES;
 }
-extern "C" int vv_codec_wide_active(vv_ctx* c, int n) {
-  return c && c->finalized && wide_on(c, c->dec, 2, n) && wide_on(c, c->dec, 3, n) ? 1 : 0;
+extern "C" int vv_codec_wide_active(vv_ctx* c, int n) {   // 1: some acoustic-decoder stage runs it now
+  if (!c || !c->finalized) return 0;
+  for (int i = 0; i < c->dec.nst; ++i)
+    if (wide_on(c, c->dec, i, n)) return 1;
+  return 0;
 }
 
 // diffusion steps whose adaLN modulations are computed in one GEMM
@@ -1017,7 +1026,8 @@ int vv_finalize(vv_ctx* c) {
     CHK(c->m16_buf.ensure(16 * 192 * sizeof(float) + 16 * (size_t)k.hidden * sizeof(bf16)));
     HIPCHK(hipMemset(c->m16_buf.p, 0, 16 * 192 * sizeof(float)));
   }
-  c->persist_capable = codec_stage_any(c->dec) || codec_stage_any(c->sem) || codec_wide_fits(256, 200, 1, 3, 6) ||
+  c->persist_capable = codec_stage_any(c->dec) || codec_stage_any(c->sem) || codec_wide_any(c->dec) ||
+                       codec_wide_any(c->sem) ||
                        (c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 16)) ||
                        lm_ffn_fits(k.hidden, k.intermediate, 2);
   if (c->persist_ok && !c->persist_follow && c->persist_capable && !c->hl_registered) {
