@@ -5,6 +5,7 @@ One configuration per process (so a rocprofv3 --pmc pass attributes every
 dispatch to it):
   python tools/head_mfma.py --n N        whole vv_diffusion_sample for N diffusing
                                          rows (M = 2N GEMV rows), real 1.5B head
+  python tools/head_mfma.py --lmffn       the LM MLP block at B = 1 (k_lm_ffn, 5 x 28 launches)
   python tools/head_mfma.py --m M        the head's gate|up (N 9216, K 1536) and
                                          down (N 1536, K 4608) shapes at M rows
                                          through vv_gemm_bf16 (the dispatch the
@@ -27,8 +28,22 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=0)
     ap.add_argument("--m", type=int, default=0)
+    ap.add_argument("--lmffn", action="store_true", help="the LM MLP block at B = 1 as the loop runs it (k_lm_ffn)")
     args = ap.parse_args()
     L = _lib.lib()
+    if args.lmffn:
+        from vibevoice_amd.modeling_vibevoice_inference import VibeVoiceForConditionalGenerationInference
+        model = VibeVoiceForConditionalGenerationInference.from_pretrained("synthetic:1.5B", device_map="cuda",
+                                                                            synthetic_seed=0, max_batch=1, max_ctx=256)
+        assert L.vv_lm_ffn_active(model.engine.h, 2) == 1
+        x = (torch.randn(2, 1536, device="cuda") * 0.5).bfloat16()
+        act = torch.empty(2, 8960, device="cuda", dtype=torch.bfloat16)
+        sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        _lib.check(L.vv_lm_mlp_replay(model.engine.h, 2, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(act.data_ptr()),
+                                      5, sp), "lm_mlp_replay")
+        torch.cuda.synchronize()
+        print("lmffn: M=2 rows, 5 passes over the 28 layers' MLP blocks")
+        return
     if args.n:
         from test_gpu_head import real_head_sd
         from tiny import tiny_config
