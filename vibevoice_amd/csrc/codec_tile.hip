@@ -36,9 +36,9 @@
 
 namespace ct {
 constexpr int NTH = 512, NW = 8;   // 8 waves
-template <int C>
+template <int C, int R_>
 struct Geo {
-  static constexpr int R = 16;                   // output rows per workgroup (one MFMA row tile)
+  static constexpr int R = R_;                   // output rows per workgroup (16, or 2048 / C for many samples)
   static constexpr int N8 = C / 8;               // 16-byte chunks per row
   static constexpr int RPP = NTH / N8;           // rows per elementwise pass
   static constexpr int F = 4 * C;
@@ -71,9 +71,9 @@ DEV void ct_load_frags(bf16x8 (&f)[K], const bf16* w, int nk, int t0, int lane) 
   for (int i = 0; i < K; ++i) f[i] = *(const bf16x8*)(w + ((long long)(t0 + i / nk) * nk + i % nk) * 512 + lane * 8);
 }
 
-template <int C, int PRE, int POST>
+template <int C, int PRE, int POST, int R>
 __global__ void __launch_bounds__(ct::NTH, 1) k_codec_tile(CodecTileArgs a) {
-  using G = ct::Geo<C>;
+  using G = ct::Geo<C, R>;
   using namespace ct;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16* xs = (bf16*)(smem + G::X);
@@ -179,9 +179,12 @@ __global__ void __launch_bounds__(ct::NTH, 1) k_codec_tile(CodecTileArgs a) {
     b2c = *(const bf16x4*)(a.b[j].fc2_b + nt2 * 16 + 4 * g4);
     g2c = *(const bf16x4*)(a.b[j].ffn_gamma + nt2 * 16 + 4 * g4);
   };
+  // C = 128: fc2's 16 fragments go out at the start of each block's fc1 instead
+  // (live through the mixer beside fc1's 16 and the block operands they spilled)
+  constexpr bool W2_LATE = K2 > 8;
   if (!GEMM_PRE) {   // (with a transition GEMM: after it, so its fragments and these are never live together)
     ct_load_frags<K1>(w1, a.b[0].fc1_w, G::NK1, nt1, lane);
-    load_w2(0);
+    if (!W2_LATE) load_w2(0);
   }
 
   // ---------------------------------------------------------------- stage input rows -> X (local row t - L0)
@@ -246,7 +249,7 @@ __global__ void __launch_bounds__(ct::NTH, 1) k_codec_tile(CodecTileArgs a) {
       }
     }
     ct_load_frags<K1>(w1, a.b[0].fc1_w, G::NK1, nt1, lane);
-    load_w2(0);
+    if (!W2_LATE) load_w2(0);
     __syncthreads();
   }
   stamp(2);
@@ -319,9 +322,7 @@ __global__ void __launch_bounds__(ct::NTH, 1) k_codec_tile(CodecTileArgs a) {
     const int rb0 = lo - L0, nmt = (B - lo + 15) >> 4;
     // ---- F1: fc1 + bias + GELU -> hidden rows
     {
-      bf16x4 b1c[S1::NTW];
-#pragma unroll
-      for (int i = 0; i < S1::NTW; ++i) b1c[i] = ax.b1[i];
+      if (W2_LATE) load_w2(j);
       for (int mt = 0; mt < nmt; ++mt) {
         const bf16* xrow = as + (rb0 + mt * 16 + r16) * G::XLD + 8 * g4;
 #pragma unroll
@@ -331,7 +332,7 @@ __global__ void __launch_bounds__(ct::NTH, 1) k_codec_tile(CodecTileArgs a) {
           for (int c = 0; c < G::NK1; ++c) acc = mfma16(w1[i * G::NK1 + c], *(const bf16x8*)(xrow + c * 32), acc);
           bf16x4 o;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = tobf(gelu_fast(rb(acc[q] + bf(b1c[i][q]))));
+          for (int q = 0; q < 4; ++q) o[q] = tobf(gelu_fast(rb(acc[q] + bf(ax.b1[i][q]))));
           *(bf16x4*)(hs + (rb0 + mt * 16 + r16) * G::HLD + (nt1 + i) * 16 + 4 * g4) = o;
         }
       }
@@ -358,7 +359,7 @@ __global__ void __launch_bounds__(ct::NTH, 1) k_codec_tile(CodecTileArgs a) {
           if (j == 2 && POST == CT_POST_NONE && t >= t0) *(bf16x4*)(rm_bfw(a.out, smp * T + t) + n) = o;
         }
       }
-      if (j < 2) load_w2(j + 1);
+      if (j < 2 && !W2_LATE) load_w2(j + 1);
       __syncthreads();
       stamp(6 + 4 * j);
     }
@@ -406,16 +407,25 @@ __global__ void __launch_bounds__(ct::NTH, 1) k_codec_tile(CodecTileArgs a) {
 }
 
 // ================================================================ host
-template <int C, int PRE, int POST>
+template <int C, int PRE, int POST, int R>
 static int ct_launch(const CodecTileArgs& a, hipStream_t st) {
-  using G = ct::Geo<C>;
+  using G = ct::Geo<C, R>;
   static const bool attr =
-      hipFuncSetAttribute((const void*)k_codec_tile<C, PRE, POST>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      hipFuncSetAttribute((const void*)k_codec_tile<C, PRE, POST, R>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           G::TOTAL) == hipSuccess;
   if (!attr) return 2;
-  hipLaunchKernelGGL((k_codec_tile<C, PRE, POST>), dim3((a.T + G::R - 1) / G::R, a.n), dim3(ct::NTH), G::TOTAL, st,
-                     a);
+  hipLaunchKernelGGL((k_codec_tile<C, PRE, POST, R>), dim3((a.T + G::R - 1) / G::R, a.n), dim3(ct::NTH), G::TOTAL,
+                     st, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+// Rows per workgroup: 16 while the launch fits one wave of workgroups (one per CU:
+// the shortest chain, the most CUs); with more samples 2048 / C, so the halo a
+// workgroup recomputes is a smaller share of its rows (B = 8 at C = 32: 400
+// workgroups of 64 rows instead of 1,600 of 16).
+template <int C, int PRE, int POST>
+static int ct_pick(const CodecTileArgs& a, hipStream_t st) {
+  if ((long long)a.n * ((a.T + 15) / 16) <= 256 || C >= 128) return ct_launch<C, PRE, POST, 16>(a, st);
+  return ct_launch<C, PRE, POST, (C >= 128 ? 16 : 2048 / C)>(a, st);
 }
 
 bool codec_tile_fits(int C, int pre, int post, int depth, int ctx) {
@@ -432,10 +442,10 @@ int launch_codec_tile(const CodecTileArgs& a, int C, int pre, int post, hipStrea
   if (a.n <= 0 || a.T <= 0) return 0;
   if (!codec_tile_fits(C, pre, post, a.depth, 6)) return 1;
   if (pre == CT_PRE_CONVT && a.T % 2) return 1;
-  if (C == 128 && pre == CT_PRE_NONE) return ct_launch<128, CT_PRE_NONE, CT_POST_NONE>(a, st);
-  if (C == 128) return ct_launch<128, CT_PRE_SCONV, CT_POST_NONE>(a, st);
-  if (C == 64 && pre == CT_PRE_CONVT) return ct_launch<64, CT_PRE_CONVT, CT_POST_NONE>(a, st);
-  if (C == 64) return ct_launch<64, CT_PRE_SCONV, CT_POST_NONE>(a, st);
-  if (C == 32 && pre == CT_PRE_CONVT) return ct_launch<32, CT_PRE_CONVT, CT_POST_HEAD>(a, st);
-  return ct_launch<32, CT_PRE_STEM, CT_POST_NONE>(a, st);
+  if (C == 128 && pre == CT_PRE_NONE) return ct_pick<128, CT_PRE_NONE, CT_POST_NONE>(a, st);
+  if (C == 128) return ct_pick<128, CT_PRE_SCONV, CT_POST_NONE>(a, st);
+  if (C == 64 && pre == CT_PRE_CONVT) return ct_pick<64, CT_PRE_CONVT, CT_POST_NONE>(a, st);
+  if (C == 64) return ct_pick<64, CT_PRE_SCONV, CT_POST_NONE>(a, st);
+  if (C == 32 && pre == CT_PRE_CONVT) return ct_pick<32, CT_PRE_CONVT, CT_POST_HEAD>(a, st);
+  return ct_pick<32, CT_PRE_STEM, CT_POST_NONE>(a, st);
 }
