@@ -265,3 +265,57 @@ def test_lm_ffn_one_launch_vs_oracle_and_gemv_pair():
     finally:
         L_.vv_lm_ffn(1)
     eng.check_sync()
+
+
+@pytest.mark.parametrize("n", [8, 3])
+def test_lm_ffn16_one_launch_vs_oracle_and_gemv_pair(n):
+    """configs[2]'s LM MLP block (B = 8: 16 rows; n = 3: 6 rows) as ONE launch
+    (lm_ffn.hip k_lm_ffn16: MFMA gate|up over 4-5 tiles per workgroup, one grid
+    wait, down split by column group x hidden range with the 4 fp32 partials of
+    a group summed in range order by its last arrival) on the 1.5B layer shapes:
+    each decode step vs the oracle (rel < 2e-2, cosine > 0.999) and vs the
+    gate|up + down GEMV pair on the same KV state (within bf16), repeated runs
+    bitwise equal."""
+    import gc
+    from vibevoice_amd import _lib
+    gc.collect()
+    L_ = _lib.lib()
+    cfg = tiny_config(hidden=1536, layers=2, heads=12, kv_heads=2, inter=8960)
+    eng, sd = make_engine(cfg, seed=5, max_batch=8, max_ctx=256)
+    R = 2 * n
+    assert L_.vv_lm_ffn_active(eng.h, R) == 1
+    lcfg = dict(cfg.decoder_config)
+    osd = oracle_sd(sd)
+    g = torch.Generator().manual_seed(11 + n)
+    lens = [5 + 3 * r for r in range(R)]
+    xs = [torch.randn(m, 1536, generator=g).bfloat16() for m in lens]
+    kvs = [olm.RowKV(2) for _ in lens]
+    for r in range(R):
+        olm.forward_rows(osd, lcfg, xs[r][None], kvs[r:r + 1])
+    x = torch.cat(xs).to(dev)
+    slots = torch.cat([torch.full((m,), r) for r, m in enumerate(lens)]).to(**I32)
+    pos = torch.cat([torch.arange(m) for m in lens]).to(**I32)
+    last = torch.cumsum(torch.tensor(lens), 0) - 1
+    eng.lm_forward(x, slots, pos, last.to(**I32))
+    Lt = torch.tensor(lens)
+    try:
+        for s in range(3):
+            step_x = torch.randn(R, 1536, generator=g).bfloat16()
+            ref = olm.forward_rows(osd, lcfg, step_x[:, None], kvs)[:, -1]
+            outs = {}
+            for on in (3, 1, 1):   # 3: the GEMV pair at > 2 rows, 1: k_lm_ffn16
+                L_.vv_lm_ffn(on)
+                h, _ = eng.lm_forward(step_x.to(dev), torch.arange(R).to(**I32), Lt.to(**I32),
+                                      torch.arange(R).to(**I32))
+                torch.cuda.synchronize()
+                outs.setdefault(on, []).append(h.clone())
+            Lt += 1
+            one, pair = outs[1][0], outs[3][0]
+            print(f"n={n} step {s}: one launch rel {rel_err(one, ref):.3e} vs oracle (GEMV pair "
+                  f"{rel_err(pair, ref):.3e}), {rel_err(one, pair):.3e} vs the GEMV pair")
+            assert torch.equal(one, outs[1][1])
+            assert rel_err(one, ref) < 2e-2 and cos(one, ref) > 0.999
+            assert rel_err(one, pair) < 2e-2 and cos(one, pair) > 0.999
+    finally:
+        L_.vv_lm_ffn(1)
+    eng.check_sync()

@@ -194,7 +194,8 @@ struct vv_ctx {
   // grid-wide waits of the one-launch kernels (persist_dev.h): head_m16.hip's
   // counters (lines 0-7 shards, line 12 its generation) + the error word (line 10)
   DevBuf hf_sync;
-  DevBuf lf_sync;   // lm_ffn.hip's wait counters
+  DevBuf lf_sync;   // lm_ffn.hip's wait counters (+ k_lm_ffn16's column-group tickets)
+  DevBuf lf_slab;   // k_lm_ffn16's down partials [48][4][16][32] fp32
   DevBuf m16_buf;   // head_m16.hip's distributed A side: row partial sums of squares [16][192] f32 + rows [16][H]
   DevBuf cs_sync;          // persistent codec stage (codec_stage.hip): its wait counters
   DevBuf cw_sync;          // wide codec stages (codec_wide.hip): one counter line per cluster, per C
@@ -915,7 +916,7 @@ void vv_destroy(vv_ctx* c) {
   DevBuf* bufs[] = {&c->norm_ws, &c->kv_k, &c->kv_v, &c->lm_ws, &c->attn_part, &c->attn_cnt, &c->valid_ids, &c->splitk_ws, &c->splitk_cnt,
                     &c->temb, &c->tfreq_tmp, &c->head_ws, &c->codec_ws, &c->slot_scratch, &c->unit_sb,
                     &c->rope_tab, &c->zero_rows, &c->hf_sync, &c->cs_sync, &c->m16_buf, &c->lf_sync,
-                    &c->cw_sync, &c->cw_slab, &c->cw_xbuf};
+                    &c->cw_sync, &c->cw_slab, &c->cw_xbuf, &c->lf_slab};
   for (DevBuf* b : bufs) b->release();
   ConvNet* nets[] = {&c->dec, &c->sem, &c->aenc, &c->senc};
   for (ConvNet* n : nets) {
@@ -1019,6 +1020,7 @@ int vv_finalize(vv_ctx* c) {
   HIPCHK(hipMemset(c->cs_sync.p, 0, SYNC_BYTES));
   CHK(c->lf_sync.ensure(SYNC_BYTES));
   HIPCHK(hipMemset(c->lf_sync.p, 0, SYNC_BYTES));
+  if (k.max_batch >= 2 && lm_ffn16_fits(k.hidden, k.intermediate, 16)) CHK(c->lf_slab.ensure(48 * 4 * 16 * 32 * sizeof(float)));
   CHK(c->cw_sync.ensure(2 * CW_LINES * 128));
   HIPCHK(hipMemset(c->cw_sync.p, 0, 2 * CW_LINES * 128));
   if (c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 16))
@@ -1029,7 +1031,7 @@ int vv_finalize(vv_ctx* c) {
   c->persist_capable = codec_stage_any(c->dec) || codec_stage_any(c->sem) || codec_wide_any(c->dec) ||
                        codec_wide_any(c->sem) ||
                        (c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 16)) ||
-                       lm_ffn_fits(k.hidden, k.intermediate, 2);
+                       lm_ffn_fits(k.hidden, k.intermediate, 2) || lm_ffn16_fits(k.hidden, k.intermediate, 16);
   if (c->persist_ok && !c->persist_follow && c->persist_capable && !c->hl_registered) {
     c->hl_registered = true;
     hl_register(c->device, +1);
@@ -1362,14 +1364,16 @@ static int lm_attn_half(vv_ctx* c, LmPass& P, int l, hipStream_t st) {
 // the LM MLP block in one launch (lm_ffn.hip) at decode with <= 2 rows, unsharded,
 // while the context is the device's only registered one; 0 = two GEMV launches
 static std::atomic<int> g_lm_ffn{1};
-extern "C" int vv_lm_ffn(int on) {
-  g_lm_ffn = on ? 1 : 0;
+extern "C" int vv_lm_ffn(int on) {   // bit 0: on; bit 1: not at 3..16 rows (k_lm_ffn16)
+  g_lm_ffn = on & 3;
   return 0;
 }
 static bool lm_ffn_on(vv_ctx* c, const LmPass& P) {
   const vv_config& k = c->cfg;
-  return g_lm_ffn && c->lf_sync.p && !P.prefill && P.ntok <= 2 && c->tp_size == 1 && !c->comm && !P.hm.idx &&
-         P.hm.sT == k.hidden && P.hm.T >= P.ntok && lm_ffn_fits(k.hidden, k.intermediate, P.ntok) && persist_on(c);
+  const bool shape = P.ntok <= 2 ? lm_ffn_fits(k.hidden, k.intermediate, P.ntok)
+                                 : (g_lm_ffn & 2) == 0 && c->lf_slab.p && lm_ffn16_fits(k.hidden, k.intermediate, P.ntok);
+  return g_lm_ffn && c->lf_sync.p && !P.prefill && c->tp_size == 1 && !c->comm && !P.hm.idx && P.hm.sT == k.hidden &&
+         P.hm.T >= P.ntok && shape && persist_on(c);
 }
 extern "C" int vv_lm_ffn_active(vv_ctx* c, int ntok) {
   LmPass P;
@@ -1397,7 +1401,9 @@ static int lm_mlp_half(vv_ctx* c, LmPass& P, int l, hipStream_t st) {
     a.act = P.act;
     a.sync = (unsigned*)c->lf_sync.p;
     a.err = (unsigned*)c->hf_sync.p + 10 * 32;
-    KCHK(launch_lm_ffn(a, st));
+    a.slab = (float*)c->lf_slab.p;
+    if (P.ntok <= 2) KCHK(launch_lm_ffn(a, st));
+    else KCHK(launch_lm_ffn16(a, st));
     return 0;
   }
   // post_attention_layernorm fused into gate|up's A load

@@ -253,11 +253,16 @@ struct LmFfnArgs {
   const bf16* gu;    // gate|up [2F][H], MFMA-packed (8 gate + 8 up rows per tile)
   const bf16* dn;    // down [H][F], MFMA-packed
   bf16* act;         // [R][F] SiLU(gate) * up, the hand-off rows
-  unsigned* sync;    // shards 0-7, generation at line 11
+  unsigned* sync;    // shards 0-7, generation at line 11 (k_lm_ffn) / 12 (k_lm_ffn16); k_lm_ffn16's
+                     // column-group tickets at word 13 x 32
   unsigned* err;     // set to 1 when the grid wait gave up
+  float* slab;       // k_lm_ffn16: [48 column groups][4 hidden ranges][16][32] fp32 partials of down
 };
 bool lm_ffn_fits(int H, int F, int R);
 int launch_lm_ffn(const LmFfnArgs& a, hipStream_t st);
+// the same block at 3 <= R <= 16 rows (k_lm_ffn16: down split by hidden range too, per-group tickets)
+bool lm_ffn16_fits(int H, int F, int R);
+int launch_lm_ffn16(const LmFfnArgs& a, hipStream_t st);
 
 // A whole codec stage of Block1Ds for one sample in ONE persistent launch
 // (codec_stage.hip): C = 2,048 at T = 1, C = 1,024 at T = 2 or 8.

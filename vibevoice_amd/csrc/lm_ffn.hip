@@ -247,3 +247,206 @@ int launch_lm_ffn(const LmFfnArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_lm_ffn, dim3(lf::G), dim3(lf::NT), lf::TOTAL, st, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
+
+// ============================================================================
+// The same block at 3 <= R <= 16 rows (B = 8: 16 rows), one launch of 256
+// workgroups, one grid-wide hand-off (DESIGN.md §8's sizing):
+//   * gate|up: workgroup w streams tiles [1120 w / 256, 1120 (w + 1) / 256) (4
+//     or 5 of the 16-row tiles, into registers: 10 compute waves, wave v = tile
+//     slot v / 2 over k-blocks [24 (v % 2), + 24)); the whole 16-row A side
+//     (48 KB) by LDS DMA, RMSNorm'd in place (xform<XF_NORM>'s rounding); MFMA;
+//     the two K halves summed in order; SiLU * up -> the act columns, written
+//     through;
+//   * one grid wait;
+//   * down, split by K as well as by columns (at 16 rows a column owner would
+//     need all 287 KB of act rows): workgroups w < 192 own column group w / 4
+//     (32 outputs = 2 tiles) over hidden range w % 4 (2,240 units: 72 KB of act
+//     rows by DMA, 140 KB of weights into registers, issued through the
+//     hand-off); the [16][32] fp32 partial goes to a slab, and the group's 4th
+//     arrival (a per-group ticket, no second grid wait) sums the 4 partials in
+//     range order + the residual -> out.
+// Arithmetic as k_lm_ffn (another summation order than the GEMV pair).
+namespace lf16 {
+constexpr int H = 1536, F = 8960, G = pk::G, RMAX = 16;
+constexpr int NWC = 10, NTC = NWC * 64, NT = NTC + 64;   // 10 compute waves + the control wave
+constexpr int KC1 = H / 32, KC2 = F / 32;                // 48 / 280 k-blocks
+constexpr int T1 = 2 * F / 16;                           // 1,120 gate|up tiles
+constexpr int KH1 = KC1 / 2;                             // 24 k-blocks per wave (a tile's K half)
+constexpr int NG = H / 32, NR = 4, KR = KC2 / NR;        // 48 column groups, 4 hidden ranges of 70 k-blocks
+constexpr int KW2 = KR / 5;                              // 14 k-blocks per wave (5 waves per output tile)
+constexpr int NCH = H / 8;                               // 192 chunks per row
+constexpr int XST = H + 8, AST = KR * 32 + 8;            // padded LDS row strides
+constexpr int XS = 0, XS_B = (RMAX * AST * 2 + 15) / 16 * 16;   // A rows (phase A) / act rows (phase B)
+constexpr int NW = XS + XS_B, NW_B = H * 2;
+constexpr int RED = NW + NW_B, RED_B = 5 * 2 * 256 * 4;  // [5 tiles][2 halves] / [2 tiles][5 K parts] f32x4 tiles
+constexpr int SU = RED + RED_B, SU_B = 5 * RMAX * 8 * 2;
+constexpr int SM = SU + SU_B, SM_B = 128;                // ok, last, inv[16]
+constexpr int TOTAL = SM + SM_B;
+constexpr int TK = 13 * pk::LINE;                        // ticket words in the sync buffer (after the 13 counter lines)
+static_assert(RMAX * XST * 2 <= XS_B && TOTAL <= 160 * 1024, "lm ffn16 LDS");
+}  // namespace lf16
+
+__global__ void __launch_bounds__(lf16::NT) k_lm_ffn16(LmFfnArgs a) {
+  using namespace lf16;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16* xs = (bf16*)(smem + XS);       // phase A: [16][XST] A rows; phase B: [16][AST] act rows
+  bf16* nw_s = (bf16*)(smem + NW);
+  float* red = (float*)(smem + RED);
+  bf16* su_s = (bf16*)(smem + SU);     // [5][16][8]
+  unsigned* ok_s = (unsigned*)(smem + SM);
+  float* inv_s = (float*)(smem + SM + 16);
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool ctl = wave == NWC;
+  const int w = blockIdx.x, lane = threadIdx.x & 63, R = a.R;
+  const int t0 = (T1 * w) >> 8, nt = ((T1 * (w + 1)) >> 8) - t0;   // 4 or 5 tiles
+  const int js = wave >> 1, kh = wave & 1;                         // this wave's tile slot / K half
+  const bool busy1 = !ctl && js < nt;
+  const bool owner = w < NR * NG;
+  const int grp = w >> 2, rng = w & 3;                             // down: columns [32 grp, +32), k-blocks [70 rng, +70)
+  unsigned g0 = 0;
+  if (ctl) __builtin_amdgcn_s_setprio(3);
+  if (ctl) g0 = __hip_atomic_load((hl_gu32*)(a.sync + 12 * pk::LINE), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~7u;
+
+  bf16x8 wb[KH1];
+  if (!ctl) {
+    const int ln = hl_vopaque(lane);
+    // the A side first (rows m >= R re-read row R - 1: their products are never stored), the norm weight
+    for (int q = wave; q < RMAX * NCH / 64; q += NWC) {   // 64-chunk piece q: row q / 3, chunks (q % 3) * 64 ..
+      const int m = q / 3, i = q - m * 3;
+      hl_dma16<false>(xs + m * XST + i * 512, hl_opaque(a.x) + (long long)min(m, R - 1) * a.ldx + (i * 64 + ln) * 8);
+    }
+    if (wave < 3) hl_dma16<false>(nw_s + wave * 512, hl_opaque(a.nw) + (wave * 64 + ln) * 8);
+    if (busy1) {
+      const bf16* gw = hl_opaque(a.gu) + ((long long)(t0 + js) * KC1 + kh * KH1) * 512 + ln * 8;
+#pragma unroll
+      for (int kk = 0; kk < KH1; ++kk) wb[kk] = hl_ldnt(gw + (long long)kk * 512);
+      asm volatile("s_waitcnt vmcnt(24)" ::: "memory");   // this wave's A-side DMA (the 24 weight loads may fly)
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  for (int m = wave; m < RMAX; m += NT / 64) {   // inverse RMS in k_rmsnorm's order
+    const int ln = hl_vopaque(lane);
+    float ss = 0.f;
+    for (int c = ln; c < NCH; c += 64) {
+      const bf16x8 v = *(const bf16x8*)(xs + m * XST + c * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += bf(v[j]) * bf(v[j]);
+    }
+    ss = wave_sum(ss);
+    if (ln == 0) inv_s[m] = rsqrtf(ss / (float)H + a.eps);
+  }
+  __syncthreads();
+  for (int e = hl_vopaque((int)threadIdx.x); e < RMAX * NCH; e += NT) {   // xform<XF_NORM> (norm weight only), in place
+    const int m = e / NCH, c = e - m * NCH;
+    const bf16x8 xv = *(const bf16x8*)(xs + m * XST + c * 8), wv = *(const bf16x8*)(nw_s + c * 8);
+    const float inv = inv_s[m];
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = tobf(rb(rb(bf(xv[j]) * inv) * bf(wv[j])));
+    *(bf16x8*)(xs + m * XST + c * 8) = o;
+  }
+  __syncthreads();
+  if (busy1) {   // gate|up tile t0 + js over this wave's K half
+    const int ln = hl_vopaque(lane);
+    f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < KH1; ++kk) {
+      const int kc = kh * KH1 + kk;
+      acc = mfma16(*(const bf16x8*)(xs + (ln & 15) * XST + kc * 32 + 8 * (ln >> 4)), wb[kk], acc);
+    }
+    *(f32x4*)(red + (js * 2 + kh) * 256 + ln * 4) = acc;
+  }
+  __syncthreads();
+  if (!ctl && owner) {
+    // the down weights, in flight through the hand-off: tile 2 grp + (v & 1),
+    // k-blocks [70 rng + 14 (v >> 1), + 14), into the registers freed by gate|up
+    const int ln = hl_vopaque(lane);
+    const bf16* dw = hl_opaque(a.dn) + ((long long)(2 * grp + (wave & 1)) * KC2 + rng * KR + (wave >> 1) * KW2) * 512 + ln * 8;
+#pragma unroll
+    for (int kk = 0; kk < KW2; ++kk) wb[kk] = hl_ldnt(dw + (long long)kk * 512);
+  }
+  for (int e = hl_vopaque((int)threadIdx.x); e < nt * RMAX * 8; e += NT) {   // SiLU(gate) * up (epi_silu8), halves in order
+    const int j = e / (RMAX * 8), r = e - j * (RMAX * 8), m = r >> 3, c = r & 7;
+    const int lg = (c + 16 * (m >> 2)) * 4 + (m & 3), lu = (c + 8 + 16 * (m >> 2)) * 4 + (m & 3);
+    const float g = red[(j * 2) * 256 + lg] + red[(j * 2 + 1) * 256 + lg];
+    const float u = red[(j * 2) * 256 + lu] + red[(j * 2 + 1) * 256 + lu];
+    su_s[(j * RMAX + m) * 8 + c] = tobf(rb(silu_f(rb(g))) * rb(u));
+  }
+  __syncthreads();
+  if (ctl) {   // act[m][8 (t0 + j) .. + 8] for rows m < R, written through; then the grid wait
+    for (int q = lane; q < nt * RMAX * 2; q += 64) {
+      const int j = q / (RMAX * 2), r = q - j * RMAX * 2, m = r >> 1, half = r & 1;
+      if (m < R)
+        MemWT::st8(hl_opaque(a.act) + (long long)m * F + 8 * (t0 + j) + 4 * half,
+                   *(const bf16x4*)(su_s + (j * RMAX + m) * 8 + 4 * half));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) ok_s[0] = hl_grid_wait_gen(a.sync, 12, g0, 1, w, a.err) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!ok_s[0] || !owner) return;
+  // ================= down over this workgroup's hidden range -> an fp32 partial of 32 columns
+  if (!ctl) {
+    const bf16* ap = hl_opaque(a.act) + (long long)rng * KR * 32;
+    const int ln = hl_vopaque(lane);
+    for (int q = wave; q < RMAX * 5; q += NWC) {   // row m, 64-chunk piece i (280 chunks: 4.375 pieces)
+      const int m = q / 5, i = q - m * 5, c = i * 64 + ln;
+      if (c < KR * 4) hl_dma16<true>(xs + m * AST + i * 512, ap + (long long)min(m, R - 1) * F + c * 8);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the act rows and the down registers
+  }
+  __syncthreads();
+  if (!ctl) {
+    const int ln = hl_vopaque(lane);
+    f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < KW2; ++kk) {
+      const int kc = (wave >> 1) * KW2 + kk;
+      acc = mfma16(*(const bf16x8*)(xs + (ln & 15) * AST + kc * 32 + 8 * (ln >> 4)), wb[kk], acc);
+    }
+    *(f32x4*)(red + ((wave & 1) * 5 + (wave >> 1)) * 256 + ln * 4) = acc;
+  }
+  __syncthreads();
+  float* slab = a.slab + ((long long)grp * NR + rng) * RMAX * 32;
+  if (threadIdx.x < RMAX * 32) {   // partial [m][c32], the 5 K parts in order
+    const int m = threadIdx.x >> 5, c32 = threadIdx.x & 31, tl = c32 >> 4, n = c32 & 15;
+    const int l = (n + 16 * (m >> 2)) * 4 + (m & 3);
+    float s = 0.f;
+#pragma unroll
+    for (int kp = 0; kp < 5; ++kp) s += red[(tl * 5 + kp) * 256 + l];
+    MemWT::stf(slab + m * 32 + c32, s);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add((hl_gu32*)(a.sync + TK + grp), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ok_s[1] = (t & 3) == 3 ? 1u : 0u;   // the group's 4th arrival of this launch sums it
+  }
+  __syncthreads();
+  if (!ok_s[1] || threadIdx.x >= RMAX * 32) return;
+  {
+    const int m = threadIdx.x >> 5, c32 = threadIdx.x & 31, col = 32 * grp + c32;
+    if (m < R) {
+      const float* sg = a.slab + (long long)grp * NR * RMAX * 32 + m * 32 + c32;
+      float s = 0.f;
+#pragma unroll
+      for (int r = 0; r < NR; ++r) s += MemWT::ldf(sg + r * RMAX * 32);
+      a.out[(long long)m * a.ldx + col] = tobf(bf(a.x[(long long)m * a.ldx + col]) + rb(s));
+    }
+  }
+}
+
+bool lm_ffn16_fits(int H, int F, int R) {
+  if (H != lf16::H || F != lf16::F || R < 3 || R > lf16::RMAX) return false;
+  static const bool ok = persist_resident_kernel((const void*)k_lm_ffn16, lf16::NT, lf16::TOTAL, lf16::G);
+  return ok;
+}
+
+int launch_lm_ffn16(const LmFfnArgs& a, hipStream_t st) {
+  if (!lm_ffn16_fits(lf16::H, lf16::F, a.R) || a.ldx < lf16::H || !a.slab) return 3;
+  hipLaunchKernelGGL(k_lm_ffn16, dim3(lf16::G), dim3(lf16::NT), lf16::TOTAL, st, a);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
