@@ -124,6 +124,9 @@ int vv_head_m16_stamps(void* buf);
  * the one-launch block applies to this context at ntok rows. */
 int vv_lm_ffn(int on);
 int vv_lm_ffn_active(vv_ctx* ctx, int ntok);
+/* Diagnostic: k_lm_ffn16 launches write per-workgroup phase stamps ([256][16]
+ * u64, overwritten per launch; NULL = off). */
+int vv_lm_ffn_stamps(void* buf);
 /* Diagnostic (bench.py): `reps` passes over the LM layers' MLP blocks alone on
  * ntok decode rows (hidden [ntok][H] in place, act [ntok][I] scratch). */
 int vv_lm_mlp_replay(vv_ctx* ctx, int ntok, void* hidden, void* act, int reps, vv_stream stream);

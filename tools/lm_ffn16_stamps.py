@@ -1,0 +1,69 @@
+"""Where k_lm_ffn16's time goes (the LM MLP block at B = 8, 16 rows): graph-replayed
+vv_lm_mlp_replay passes over the 28 layers of the 1.5B LM with per-workgroup
+s_memrealtime stamps (10 ns ticks) of the last launch: 0 start, 1 A side in LDS,
+2 normalised, 3 gate|up products, 4 SiLU * up, 5 hand-off released, 6 act rows
++ down weights landed, 7 down products, 8 partial published, 9 end.  Prints the
+median per phase since each workgroup's start (owners / all) and the launch span.
+usage: python tools/lm_ffn16_stamps.py"""
+import ctypes
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from vibevoice_amd import _lib  # noqa: E402
+from vibevoice_amd.modeling_vibevoice_inference import VibeVoiceForConditionalGenerationInference  # noqa: E402
+
+
+def main():
+    L = _lib.lib()
+    model = VibeVoiceForConditionalGenerationInference.from_pretrained("synthetic:1.5B", device_map="cuda",
+                                                                        synthetic_seed=0, max_batch=8, max_ctx=256)
+    M = 16
+    assert L.vv_lm_ffn_active(model.engine.h, M) == 1
+    x = (torch.randn(M, 1536, device="cuda") * 0.5).bfloat16()
+    act = torch.empty(M, 8960, device="cuda", dtype=torch.bfloat16)
+    s = torch.cuda.Stream()
+
+    def call(n):
+        return L.vv_lm_mlp_replay(model.engine.h, M, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(act.data_ptr()),
+                                  n, ctypes.c_void_p(s.cuda_stream))
+    with torch.cuda.stream(s):
+        _lib.check(call(1), "replay")
+    torch.cuda.synchronize()
+    times = []
+    for n in (1, 3):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            g.capture_begin(capture_error_mode="thread_local")
+            call(n)
+            g.capture_end()
+            g.replay()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(4):
+                g.replay()
+            e1.record(s)
+        e1.synchronize()
+        times.append(e0.elapsed_time(e1) * 1e3 / 4)
+    print(f"k_lm_ffn16: {(times[1] - times[0]) / (2 * 28):.2f} us per block (graph replays, 28 layers)")
+    st = torch.zeros(256 * 16, dtype=torch.int64, device="cuda")
+    L.vv_lm_ffn_stamps(st.data_ptr())
+    with torch.cuda.stream(s):
+        _lib.check(call(1), "replay")
+    torch.cuda.synchronize()
+    L.vv_lm_ffn_stamps(None)
+    model.engine.check_sync()
+    t = st.view(256, 16).cpu().double() * 10e-3
+    for name, rows in (("owners", t[:192]), ("non-owners", t[192:])):
+        used = [k for k in range(10) if bool((rows[:, k] != 0).all())]
+        rel = rows[:, used] - rows[:, :1]
+        med = rel.median(0).values
+        print(f"{name}: " + ", ".join(f"{k}:{float(m):.2f}" for k, m in zip(used, med)))
+    print(f"launch span {float(t[:192, 9].max() - t[:, 0].min()):.2f} us, start skew {float(t[:, 0].max() - t[:, 0].min()):.2f}")
+
+
+if __name__ == "__main__":
+    main()

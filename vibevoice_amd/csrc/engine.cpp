@@ -1364,6 +1364,11 @@ static int lm_attn_half(vv_ctx* c, LmPass& P, int l, hipStream_t st) {
 // the LM MLP block in one launch (lm_ffn.hip) at decode with <= 2 rows, unsharded,
 // while the context is the device's only registered one; 0 = two GEMV launches
 static std::atomic<int> g_lm_ffn{1};
+static std::atomic<unsigned long long*> g_lm_ffn_stamps{nullptr};
+extern "C" int vv_lm_ffn_stamps(void* buf) {   // diagnostic: k_lm_ffn16 launches record [256][16] phase stamps
+  g_lm_ffn_stamps = (unsigned long long*)buf;
+  return 0;
+}
 extern "C" int vv_lm_ffn(int on) {   // bit 0: on; bit 1: not at 3..16 rows (k_lm_ffn16)
   g_lm_ffn = on & 3;
   return 0;
@@ -1402,6 +1407,7 @@ static int lm_mlp_half(vv_ctx* c, LmPass& P, int l, hipStream_t st) {
     a.sync = (unsigned*)c->lf_sync.p;
     a.err = (unsigned*)c->hf_sync.p + 10 * 32;
     a.slab = (float*)c->lf_slab.p;
+    a.stamps = g_lm_ffn_stamps.load();
     if (P.ntok <= 2) KCHK(launch_lm_ffn(a, st));
     else KCHK(launch_lm_ffn16(a, st));
     return 0;

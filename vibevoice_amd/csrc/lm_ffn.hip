@@ -307,6 +307,12 @@ __global__ void __launch_bounds__(lf16::NT) k_lm_ffn16(LmFfnArgs a) {
   unsigned g0 = 0;
   if (ctl) __builtin_amdgcn_s_setprio(3);
   if (ctl) g0 = __hip_atomic_load((hl_gu32*)(a.sync + 12 * pk::LINE), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~7u;
+  // diagnostics: 0 start, 1 A side in LDS, 2 A side normalised, 3 gate|up products, 4 SiLU * up,
+  // 5 hand-off released, 6 act rows + down weights landed, 7 down products, 8 partial published, 9 end
+  auto stamp = [&](int k) {
+    if (a.stamps && threadIdx.x == 0) a.stamps[w * 16 + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
 
   bf16x8 wb[KH1];
   if (!ctl) {
@@ -327,6 +333,7 @@ __global__ void __launch_bounds__(lf16::NT) k_lm_ffn16(LmFfnArgs a) {
     }
   }
   __syncthreads();
+  stamp(1);
   for (int m = wave; m < RMAX; m += NT / 64) {   // inverse RMS in k_rmsnorm's order
     const int ln = hl_vopaque(lane);
     float ss = 0.f;
@@ -349,6 +356,7 @@ __global__ void __launch_bounds__(lf16::NT) k_lm_ffn16(LmFfnArgs a) {
     *(bf16x8*)(xs + m * XST + c * 8) = o;
   }
   __syncthreads();
+  stamp(2);
   if (busy1) {   // gate|up tile t0 + js over this wave's K half
     const int ln = hl_vopaque(lane);
     f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -360,6 +368,7 @@ __global__ void __launch_bounds__(lf16::NT) k_lm_ffn16(LmFfnArgs a) {
     *(f32x4*)(red + (js * 2 + kh) * 256 + ln * 4) = acc;
   }
   __syncthreads();
+  stamp(3);
   if (!ctl && owner) {
     // the down weights, in flight through the hand-off: tile 2 grp + (v & 1),
     // k-blocks [70 rng + 14 (v >> 1), + 14), into the registers freed by gate|up
@@ -376,6 +385,7 @@ __global__ void __launch_bounds__(lf16::NT) k_lm_ffn16(LmFfnArgs a) {
     su_s[(j * RMAX + m) * 8 + c] = tobf(rb(silu_f(rb(g))) * rb(u));
   }
   __syncthreads();
+  stamp(4);
   if (ctl) {   // act[m][8 (t0 + j) .. + 8] for rows m < R, written through; then the grid wait
     for (int q = lane; q < nt * RMAX * 2; q += 64) {
       const int j = q / (RMAX * 2), r = q - j * RMAX * 2, m = r >> 1, half = r & 1;
@@ -387,6 +397,7 @@ __global__ void __launch_bounds__(lf16::NT) k_lm_ffn16(LmFfnArgs a) {
     if (lane == 0) ok_s[0] = hl_grid_wait_gen(a.sync, 12, g0, 1, w, a.err) ? 1u : 0u;
   }
   __syncthreads();
+  stamp(5);
   if (!ok_s[0] || !owner) return;
   // ================= down over this workgroup's hidden range -> an fp32 partial of 32 columns
   if (!ctl) {
@@ -399,6 +410,7 @@ __global__ void __launch_bounds__(lf16::NT) k_lm_ffn16(LmFfnArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the act rows and the down registers
   }
   __syncthreads();
+  stamp(6);
   if (!ctl) {
     const int ln = hl_vopaque(lane);
     f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -410,6 +422,7 @@ __global__ void __launch_bounds__(lf16::NT) k_lm_ffn16(LmFfnArgs a) {
     *(f32x4*)(red + ((wave & 1) * 5 + (wave >> 1)) * 256 + ln * 4) = acc;
   }
   __syncthreads();
+  stamp(7);
   float* slab = a.slab + ((long long)grp * NR + rng) * RMAX * 32;
   if (threadIdx.x < RMAX * 32) {   // partial [m][c32], the 5 K parts in order
     const int m = threadIdx.x >> 5, c32 = threadIdx.x & 31, tl = c32 >> 4, n = c32 & 15;
@@ -426,6 +439,7 @@ __global__ void __launch_bounds__(lf16::NT) k_lm_ffn16(LmFfnArgs a) {
     ok_s[1] = (t & 3) == 3 ? 1u : 0u;   // the group's 4th arrival of this launch sums it
   }
   __syncthreads();
+  stamp(8);
   if (!ok_s[1] || threadIdx.x >= RMAX * 32) return;
   {
     const int m = threadIdx.x >> 5, c32 = threadIdx.x & 31, col = 32 * grp + c32;
@@ -437,6 +451,7 @@ __global__ void __launch_bounds__(lf16::NT) k_lm_ffn16(LmFfnArgs a) {
       a.out[(long long)m * a.ldx + col] = tobf(bf(a.x[(long long)m * a.ldx + col]) + rb(s));
     }
   }
+  stamp(9);
 }
 
 bool lm_ffn16_fits(int H, int F, int R) {
