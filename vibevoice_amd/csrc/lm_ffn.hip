@@ -251,9 +251,11 @@ int launch_lm_ffn(const LmFfnArgs& a, hipStream_t st) {
 // ============================================================================
 // The same block at 3 <= R <= 16 rows (B = 8: 16 rows), one launch of 256
 // workgroups, one grid-wide hand-off (DESIGN.md §8's sizing):
-//   * gate|up: workgroup w streams tiles [1120 w / 256, 1120 (w + 1) / 256) (4
-//     or 5 of the 16-row tiles, into registers: 10 compute waves, wave v = tile
-//     slot v / 2 over k-blocks [24 (v % 2), + 24)); the whole 16-row A side
+//   * gate|up: the 192 down owners stream 4 of the 16-row tiles each, the other
+//     64 workgroups the remaining 352 (5 or 6), into registers (12 compute
+//     waves, wave v = tile slot v / 2 over k-blocks [24 (v % 2), + 24)): at most
+//     452 KB per CU (stamps: both phases run at the per-CU ingest rate, so the
+//     owners' down phase must not sit on top of a 5th tile); the whole 16-row A side
 //     (48 KB) by LDS DMA, RMSNorm'd in place (xform<XF_NORM>'s rounding); MFMA;
 //     the two K halves summed in order; SiLU * up -> the act columns, written
 //     through;
@@ -268,7 +270,7 @@ int launch_lm_ffn(const LmFfnArgs& a, hipStream_t st) {
 // Arithmetic as k_lm_ffn (another summation order than the GEMV pair).
 namespace lf16 {
 constexpr int H = 1536, F = 8960, G = pk::G, RMAX = 16;
-constexpr int NWC = 10, NTC = NWC * 64, NT = NTC + 64;   // 10 compute waves + the control wave
+constexpr int NWC = 12, NTC = NWC * 64, NT = NTC + 64;   // 12 compute waves + the control wave
 constexpr int KC1 = H / 32, KC2 = F / 32;                // 48 / 280 k-blocks
 constexpr int T1 = 2 * F / 16;                           // 1,120 gate|up tiles
 constexpr int KH1 = KC1 / 2;                             // 24 k-blocks per wave (a tile's K half)
@@ -278,8 +280,8 @@ constexpr int NCH = H / 8;                               // 192 chunks per row
 constexpr int XST = H + 8, AST = KR * 32 + 8;            // padded LDS row strides
 constexpr int XS = 0, XS_B = (RMAX * AST * 2 + 15) / 16 * 16;   // A rows (phase A) / act rows (phase B)
 constexpr int NW = XS + XS_B, NW_B = H * 2;
-constexpr int RED = NW + NW_B, RED_B = 5 * 2 * 256 * 4;  // [5 tiles][2 halves] / [2 tiles][5 K parts] f32x4 tiles
-constexpr int SU = RED + RED_B, SU_B = 5 * RMAX * 8 * 2;
+constexpr int RED = NW + NW_B, RED_B = 6 * 2 * 256 * 4;  // [6 tiles][2 halves] / [2 tiles][5 K parts] f32x4 tiles
+constexpr int SU = RED + RED_B, SU_B = 6 * RMAX * 8 * 2;
 constexpr int SM = SU + SU_B, SM_B = 128;                // ok, last, inv[16]
 constexpr int TOTAL = SM + SM_B;
 constexpr int TK = 13 * pk::LINE;                        // ticket words in the sync buffer (after the 13 counter lines)
@@ -299,10 +301,12 @@ __global__ void __launch_bounds__(lf16::NT) k_lm_ffn16(LmFfnArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool ctl = wave == NWC;
   const int w = blockIdx.x, lane = threadIdx.x & 63, R = a.R;
-  const int t0 = (T1 * w) >> 8, nt = ((T1 * (w + 1)) >> 8) - t0;   // 4 or 5 tiles
+  const bool owner = w < NR * NG;
+  const int u = w - NR * NG;                                       // non-owner index
+  const int t0 = owner ? 4 * w : 768 + ((352 * u) >> 6);
+  const int nt = owner ? 4 : 768 + ((352 * (u + 1)) >> 6) - t0;   // 4, or 5 / 6
   const int js = wave >> 1, kh = wave & 1;                         // this wave's tile slot / K half
   const bool busy1 = !ctl && js < nt;
-  const bool owner = w < NR * NG;
   const int grp = w >> 2, rng = w & 3;                             // down: columns [32 grp, +32), k-blocks [70 rng, +70)
   unsigned g0 = 0;
   if (ctl) __builtin_amdgcn_s_setprio(3);
@@ -369,14 +373,6 @@ __global__ void __launch_bounds__(lf16::NT) k_lm_ffn16(LmFfnArgs a) {
   }
   __syncthreads();
   stamp(3);
-  if (!ctl && owner) {
-    // the down weights, in flight through the hand-off: tile 2 grp + (v & 1),
-    // k-blocks [70 rng + 14 (v >> 1), + 14), into the registers freed by gate|up
-    const int ln = hl_vopaque(lane);
-    const bf16* dw = hl_opaque(a.dn) + ((long long)(2 * grp + (wave & 1)) * KC2 + rng * KR + (wave >> 1) * KW2) * 512 + ln * 8;
-#pragma unroll
-    for (int kk = 0; kk < KW2; ++kk) wb[kk] = hl_ldnt(dw + (long long)kk * 512);
-  }
   for (int e = hl_vopaque((int)threadIdx.x); e < nt * RMAX * 8; e += NT) {   // SiLU(gate) * up (epi_silu8), halves in order
     const int j = e / (RMAX * 8), r = e - j * (RMAX * 8), m = r >> 3, c = r & 7;
     const int lg = (c + 16 * (m >> 2)) * 4 + (m & 3), lu = (c + 8 + 16 * (m >> 2)) * 4 + (m & 3);
@@ -386,6 +382,16 @@ __global__ void __launch_bounds__(lf16::NT) k_lm_ffn16(LmFfnArgs a) {
   }
   __syncthreads();
   stamp(4);
+  if (wave < 10 && owner) {
+    // the down weights, in flight through the hand-off (issued after SiLU * up:
+    // issued before it, their 14 loads per thread held the owners' arrival back
+    // ~3.5 us): tile 2 grp + (v & 1), k-blocks [70 rng + 14 (v >> 1), + 14), into
+    // the registers freed by gate|up
+    const int ln = hl_vopaque(lane);
+    const bf16* dw = hl_opaque(a.dn) + ((long long)(2 * grp + (wave & 1)) * KC2 + rng * KR + (wave >> 1) * KW2) * 512 + ln * 8;
+#pragma unroll
+    for (int kk = 0; kk < KW2; ++kk) wb[kk] = hl_ldnt(dw + (long long)kk * 512);
+  }
   if (ctl) {   // act[m][8 (t0 + j) .. + 8] for rows m < R, written through; then the grid wait
     for (int q = lane; q < nt * RMAX * 2; q += 64) {
       const int j = q / (RMAX * 2), r = q - j * RMAX * 2, m = r >> 1, half = r & 1;
@@ -411,7 +417,7 @@ __global__ void __launch_bounds__(lf16::NT) k_lm_ffn16(LmFfnArgs a) {
   }
   __syncthreads();
   stamp(6);
-  if (!ctl) {
+  if (wave < 10) {
     const int ln = hl_vopaque(lane);
     f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
