@@ -127,6 +127,14 @@ int vv_lm_ffn_active(vv_ctx* ctx, int ntok);
 /* Diagnostic: k_lm_ffn16 launches write per-workgroup phase stamps ([256][16]
  * u64, overwritten per launch; NULL = off). */
 int vv_lm_ffn_stamps(void* buf);
+/* Diagnostic switch: the LM attention half at decode (input_layernorm .. o_proj
+ * + residual, <= 16 rows, contexts <= 4,096 keys) as one launch (lm_attn.hip;
+ * 1, default) or the q|k|v, attention and o_proj launches (0); whether it applies
+ * to this context at ntok rows over max_pos_p1 keys; and per-workgroup phase
+ * stamps of its launches ([256][16] u64, overwritten per launch; NULL = off). */
+int vv_lm_attn(int on);
+int vv_lm_attn_active(vv_ctx* ctx, int ntok, int max_pos_p1);
+int vv_lm_attn_stamps(void* buf);
 /* Diagnostic (bench.py): `reps` passes over the LM layers' MLP blocks alone on
  * ntok decode rows (hidden [ntok][H] in place, act [ntok][I] scratch). */
 int vv_lm_mlp_replay(vv_ctx* ctx, int ntok, void* hidden, void* act, int reps, vv_stream stream);

@@ -176,6 +176,7 @@ def test_attn_defer_bit_identical(nrows, chunk, maxpos):
     ns = -(-maxpos // chunk)
     eff = chunk if ns <= 8 else (-(-maxpos // 8) + 31) // 32 * 32
     outs = {}
+    L.vv_lm_attn(0)   # the three-launch attention half (the one-launch form has no split plans)
     try:
         for name, defer, tune in (("defer", 1, 0), ("inkernel", 0, eff), ("default", 0, 0)):
             _lib.check(L.vv_attn_defer(16 if defer else 0, chunk), "attn_defer")   # <= 16 rows defer
@@ -186,6 +187,7 @@ def test_attn_defer_bit_identical(nrows, chunk, maxpos):
     finally:
         L.vv_attn_defer(1, 128)
         L.vv_attn_tune(0, -1)
+        L.vv_lm_attn(1)
     assert torch.equal(outs["defer"][0], outs["inkernel"][0])
     assert torch.equal(outs["defer"][1], outs["inkernel"][1])
     h, ref = outs["defer"][0].float(), outs["default"][0].float()
@@ -330,3 +332,80 @@ def test_lm_ffn16_one_launch_vs_oracle_and_gemv_pair(n):
     finally:
         L_.vv_lm_ffn(1)
     eng.check_sync()
+
+
+@pytest.mark.parametrize("n,lens", [(1, [600, 33]), (3, [1, 31, 32, 64, 200, 97]),
+                                    (8, [5 + 61 * r for r in range(16)])])
+def test_lm_attn_one_launch_vs_oracle_and_three_launches(n, lens):
+    """The LM attention half at decode as ONE launch (lm_attn.hip k_lm_attn:
+    q|k|v tiles + RoPE + cache append, one grid wait, attention in 32-key units
+    over all 256 workgroups, one wait, per-head merge of the units, one wait,
+    o_proj from resident weights + residual) on the 1.5B layer shapes at 2 n
+    rows: each decode step vs the oracle (rel < 2e-2, cosine > 0.999) and vs the
+    q|k|v + k_attn + o_proj launches on the same KV state (within bf16: the
+    projections sum in another order, the keys merge in 32-key units), repeated
+    runs bitwise equal.  Contexts from 2 keys to ~1,000, across unit edges."""
+    import gc
+    from vibevoice_amd import _lib
+    gc.collect()
+    L_ = _lib.lib()
+    R = 2 * n
+    assert len(lens) == R
+    cfg = tiny_config(hidden=1536, layers=2, heads=12, kv_heads=2, inter=8960)
+    eng, sd = make_engine(cfg, seed=13 + n, max_batch=max(n, 1), max_ctx=1024)
+    assert L_.vv_lm_attn_active(eng.h, R, max(lens) + 3) == 1
+    lcfg = dict(cfg.decoder_config)
+    osd = oracle_sd(sd)
+    g = torch.Generator().manual_seed(21 + n)
+    xs = [torch.randn(m, 1536, generator=g).bfloat16() for m in lens]
+    kvs = [olm.RowKV(2) for _ in lens]
+    for r in range(R):
+        olm.forward_rows(osd, lcfg, xs[r][None], kvs[r:r + 1])
+    x = torch.cat(xs).to(dev)
+    slots = torch.cat([torch.full((m,), r) for r, m in enumerate(lens)]).to(**I32)
+    pos = torch.cat([torch.arange(m) for m in lens]).to(**I32)
+    last = torch.cumsum(torch.tensor(lens), 0) - 1
+    eng.lm_forward(x, slots, pos, last.to(**I32))
+    Lt = torch.tensor(lens)
+    try:
+        for s in range(3):
+            step_x = torch.randn(R, 1536, generator=g).bfloat16()
+            ref = olm.forward_rows(osd, lcfg, step_x[:, None], kvs)[:, -1]
+            outs = {}
+            for on in (0, 1, 1):
+                L_.vv_lm_attn(on)
+                h, _ = eng.lm_forward(step_x.to(dev), torch.arange(R).to(**I32), Lt.to(**I32),
+                                      torch.arange(R).to(**I32))
+                torch.cuda.synchronize()
+                outs.setdefault(on, []).append(h.clone())
+            Lt += 1
+            one, three = outs[1][0], outs[0][0]
+            print(f"n={n} step {s}: one launch rel {rel_err(one, ref):.3e} vs oracle (three launches "
+                  f"{rel_err(three, ref):.3e}), {rel_err(one, three):.3e} vs the three launches")
+            assert torch.equal(one, outs[1][1])
+            assert rel_err(one, ref) < 2e-2 and cos(one, ref) > 0.999
+            assert rel_err(one, three) < 2e-2 and cos(one, three) > 0.999
+    finally:
+        L_.vv_lm_attn(1)
+    eng.check_sync()
+
+
+def test_lm_attn_one_launch_limits():
+    """Where the one-launch attention half does not apply: more than 16 rows,
+    contexts past 4,096 keys (the split plans of k_attn take them), the switch
+    off."""
+    import gc
+    from vibevoice_amd import _lib
+    gc.collect()
+    L_ = _lib.lib()
+    cfg = tiny_config(hidden=1536, layers=2, heads=12, kv_heads=2, inter=8960)
+    eng, _ = make_engine(cfg, seed=2, max_batch=8, max_ctx=8192)
+    assert L_.vv_lm_attn_active(eng.h, 16, 4096) == 1
+    assert L_.vv_lm_attn_active(eng.h, 16, 4097) == 0
+    assert L_.vv_lm_attn_active(eng.h, 17, 100) == 0
+    L_.vv_lm_attn(0)
+    try:
+        assert L_.vv_lm_attn_active(eng.h, 2, 100) == 0
+    finally:
+        L_.vv_lm_attn(1)
+    assert L_.vv_lm_attn_active(eng.h, 2, 100) == 1

@@ -63,6 +63,15 @@ def main():
         med = rel.median(0).values
         print(f"{name}: " + ", ".join(f"{k}:{float(m):.2f}" for k, m in zip(used, med)))
     print(f"launch span {float(t[:192, 9].max() - t[:, 0].min()):.2f} us, start skew {float(t[:, 0].max() - t[:, 0].min()):.2f}")
+    # who holds the hand-off back: SiLU * up done (stamp 4) since the launch's first start
+    a4 = t[:, 4] - t[:, 0].min()
+    q = torch.quantile(a4, torch.tensor([0.5, 0.9, 0.99, 1.0], dtype=a4.dtype))
+    print("stamp 4 since launch: p50 %.2f p90 %.2f p99 %.2f max %.2f" % tuple(float(v) for v in q))
+    print("latest 12:", ", ".join(f"wg{int(i)}(xcd{int(i) % 8},{'o' if i < 192 else 'n'}):{float(a4[i]):.2f}"
+                                   for i in a4.argsort(descending=True)[:12]))
+    print("per-XCD max:", ", ".join(f"{x}:{float(a4[x::8].max()):.2f}" for x in range(8)))
+    print("stamp 0 since launch, max per XCD:", ", ".join(f"{x}:{float((t[x::8, 0] - t[:, 0].min()).max()):.2f}"
+                                                          for x in range(8)))
 
 
 if __name__ == "__main__":

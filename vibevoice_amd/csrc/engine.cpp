@@ -196,6 +196,7 @@ struct vv_ctx {
   DevBuf hf_sync;
   DevBuf lf_sync;   // lm_ffn.hip's wait counters (+ k_lm_ffn16's column-group tickets)
   DevBuf lf_slab;   // k_lm_ffn16's down partials [48][4][16][32] fp32
+  DevBuf la_part;   // k_lm_attn's per-unit attention partials (lm_attn_part_floats)
   DevBuf m16_buf;   // head_m16.hip's distributed A side: row partial sums of squares [16][192] f32 + rows [16][H]
   DevBuf cs_sync;          // persistent codec stage (codec_stage.hip): its wait counters
   DevBuf cw_sync;          // wide codec stages (codec_wide.hip): one counter line per cluster, per C
@@ -916,7 +917,7 @@ void vv_destroy(vv_ctx* c) {
   DevBuf* bufs[] = {&c->norm_ws, &c->kv_k, &c->kv_v, &c->lm_ws, &c->attn_part, &c->attn_cnt, &c->valid_ids, &c->splitk_ws, &c->splitk_cnt,
                     &c->temb, &c->tfreq_tmp, &c->head_ws, &c->codec_ws, &c->slot_scratch, &c->unit_sb,
                     &c->rope_tab, &c->zero_rows, &c->hf_sync, &c->cs_sync, &c->m16_buf, &c->lf_sync,
-                    &c->cw_sync, &c->cw_slab, &c->cw_xbuf, &c->lf_slab};
+                    &c->cw_sync, &c->cw_slab, &c->cw_xbuf, &c->lf_slab, &c->la_part};
   for (DevBuf* b : bufs) b->release();
   ConvNet* nets[] = {&c->dec, &c->sem, &c->aenc, &c->senc};
   for (ConvNet* n : nets) {
@@ -1021,6 +1022,10 @@ int vv_finalize(vv_ctx* c) {
   CHK(c->lf_sync.ensure(SYNC_BYTES));
   HIPCHK(hipMemset(c->lf_sync.p, 0, SYNC_BYTES));
   if (k.max_batch >= 2 && lm_ffn16_fits(k.hidden, k.intermediate, 16)) CHK(c->lf_slab.ensure(48 * 4 * 16 * 32 * sizeof(float)));
+  const int la_rows = std::min(2 * k.max_batch, 16), la_keys = std::min(k.max_ctx, LA_MAX_KEYS);
+  const bool la_fits = lm_attn_fits(k.hidden, k.n_heads, k.n_kv_heads, k.head_dim, la_rows, la_keys) &&
+                       c->qkv_n == (k.n_heads + 2 * k.n_kv_heads) * k.head_dim;
+  if (la_fits) CHK(c->la_part.ensure(lm_attn_part_floats(la_rows, la_keys) * sizeof(float)));
   CHK(c->cw_sync.ensure(2 * CW_LINES * 128));
   HIPCHK(hipMemset(c->cw_sync.p, 0, 2 * CW_LINES * 128));
   if (c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 16))
@@ -1031,7 +1036,7 @@ int vv_finalize(vv_ctx* c) {
   c->persist_capable = codec_stage_any(c->dec) || codec_stage_any(c->sem) || codec_wide_any(c->dec) ||
                        codec_wide_any(c->sem) ||
                        (c->head_gemv && head_m16_fits(k.hidden, k.head_ffn, 16)) ||
-                       lm_ffn_fits(k.hidden, k.intermediate, 2) || lm_ffn16_fits(k.hidden, k.intermediate, 16);
+                       lm_ffn_fits(k.hidden, k.intermediate, 2) || lm_ffn16_fits(k.hidden, k.intermediate, 16) || la_fits;
   if (c->persist_ok && !c->persist_follow && c->persist_capable && !c->hl_registered) {
     c->hl_registered = true;
     hl_register(c->device, +1);
@@ -1185,6 +1190,7 @@ extern "C" int vv_attn_group(int on) {      // 1 = default; n >= 2: at most n sp
 }
 struct LmPass {
   int ntok = 0, nsplit = 1, chunk = 64, prefill = 0, defer = 0, group = 0, ngroups = 0;
+  int maxp = 0;   // keys of the longest row (max position + 1)
   bf16 *h = nullptr, *q = nullptr, *att = nullptr, *act = nullptr;
   RowMap in_m, hm;
   const int *slot = nullptr, *pos = nullptr;
@@ -1253,6 +1259,7 @@ static int lm_begin(vv_ctx* c, LmPass& P, int ntok, const void* embeds, int embe
     c->lm_ws_tokens = ntok;
   }
   P.ntok = ntok;
+  P.maxp = max_pos_p1;
   P.h = (bf16*)c->lm_ws.p;
   bf16* a = P.h + (size_t)ntok * H;
   bf16* qkv = a + (size_t)ntok * H;
@@ -1292,6 +1299,37 @@ static void tp_residual(vv_ctx* c, GemmArgs& g, const RowMap& res) {
   }
 }
 
+// the LM attention half at decode in one launch (lm_attn.hip): <= 16 rows of the
+// 1.5B shapes, contexts <= LA_MAX_KEYS, unsharded, while the context is the
+// device's only registered one; 0 = the three launches (q|k|v, k_attn, o_proj)
+static std::atomic<int> g_lm_attn{1};
+static std::atomic<unsigned long long*> g_lm_attn_stamps{nullptr};
+extern "C" int vv_lm_attn(int on) {
+  g_lm_attn = on ? 1 : 0;
+  return 0;
+}
+extern "C" int vv_lm_attn_stamps(void* buf) {   // diagnostic: k_lm_attn launches record [256][16] phase stamps
+  g_lm_attn_stamps = (unsigned long long*)buf;
+  return 0;
+}
+static bool lm_attn_on(vv_ctx* c, const LmPass& P) {
+  const vv_config& k = c->cfg;
+  return g_lm_attn && c->la_part.p && c->lf_sync.p && !P.prefill && c->tp_size == 1 && !c->comm &&
+         c->qkv_n == (k.n_heads + 2 * k.n_kv_heads) * k.head_dim && !P.hm.idx && P.hm.sT == k.hidden &&
+         P.hm.T >= P.ntok && P.maxp <= std::min(k.max_ctx, LA_MAX_KEYS) &&
+         lm_attn_fits(k.hidden, k.n_heads, k.n_kv_heads, k.head_dim, P.ntok, P.maxp) &&
+         lm_attn_part_floats(P.ntok, P.maxp) * sizeof(float) <= c->la_part.bytes && persist_on(c);
+}
+extern "C" int vv_lm_attn_active(vv_ctx* c, int ntok, int max_pos_p1) {
+  if (!c || !c->finalized) return 0;
+  LmPass P;
+  P.ntok = ntok;
+  P.maxp = max_pos_p1;
+  P.prefill = attn_use_prefill(ntok, c->lm_slots) ? 1 : 0;
+  P.hm = rowmap(nullptr, c->cfg.hidden);
+  return lm_attn_on(c, P) ? 1 : 0;
+}
+
 // input_layernorm .. o_proj (+ residual on rank 0)
 static int lm_attn_half(vv_ctx* c, LmPass& P, int l, hipStream_t st) {
   const vv_config& k = c->cfg;
@@ -1311,6 +1349,25 @@ static int lm_attn_half(vv_ctx* c, LmPass& P, int l, hipStream_t st) {
     g.rope.inv_freq = P.inv_freq;
     g.rope.cs_tab = g_rope_tab ? (const bf16*)c->rope_tab.p : nullptr;
     g.rope.kv = c->kv;
+    if (lm_attn_on(c, P)) {
+      LmAttnArgs a;
+      memset(&a, 0, sizeof(a));
+      a.qkv = g;
+      a.nw = W(c, p + ".in_norm");
+      a.eps = k.rms_eps;
+      a.scale = 1.0f / sqrtf((float)d);
+      a.R = P.ntok;
+      a.ow = W(c, p + ".o_w");
+      a.res = l == 0 ? P.in_m : P.hm;
+      a.out = P.hm;
+      a.att = P.att;
+      a.part = (float*)c->la_part.p;
+      a.sync = (unsigned*)c->lf_sync.p;
+      a.err = (unsigned*)c->hf_sync.p + 10 * 32;
+      a.stamps = g_lm_attn_stamps.load();
+      KCHK(launch_lm_attn(a, P.maxp, st));
+      return 0;
+    }
     CHK(gemm(c, g, st));
   }
   AttnArgs at;

@@ -265,6 +265,28 @@ int launch_lm_ffn(const LmFfnArgs& a, hipStream_t st);
 bool lm_ffn16_fits(int H, int F, int R);
 int launch_lm_ffn16(const LmFfnArgs& a, hipStream_t st);
 
+// ---- the LM attention half at decode in one launch (lm_attn.hip): input_layernorm
+// -> q|k|v + RoPE + KV append -> attention -> o_proj + residual, R <= 16 rows of
+// the 1.5B shapes, contexts <= LA_MAX_KEYS keys
+constexpr int LA_MAX_KEYS = 4096;
+struct LmAttnArgs {
+  GemmArgs qkv;      // the q|k|v projection as launch_gemm would run it: M = R, a = the A rows,
+                     // w = qkv_w, epi = EPI_ROPE (+ bias), rope = q_out / KV cache / pos / slots
+  const bf16* nw;    // input_layernorm weight [H]
+  float eps, scale;  // RMSNorm eps, 1 / sqrt(head_dim)
+  int R, pad_;
+  const bf16* ow;    // o_proj [H][H], MFMA-packed
+  RowMap res, out;   // residual rows (read) and output rows (written): x + o_proj(attention)
+  bf16* att;         // [R][H] merged attention rows (the o_proj hand-off, written through)
+  float* part;       // [units][6 * 128 + 12] per-unit (O, m, l) partials
+  unsigned* sync;    // shards 0-7, this kernel's generation at line 15
+  unsigned* err;     // set to 1 when a grid wait gave up
+  unsigned long long* stamps;   // diagnostics: [256][16] s_memrealtime per phase, or nullptr
+};
+bool lm_attn_fits(int H, int nh, int nkv, int d, int R, int keys);
+size_t lm_attn_part_floats(int R, int keys);
+int launch_lm_attn(const LmAttnArgs& a, int keys, hipStream_t st);
+
 // A whole codec stage of Block1Ds for one sample in ONE persistent launch
 // (codec_stage.hip): C = 2,048 at T = 1, C = 1,024 at T = 2 or 8.
 struct CodecStageBlock {
