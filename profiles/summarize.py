@@ -65,6 +65,21 @@ def main(path, n_steps=None, out_json=None):
     print("\nby (kernel, grid), top 30:")
     for (n, g), (c, t) in sorted(per.items(), key=lambda x: -x[1][1])[:30]:
         print(f"{n:40s} {str(g):>16s} {c / k:8.1f}/step {t / k / 1e3:9.1f} us/step  avg {t / c / 1e3:8.2f} us")
+    # the last step in launch order (runs of one (kernel, grid) collapsed), with the
+    # gap before each launch: where the codec / head / LM phases sit in the step
+    a, b = steps[-1]
+    seg = rows[a + 1:b + 1]
+    print("\nlast step in launch order: start us, kernel, grid, launches x avg us, gap before (us):")
+    t0, i = seg[0][0], 0
+    while i < len(seg):
+        j = i
+        while j + 1 < len(seg) and seg[j + 1][2:] == seg[i][2:]:
+            j += 1
+        run = seg[i:j + 1]
+        avg = sum(e - s for s, e, _, _ in run) / len(run) / 1e3
+        gap = (seg[i][0] - seg[i - 1][1]) / 1e3 if i else 0.0
+        print(f"{(seg[i][0] - t0) / 1e3:9.1f}  {seg[i][2]:40s} {str(seg[i][3]):>16s} {len(run):3d} x {avg:7.2f}  gap {gap:5.2f}")
+        i = j + 1
 
 
 if __name__ == "__main__":
