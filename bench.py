@@ -283,16 +283,86 @@ def measure_lm_ffn(model, B, reps=2, iters=4):
     alg = 3 * I * H * 2 + M * H * 2 * 2
     shape = f"rows={M} H={H} I={I}"
     traffic = None
-    pf = os.path.join(ROOT, "profiles", f"r05_pmc_lm_ffn_r{M}.json")
-    if os.path.exists(pf):
-        with open(pf) as f:
-            pmc = json.load(f)
-        if pmc.get("kernel") == "k_lm_ffn" and pmc.get("shape") == shape:
-            traffic = pmc["hbm_bytes_per_launch"]
-    return roof("k_lm_ffn (LM post-norm + gate|up + SiLU*up + down + residual in one launch, one grid-wide "
+    for pf in (os.path.join(ROOT, "profiles", f"r06_pmc_lm_ffn_r{M}.json"),
+               os.path.join(ROOT, "profiles", f"r05_pmc_lm_ffn_r{M}.json")):
+        if traffic is None and os.path.exists(pf):
+            with open(pf) as f:
+                pmc = json.load(f)
+            if pmc.get("kernel") == ("k_lm_ffn" if M <= 2 else "k_lm_ffn16") and pmc.get("shape") == shape:
+                traffic = pmc["hbm_bytes_per_launch"]
+    kname = "k_lm_ffn" if M <= 2 else "k_lm_ffn16"
+    return roof(f"{kname} (LM post-norm + gate|up + SiLU*up + down + residual in one launch, one grid-wide "
                 "hand-off; graph-replayed)", shape, alg, per, traffic, launches_per_token=nl,
                 note="graph-replayed MLP blocks of the 28 layers (vv_lm_mlp_replay), HIP events on the replay "
                      "stream; weights read once per pass (2.3 GB rotation), non-temporal")
+
+
+def measure_lm_attn(model, B, ctx, reps=2, iters=4):
+    """The LM attention half as the loop runs it at this batch: ONE k_lm_attn
+    launch per layer (lm_attn.hip: input_layernorm + q|k|v + RoPE + KV append,
+    attention, o_proj + residual; decode with 2B <= 16 rows and <= 4,096 keys).
+    vv_lm_attn_replay runs 1 or 1 + reps passes over the 28 layers' attention
+    halves, 2B rows at position ~ctx (the loop's average context; after the timed
+    loop, so the cache rows it overwrites are no longer read), inside two captured
+    graphs; the difference of their replay times (HIP events on the replay
+    stream) over reps x layers is the time per half.  Algorithmic bytes: q|k|v
+    (+bias) and o_proj weights, the norm weight, the rows in / out, the K / V
+    rows read (ctx + 1 keys per row) and appended."""
+    from vibevoice_amd import _lib
+    eng = model.engine
+    lmc = model.config.decoder_config
+    H, nl = lmc.hidden_size, lmc.num_hidden_layers
+    nh, nkv = lmc.num_attention_heads, lmc.num_key_value_heads
+    d = H // nh
+    M = 2 * B
+    lib = _lib.lib()
+    keys = int(ctx) + 1
+    if lib.vv_lm_attn_active(eng.h, M, keys) != 1:
+        return None
+    dev = model.device
+    x = (torch.randn(M, H, device=dev) * 0.5).bfloat16()
+    slots = torch.arange(M, device=dev, dtype=torch.int32)
+    pos = torch.full((M,), keys - 1, device=dev, dtype=torch.int32)
+    stream = torch.cuda.Stream(dev)
+
+    def call(n):
+        return lib.vv_lm_attn_replay(eng.h, M, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(slots.data_ptr()),
+                                     ctypes.c_void_p(pos.data_ptr()), keys, n, ctypes.c_void_p(stream.cuda_stream))
+    with torch.cuda.stream(stream):
+        _lib.check(call(1), "lm_attn_replay")
+    stream.synchronize()
+
+    def graph(n):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(stream):
+            g.capture_begin(capture_error_mode="thread_local")
+            try:
+                rc = call(n)
+            finally:
+                g.capture_end()
+        _lib.check(rc, "lm_attn_replay")
+        return g
+    g1, gn = graph(1), graph(1 + reps)
+    times = []
+    with torch.cuda.stream(stream):
+        for g in (g1, gn):
+            g.replay()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(iters):
+                g.replay()
+            e1.record(stream)
+            e1.synchronize()
+            times.append(e0.elapsed_time(e1) / 1e3 / iters)
+    eng.check_sync()
+    per = (times[1] - times[0]) / (reps * nl)
+    nq = (nh + 2 * nkv) * d
+    alg = (nq * H + nq + H * H + H) * 2 + M * H * 2 * 2 + M * keys * nkv * d * 2 * 2 + M * nkv * d * 2 * 2
+    return roof("k_lm_attn (LM attention half in one launch: input_layernorm + q|k|v + RoPE + KV append, "
+                "attention over 32-key units, merge, o_proj + residual; three grid waits; graph-replayed)",
+                f"rows={M} H={H} keys={keys}", alg, per, None, launches_per_token=nl,
+                note="graph-replayed attention halves of the 28 layers (vv_lm_attn_replay), HIP events on the "
+                     "replay stream; latency-bound (11 MB of weights + the KV rows per launch)")
 
 
 def measure_head_layers(model, B, reps=10, iters=4):
@@ -668,7 +738,12 @@ def main():
         except Exception as e:   # noqa: BLE001
             print(f"bench: head roofline not measured: {e}", file=sys.stderr, flush=True)
             roof_head = {"error": str(e)[:200]}
-    roofline, roofline_2 = pick_roofline(roof_lm, roof_head)
+    roof_attn = None
+    try:
+        roof_attn = measure_lm_attn(model, B, ctx_avg)
+    except Exception as e:   # noqa: BLE001
+        print(f"bench: LM attention half roofline not measured: {e}", file=sys.stderr, flush=True)
+    roofline, roofline_2 = pick_roofline(roof_lm, roof_head, roof_attn)
     for r in (roofline, roofline_2):
         if r and "error" not in r:
             in_loop_average(r, B)

@@ -135,6 +135,11 @@ int vv_lm_ffn_stamps(void* buf);
 int vv_lm_attn(int on);
 int vv_lm_attn_active(vv_ctx* ctx, int ntok, int max_pos_p1);
 int vv_lm_attn_stamps(void* buf);
+/* Diagnostic (bench.py): `reps` passes over the LM layers' attention halves alone
+ * on ntok decode rows (embeds [ntok][H] as layer 0's input, slots / positions as
+ * for vv_lm_forward). */
+int vv_lm_attn_replay(vv_ctx* ctx, int ntok, const void* embeds, const int* slot, const int* pos, int max_pos_p1,
+                      int reps, vv_stream stream);
 /* Diagnostic (bench.py): `reps` passes over the LM layers' MLP blocks alone on
  * ntok decode rows (hidden [ntok][H] in place, act [ntok][I] scratch). */
 int vv_lm_mlp_replay(vv_ctx* ctx, int ntok, void* hidden, void* act, int reps, vv_stream stream);

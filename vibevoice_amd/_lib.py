@@ -92,6 +92,7 @@ EXPORTS = [
     ("vv_lm_attn", I, [I]),
     ("vv_lm_attn_active", I, [P, I, I]),
     ("vv_lm_attn_stamps", I, [P]),
+    ("vv_lm_attn_replay", I, [P, I, P, P, P, I, I, P]),
     ("vv_lm_mlp_replay", I, [P, I, P, P, I, P]),
     ("vv_head_m16_pre", I, [I]),
     ("vv_attn_defer_max", I, [I]),

@@ -1548,6 +1548,21 @@ int vv_lm_forward(vv_ctx* c, int ntok, const void* embeds, int embed_rows, const
   return lm_end(c, P, nout, out_idx, hidden_out, logits_out, st);
 }
 
+// Diagnostic (bench.py's candidate roofline of the LM attention half): `reps`
+// passes over the LM layers' attention halves alone on `ntok` decode rows
+// (embeds [ntok][H] as layer 0's input; later layers read / write the pass's own
+// hidden rows), as lm_attn_half runs them (k_lm_attn or the three launches).
+extern "C" int vv_lm_attn_replay(vv_ctx* c, int ntok, const void* embeds, const int* slot, const int* pos,
+                                 int max_pos_p1, int reps, vv_stream vst) {
+  if (!c || !c->finalized || ntok < 1 || ntok > 2 * c->cfg.max_batch || !embeds || !slot || !pos)
+    FAIL("vv_lm_attn_replay: bad arguments");
+  LmPass P;
+  CHK(lm_begin(c, P, ntok, embeds, ntok, slot, pos, max_pos_p1));
+  for (int r = 0; r < reps; ++r)
+    for (int l = 0; l < c->cfg.n_layers; ++l) CHK(lm_attn_half(c, P, l, (hipStream_t)vst));
+  return 0;
+}
+
 int vv_lm_forward_group(int n, vv_ctx* const* ctxs, int ntok, const void* embeds, int embed_rows, const int* slot,
                         const int* pos, int max_pos_p1, int nout, const int* out_idx, void* hidden_out,
                         float* logits_out, vv_stream vst) {
