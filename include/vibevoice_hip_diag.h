@@ -180,6 +180,10 @@ int vv_codec_tile_stamps(void* buf);
  * of n samples on ctx runs them now.  _stamps: per-workgroup phase stamps
  * ([n][tiles x S][16] u64 at buf + 8192 x (2 x net + (C == 512))); NULL = off. */
 int vv_codec_wide(int on);
+/* Diagnostic: wide-stage grids past one resident wave (1: clusters complete in
+ * dispatch order; slower at B = 8 than the GEMM path) or only grids resident at
+ * once (0, default). */
+int vv_codec_wide_over(int on);
 int vv_codec_wide_active(vv_ctx* ctx, int n);
 int vv_codec_wide_stamps(void* buf);
 /* A/B switch: 1 (default) = the balanced many-tile GEMV plan at M >= 8 (one

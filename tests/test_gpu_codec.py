@@ -317,7 +317,7 @@ def test_codec_tile_narrow_stages(slots_sched):
             assert e_b < 3e-2 and cos(got, base) > 0.999, (f, name, e_b)
 
 
-@pytest.mark.parametrize("n", [1, 2])
+@pytest.mark.parametrize("n", [1, 2, 8])
 def test_codec_wide_stages(n):
     """The wide stages (C = 256 at T = 200, C = 512 at T = 40; decoder and
     semantic encoder) as ONE launch each (codec_wide.hip: clusters of C / 32
@@ -325,14 +325,20 @@ def test_codec_wide_stages(n):
     reduce-scattered and block outputs all-gathered inside the cluster) vs the
     oracle and vs the k_mix + GEMM path over four streamed frames, n samples
     (their conv histories carried frame to frame), bitwise equal run to run
-    (the member order of the partial sums is fixed).  The codec tolerance: rel L2
-    < 3e-2, cosine > 0.999."""
+    (the member order of the partial sums is fixed).  n = 8 (configs[2]) runs
+    grids past one resident wave (832 / 384 workgroups; clusters complete in
+    dispatch order; vv_codec_wide_over, off by default).  The codec tolerance:
+    rel L2 < 3e-2, cosine > 0.999."""
     from vibevoice_amd import _lib
     L = _lib.lib()
+    L.vv_codec_wide_over(1 if n > 2 else 0)
     cfg = tiny_config(ratios=(8, 5, 5, 4, 2, 2), depths="3-3-3-3-3-3-8", nf=32)
     sd = synthetic_state_dict(cfg, seed=3, device="cpu", mode="test", with_acoustic_encoder=False)
-    eng = Engine(cfg, sd, dev, max_batch=2, max_ctx=64)
-    assert L.vv_codec_wide_active(eng.h, n) == 1
+    eng = Engine(cfg, sd, dev, max_batch=max(2, n), max_ctx=64)
+    active = L.vv_codec_wide_active(eng.h, n)
+    if active != 1:
+        L.vv_codec_wide_over(0)
+    assert active == 1
     H = cfg.decoder_config.hidden_size
     dd = ocodec.codec_dims(cfg.acoustic_tokenizer_config, "decoder")
     ed = ocodec.codec_dims(cfg.semantic_tokenizer_config, "encoder")
@@ -357,8 +363,9 @@ def test_codec_wide_stages(n):
             outs.setdefault(mode, []).append(res)
     finally:
         L.vv_codec_wide(1)
+        L.vv_codec_wide_over(0)
     eng.check_sync()
-    st_a, st_s = ocodec.StreamState(2), ocodec.StreamState(2)
+    st_a, st_s = ocodec.StreamState(max(2, n)), ocodec.StreamState(max(2, n))
     idx = torch.arange(n)
     for f, lat in enumerate(lats):
         a_ref = ocodec.decode(sd_a, dd, (lat / s_f - b_f).unsqueeze(-1), st_a, idx)

@@ -81,6 +81,7 @@ EXPORTS = [
     ("vv_codec_tile", I, [I]),
     ("vv_codec_tile_stamps", I, [P]),
     ("vv_codec_wide", I, [I]),
+    ("vv_codec_wide_over", I, [I]),
     ("vv_codec_wide_active", I, [P, I]),
     ("vv_codec_wide_stamps", I, [P]),
     ("vv_head_m16", I, [I]),

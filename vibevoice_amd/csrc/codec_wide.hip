@@ -24,6 +24,8 @@
 // n x tiles x S workgroups co-resident (<= 256 at one per CU): the engine runs
 // it only under the grid-waiting kernels' rule (persist_on) and otherwise takes
 // the launch-per-op path.
+#include <atomic>
+
 #include "persist_dev.h"
 
 namespace cw {
@@ -345,6 +347,20 @@ static int cw_launch(const CodecWideArgs& a, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+// Grids larger than one resident wave (B = 8: n x tiles x S = 384 / 832
+// workgroups): only a CLUSTER waits on its own members, never on another
+// cluster, and workgroups are dispatched in index order (x fastest, so a
+// cluster's S members are consecutive).  The lowest-indexed cluster that is not
+// wholly resident then only waits for slots held by lower-indexed workgroups, of
+// complete clusters that finish without waiting on anything later -- so every
+// cluster completes; the waits stay bounded (~200 ms, error word) regardless.
+// Off by default: at B = 8 every one of the 832 / 384 workgroups re-reads its
+// member's weights (320 MB of L2 / Infinity-Cache reads for the C = 256 stage),
+// and the step measured 4.015 ms against 3.968 with the k_mix + GEMM path
+// (same build, bench.py --batch 8); tests/test_gpu_codec.py runs it at n = 8.
+static std::atomic<int> g_cw_over{0};
+void codec_wide_oversubscribe(int on) { g_cw_over = on ? 1 : 0; }
+
 template <int C>
 static bool cw_resident(int n, int T) {
   using G = cw::Geo<C>;
@@ -355,7 +371,7 @@ static bool cw_resident(int n, int T) {
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_codec_wide<C>, cw::NTH, G::TOTAL) != hipSuccess)
     return false;
   const int grid = n * ((T + G::R - 1) / G::R) * G::S;
-  return persist_resident(nb, cus, 0, grid);
+  return persist_resident(nb, cus, 0, grid) || (g_cw_over && persist_resident(nb, cus, 0, G::S));
 }
 
 // shapes the cluster kernel takes, with every workgroup of the launch co-resident

@@ -551,6 +551,10 @@ extern "C" int vv_codec_wide(int on) {
   g_codec_wide = on ? 1 : 0;
   return 0;
 }
+extern "C" int vv_codec_wide_over(int on) {   // diagnostic: 1 = grids past one resident wave too (B = 8)
+  codec_wide_oversubscribe(on);
+  return 0;
+}
 static std::atomic<unsigned long long*> g_codec_wide_stamps{nullptr};
 extern "C" int vv_codec_wide_stamps(void* buf) {   // diagnostic: [n][tiles x S][16] at buf + 8192 x (2 x net + (C == 512))
   g_codec_wide_stamps = (unsigned long long*)buf;

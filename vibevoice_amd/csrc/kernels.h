@@ -365,6 +365,8 @@ bool codec_wide_fits(int C, int T, int n, int depth, int ctx);
 size_t codec_wide_slab_floats(int C, int T, int n);
 size_t codec_wide_xbuf_elems(int C, int T, int n);
 int launch_codec_wide(const CodecWideArgs& a, int C, hipStream_t st);
+// 1: grids past one resident wave run too (clusters complete in dispatch order); 0 (default): whole grid resident
+void codec_wide_oversubscribe(int on);
 
 size_t gemv_mix_lds(int M, int T, int C);
 int launch_gemm(GemmArgs a, hipStream_t st);
