@@ -68,11 +68,17 @@ __global__ void __launch_bounds__(lf::NT) k_lm_ffn(LmFfnArgs a) {
   // the 192 down owners (w % 4 != 3) stream 4 gate|up tiles each (tiles [0, 768));
   // the other 64 the remaining 352 (5 or 6 each): per CU 332 KB (owner: 4 tiles
   // + 140 KB of down) or 240-288 KB, against 380 KB when owners took 5
-  const bool owner = (w & 3) != 3;
-  const int d = 3 * (w >> 2) + (w & 3);                             // down columns [8d, 8d + 8)
-  const int u = w >> 2;
-  const int t0 = owner ? 4 * d : 768 + ((352 * u) >> 6);
-  const int nt = owner ? 4 : 768 + ((352 * (u + 1)) >> 6) - t0;   // 4, or 5 / 6
+  // XCD-balanced (workgroup w runs on XCD w % 8): in each group of 32 workgroups,
+  // rows (w >> 3) & 3 = 0..2 are owners and row 3 the others, so every XCD holds
+  // 24 owners and 8 others; the others' 5 / 6 tiles alternate by group, so every
+  // XCD streams the same bytes (with owner = w % 4 != 3 all 64 others, the
+  // heaviest gate|up streams, sat on XCDs 3 and 7)
+  const int grp = w >> 5, sub = (w >> 3) & 3;
+  const bool owner = sub != 3;
+  const int d = grp * 24 + sub * 8 + (w & 7);                       // down columns [8d, 8d + 8)
+  const int u = grp * 8 + (w & 7);                                  // the others: u = 16 q + r
+  const int t0 = owner ? 4 * d : 768 + 88 * (u >> 4) + ((u & 15) < 8 ? 5 * (u & 15) : 40 + 6 * ((u & 15) - 8));
+  const int nt = owner ? 4 : 5 + ((u >> 3) & 1);                    // 4, or 5 / 6
   const int nlds = nt - NREG1;                                      // tiles in LDS (0, 1, 2; uniform)
   const int col0 = 8 * d;
   unsigned g0 = 0;
@@ -302,9 +308,10 @@ __global__ void __launch_bounds__(lf16::NT) k_lm_ffn16(LmFfnArgs a) {
   const bool ctl = wave == NWC;
   const int w = blockIdx.x, lane = threadIdx.x & 63, R = a.R;
   const bool owner = w < NR * NG;
-  const int u = w - NR * NG;                                       // non-owner index
-  const int t0 = owner ? 4 * w : 768 + ((352 * u) >> 6);
-  const int nt = owner ? 4 : 768 + ((352 * (u + 1)) >> 6) - t0;   // 4, or 5 / 6
+  const int u = w - NR * NG;                                       // non-owner index (XCD u % 8)
+  // 5 / 6 tiles alternating every 8 (by parity all 6-tile streams sat on the odd XCDs)
+  const int t0 = owner ? 4 * w : 768 + 88 * (u >> 4) + ((u & 15) < 8 ? 5 * (u & 15) : 40 + 6 * ((u & 15) - 8));
+  const int nt = owner ? 4 : 5 + ((u >> 3) & 1);                   // 4, or 5 / 6
   const int js = wave >> 1, kh = wave & 1;                         // this wave's tile slot / K half
   const bool busy1 = !ctl && js < nt;
   const int grp = w >> 2, rng = w & 3;                             // down: columns [32 grp, +32), k-blocks [70 rng, +70)
@@ -382,6 +389,18 @@ __global__ void __launch_bounds__(lf16::NT) k_lm_ffn16(LmFfnArgs a) {
   }
   __syncthreads();
   stamp(4);
+  if (ctl) {   // act[m][8 (t0 + j) .. + 8] for rows m < R, written through, and the arrival: both
+               // ahead of the down weights in this CU's memory queue (behind them they waited ~3 us)
+    for (int q = lane; q < nt * RMAX * 2; q += 64) {
+      const int j = q / (RMAX * 2), r = q - j * RMAX * 2, m = r >> 1, half = r & 1;
+      if (m < R)
+        MemWT::st8(hl_opaque(a.act) + (long long)m * F + 8 * (t0 + j) + 4 * half,
+                   *(const bf16x4*)(su_s + (j * RMAX + m) * 8 + 4 * half));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) hl_arrive_gen(a.sync, 12, w);
+  }
+  __syncthreads();
   if (wave < 10 && owner) {
     // the down weights, in flight through the hand-off (issued after SiLU * up:
     // issued before it, their 14 loads per thread held the owners' arrival back
@@ -392,16 +411,7 @@ __global__ void __launch_bounds__(lf16::NT) k_lm_ffn16(LmFfnArgs a) {
 #pragma unroll
     for (int kk = 0; kk < KW2; ++kk) wb[kk] = hl_ldnt(dw + (long long)kk * 512);
   }
-  if (ctl) {   // act[m][8 (t0 + j) .. + 8] for rows m < R, written through; then the grid wait
-    for (int q = lane; q < nt * RMAX * 2; q += 64) {
-      const int j = q / (RMAX * 2), r = q - j * RMAX * 2, m = r >> 1, half = r & 1;
-      if (m < R)
-        MemWT::st8(hl_opaque(a.act) + (long long)m * F + 8 * (t0 + j) + 4 * half,
-                   *(const bf16x4*)(su_s + (j * RMAX + m) * 8 + 4 * half));
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) ok_s[0] = hl_grid_wait_gen(a.sync, 12, g0, 1, w, a.err) ? 1u : 0u;
-  }
+  if (ctl && lane == 0) ok_s[0] = hl_poll_gen(a.sync, 12, g0, 1, a.err) ? 1u : 0u;
   __syncthreads();
   stamp(5);
   if (!ok_s[0] || !owner) return;

@@ -112,6 +112,30 @@ DEV bool hl_grid_wait(unsigned* sync, unsigned g0, unsigned k, int w, unsigned* 
   return hl_poll(sync, g0, k, err);
 }
 
+// the arrival half of hl_grid_wait_gen (lane 0 of a wave, behind that wave's vmcnt(0))
+DEV void hl_arrive_gen(unsigned* sync, int gen_line, int w) {
+  using namespace pk;
+  const unsigned v = __hip_atomic_fetch_add((hl_gu32*)(sync + (w & 7) * LINE), 1u, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+  if ((v + 1) % (G / 8) == 0)
+    __hip_atomic_fetch_add((hl_gu32*)(sync + gen_line * LINE), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the poll half: until k waits of this launch (base g0) completed; false: gave up
+// after ~200 ms (error word set).  (Polling by scalar loads that miss the scalar
+// cache was tried: the hand-offs took 11-20 us instead of 1.4-3.)
+DEV bool hl_poll_gen(unsigned* sync, int gen_line, unsigned g0, unsigned k, unsigned* err) {
+  unsigned* gen = sync + gen_line * pk::LINE;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while ((unsigned)(__hip_atomic_load((hl_gu32*)gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - g0) < 8 * k) {
+    __builtin_amdgcn_s_sleep(1);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {   // ~200 ms at 100 MHz
+      __hip_atomic_store((hl_gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  }
+  return true;
+}
+
 // the same wait on the generation word at line `gen_line` of `sync` (a kernel of
 // its own: only it bumps that word, 8 per wait; the shard lines are shared)
 DEV bool hl_grid_wait_gen(unsigned* sync, int gen_line, unsigned g0, unsigned k, int w, unsigned* err) {
