@@ -76,9 +76,15 @@ __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool ctl = wave == NTC / 64;
   const int w = blockIdx.x, lane = threadIdx.x & 63, R = a.R;
-  const int t0 = (w * 9) >> 2, nt = (((w + 1) * 9) >> 2) - t0;   // gate|up tiles (2 or 3)
-  const bool owner = (w & 3) != 3;                                // the two-tile workgroups own down columns
-  const int d = 3 * (w >> 2) + (w & 3);                           // down columns [8d, 8d + 8)
+  // XCD-balanced (workgroup w runs on XCD w % 8): in each group of 32 workgroups,
+  // rows (w >> 3) & 3 = 0..2 own down columns and stream 2 gate|up tiles, row 3
+  // streams 3, so every XCD holds 24 owners and 8 three-tile workgroups (with
+  // owner = w % 4 != 3, all 64 three-tile streams sat on XCDs 3 and 7)
+  const int sub = (w >> 3) & 3;
+  const bool owner = sub != 3;                                    // the two-tile workgroups own down columns
+  const int d = (w >> 5) * 24 + sub * 8 + (w & 7);                // down columns [8d, 8d + 8)
+  const int u = (w >> 5) * 8 + (w & 7);                           // the three-tile workgroups 0..63
+  const int t0 = owner ? 2 * d : 2 * NOWN + 3 * u, nt = owner ? 2 : 3;   // gate|up tiles
   const int col0 = 8 * d;
   unsigned g0 = 0;
   // diagnostics: 0 entry, 1 A side landed (wave 0), 2 row norms, 3 transform,
