@@ -82,6 +82,9 @@ def test_gemv_plan_rules():
     # B = 8 LM down: K split until the A slice fits 64 KB of LDS (5 ways), staged once
     p = _plan(16, 1536, 8960)
     assert (p["kernel"], p["ksplit"], p["waves"]) == (0, 5, 8) and p["lds"] <= 65536
+    # codec fc1 at C = 2,048 (512 tiles), B = 8: two tiles per workgroup (256 workgroups)
+    p = _plan(8, 8192, 2048)
+    assert (p["kernel"], p["tpw"], p["waves"]) == (0, 2, 8)
     # codec fc2 at C = 2,048 keeps its 2-way split on k_gemv (the split-to-fit rule cost 20 us there)
     p = _plan(16, 2048, 8192)
     assert (p["kernel"], p["ksplit"], p["waves"]) == (1, 2, 8)

@@ -1218,7 +1218,10 @@ static GemmPlan gemv_plan(int N, int K, int M) {
       tpw = 8;
       u = M > 8 ? 4 : 8;
     } else if (tiles >= 512) {
-      tpw = 4;
+      // 2 tiles per workgroup (256 workgroups: the codec fc1 at C = 2,048, N 8,192 x
+      // K 2,048, B = 8) -- 4 reached only 128 CUs; interleaved in-loop pairs, B = 8
+      // step 3.953 / 3.948 -> 3.927 / 3.920 ms (tools/ab_bench.py gemv_tune_shape)
+      tpw = 2;
       u = 4;
     }
   } else if (tiles >= 1024) {
