@@ -1191,7 +1191,13 @@ static GemmPlan gemv_plan(int N, int K, int M) {
         while (ks < 8 && (size_t)M * ((chunks + ks - 1) / ks * 32 + 8) * 2 > 65536) ++ks;
         nw = 8;
       } else if (chunks >= 256) u = 8;
-      else nw = 8;
+      else {
+        nw = 8;
+        // 4 splits at M > 16 (the codec fc2 at C = 1,024, B = 8: 64 rows x N 1,024 x
+        // K 4,096 on 64 tiles; interleaved in-loop pairs, B = 8 step 3.921 / 3.923 ->
+        // 3.893 / 3.896 ms; 8 splits x 2 chunks 3.935)
+        if (M > 16) ks = 4;
+      }
     } else if (tiles < 128 && chunks >= 256) {   // M < 8 LM down: 2-way split-K, 8 waves x 4
       ks = 2;
       nw = 8;
