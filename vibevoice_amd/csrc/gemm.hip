@@ -936,6 +936,8 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
   const bf16* wrow[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) wrow[nt] = a.w + (long long)((n_base >> 4) + nt) * a.K * 16 + lane * 8;
+  // rows past M read row M - 1 (unconditional loads: a guarded load compiles to a
+  // branch + a vmcnt(0) wait); their products land in rows the epilogue drops
   const bf16* xrow[2];
   bool xok[2];
   float inv[2];
@@ -943,8 +945,8 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
   for (int mt = 0; mt < 2; ++mt) {
     const int m = m_base + mt * 16 + r;
     xok[mt] = m < a.M;
-    xrow[mt] = xok[mt] ? rm_bf(a.a, m) + 8 * g : nullptr;
-    inv[mt] = XF == XF_NORM ? inv_s[m - m_blk] : 0.f;
+    xrow[mt] = rm_bf(a.a, min(m, a.M - 1)) + 8 * g;
+    inv[mt] = XF == XF_NORM ? inv_s[min(m, a.M - 1) - m_blk] : 0.f;
   }
   f32x4 acc[2][NT];
 #pragma unroll
@@ -953,16 +955,21 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
     for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
   const int nk = a.K >> 5;
-  for (int c = 0; c < nk; c += 2) {
-    bf16x8 wf[2][NT], xf[2][2];
+  // two register sets of 2 chunks each: the loads of chunks c + 4 .. go out while
+  // chunks c .. compute (one set in flight per round trip left the loop
+  // latency-bound: the 320-row codec fc2 at C = 512, K 2,048, took 24 us)
+  bf16x8 wfA[2][NT], xfA[2][2], wfB[2][NT], xfB[2][2];
+  auto load = [&](int c, bf16x8 (&wf)[2][NT], bf16x8 (&xf)[2][2]) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int cc = min(c + u, nk - 1);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) wf[u][nt] = *(const bf16x8*)(wrow[nt] + cc * 512);   // re-read across row tiles: default policy
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) xf[u][mt] = xok[mt] ? *(const bf16x8*)(xrow[mt] + cc * 32) : zero8;
+      for (int mt = 0; mt < 2; ++mt) xf[u][mt] = *(const bf16x8*)(xrow[mt] + cc * 32);
     }
+  };
+  auto comp = [&](int c, bf16x8 (&wf)[2][NT], bf16x8 (&xf)[2][2]) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       if (c + u >= nk) {
@@ -979,6 +986,16 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma(wf[u][nt], xf[u][mt], acc[mt][nt]);
+    }
+  };
+  load(0, wfA, xfA);
+  if (2 < nk) load(2, wfB, xfB);
+  for (int c = 0; c < nk; c += 4) {
+    comp(c, wfA, xfA);
+    if (c + 4 < nk) load(c + 4, wfA, xfA);
+    if (c + 2 < nk) {
+      comp(c + 2, wfB, xfB);
+      if (c + 6 < nk) load(c + 6, wfB, xfB);
     }
   }
 #pragma unroll
