@@ -277,3 +277,49 @@ def test_head_m16_vs_oracle_and_gemv_pair(n):
     assert e < 2e-2 and cos(m16, ref) > 0.999
     assert eb < 2e-2 and cos(m16, pair) > 0.999
     assert ew < 2e-2 and cos(whole, ref) > 0.999 and ewd < 2e-2
+
+
+@pytest.mark.parametrize("n,S,sde", [(1, 10, False), (2, 5, False), (1, 7, True)])
+def test_head_fin_one_launch_vs_oracle_and_gemv_pair(n, S, sde):
+    """The step boundary (step s's final layer + CFG + DPM update, step s + 1's
+    noisy projection) as ONE launch (head_fin.hip k_head_fin, 2n <= 4 rows: every
+    workgroup computes the whole final layer, then its noisy tiles; latents, DPM
+    history and state rows double-buffered over an even number of fused steps)
+    at the 1.5B head shapes: vs the oracle (rel < 2e-2, cosine > 0.999), vs the
+    two GEMV launches (within bf16: MFMA sums in another order), repeated runs
+    bitwise equal.  S = 10: steps 1..8 fused; S = 5: 0..3; S = 7 with
+    sde-dpmsolver++ noise: 0..5."""
+    from vibevoice_amd import _lib
+    from vibevoice_amd.schedule import Schedule
+    L = _lib.lib()
+    g = torch.Generator().manual_seed(31 + n + S)
+    sd, hc, H = real_head_sd(g)
+    tiny = tiny_config(hidden=H, layers=1, heads=12, kv_heads=2, inter=256)
+    eng, _ = engine_with_head(tiny, sd)
+    if sde:
+        eng.set_schedule(Schedule.from_config(eng.schedule.config, algorithm_type="sde-dpmsolver++",
+                                              beta_schedule="squaredcos_cap_v2"))
+    eng.set_steps(S)
+    assert L.vv_head_fin_active(eng.h, n) == 1
+    pos = (torch.randn(n, H, generator=g)).bfloat16()
+    neg = (torch.randn(n, H, generator=g)).bfloat16()
+    noise = torch.randn(2 * n, 64, generator=g).bfloat16()
+    z = torch.randn(S, 2 * n, 64, generator=g) if sde else None
+    outs = {}
+    try:
+        for on in (1, 0, 1):
+            L.vv_head_fin(on)
+            x = noise[:n].to(dev).contiguous()
+            eng.diffusion_sample(pos.to(dev), neg.to(dev), x, 1.3, sde_noise=z.to(dev) if sde else None)
+            torch.cuda.synchronize()
+            outs.setdefault(on, []).append(x.clone())
+    finally:
+        L.vv_head_fin(1)
+    eng.check_sync()
+    ref = ohead.sample_speech_tokens(sd, pos, neg, noise, S, 1.3, hc.head_layers, sde_noise=z)
+    one, pair = outs[1][0], outs[0][0]
+    print(f"n={n} S={S} sde={sde}: one launch rel {rel_err(one, ref):.3e} vs oracle (GEMV pair "
+          f"{rel_err(pair, ref):.3e}), {rel_err(one, pair):.3e} vs the pair")
+    assert torch.equal(one, outs[1][1])
+    assert rel_err(one, ref) < 2e-2 and cos(one, ref) > 0.999
+    assert rel_err(one, pair) < 2e-2 and cos(one, pair) > 0.999
