@@ -132,6 +132,12 @@ int vv_lm_ffn_stamps(void* buf);
  * 1, default) or the q|k|v, attention and o_proj launches (0); whether it applies
  * to this context at ntok rows over max_pos_p1 keys; and per-workgroup phase
  * stamps of its launches ([256][16] u64, overwritten per launch; NULL = off). */
+/* Diagnostic switch: the diffusion head's step boundary (final layer + DPM of
+ * step s, noisy projection of step s + 1) as one launch at 2n <= 4 rows
+ * (head_fin.hip; 1, default) or the two GEMV launches (0); and whether it
+ * applies to this context at n samples. */
+int vv_head_fin(int on);
+int vv_head_fin_active(vv_ctx* ctx, int n);
 int vv_lm_attn(int on);
 int vv_lm_attn_active(vv_ctx* ctx, int ntok, int max_pos_p1);
 int vv_lm_attn_stamps(void* buf);

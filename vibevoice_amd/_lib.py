@@ -90,6 +90,8 @@ EXPORTS = [
     ("vv_lm_ffn", I, [I]),
     ("vv_lm_ffn_active", I, [P, I]),
     ("vv_lm_ffn_stamps", I, [P]),
+    ("vv_head_fin", I, [I]),
+    ("vv_head_fin_active", I, [P, I]),
     ("vv_lm_attn", I, [I]),
     ("vv_lm_attn_active", I, [P, I, I]),
     ("vv_lm_attn_stamps", I, [P]),

@@ -1722,6 +1722,7 @@ struct HeadRun {
   long long MODW = 0;
   bf16 *cat = nullptr, *condp = nullptr, *xh = nullptr, *mods = nullptr, *sa = nullptr, *act = nullptr, *v = nullptr,
        *m1 = nullptr;
+  bf16 *xh2 = nullptr, *lat2 = nullptr, *m12 = nullptr;   // k_head_fin's double buffers (state rows, latents, history)
   const bf16* cond = nullptr;
   RowMap xh_m;
   bool keep = false;
@@ -1745,6 +1746,9 @@ static int head_begin(vv_ctx* c, int n, const void* pos_h, const void* neg_h, He
   h.act = h.sa + (size_t)HEAD_SC * R * H;
   h.v = h.act + (size_t)R * F;
   h.m1 = h.v + (size_t)R * D;
+  h.lat2 = h.m1 + (size_t)R * D;        // (head_ws: R * D * 3 + max_batch * D * 2 after act)
+  h.m12 = h.lat2 + (size_t)R * D;
+  h.xh2 = a;                            // (head_ws: the spare [R][H] after xh)
   h.xh_m = rowmap(h.xh, H);
   // condition rows cat[pos_h, neg_h]: used in place when the caller's rows are adjacent
   h.cond = (const bf16*)pos_h;
@@ -1943,6 +1947,56 @@ int vv_tp_shard_head(vv_ctx* c, int on) {
   return 0;
 }
 
+// step s's final layer + DPM and step s + 1's noisy projection as ONE launch
+// (head_fin.hip) at 2n <= 4 rows with the head's weights cache-resident; 0 = the
+// two GEMV launches (A/B and tests)
+static std::atomic<int> g_head_fin{1};
+extern "C" int vv_head_fin(int on) {
+  g_head_fin = on ? 1 : 0;
+  return 0;
+}
+static bool head_fin_on(vv_ctx* c, const HeadRun& h) {
+  const vv_config& k = c->cfg;
+  return g_head_fin && !c->head_tp && h.keep && head_fin_fits(k.hidden, k.latent_dim, h.R) && c->steps >= 3;
+}
+extern "C" int vv_head_fin_active(vv_ctx* c, int n) {
+  if (!c || !c->finalized) return 0;
+  HeadRun h;
+  h.n = n;
+  h.R = 2 * n;
+  const vv_config& k = c->cfg;
+  h.keep = (size_t)k.head_layers * 3 * k.head_ffn * k.hidden * sizeof(bf16) <= (192ull << 20) && !(c->head_tp && c->tp_size > 1);
+  return head_fin_on(c, h) ? 1 : 0;
+}
+// lat / m1 read, lat_out / m1_out written; the state rows h.xh read, xo written
+static int head_fin(vv_ctx* c, const HeadRun& h, int s, const bf16* lat, bf16* lat_out, const bf16* m1, bf16* m1_out,
+                    bf16* xo, float cfg_scale, const float* sde_noise, hipStream_t st) {
+  const vv_config& k = c->cfg;
+  const int H = k.hidden, D = k.latent_dim, L = k.head_layers;
+  HeadFinArgs a;
+  memset(&a, 0, sizeof(a));
+  a.n = h.n;
+  a.R = h.R;
+  a.eps = k.head_eps;
+  a.shift_off = 3 * H * L;
+  a.scale_off = 3 * H * L + H;
+  a.ldmod = h.MODW;
+  a.x = h.xh;
+  a.mod = h.mods + (size_t)(s % HEAD_SC) * h.R * h.MODW;
+  a.fw = W(c, "head.final_w");
+  a.k = c->coef[s];
+  a.k.cfg = cfg_scale;
+  a.lat = lat;
+  a.lat_out = lat_out;
+  a.m1 = m1;
+  a.m1_out = m1_out;
+  a.noise = sde_noise ? sde_noise + (size_t)s * h.R * D : nullptr;
+  a.nw = W(c, "head.noisy_w");
+  a.xo = xo;
+  KCHK(launch_head_fin(a, st));
+  return 0;
+}
+
 int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, void* x_io, float cfg_scale,
                         const float* sde_noise, vv_stream vst) {
   hipStream_t st = (hipStream_t)vst;
@@ -1958,9 +2012,23 @@ int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, 
   CHK(head_begin(c, n, pos_h, neg_h, h, st));
   const int R = h.R;
   const long long MODW = h.MODW;
+  // k_head_fin fuses step s's final layer with step s + 1's noisy projection for
+  // an EVEN number of steps [s0, S - 1), so that the latents, the DPM history and
+  // the state rows ping-pong back to x_io / m1 / xh for the last step's final
+  // layer (the GEMV path, in place)
+  const bool fin = !sharded && head_fin_on(c, h);
+  const int nfused = !fin ? 0 : (c->steps - 1) % 2 == 0 ? c->steps - 1 : c->steps - 2;
+  const int s0 = c->steps - 1 - nfused;
+  bf16* lat[2] = {(bf16*)x_io, h.lat2};
+  bf16* hist[2] = {h.m1, h.m12};
+  bf16* xs[2] = {h.xh, h.xh2};
+  int cur = 0;
   for (int s = 0; s < c->steps; ++s) {
+    h.xh = xs[cur];
+    h.xh_m = rowmap(h.xh, H);
+    h.m1 = hist[cur];
     CHK(head_mods(c, h, s, st));
-    CHK(head_noisy(c, h, x_io, st));
+    if (!(nfused && s > s0)) CHK(head_noisy(c, h, lat[cur], st));   // (else: the previous k_head_fin)
     for (int l = 0; l < L; ++l) {
       CHK(head_layer(c, h, s, l, st));
       if (sharded && !g_tp_null) {   // x = sum over the ranks (rank 0 carried the residual)
@@ -1968,8 +2036,14 @@ int vv_diffusion_sample(vv_ctx* c, int n, const void* pos_h, const void* neg_h, 
         if (r != ncclSuccess) FAIL(std::string("ncclAllReduce (head): ") + ncclGetErrorString(r));
       }
     }
-    CHK(head_final(c, h, s, x_io, cfg_scale, sde_noise, st));
+    if (nfused && s >= s0 && s + 1 < c->steps) {
+      CHK(head_fin(c, h, s, lat[cur], lat[cur ^ 1], hist[cur], hist[cur ^ 1], xs[cur ^ 1], cfg_scale, sde_noise, st));
+      cur ^= 1;
+    } else {
+      CHK(head_final(c, h, s, lat[cur], cfg_scale, sde_noise, st));
+    }
   }
+  if (cur != 0) FAIL("vv_diffusion_sample: internal (latent buffers did not return)");
   return 0;
 }
 

@@ -243,6 +243,28 @@ struct HeadNoisyArgs {
 };
 int launch_head_noisy16(const HeadNoisyArgs& a, hipStream_t st);
 
+// ---- the diffusion head's step boundary at 2n <= 4 rows in one launch (head_fin.hip):
+// step s's final layer + CFG + DPM update, then step s+1's noisy projection
+struct HeadFinArgs {
+  int n, R;                 // samples, rows (2n: [cond n | uncond n])
+  float eps;
+  int shift_off, scale_off; // the final adaLN's shift / scale in the mod rows
+  long long ldmod;
+  const bf16* x;            // [R][H] state rows after the last FFN layer (read)
+  const bf16* mod;          // adaLN rows [R][ldmod]
+  const bf16* fw;           // final_layer.linear [D][H], MFMA-packed
+  DpmCoef k;
+  const bf16* lat;          // [n][D] latents (read)
+  bf16* lat_out;            // [n][D] updated latents (written by workgroup 0)
+  const bf16* m1;           // [n][D] DPM history (read)
+  bf16* m1_out;             // [n][D] (written by workgroup 0)
+  const float* noise;       // [R][D] sde-dpmsolver++ draw of this step, or nullptr
+  const bf16* nw;           // noisy_images_proj [H][D], MFMA-packed
+  bf16* xo;                 // [R][H] the next step's state rows = noisy(updated latents)
+};
+bool head_fin_fits(int H, int D, int R);
+int launch_head_fin(const HeadFinArgs& a, hipStream_t st);
+
 // ---- one LM MLP block at decode (R <= 2 rows) in one launch (lm_ffn.hip), GEMV layout weights
 struct LmFfnArgs {
   const bf16* x;     // [R][ldx] hidden rows (read: the A side and the residual)
