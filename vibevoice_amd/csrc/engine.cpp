@@ -1948,8 +1948,8 @@ int vv_tp_shard_head(vv_ctx* c, int on) {
 }
 
 // step s's final layer + DPM and step s + 1's noisy projection as ONE launch
-// (head_fin.hip) at 2n <= 4 rows with the head's weights cache-resident; 0 = the
-// two GEMV launches (A/B and tests)
+// (head_fin.hip) at 2n <= 16 rows with the head's weights cache-resident; 0 = the
+// two launches (A/B and tests)
 static std::atomic<int> g_head_fin{1};
 extern "C" int vv_head_fin(int on) {
   g_head_fin = on ? 1 : 0;
@@ -1993,6 +1993,7 @@ static int head_fin(vv_ctx* c, const HeadRun& h, int s, const bf16* lat, bf16* l
   a.noise = sde_noise ? sde_noise + (size_t)s * h.R * D : nullptr;
   a.nw = W(c, "head.noisy_w");
   a.xo = xo;
+  a.ssp = m16_pre(c, h.R) ? (float*)c->m16_buf.p : nullptr;   // (layer 0's distributed A side at > 4 rows)
   KCHK(launch_head_fin(a, st));
   return 0;
 }

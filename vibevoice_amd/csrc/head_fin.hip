@@ -1,4 +1,4 @@
-// The diffusion head's step boundary in ONE launch at 2n <= 4 rows (B <= 2):
+// The diffusion head's step boundary in ONE launch at 2n <= 16 rows (B <= 8):
 // step s's final layer -> CFG + DPM-Solver++ update of the latents -> step
 // s+1's noisy_images_proj of the new latents (prediction_head's FinalLayer and
 // noisy_images_proj, modular_vibevoice_diffusion_head.py:254-280;
@@ -20,7 +20,8 @@
 #include "persist_dev.h"
 
 namespace hf {
-constexpr int H = 1536, D = 64, RMAX = 4, NW = 8, NT = NW * 64;
+constexpr int H = 1536, D = 64, RMAX = 16, NW = 8, NT = NW * 64;
+constexpr int NOWN = 192;                       // k_head_m16's down owners (8 columns each)
 constexpr int KC = H / 32, KPW = KC / NW;       // 48 k-blocks, 6 per wave
 constexpr int TF = D / 16, TN = H / 16;         // 4 final tiles, 96 noisy tiles
 constexpr int G = 24, TPG = TN / G;             // 24 workgroups x 4 noisy tiles
@@ -28,11 +29,11 @@ constexpr int XST = H + 8;
 constexpr int XS = 0, XS_B = 16 * XST * 2;      // normalised rows (16: the MFMA's padded rows)
 constexpr int SH = XS + XS_B, SH_B = RMAX * H * 2;
 constexpr int SC = SH + SH_B, SC_B = RMAX * H * 2;
-constexpr int RED = SC + SC_B, RED_B = NW * TF * 256 * 4;
-constexpr int LAT = RED + RED_B, LAT_B = 16 * D * 2;   // new latents, as noisy's B rows [16][64]
+constexpr int RED = SH, RED_B = NW * TF * 256 * 4;   // over shift / scale once they are consumed
+constexpr int LAT = SC + SC_B, LAT_B = 16 * D * 2;     // new latents, as noisy's B rows [16][64]
 constexpr int SM = LAT + LAT_B, SM_B = 64;
 constexpr int TOTAL = SM + SM_B;
-static_assert(TOTAL <= 160 * 1024 && TPG * G == TN, "head fin geometry");
+static_assert(TOTAL <= 160 * 1024 && TPG * G == TN && RED_B <= SH_B + SC_B, "head fin geometry");
 }  // namespace hf
 
 __global__ void __launch_bounds__(hf::NT) k_head_fin(HeadFinArgs a) {
@@ -153,7 +154,33 @@ __global__ void __launch_bounds__(hf::NT) k_head_fin(HeadFinArgs a) {
     }
   }
   __syncthreads();
-  // ---- noisy_images_proj of the new latents: wave v < 4, tile TPG w + v, EPI_STORE
+  // ---- noisy_images_proj of the new latents
+  if (R > 4) {
+    // k_head_noisy16's arithmetic (fp32 fmaf in k order, bf16 store) and its row
+    // partial sums of squares per 8-column owner, which layer 0's distributed A
+    // side reads: owners [8 TPG w, + 8 TPG), thread (owner, row m, column c)
+    for (int t = threadIdx.x; t < 2 * TPG * 128; t += NT) {
+      const int d = 2 * TPG * w + (t >> 7), m = (t & 127) >> 3, c = t & 7, j = 8 * d + c;
+      float q = 0.f;
+      if (m < R) {
+        float acc = 0.f;
+        for (int k = 0; k < D; k += 8) {
+          const bf16x8 wv = *(const bf16x8*)hl_packed(a.nw, D, j, k), xv = *(const bf16x8*)(lat_s + m * D + k);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc = fmaf(bf(xv[e]), bf(wv[e]), acc);
+        }
+        const bf16 ov = tobf(acc);
+        a.xo[(long long)m * H + j] = ov;
+        q = bf(ov) * bf(ov);
+      }
+      q += __shfl_xor(q, 1);
+      q += __shfl_xor(q, 2);
+      q += __shfl_xor(q, 4);
+      if (a.ssp && c == 0 && m < R) a.ssp[m * NOWN + d] = q;
+    }
+    return;
+  }
+  // 2n <= 4 rows: wave v < 4, tile TPG w + v, MFMA (EPI_STORE)
   if (wave < TPG) {
     f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -167,7 +194,10 @@ __global__ void __launch_bounds__(hf::NT) k_head_fin(HeadFinArgs a) {
   }
 }
 
-bool head_fin_fits(int H, int D, int R) { return H == hf::H && D == hf::D && R >= 2 && R <= hf::RMAX; }
+bool head_fin_fits(int H, int D, int R) {
+  static_assert(2 * hf::TPG * 8 * hf::G == hf::NOWN * 8, "owners x columns");
+  return H == hf::H && D == hf::D && R >= 2 && R <= hf::RMAX;
+}
 
 int launch_head_fin(const HeadFinArgs& a, hipStream_t st) {
   if (!head_fin_fits(hf::H, hf::D, a.R) || 2 * a.n != a.R || a.x == a.xo || a.lat == a.lat_out || a.m1 == a.m1_out)

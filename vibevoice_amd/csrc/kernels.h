@@ -243,7 +243,7 @@ struct HeadNoisyArgs {
 };
 int launch_head_noisy16(const HeadNoisyArgs& a, hipStream_t st);
 
-// ---- the diffusion head's step boundary at 2n <= 4 rows in one launch (head_fin.hip):
+// ---- the diffusion head's step boundary at 2n <= 16 rows in one launch (head_fin.hip):
 // step s's final layer + CFG + DPM update, then step s+1's noisy projection
 struct HeadFinArgs {
   int n, R;                 // samples, rows (2n: [cond n | uncond n])
@@ -261,6 +261,7 @@ struct HeadFinArgs {
   const float* noise;       // [R][D] sde-dpmsolver++ draw of this step, or nullptr
   const bf16* nw;           // noisy_images_proj [H][D], MFMA-packed
   bf16* xo;                 // [R][H] the next step's state rows = noisy(updated latents)
+  float* ssp;               // R > 4: [16][192] row partial sums of squares (k_head_m16's distributed A side), or nullptr
 };
 bool head_fin_fits(int H, int D, int R);
 int launch_head_fin(const HeadFinArgs& a, hipStream_t st);
