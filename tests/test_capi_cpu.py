@@ -137,6 +137,13 @@ def test_attention_pass_plan_rules():
     finally:
         L.vv_attn_group(1)
     assert _attn(2, 65040)["nsplit"] == 120
+    # the kernels' limits, over every context the group plan takes: k_attn's group
+    # merge holds <= 16 split partials, o_proj's XF_ATTN_MERGE <= 8 group partials
+    for max_len in range(8193, 65537, 997):
+        p = _attn(2, max_len)
+        if p["group"]:
+            assert p["group"] <= 16 and p["ngroups"] <= 8 and p["nsplit"] <= 128
+            assert p["ngroups"] * p["group"] * p["chunk"] >= max_len
     # grouped merge, ragged rows in one pass (the plan is sized by the longest row):
     # the producer's active groups for a row of n keys, ceil(ceil(n / chunk) / group),
     # equal the consumer's ceil(n / (group * chunk)) and never exceed ngroups
