@@ -183,9 +183,9 @@ def test_codec_stage_persistent_launch():
     slot = torch.tensor([1], dtype=torch.int32, device=dev)
     outs = {}
     try:
-        for mode in (1, 0, 1):
+        for mode in (1, 0, 1, 3):   # 3: the stage with round 5's whole-block weight stream
             L.vv_codec_stage(mode)
-            assert L.vv_codec_stage_active(eng.h) == mode
+            assert L.vv_codec_stage_active(eng.h) == (mode & 1)
             eng.codec_reset(slot)
             res = []
             for lat in lats:
@@ -211,6 +211,7 @@ def test_codec_stage_persistent_launch():
             print(f"frame {f} {name}: rel {e_o:.3e} vs oracle ({rel_err(base, ref):.3e} GEMV path), "
                   f"{e_b:.3e} vs the GEMV path")
             assert torch.equal(got, again), (f, name)
+            assert torch.equal(got, outs[3][0][f][k]), (f, name)   # issue order only: same sums
             assert e_o < 3e-2 and cos(got, ref) > 0.999, (f, name, e_o)
             assert e_b < 3e-2 and cos(got, base) > 0.999, (f, name, e_b)
 

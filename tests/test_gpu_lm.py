@@ -344,7 +344,8 @@ def test_lm_attn_one_launch_vs_oracle_and_three_launches(n, lens):
     rows: each decode step vs the oracle (rel < 2e-2, cosine > 0.999) and vs the
     q|k|v + k_attn + o_proj launches on the same KV state (within bf16: the
     projections sum in another order, the keys merge in 32-key units), repeated
-    runs bitwise equal.  Contexts from 2 keys to ~1,000, across unit edges."""
+    runs and the issue-order variants bitwise equal.  Contexts from 2 keys to
+    ~1,000, across unit edges."""
     import gc
     from vibevoice_amd import _lib
     gc.collect()
@@ -372,7 +373,7 @@ def test_lm_attn_one_launch_vs_oracle_and_three_launches(n, lens):
             step_x = torch.randn(R, 1536, generator=g).bfloat16()
             ref = olm.forward_rows(osd, lcfg, step_x[:, None], kvs)[:, -1]
             outs = {}
-            for on in (0, 1, 1):
+            for on in (0, 1, 1, 15):   # 15: the round-6 first form (16 A rows, o_proj weights at entry)
                 L_.vv_lm_attn(on)
                 h, _ = eng.lm_forward(step_x.to(dev), torch.arange(R).to(**I32), Lt.to(**I32),
                                       torch.arange(R).to(**I32))
@@ -382,7 +383,7 @@ def test_lm_attn_one_launch_vs_oracle_and_three_launches(n, lens):
             one, three = outs[1][0], outs[0][0]
             print(f"n={n} step {s}: one launch rel {rel_err(one, ref):.3e} vs oracle (three launches "
                   f"{rel_err(three, ref):.3e}), {rel_err(one, three):.3e} vs the three launches")
-            assert torch.equal(one, outs[1][1])
+            assert torch.equal(one, outs[1][1]) and torch.equal(one, outs[15][0])   # same sums
             assert rel_err(one, ref) < 2e-2 and cos(one, ref) > 0.999
             assert rel_err(one, three) < 2e-2 and cos(one, three) > 0.999
     finally:

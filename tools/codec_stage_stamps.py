@@ -10,7 +10,8 @@ codec shapes (seeded weights), captured into a hipGraph and replayed.
     wait released; median / max over the 256 workgroups relative to the first
     stamp, and the phase-to-phase medians.
 
-usage: python tools/codec_stage_stamps.py [stage]   (the decoder's stage: 0 = C 2,048 T 1, 1 = C 1,024 T 8)"""
+usage: python tools/codec_stage_stamps.py [stage] [modes]   (the decoder's stage: 0 = C 2,048 T 1, 1 = C 1,024 T 8;
+modes: comma-separated vv_codec_stage values, e.g. 1,3,1,3: bits 1..3 pick the weight-stream issue, engine.cpp)"""
 import os
 import sys
 
@@ -49,9 +50,10 @@ def main():
             gr.capture_end()
         return gr
 
-    for mode in (0, 1, 0, 1):
+    modes = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 1, 0, 1]
+    for mode in modes:   # vv_codec_stage values; stamps taken with the last
         L.vv_codec_stage(mode)
-        assert L.vv_codec_stage_active(eng.h) == mode
+        assert L.vv_codec_stage_active(eng.h) == (mode & 1)
         gr = capture()
         best = 1e9
         for _ in range(20):
@@ -63,7 +65,7 @@ def main():
                 e1.record(s)
             torch.cuda.synchronize()
             best = min(best, e0.elapsed_time(e1) * 1e3)
-        print(f"codec step, {'stage launch' if mode else 'launch per GEMV'}: best of 20 graph replays {best:.1f} us",
+        print(f"codec step, vv_codec_stage({mode}): best of 20 graph replays {best:.1f} us",
               flush=True)
     st = torch.zeros(256 * 64, dtype=torch.int64, device="cuda")
     L.vv_codec_stage_stamps(st.data_ptr(), stage)

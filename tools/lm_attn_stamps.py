@@ -5,7 +5,7 @@ then per-workgroup s_memrealtime stamps (10 ns ticks) of the last k_lm_attn
 launch: 0 start, 1 A side / weights issued, 2 q|k|v stored, 3 wait 1 released,
 4 attention units done, 5 wait 2 released, 6 merge done, 7 wait 3 released,
 8 o_proj stored.  Prints the median per phase since each workgroup's start.
-usage: python tools/lm_attn_stamps.py [B] [ctx]"""
+usage: python tools/lm_attn_stamps.py [B] [ctx] [vv_lm_attn modes, e.g. 1,3,5,7]"""
 import ctypes
 import os
 import sys
@@ -60,6 +60,9 @@ def main():
         return e0.elapsed_time(e1) * 1e3 / 20
     t3, t1 = timed(0), timed(1)
     print(f"LM pass: three launches {t3:.1f} us, one launch {t1:.1f} us -> {(t3 - t1) / 28:.2f} us per layer saved")
+    modes = [int(v) for v in sys.argv[3].split(",")] if len(sys.argv) > 3 else []
+    for mode in modes:   # vv_lm_attn values (bits 1..: LmAttnArgs::variant); stamps taken with the last
+        print(f"LM pass, vv_lm_attn({mode}): {timed(mode):.1f} us", flush=True)
     st = torch.zeros(256 * 16, dtype=torch.int64, device="cuda")
     L.vv_lm_attn_stamps(st.data_ptr())
     with torch.cuda.stream(s):

@@ -37,6 +37,8 @@
 // a different order than the MFMA GEMVs', so not bit-identical to the
 // launch-per-GEMV path (tests: within bf16 of it and of the oracle, bitwise
 // run to run).  Epilogues are epi_row8's EPI_GELU / EPI_RES.
+#include <type_traits>
+
 #include "persist_dev.h"
 
 namespace cs {
@@ -114,6 +116,35 @@ __global__ void __launch_bounds__(cs::NT) k_codec_stage(CodecStageArgs a) {
       w2[i] = hl_ldnt(g2 + (long long)kc * 512 + (16 * s + r) * 8);
     }
   };
+  // Paced halves (pubfirst == 3): chunks [8 h, 8 h + 8) of a slice, at most 6 of
+  // this wave's loads in flight (48 KB per CU).  A hand-off read waits behind
+  // every load queued chip-wide ahead of it (a whole 256 KB per CU block stream:
+  // ~9 us); ~2 us of stream in flight still keeps each CU at its ~25 GB/s.
+  auto pace = [&]() {   // pubfirst 3 / 4 / 5: at most 6 / 10 / 14 in flight
+    if (a.pubfirst == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (a.pubfirst == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  };
+  auto issue_fc1_half = [&](int j, int t, auto hc) {
+    constexpr int h = decltype(hc)::value;
+    const bf16* g1 = hl_opaque(a.b[j].fc1_w) + (long long)w * ROWS1 * C;
+#pragma unroll
+    for (int i = 8 * h; i < 8 * h + 8; ++i) {
+      hl_dma16<false, true>(w1_s + (i * NTC + 64 * wave) * 8, g1 + ((long long)i * NTC + t) * 8);
+      if (i & 1) pace();
+    }
+  };
+  auto issue_fc2_half = [&](int j, int t, auto hc) {
+    constexpr int h = decltype(hc)::value;
+    const bf16* g2 = hl_opaque(a.b[j].fc2_w) + (long long)(w >> 1) * F * 16 + (w & 1) * 64;
+    const int r = t & 7, s = (t >> 3) & 3;
+#pragma unroll
+    for (int i = 8 * h; i < 8 * h + 8; ++i) {
+      const int kc = (i * NTC + t) >> 5;
+      w2[i] = hl_ldnt(g2 + (long long)kc * 512 + (16 * s + r) * 8);
+      if (i & 1) pace();
+    }
+  };
 
   // ---- the conv's history taps of block jb for chunks c = lane + 64 q, q in
   // {q0, q0 + 1} (control wave): XF_MIX's tap order, taps 0..5 summed; the
@@ -157,10 +188,12 @@ __global__ void __launch_bounds__(cs::NT) k_codec_stage(CodecStageArgs a) {
   // ---- the front half of block j (control wave; chunks c = lane + 64 q):
   // y = x + gamma * dwconv(norm(x)) (workgroup 0 appends norm(x) to the conv
   // buffer), a = ffn_norm(y) -> LDS; this workgroup's 8 columns of y -> LDS
-  auto front = [&](int j) {
+  // (split in two: with pubfirst == 2 the loads go out before the compute waves
+  // issue the block's weight stream, so they are not queued behind it)
+  bf16x8 xv[4], nw[4], db[4], gm[4], fw[4];
+  auto front_load = [&](int j) {
     const int lane = hl_vopaque((int)threadIdx.x & 63);
     const CodecStageBlock& B = a.b[j];
-    bf16x8 xv[4], nw[4], db[4], gm[4], fw[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int c = lane + 64 * q;
@@ -170,6 +203,10 @@ __global__ void __launch_bounds__(cs::NT) k_codec_stage(CodecStageArgs a) {
       gm[q] = hl_ld(B.gamma + c * 8);
       fw[q] = hl_ld(B.ffn_norm + c * 8);
     }
+  };
+  auto front = [&](int j) {
+    const int lane = hl_vopaque((int)threadIdx.x & 63);
+    const CodecStageBlock& B = a.b[j];
     float ss = 0.f;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {   // per-chunk sums, then chunks in ascending order (XF_MIX's)
@@ -233,6 +270,8 @@ __global__ void __launch_bounds__(cs::NT) k_codec_stage(CodecStageArgs a) {
     for (int j = 0; j < a.depth; ++j) {
       const bool last = j + 1 == a.depth;
       stamp(8 * j + 0, true);
+      front_load(j);
+      if (j > 0 && a.pubfirst == 2) __syncthreads();   // B0: these loads ahead of the block's stream
       front(j);
       __syncthreads();   // B1: fc1's input row in LDS
       stamp(8 * j + 1, true);
@@ -279,14 +318,88 @@ __global__ void __launch_bounds__(cs::NT) k_codec_stage(CodecStageArgs a) {
         if (last) rm_bfw(a.out, 0)[col] = o;   // the launch's end publishes it
         else MemWT::st2(a.xe + col, o);
       }
-      if (!last && !grid_wait([] {})) return;   // B6
+      if (!last && a.pubfirst) {
+        // the output and the arrival go out ahead of the next block's stream
+        // (behind it they waited up to its whole length), then B5b releases the
+        // compute waves to issue it; the poll follows
+        ++nwait;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) hl_arrive(a.sync, w);
+        __syncthreads();   // B5b
+        if (lane == 0) ok_s[0] = hl_poll(a.sync, g0, nwait, a.err) ? 1u : 0u;
+        __syncthreads();   // B6
+        if (!ok_s[0]) return;
+      } else if (!last && !grid_wait([] {})) return;   // B6
       stamp(8 * j + 7, true);
+    }
+  } else if (a.pubfirst >= 3) {
+    // paced: block j's fc1 slice in two halves (during the previous block's
+    // second wait and this block's front half), its fc2 slice in two halves
+    // (during the first wait and the hidden-row DMA); barriers as below
+    using H0 = std::integral_constant<int, 0>;
+    using H1 = std::integral_constant<int, 1>;
+    issue_fc1(0, threadIdx.x);
+    for (int j = 0; j < a.depth; ++j) {
+      const bool last = j + 1 == a.depth;
+      if (j > 0) issue_fc1_half(j, hl_vopaque((int)threadIdx.x), H1());
+      __syncthreads();   // B1
+      {   // fc1: row (t & 15) of tiles 2w / 2w + 1 over this thread's 16 chunks
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's fc1 DMA
+        stamp(8 * j + 2, false);
+        const int t = hl_vopaque((int)threadIdx.x), s = (t & 63) >> 4;
+        float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+          const int kc = (8 * i + wave) & 63;
+          const bf16x8 wv = *(const bf16x8*)(w1_s + (i * NTC + t) * 8);
+          const bf16x8 av = *(const bf16x8*)(a_s + kc * 32 + 8 * s);
+          if (i < CPT / 2) acc0 = hl_dot8(wv, av, acc0);
+          else acc1 = hl_dot8(wv, av, acc1);
+        }
+        acc0 = cs_rows_sum(acc0);
+        acc1 = cs_rows_sum(acc1);
+        if ((t & 63) < 16) {
+          red[wave * ROWS1 + (t & 15)] = acc0;
+          red[wave * ROWS1 + 16 + (t & 15)] = acc1;
+        }
+      }
+      __syncthreads();   // B2
+      issue_fc2_half(j, hl_vopaque((int)threadIdx.x), H0());
+      __syncthreads();   // B3
+      if (!ok_s[0]) return;
+      issue_fc2_half(j, hl_vopaque((int)threadIdx.x), H1());
+      __syncthreads();   // B4
+      {   // fc2: row (t & 7) of the half tile over this thread's 16 chunks
+        const int t = hl_vopaque((int)threadIdx.x), s = (t >> 3) & 3;
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+          const int kc = (i * NTC + t) >> 5;
+          acc = hl_dot8(w2[i], *(const bf16x8*)(h_s + kc * 32 + 8 * s), acc);
+        }
+        acc += __shfl_xor(acc, 8);
+        acc += __shfl_xor(acc, 16);
+        acc += __shfl_xor(acc, 32);
+        if ((t & 63) < ROWS2) red[wave * ROWS2 + (t & 63)] = acc;
+      }
+      __syncthreads();   // B5
+      if (!last) {
+        __syncthreads();   // B5b: the control wave's output and arrival issued
+        issue_fc1_half(j + 1, hl_vopaque((int)threadIdx.x), H0());
+        __syncthreads();   // B6
+        if (!ok_s[0]) return;
+      }
     }
   } else {
     issue_fc1(0, threadIdx.x);
     issue_fc2(0, threadIdx.x);
     for (int j = 0; j < a.depth; ++j) {
       const bool last = j + 1 == a.depth;
+      if (j > 0 && a.pubfirst == 2) {   // B0: the control wave's front-half loads issued; then this block's stream
+        __syncthreads();
+        issue_fc1(j, hl_vopaque((int)threadIdx.x));
+        issue_fc2(j, hl_vopaque((int)threadIdx.x));
+      }
       __syncthreads();   // B1
       {   // fc1: row (t & 15) of tiles 2w / 2w + 1 over this thread's 16 chunks
         asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // this wave's fc1 DMA (the fc2 loads may fly)
@@ -327,10 +440,13 @@ __global__ void __launch_bounds__(cs::NT) k_codec_stage(CodecStageArgs a) {
       }
       __syncthreads();   // B5
       if (!last) {
-        // the next block's slices: fc1 into this wave's own LDS chunks (read by
-        // no other wave), then fc2 into the registers
-        issue_fc1(j + 1, hl_vopaque((int)threadIdx.x));
-        issue_fc2(j + 1, hl_vopaque((int)threadIdx.x));
+        if (a.pubfirst) __syncthreads();   // B5b: the control wave's output and arrival issued
+        if (a.pubfirst != 2) {
+          // the next block's slices: fc1 into this wave's own LDS chunks (read by
+          // no other wave), then fc2 into the registers
+          issue_fc1(j + 1, hl_vopaque((int)threadIdx.x));
+          issue_fc2(j + 1, hl_vopaque((int)threadIdx.x));
+        }
         __syncthreads();   // B6
         if (!ok_s[0]) return;
       }

@@ -488,8 +488,11 @@ extern "C" int vv_codec_mix_fusion(int mask) {
 // T = 2 / 8) runs as ONE persistent launch (codec_stage.hip) while the context is the device's only one registered for
 // persistent kernels (persist_on); 0 = the launch-per-GEMV path (A/B and tests).
 static std::atomic<int> g_codec_stage{1};
+// Bits 1..3 pick how the C = 2,048 form issues its weight stream (A/B only):
+// 0 = the default, the split, paced stream (CodecStageArgs::pubfirst 5); v > 0 =
+// pubfirst v - 1 (1: round 5's whole-block stream at each block's end).
 extern "C" int vv_codec_stage(int on) {
-  g_codec_stage = on ? 1 : 0;
+  g_codec_stage = on & 15;
   return 0;
 }
 static bool codec_stage_any(const ConvNet& net) {
@@ -761,6 +764,10 @@ static int convnet_run(vv_ctx* c, ConvNet& net, int n, const int* slots, RowMap 
       A.sync = (unsigned*)c->cs_sync.p;
       A.err = (unsigned*)c->hf_sync.p + 10 * 32;
       A.stamps = net.decoder && i == g_codec_stage_stamp_at ? g_codec_stage_stamps.load() : nullptr;
+      {
+        const int v = (g_codec_stage.load() >> 1) & 7;
+        A.pubfirst = v ? v - 1 : 5;
+      }
       const int rc = launch_codec_stage(A, st);
       if (rc) FAIL("persistent codec stage: launch failed (" + std::to_string(rc) + ": " +
                    hipGetErrorString(hipGetLastError()) + ")");
@@ -1311,7 +1318,7 @@ static void tp_residual(vv_ctx* c, GemmArgs& g, const RowMap& res) {
 static std::atomic<int> g_lm_attn{1};
 static std::atomic<unsigned long long*> g_lm_attn_stamps{nullptr};
 extern "C" int vv_lm_attn(int on) {
-  g_lm_attn = on ? 1 : 0;
+  g_lm_attn = on & 15;   // bits 1..3 (A/B): clear those LmAttnArgs::variant bits
   return 0;
 }
 extern "C" int vv_lm_attn_stamps(void* buf) {   // diagnostic: k_lm_attn launches record [256][16] phase stamps
@@ -1371,6 +1378,7 @@ static int lm_attn_half(vv_ctx* c, LmPass& P, int l, hipStream_t st) {
       a.sync = (unsigned*)c->lf_sync.p;
       a.err = (unsigned*)c->hf_sync.p + 10 * 32;
       a.stamps = g_lm_attn_stamps.load();
+      a.variant = 7 ^ (g_lm_attn.load() >> 1);
       KCHK(launch_lm_attn(a, P.maxp, st));
       return 0;
     }

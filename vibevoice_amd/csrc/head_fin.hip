@@ -52,7 +52,9 @@ __global__ void __launch_bounds__(hf::NT) k_head_fin(HeadFinArgs a) {
 
   // ---- the A side (x rows, adaLN shift / scale) by LDS DMA, then the weights:
   // the final tiles' k-blocks [6 wave, + 6), this wave's noisy k-block
-  for (int q = wave; q < RMAX * 3 * 3; q += NW) {   // (row, x | shift | scale, 64-chunk piece)
+  // (the R rows only: rows >= R are zeroed by the modulate; loading 16 rows at
+  // R = 2 queued 126 KB of redundant reads ahead of the weights)
+  for (int q = wave; q < R * 3 * 3; q += NW) {   // (row, x | shift | scale, 64-chunk piece)
     const int m = q / 9, k = (q / 3) % 3, i = q % 3, mm = min(m, R - 1);
     const bf16* src = k == 0 ? a.x + (long long)mm * H
                              : a.mod + (long long)mm * a.ldmod + (k == 1 ? a.shift_off : a.scale_off);

@@ -305,6 +305,10 @@ struct LmAttnArgs {
   unsigned* sync;    // shards 0-7, this kernel's generation at line 15
   unsigned* err;     // set to 1 when a grid wait gave up
   unsigned long long* stamps;   // diagnostics: [256][16] s_memrealtime per phase, or nullptr
+  int variant;              // bits (all set by default; vv_lm_attn bits 1..3 clear them, A/B): 1 = A
+                            // and attention rows of the R rows only (not 16); 2 = o_proj weights
+                            // issued after the first wait, not at entry; 4 = o_proj's residual
+                            // operand loaded at entry
 };
 bool lm_attn_fits(int H, int nh, int nkv, int d, int R, int keys);
 size_t lm_attn_part_floats(int R, int keys);
@@ -331,6 +335,10 @@ struct CodecStageArgs {
   unsigned* sync;           // 12 lines of 32 words (shards 0-7, generation 11)
   unsigned* err;            // set to 1 when a grid wait gave up
   unsigned long long* stamps;   // diagnostics: [G][64] s_memrealtime per phase, or nullptr
+  int pubfirst;             // C = 2,048 weight-stream issue (codec_stage.hip): 0 = a block's whole
+                            // stream at the previous block's end (round 5); 1 = the same after the
+                            // output and arrival; 2 = after the wait; 3..5 = in four halves at the
+                            // phase points, at most 6 / 10 / 14 loads in flight per wave (default 5)
 };
 bool codec_stage_fits(int C, int T, int n, int depth);
 int launch_codec_stage(const CodecStageArgs& a, hipStream_t st);

@@ -110,6 +110,9 @@ __global__ void __launch_bounds__(la::NT) k_lm_attn(LmAttnArgs a) {
     nunit = qi < R ? (RP.pos[qi] + 1 + 31) / 32 : 0;
   }
   la_stamp(a, 0);
+  bf16x4 rv_pre = (bf16x4){0, 0, 0, 0};   // o_proj's residual operand (variant 4: loaded at entry)
+  if ((a.variant & 4) && ot && wave == 0 && r16 < R)
+    rv_pre = *(const bf16x4*)(rm_bf(a.res, r16) + 16 * (w - O0) + 4 * g4);
 
   // ================= phase 1: q|k|v tile (workgroups < 128) / o_proj weights (128..223)
   bf16x8 wq[KPW], wo[KPW];
@@ -125,7 +128,8 @@ __global__ void __launch_bounds__(la::NT) k_lm_attn(LmAttnArgs a) {
     rb4 = *(const bf16x4*)(a.qkv.epi.bias + 16 * w + 4 * g4);
   }
   if (qt) {
-    for (int q = wave; q < RMAX * 3; q += NW) {   // row q / 3, 64-chunk piece q % 3 (rows >= R re-read R - 1)
+    const int qn = (a.variant & 1) ? R * 3 : RMAX * 3;
+    for (int q = wave; q < qn; q += NW) {   // row q / 3, 64-chunk piece q % 3 (rows >= R re-read R - 1)
       const int m = q / 3, i = q - m * 3;
       hl_dma16<false>(xs + m * XST + i * 512, rm_bf(a.qkv.a, min(m, R - 1)) + (i * 64 + ln) * 8);
     }
@@ -139,7 +143,7 @@ __global__ void __launch_bounds__(la::NT) k_lm_attn(LmAttnArgs a) {
       cs4 = *(const bf16x4*)(RP.cs_tab + (long long)rp * D + j);
       sn4 = *(const bf16x4*)(RP.cs_tab + (long long)rp * D + 64 + j);
     }
-  } else if (ot) {
+  } else if (ot && !(a.variant & 2)) {
     const bf16* wp = hl_opaque(a.ow) + ((long long)(w - O0) * KC + wave * KPW) * 512 + ln * 8;
 #pragma unroll
     for (int kk = 0; kk < KPW; ++kk) wo[kk] = hl_ldnt(wp + (long long)kk * 512);
@@ -152,7 +156,8 @@ __global__ void __launch_bounds__(la::NT) k_lm_attn(LmAttnArgs a) {
   }
   la_stamp(a, 1);
   if (qt) {
-    for (int m = wave; m < RMAX; m += NW) {   // inverse RMS in k_rmsnorm's order
+    const int mr = (a.variant & 1) ? R : RMAX;   // (rows >= R of the MFMA are never stored)
+    for (int m = wave; m < mr; m += NW) {   // inverse RMS in k_rmsnorm's order
       float ss = 0.f;
       for (int c = ln; c < H / 8; c += 64) {
         const bf16x8 v = *(const bf16x8*)(xs + m * XST + c * 8);
@@ -163,7 +168,7 @@ __global__ void __launch_bounds__(la::NT) k_lm_attn(LmAttnArgs a) {
       if (ln == 0) inv_s[m] = rsqrtf(ss / (float)H + a.eps);
     }
     __syncthreads();
-    for (int e = hl_vopaque((int)threadIdx.x); e < RMAX * (H / 8); e += NT) {   // xform<XF_NORM>, in place
+    for (int e = hl_vopaque((int)threadIdx.x); e < mr * (H / 8); e += NT) {   // xform<XF_NORM>, in place
       const int m = e / (H / 8), c = e - m * (H / 8);
       const bf16x8 xv = *(const bf16x8*)(xs + m * XST + c * 8);
       const bf16x8 wv = *(const bf16x8*)(nw_s + c * 8);
@@ -242,6 +247,11 @@ __global__ void __launch_bounds__(la::NT) k_lm_attn(LmAttnArgs a) {
   __syncthreads();
   la_stamp(a, 3);
   if (!ok_s[0]) return;
+  if (ot && (a.variant & 2)) {
+    const bf16* wp = hl_opaque(a.ow) + ((long long)(w - O0) * KC + wave * KPW) * 512 + ln * 8;
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk) wo[kk] = hl_ldnt(wp + (long long)kk * 512);
+  }
 
   // ================= phase 2: attention units (row, kv head, 32 keys), one wave each
   const int U = pre[2 * R];
@@ -395,7 +405,7 @@ __global__ void __launch_bounds__(la::NT) k_lm_attn(LmAttnArgs a) {
   if (!ok_s[0] || !ot) return;
 
   // ================= phase 4: o_proj tile w - O0 over the attention rows + residual
-  for (int q = wave; q < RMAX * 3; q += NW) {
+  for (int q = wave; q < ((a.variant & 1) ? R * 3 : RMAX * 3); q += NW) {
     const int m = q / 3, i = q - m * 3;
     hl_dma16<true>(xs + m * XST + i * 512, a.att + (long long)min(m, R - 1) * H + (i * 64 + ln) * 8);
   }
@@ -413,7 +423,7 @@ __global__ void __launch_bounds__(la::NT) k_lm_attn(LmAttnArgs a) {
   __syncthreads();
   if (wave == 0 && r16 < R) {   // EPI_RES: out = bf16(res + bf16(acc)), row m = lane & 15
     const int m = r16, n = 16 * (w - O0) + 4 * g4;
-    const bf16x4 rv = *(const bf16x4*)(rm_bf(a.res, m) + n);
+    const bf16x4 rv = (a.variant & 4) ? rv_pre : *(const bf16x4*)(rm_bf(a.res, m) + n);
     bf16x4 o;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
