@@ -100,7 +100,6 @@ __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
   if (ctl) g0 = __hip_atomic_load((hl_gu32*)(a.sync + 12 * pk::LINE), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~7u;
 
   bf16x8 wb[WB];
-  const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
   // this workgroup's half down tile into the registers (in flight through the
   // hand-off); lanes of the other half of the tile feed only output columns this
   // workgroup does not store: they read one line instead (unconditional loads)
@@ -318,12 +317,18 @@ __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
   if (!ctl) {
     const int ln = hl_vopaque(lane);
     f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-    auto a_blk = [&](int kk) {
-      const int kc = wave * KPW2 + kk;
-      return (ln & 15) < R ? *(const bf16x8*)(act_s + (ln & 15) * AST + kc * 32 + 8 * (ln >> 4)) : zero8;
-    };
+    // A rows >= R read row R - 1 again (D row m depends on A row m only: never
+    // stored); unconditional reads in groups of 6 ahead of their MFMAs (a guarded
+    // read per k-block serialised ~35 LDS round trips with the MFMAs)
+    const bf16* ab = act_s + min(ln & 15, R - 1) * AST + wave * KPW2 * 32 + 8 * (ln >> 4);
 #pragma unroll
-    for (int kk = 0; kk < KPW2; ++kk) acc = mfma16(a_blk(kk), wb[kk], acc);
+    for (int k0 = 0; k0 < KPW2; k0 += 6) {
+      bf16x8 av[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) av[i] = *(const bf16x8*)(ab + (k0 + i) * 32);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) acc = mfma16(av[i], wb[k0 + i], acc);
+    }
     *(f32x4*)(red2 + wave * 256 + ln * 4) = acc;
   }
   __syncthreads();

@@ -280,7 +280,7 @@ struct LmFfnArgs {
                      // column-group tickets at word 13 x 32
   unsigned* err;     // set to 1 when the grid wait gave up
   float* slab;       // k_lm_ffn16: [48 column groups][4 hidden ranges][16][32] fp32 partials of down
-  unsigned long long* stamps;   // k_lm_ffn16 diagnostics: [256][16] s_memrealtime per phase, or nullptr
+  unsigned long long* stamps;   // diagnostics: [256][16] s_memrealtime per phase, or nullptr
 };
 bool lm_ffn_fits(int H, int F, int R);
 int launch_lm_ffn(const LmFfnArgs& a, hipStream_t st);

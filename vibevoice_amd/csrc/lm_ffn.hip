@@ -84,9 +84,28 @@ __global__ void __launch_bounds__(lf::NT) k_lm_ffn(LmFfnArgs a) {
   unsigned g0 = 0;
   if (ctl) __builtin_amdgcn_s_setprio(3);
   if (ctl) g0 = __hip_atomic_load((hl_gu32*)(a.sync + 11 * pk::LINE), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~7u;
+  // diagnostics (k_lm_ffn16's numbering): 0 start, 1 A side in LDS, 2 normalised, 3 gate|up
+  // products, 4 SiLU * up, 5 hand-off released, 6 act rows + down weights landed, 9 end
+  auto stamp = [&](int k) {
+    if (a.stamps && threadIdx.x == 0) a.stamps[w * 16 + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+  auto issue_dn_lds = [&]() {
+    // k-blocks [+18, +35) of the down weights by DMA into LDS slot wave, only
+    // this workgroup's 8 rows of each 1 KB block (512 B: lanes 0-31 block b,
+    // 32-63 block b + 1; the last pair's second block is padding)
+    const int ln = hl_vopaque(lane);
+    const bf16* dw = hl_opaque(a.dn) + (long long)(d >> 1) * KC2 * 512;
+    const int p = ln & 31, L = 16 * (p >> 3) + 8 * (d & 1) + (p & 7);   // compact position p <- packed lane L
+#pragma unroll
+    for (int q = 0; q < SLOT2 / 2; ++q) {
+      int kb = NREG2 + 2 * q + (ln >> 5);
+      kb = kb < KPW2 ? kb : KPW2 - 1;
+      hl_dma16<false, true>(dn_s + (wave * SLOT2 + 2 * q) * 256, dw + (long long)(wave * KPW2 + kb) * 512 + L * 8);
+    }
+  };
 
   bf16x8 wb[NREG1 * KPW1];
-  const bf16x8 zero8 = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
   if (ctl && owner && lane < R) hl_dma16<false>(xraw_s, hl_opaque(a.x) + (long long)lane * a.ldx + col0);
   if (!ctl) {
     const int ln = hl_vopaque(lane);
@@ -118,6 +137,7 @@ __global__ void __launch_bounds__(lf::NT) k_lm_ffn(LmFfnArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the x columns landed
   }
   __syncthreads();
+  stamp(1);
   for (int m = wave; m < R; m += NT / 64) {   // inverse RMS in k_rmsnorm's order
     const int ln = hl_vopaque(lane);
     float ss = 0.f;
@@ -140,6 +160,7 @@ __global__ void __launch_bounds__(lf::NT) k_lm_ffn(LmFfnArgs a) {
     *(bf16x8*)(xs + m * XST + c * 8) = o;
   }
   __syncthreads();
+  stamp(2);
   if (!ctl) {   // gate|up: D[row][tile row] over this wave's 6 k-blocks, per tile (rows >= R: never read)
     const int ln = hl_vopaque(lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the LDS tiles (and the register tiles)
@@ -161,6 +182,7 @@ __global__ void __launch_bounds__(lf::NT) k_lm_ffn(LmFfnArgs a) {
       if (j < nt) *(f32x4*)(red1 + (j * 8 + wave) * 256 + ln * 4) = acc[j];
   }
   __syncthreads();
+  stamp(3);
   for (int e = hl_vopaque((int)threadIdx.x); e < nt * R * 8; e += NT) {   // SiLU(gate) * up (epi_silu8)
     const int j = e / (R * 8), r = e - j * (R * 8), m = r >> 3, c = r & 7;
     float g = 0.f, u = 0.f;
@@ -172,6 +194,11 @@ __global__ void __launch_bounds__(lf::NT) k_lm_ffn(LmFfnArgs a) {
     su_s[(j * RMAX + m) * 8 + c] = tobf(rb(silu_f(rb(g))) * rb(u));
   }
   __syncthreads();
+  stamp(4);
+  // (A/B, tools/lm_ffn16_stamps.py 2: the LDS half of the down weights issued at
+  // entry, 18.3 -> 20.3 us; k_lm_ffn16's order -- act stores and the arrival
+  // ahead of the down weights, the poll after them -- 19.0 us: at 2 rows the
+  // stream, not the hand-off, sets the time, and both left HBM idle longer)
   if (!ctl && owner) {
     // the down weights, in flight through the hand-off: k-blocks [35 wave,
     // +18) into the registers (lanes of the other half tile read one line:
@@ -184,13 +211,7 @@ __global__ void __launch_bounds__(lf::NT) k_lm_ffn(LmFfnArgs a) {
 #pragma unroll
     for (int kk = 0; kk < NREG2; ++kk)
       wb[kk] = hl_ldnt(mine ? dw + (long long)(wave * KPW2 + kk) * 512 + ln * 8 : dw);
-    const int p = ln & 31, L = 16 * (p >> 3) + 8 * (d & 1) + (p & 7);   // compact position p <- packed lane L
-#pragma unroll
-    for (int q = 0; q < SLOT2 / 2; ++q) {
-      int kb = NREG2 + 2 * q + (ln >> 5);
-      kb = kb < KPW2 ? kb : KPW2 - 1;
-      hl_dma16<false, true>(dn_s + (wave * SLOT2 + 2 * q) * 256, dw + (long long)(wave * KPW2 + kb) * 512 + L * 8);
-    }
+    issue_dn_lds();
   }
   if (ctl) {   // act[m][8 (t0 + j) .. + 8], written through
     for (int q = lane; q < nt * R * 2; q += 64) {
@@ -202,6 +223,7 @@ __global__ void __launch_bounds__(lf::NT) k_lm_ffn(LmFfnArgs a) {
     if (lane == 0) ok_s[0] = hl_grid_wait_gen(a.sync, 11, g0, 1, w, a.err) ? 1u : 0u;
   }
   __syncthreads();
+  stamp(5);
   if (!ok_s[0] || !owner) return;
   // ================= down: act rows -> 8 output columns, residual
   if (!ctl) {
@@ -214,19 +236,26 @@ __global__ void __launch_bounds__(lf::NT) k_lm_ffn(LmFfnArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the act rows, the down registers and the LDS blocks
   }
   __syncthreads();
+  stamp(6);
   if (!ctl) {
     const int ln = hl_vopaque(lane);
     const int p = (ln >> 4) * 8 + (ln & 7);   // this lane's compact position (the other half tile's lanes: garbage, never stored)
     f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-    auto a_blk = [&](int kk) {
-      const int kc = wave * KPW2 + kk;
-      return (ln & 15) < R ? *(const bf16x8*)(act_s + (ln & 15) * AST + kc * 32 + 8 * (ln >> 4)) : zero8;
-    };
+    // A rows >= R read row R - 1 again (D row m depends on A row m only: never
+    // stored); unconditional reads in groups of 5 ahead of their MFMAs (a guarded
+    // read per k-block serialised 35 LDS round trips with the MFMAs: ~1.9 us)
+    const bf16* ab = act_s + min(ln & 15, R - 1) * AST + wave * KPW2 * 32 + 8 * (ln >> 4);
 #pragma unroll
-    for (int kk = 0; kk < NREG2; ++kk) acc = mfma16(a_blk(kk), wb[kk], acc);
+    for (int k0 = 0; k0 < KPW2; k0 += 5) {
+      bf16x8 av[5], wv[5];
 #pragma unroll
-    for (int kk = NREG2; kk < KPW2; ++kk)
-      acc = mfma16(a_blk(kk), *(const bf16x8*)(dn_s + (wave * SLOT2 + kk - NREG2) * 256 + p * 8), acc);
+      for (int i = 0; i < 5; ++i) {
+        av[i] = *(const bf16x8*)(ab + (k0 + i) * 32);
+        if (k0 + i >= NREG2) wv[i] = *(const bf16x8*)(dn_s + (wave * SLOT2 + k0 + i - NREG2) * 256 + p * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < 5; ++i) acc = mfma16(av[i], k0 + i < NREG2 ? wb[k0 + i] : wv[i], acc);
+    }
     *(f32x4*)(red2 + wave * 256 + ln * 4) = acc;
   }
   __syncthreads();
@@ -240,6 +269,7 @@ __global__ void __launch_bounds__(lf::NT) k_lm_ffn(LmFfnArgs a) {
       a.out[(long long)m * a.ldx + col0 + c] = tobf(bf(xraw_s[m * 8 + c]) + rb(s));
     }
   }
+  stamp(9);
 }
 
 bool lm_ffn_fits(int H, int F, int R) {
