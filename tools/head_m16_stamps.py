@@ -15,7 +15,8 @@ first entry, and the phase-to-phase medians.
   10 A side landed (wave 7)  11 gate / x columns landed (control wave)
   12 / 13 wave 0's norm / transform loop done (before the barrier)
 The stamped run uses the variant given (vv_head_m16's value: 1 default, + 2 =
-every A-side DMA issued before any weight load, + 4 = the down weights issued
+every A-side DMA issued before any weight load (default at > 8 rows), + 8 =
+never, + 4 = the down weights issued
 right after the gate|up products instead of after SiLU * up).
 
 usage: python tools/head_m16_stamps.py [n] [variant]"""
@@ -45,7 +46,7 @@ def capture(eng, pos, neg, x, s):
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-    variant = int(sys.argv[2]) if len(sys.argv) > 2 else 1   # vv_head_m16's value: 2 = A side first
+    variant = int(sys.argv[2]) if len(sys.argv) > 2 else 1   # vv_head_m16's value: 2 = A side first, 8 = not first (default: first at > 8 rows)
     g = torch.Generator().manual_seed(5)
     sdh, hc, H = real_head_sd(g)
     cfg = tiny_config(hidden=H, layers=1, heads=12, kv_heads=2, inter=256)
@@ -60,7 +61,7 @@ def main():
     x = x0.clone()
     L = _lib.lib()
     s = torch.cuda.Stream()
-    for mode, pre in ((0, 1), (5, 0), (1, 0), (5, 1), (3, 1), (1, 1), (variant, 1)):
+    for mode, pre in ((0, 1), (5, 0), (1, 0), (5, 1), (3, 1), (9, 1), (1, 1), (variant, 1)):
         L.vv_head_m16(mode)
         L.vv_head_m16_pre(pre)
         assert L.vv_head_m16_active(eng.h, n) == (1 if mode else 0)
@@ -77,7 +78,7 @@ def main():
                 ev1.record(s)
             torch.cuda.synchronize()
             best = min(best, ev0.elapsed_time(ev1) * 1e3)
-        print(f"{'k_head_m16' if mode else 'GEMV pair'}{' A side first' if mode & 2 else ''}"
+        print(f"{'k_head_m16' if mode else 'GEMV pair'}{' A side first' if mode & 2 else ' A side not first' if mode & 8 else ''}"
               f"{' down issued after gate|up' if mode & 4 else ''}"
               f"{' (distributed A side)' if mode and pre else ''}: whole head sample (cond + adaLN + "
               f"{eng.steps} steps x {hc.head_layers} layers), best of 8 graph replays: {best:.1f} us")

@@ -1810,7 +1810,8 @@ extern "C" int vv_head_m16_stamps(void* buf) {   // diagnostic: [256][16] per-wo
   return 0;
 }
 extern "C" int vv_head_m16(int on) {
-  g_head_m16 = on;   // A/B variants: bit 1 HeadM16Args::a_first, bit 2 the down weights' earlier issue point
+  g_head_m16 = on;   // A/B variants: bit 1 / bit 3 HeadM16Args::a_first on / off (default: > 8 rows),
+                     // bit 2 the down weights' earlier issue point
   return 0;
 }
 // the one-launch layer applies (R <= 16 rows, GEMV layout, unsharded, sole context)
@@ -1888,7 +1889,9 @@ static int head_layer(vv_ctx* c, const HeadRun& h, int s, int l, hipStream_t st)
     a.sync = (unsigned*)c->hf_sync.p;
     a.err = (unsigned*)c->hf_sync.p + 10 * 32;
     a.stamps = g_head_m16_stamps;
-    a.a_first = (g_head_m16.load() & 2) ? 1 : 0;
+    // the A side ahead of every weight load: at 16 rows (B = 8) a whole head
+    // sample 890 -> 860 us, at 2 rows (B = 1) 595 -> 603 us (tools/head_m16_stamps.py)
+    a.a_first = (g_head_m16.load() & 2) ? 1 : (g_head_m16.load() & 8) ? 0 : (h.R > 8 ? 1 : 0);
     a.late_down = (g_head_m16.load() & 4) ? 0 : 1;
     a.ssp = (float*)c->m16_buf.p;
     a.xt = (bf16*)((char*)c->m16_buf.p + 16 * 192 * sizeof(float));
