@@ -13,7 +13,7 @@ Prints per phase the median / max over the 256 workgroups relative to the
 first entry, and the phase-to-phase medians.
 
   10 A side landed (wave 7)  11 gate / x columns landed (control wave)
-  12 / 13 wave 0's norm / transform loop done (before the barrier)
+  12 / 13 wave 0's norm / transform loop done (before the barrier)  14 wave 0 past the barrier before the norm
 The stamped run uses the variant given (vv_head_m16's value: 1 default, + 2 =
 every A-side DMA issued before any weight load (default at > 8 rows), + 8 =
 never, + 4 = the down weights issued
@@ -97,10 +97,10 @@ def main():
     rel = t - t0
     names = ["entry", "A side landed", "row norms", "transform", "gate|up partials", "SiLU * up",
              "hand-off released", "act rows in LDS", "down partials", "end (owners)",
-             "A side landed (w7)", "gate / x cols (ctl)", "norm loop done (w0)", "transform loop done (w0)"]
+             "A side landed (w7)", "gate / x cols (ctl)", "norm loop done (w0)", "transform loop done (w0)", "barrier passed (w0)"]
     print("last launch's phases, us from the first workgroup's entry (median / max over workgroups):")
     prev = None
-    for k in (0, 11, 1, 10, 12, 2, 13, 3, 4, 5, 6, 7, 8, 9):   # in phase order
+    for k in (0, 11, 1, 10, 14, 12, 2, 13, 3, 4, 5, 6, 7, 8, 9):   # in phase order
         name = names[k]
         col = rel[:, k]
         ok = t[:, k] >= t[:, 0]   # (a stamp the last launch's form does not write holds an earlier launch's)

@@ -603,9 +603,13 @@ __global__ void __launch_bounds__(cs2::NT) k_codec_stage_s(CodecStageArgs a) {
 
   if (!ctl) issue(0, threadIdx.x);
   if (ctl) prefetch(0);
+  // pubfirst >= 3: block j + 1's weights (64 KB per CU) issued after the second
+  // wait, under the front half, instead of ahead of the output and the wait
+  const bool late = a.pubfirst >= 3;
   for (int j = 0; j < a.depth; ++j) {
     const bool last = j + 1 == a.depth;
     stamp(8 * j + 0, true);
+    if (late && j > 0 && !ctl) issue(j, hl_vopaque((int)threadIdx.x));
     // ================= front half over the M rows (all waves, from LDS)
     if (ctl) {   // the block's input rows (this launch's: sc1)
       const int ln = hl_vopaque(lane);
@@ -746,7 +750,7 @@ __global__ void __launch_bounds__(cs2::NT) k_codec_stage_s(CodecStageArgs a) {
     }
     __syncthreads();   // B5
     stamp(8 * j + 6, true);
-    if (!ctl && !last) issue(j + 1, hl_vopaque((int)threadIdx.x));
+    if (!late && !ctl && !last) issue(j + 1, hl_vopaque((int)threadIdx.x));
     if (ctl && lane < M * ROWS2) {   // epi_row8's EPI_RES with ffn_gamma
       const int ln = hl_vopaque(lane), m = ln / ROWS2, r = ln - m * ROWS2, col = ROWS2 * w + r;
       float sacc = 0.f;

@@ -214,6 +214,7 @@ __global__ void __launch_bounds__(hm::NT) k_head_m16(HeadM16Args a) {
     stamp(3, true);
   } else {
   __syncthreads();
+  if (wave == 0 && a.stamps && lane == 0) a.stamps[w * 16 + 14] = __builtin_amdgcn_s_memrealtime();
   for (int m = wave; m < R; m += NT / 64) {   // inverse RMS in k_rmsnorm's order
     const int ln = hl_vopaque(lane);
     float ss = 0.f;
