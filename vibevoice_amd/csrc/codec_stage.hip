@@ -642,27 +642,56 @@ __global__ void __launch_bounds__(cs2::NT) k_codec_stage_s(CodecStageArgs a) {
       bf16* nb = hl_opaque(a.b[j].mix) + slot * a.b[j].mix_sB + (long long)a.ctx * C;
       for (int e = hl_vopaque(lane); e < M * NCH; e += 64) *(bf16x8*)(nb + e * 8) = *(const bf16x8*)(nrm_s + CTX * C + e * 8);
     }
-    for (int e = hl_vopaque((int)threadIdx.x); e < M * NCH; e += NT) {   // depthwise conv + gamma residual: y over x
-      const int m = e / NCH, c = e - m * NCH;
-      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // depthwise conv + gamma residual: y over x.  Thread (chunk c, row group):
+    // the 8 channels [8c, 8c + 8) of RPT consecutive rows, so the 7 taps and the
+    // window's input rows are converted once for RPT rows (one element per
+    // thread converted every tap for every element: 3.3 us per block, VALU-bound
+    // in all 256 workgroups).  Each output still sums its taps k = 0 .. 6 in order.
+    constexpr int RPT = M >= 4 ? 4 : M;
+    for (int e = hl_vopaque((int)threadIdx.x); e < NCH * (M / RPT); e += NT) {
+      const int c = e % NCH, m0 = RPT * (e / NCH);
+      float wt[K7][8];
 #pragma unroll
       for (int k = 0; k < K7; ++k) {
-        const bf16x8 v = *(const bf16x8*)(nrm_s + (m + k) * C + c * 8);
         const bf16x8 wk = *(const bf16x8*)(vec_s + 4 * C + k * C + c * 8);   // tap k of the chunk's 8 columns
 #pragma unroll
-        for (int q = 0; q < 8; ++q) acc[q] += bf(wk[q]) * bf(v[q]);
+        for (int q = 0; q < 8; ++q) wt[k][q] = bf(wk[q]);
       }
-      const bf16x8 xv = *(const bf16x8*)(x_s + e * 8), bb = *(const bf16x8*)(vec_s + C + c * 8),
-                   gv = *(const bf16x8*)(vec_s + 2 * C + c * 8);
-      bf16x8 y8;
-      float s8 = 0.f;
+      float acc[RPT][8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        y8[q] = tobf(bf(xv[q]) + rb(rb(acc[q] + bf(bb[q])) * bf(gv[q])));
-        s8 += bf(y8[q]) * bf(y8[q]);
+      for (int i = 0; i < RPT; ++i)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[i][q] = 0.f;
+#pragma unroll
+      for (int r = 0; r < RPT + K7 - 1; ++r) {   // window row m0 + r: tap r - i of output row m0 + i
+        const bf16x8 v = *(const bf16x8*)(nrm_s + (m0 + r) * C + c * 8);
+        float vf[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) vf[q] = bf(v[q]);
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+          const int k = r - i;
+          if (k >= 0 && k < K7) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc[i][q] += wt[k][q] * vf[q];
+          }
+        }
       }
-      *(bf16x8*)(x_s + e * 8) = y8;
-      ssp[e] = s8;
+      const bf16x8 bb = *(const bf16x8*)(vec_s + C + c * 8), gv = *(const bf16x8*)(vec_s + 2 * C + c * 8);
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) {
+        const int ei = (m0 + i) * NCH + c;
+        const bf16x8 xv = *(const bf16x8*)(x_s + ei * 8);
+        bf16x8 y8;
+        float s8 = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          y8[q] = tobf(bf(xv[q]) + rb(rb(acc[i][q] + bf(bb[q])) * bf(gv[q])));
+          s8 += bf(y8[q]) * bf(y8[q]);
+        }
+        *(bf16x8*)(x_s + ei * 8) = y8;
+        ssp[ei] = s8;
+      }
     }
     __syncthreads();
     stamp(42 + 4 * j, true);
