@@ -93,10 +93,11 @@ DEV void hl_arrive(unsigned* sync, int w) {
                                             __HIP_MEMORY_SCOPE_AGENT);
   if ((v + 1) % (G / 8) == 0) __hip_atomic_fetch_add((hl_gu32*)hl_gen(sync), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// poll until k waits of this launch (base generation g0) have completed; false:
-// gave up after ~200 ms (error word set)
-DEV bool hl_poll(unsigned* sync, unsigned g0, unsigned k, unsigned* err) {
-  unsigned* gen = hl_gen(sync);
+// poll the generation word until it has advanced by 8 k from g0; false: gave up
+// after ~200 ms (error word set).  (A/B builds, tools/ab_lib.sh: two polls in
+// flight half a round trip apart, or s_sleep 4 between polls: B = 1 within
+// +-0.01 ms of this one-at-a-time loop.)
+DEV bool hl_poll_word(unsigned* gen, unsigned g0, unsigned k, unsigned* err) {
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   while ((unsigned)(__hip_atomic_load((hl_gu32*)gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - g0) < 8 * k) {
     __builtin_amdgcn_s_sleep(1);
@@ -106,6 +107,11 @@ DEV bool hl_poll(unsigned* sync, unsigned g0, unsigned k, unsigned* err) {
     }
   }
   return true;
+}
+// poll until k waits of this launch (base generation g0) have completed; false:
+// gave up after ~200 ms (error word set)
+DEV bool hl_poll(unsigned* sync, unsigned g0, unsigned k, unsigned* err) {
+  return hl_poll_word(hl_gen(sync), g0, k, err);
 }
 DEV bool hl_grid_wait(unsigned* sync, unsigned g0, unsigned k, int w, unsigned* err) {
   hl_arrive(sync, w);
@@ -124,16 +130,7 @@ DEV void hl_arrive_gen(unsigned* sync, int gen_line, int w) {
 // after ~200 ms (error word set).  (Polling by scalar loads that miss the scalar
 // cache was tried: the hand-offs took 11-20 us instead of 1.4-3.)
 DEV bool hl_poll_gen(unsigned* sync, int gen_line, unsigned g0, unsigned k, unsigned* err) {
-  unsigned* gen = sync + gen_line * pk::LINE;
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  while ((unsigned)(__hip_atomic_load((hl_gu32*)gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - g0) < 8 * k) {
-    __builtin_amdgcn_s_sleep(1);
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {   // ~200 ms at 100 MHz
-      __hip_atomic_store((hl_gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-  }
-  return true;
+  return hl_poll_word(sync + gen_line * pk::LINE, g0, k, err);
 }
 
 // the same wait on the generation word at line `gen_line` of `sync` (a kernel of
@@ -144,13 +141,5 @@ DEV bool hl_grid_wait_gen(unsigned* sync, int gen_line, unsigned g0, unsigned k,
   const unsigned v = __hip_atomic_fetch_add((hl_gu32*)(sync + (w & 7) * LINE), 1u, __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT);
   if ((v + 1) % (G / 8) == 0) __hip_atomic_fetch_add((hl_gu32*)gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  while ((unsigned)(__hip_atomic_load((hl_gu32*)gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - g0) < 8 * k) {
-    __builtin_amdgcn_s_sleep(1);
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {   // ~200 ms at 100 MHz
-      __hip_atomic_store((hl_gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-  }
-  return true;
+  return hl_poll_word(gen, g0, k, err);
 }
