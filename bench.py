@@ -425,12 +425,13 @@ def measure_head_layers(model, B, reps=10, iters=4):
               "grid-wide hand-off, MFMA down + gated residual; above 4 rows the A side built distributed)" if m16 else
               "k_gemv1 gate|up + k_gemv/k_gemv1 down (one head FFN layer = two GEMV launches, timed together)")
     traffic = None
-    pf = os.path.join(ROOT, "profiles", f"r05_pmc_head_r{R}.json")
-    if os.path.exists(pf):
-        with open(pf) as f:
-            pmc = json.load(f)
-        if pmc.get("kernel") == kernel.split(" (")[0] and pmc.get("shape") == f"rows={R} H={H} F={F}":
-            traffic = pmc["hbm_bytes_per_launch"]
+    for pf in (os.path.join(ROOT, "profiles", f"r06_pmc_head_r{R}.json"),
+               os.path.join(ROOT, "profiles", f"r05_pmc_head_r{R}.json")):
+        if traffic is None and os.path.exists(pf):
+            with open(pf) as f:
+                pmc = json.load(f)
+            if pmc.get("kernel") == kernel.split(" (")[0] and pmc.get("shape") == f"rows={R} H={H} F={F}":
+                traffic = pmc["hbm_bytes_per_launch"]
     return roof(kernel, f"rows={R} H={H} F={F}", alg, per_layer, traffic,
                 launches_per_token=int(model.ddpm_inference_steps * L),
                 note="graph-replayed head FFN layers (vv_head_layers_replay), HIP events on the replay stream; "

@@ -10,7 +10,7 @@ usage (GPU box):
                                               # profiles/r05_pmc_traffic_m<M>.json
   python tools/pmc_traffic.py collect-head [R]  # the same for the diffusion head's FFN layer kernel
                                               # (k_head_m16 at R = 2n rows)
-                                              # -> profiles/r05_pmc_head_r<R>.json
+                                              # -> profiles/r06_pmc_head_r<R>.json
   python tools/pmc_traffic.py collect-lmffn 2  # the LM MLP block in one launch (k_lm_ffn, B = 1;
                                               # 16: k_lm_ffn16, B = 8) -> profiles/r06_pmc_lm_ffn_r<M>.json
 M = 2 (B = 1, one tile per workgroup) or 16 (B = 8: the balanced form, 4-5 tiles per workgroup).
@@ -146,7 +146,7 @@ def collect():
                    alg_bytes_per_launch=alg, traffic_over_alg=round((fetch + write) / alg, 4),
                    method="rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, tools/pmc_traffic.py run; "
                           "FETCH_SIZE x 2 (gfx950), KiB -> bytes")
-    name = (f"r05_pmc_head_r{M}.json" if HEAD else f"r06_pmc_lm_ffn_r{M}.json" if LMF else
+    name = (f"r06_pmc_head_r{M}.json" if HEAD else f"r06_pmc_lm_ffn_r{M}.json" if LMF else
             f"r05_pmc_traffic_m{M}.json")
     for path in (os.path.join(ROOT, "profiles", name), os.path.join(out, "pmc_traffic.json")):
         with open(path, "w") as f:
