@@ -445,9 +445,14 @@ def measure_head_layers(model, B, reps=10, iters=4):
 
 
 def us_per_step(r):
-    """A roofline candidate's time per loop step: avg x launches per step."""
+    """A roofline candidate's time per loop step: from the committed step profile
+    of the loop when it holds the kernel (the loop's own clock: the isolated
+    replays of the three candidates differ from it by up to ~5 %), else the
+    replay average x launches per step."""
     if not r or "error" in r or not r.get("avg_us"):
         return -1.0
+    if r.get("in_loop"):
+        return r["in_loop"]["us_per_step"]
     return r["avg_us"] * r.get("launches_per_token", 1)
 
 
@@ -744,10 +749,10 @@ def main():
         roof_attn = measure_lm_attn(model, B, ctx_avg)
     except Exception as e:   # noqa: BLE001
         print(f"bench: LM attention half roofline not measured: {e}", file=sys.stderr, flush=True)
-    roofline, roofline_2 = pick_roofline(roof_lm, roof_head, roof_attn)
-    for r in (roofline, roofline_2):
+    for r in (roof_lm, roof_head, roof_attn):
         if r and "error" not in r:
             in_loop_average(r, B)
+    roofline, roofline_2 = pick_roofline(roof_lm, roof_head, roof_attn)
     tp_coll = None
     if T > 1:   # after the timed loop: the null-collective passes corrupt the session's state
         tp_coll = measure_tp_collective(lm_pass_maker(model, sess), model.config.decoder_config.num_hidden_layers,
