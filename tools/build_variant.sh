@@ -6,7 +6,7 @@ name=$1; shift
 src=$(cd "$(dirname "$0")/../vibevoice_amd/csrc" && pwd)
 out=/tmp/vv_$name; mkdir -p $out
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -Wno-unused-variable $*"
-for f in gemm chain elementwise attention codec_block; do /opt/rocm/bin/hipcc $F -c $src/$f.hip -o $out/$f.o & done
+for f in $src/*.hip; do b=$(basename $f .hip); /opt/rocm/bin/hipcc $F -c $f -o $out/$b.o & done
 /opt/rocm/bin/hipcc $F -x hip -c $src/engine.cpp -o $out/engine.o &
 wait
 /opt/rocm/bin/hipcc $F -shared $out/*.o -o "$(dirname "$0")/lib_$name.so" -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
